@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mpixels/s of the fused DCT(B=8)+deadzone encode at 4K.
+
+BASELINE.json metric: "Mpixels/s encode (DCT+deadzone) at 4K; % HBM roofline;
+1/2/4/8-GPU scaling".  One step = one launch of the encode kernel over a batch
+of 4K RGB frames already resident in HBM (the hot path of src/2D-DCT.py
+encode_fn :276-361 for every frame of the batch).  Frames shard across ranks
+with no data-path collective (frames are independent units), so scaling is
+weak: every rank encodes its own batch; value = all ranks' pixels / the
+slowest rank's wall time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints one JSON line.  The roofline block is measured live with HIP
+events on the stream the kernel runs on; the cpu_baseline block times the C
+oracle (oracle/vcf_oracle.c, the CPU restatement of the same path, 1 thread)
+on a bounded sample of the same frames.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+ALG_BYTES_PER_PIXEL = 6  # 3 B RGB read + 3 B index write
+
+
+def synth_frame(H: int, W: int, seed: int) -> np.ndarray:
+    """S-smooth of SURVEY.md §8(d): natural-like synthetic RGB (seeded)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    y = np.arange(H, dtype=np.float32)[:, None]
+    x = np.arange(W, dtype=np.float32)[None, :]
+    chans = []
+    for c in range(3):
+        v = 128 + 60 * np.sin(x / 97 + c + seed) + 50 * np.cos(y / 61 - c - seed)
+        v = v + rng.normal(0, 4, (H, W)).astype(np.float32)
+        chans.append(v)
+    return np.clip(np.rint(np.stack(chans, -1)), 0, 255).astype(np.uint8)
+
+
+def dist_setup(ngpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != ngpus:
+        if world == 1 and ngpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run "
+                             "(one process per GPU)")
+        raise SystemExit(f"WORLD_SIZE={world} does not match --gpus {ngpus}")
+    pg = None
+    if world > 1:
+        import torch.distributed as dist  # host-side barrier / max only (gloo)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def allreduce_max(pg, v: float) -> float:
+    if pg is None:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(pg, v: float) -> float:
+    if pg is None:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return float(t.item())
+
+
+def cpu_baseline(frame: np.ndarray, Q: int, budget_s: float):
+    """Time the C oracle (1 thread) on whole 4K frames for ~budget_s seconds."""
+    from oracle import oracle as O   # test infrastructure: the checker, timed as the CPU port
+    O.lib()
+    n, t0 = 0, time.perf_counter()
+    k = None
+    while True:
+        k = O.encode_frame(frame, Q)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 64:
+            break
+    H, W = frame.shape[:2]
+    return dict(value=n * H * W / el / 1e6, unit="Mpixels/s", cores=1, kind="port",
+                sample=f"{n} x {H}x{W} S-smooth frame(s), oracle/vcf_oracle.c (gcc -O2, "
+                       f"-ffp-contract=off), 1 thread, {el:.1f} s"), k
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc pass (if it matches)."""
+    p = os.path.join(ROOT, "profiles", "pmc_encode_4k.json")
+    try:
+        d = json.load(open(p))
+    except Exception:
+        return None, None
+    if d.get("workload") != workload:
+        return None, None
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--frames", type=int, default=64, help="4K frames per step per GPU")
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("-q", "--QSS", type=int, default=32)
+    ap.add_argument("--cpu-budget", type=float, default=12.0,
+                    help="seconds of oracle CPU time for cpu_baseline (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local, pg = dist_setup(args.gpus)
+    import vcf_amd.dct as D
+    from vcf_amd.device import DeviceBuffer, Event, Stream, set_device, synchronize
+
+    set_device(local)
+    H, W, F, Q = args.height, args.width, args.frames, args.QSS
+    Hp, Wp = D.padded_shape(H, W)
+    frame_bytes = H * W * 3
+    distinct = [synth_frame(H, W, seed=rank * 1000 + s) for s in range(4)]
+    din = DeviceBuffer(F * frame_bytes)
+    for f in range(F):
+        din.upload(distinct[f % len(distinct)], offset=f * frame_bytes)
+    dout = DeviceBuffer(F * Hp * Wp * 3)
+    stream = Stream()
+
+    def step():
+        D.encode_device(din, F, H, W, Q, 0, out=dout, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+
+    # parity spot check of the timed kernel's output: frame 0 vs the C oracle
+    parity = None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, k_ref = cpu_baseline(distinct[0], Q, args.cpu_budget)
+        k_gpu = dout.download(np.empty((Hp, Wp, 3), np.uint8))
+        parity = "bit-exact vs oracle (frame 0)" if np.array_equal(k_gpu, k_ref) else "MISMATCH"
+
+    e0, e1 = Event(), Event()
+    barrier(pg)
+    synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    stream.synchronize()
+    synchronize()
+    t1 = time.perf_counter()
+    barrier(pg)
+    wall = t1 - t0
+    kernel_ms = e0.elapsed_ms(e1) / args.steps   # average launch duration (event-timed)
+
+    wall_max = allreduce_max(pg, wall)
+    pixels = allreduce_sum(pg, float(args.steps * F * H * W))
+    value = pixels / wall_max / 1e6
+
+    workload = (f"dct_dz_encode {H}x{W}x3 u8 RGB frames (4K), B=8, YCoCg, deadzone Q={Q}, "
+                f"subband layout, {F} frames/step/GPU resident in HBM")
+    alg_bytes = F * H * W * 3 + F * Hp * Wp * 3
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic, tsrc = load_traffic(workload)
+    if rank == 0:
+        out = {
+            "metric": "Mpixels/s encode (DCT+deadzone) at 4K",
+            "value": round(value, 1),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (S-smooth 4K RGB, seeded)",
+            "config": {"workload": workload, "global_batch": F * world, "frame": [H, W, 3],
+                       "block_size": 8, "QSS": Q, "parallelism": f"frame-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel_ms_per_launch": round(kernel_ms, 4),
+                         "alg_bytes_per_launch": alg_bytes,
+                         "traffic_source": tsrc},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,53 @@
+"""CPU check of the HIP kernels' per-block arithmetic (vcf_dct_block.h, built
+for the host with g++ -ffp-contract=off) against the oracle, bit for bit."""
+import ctypes
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import oracle as O
+
+HARNESS_SRC = os.path.join(ROOT, "tests", "cpu", "block_harness.cpp")
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    so = str(tmp_path_factory.mktemp("hb") / "block_harness.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+                    "-I", os.path.join(ROOT, "vcf_amd", "csrc"), HARNESS_SRC, "-o", so], check=True)
+    L = ctypes.CDLL(so)
+    u8 = ctypes.POINTER(ctypes.c_uint8)
+    L.hb_encode_block.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
+    L.hb_decode_block.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
+    return L
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+@pytest.mark.parametrize("Q,flags", [(32, 0), (7, 0), (1, 0), (64, 2), (5, 2), (3, 0), (1024, 0)])
+def test_block_encode_decode_vs_oracle(harness, Q, flags):
+    rng = np.random.Generator(np.random.PCG64(Q * 10 + flags))
+    for it in range(300):
+        if it % 3 == 0:
+            blk = rng.integers(0, 256, (8, 8, 3), dtype=np.uint8)
+        elif it % 3 == 1:
+            blk = np.full((8, 8, 3), rng.integers(0, 256, 3), dtype=np.uint8)
+        else:
+            blk = (rng.integers(0, 2, (8, 8, 3)) * 255).astype(np.uint8)
+        k = np.empty((8, 8, 3), np.uint8)
+        harness.hb_encode_block(_p(blk), Q, flags, _p(k))
+        kref = O.encode_frame(blk, Q, flags)
+        assert np.array_equal(k, kref), (it, Q, flags)
+        # decode arbitrary index blocks too (not only encoder outputs)
+        kin = kref if it % 2 else rng.integers(0, 256, (8, 8, 3), dtype=np.uint8)
+        out = np.empty((8, 8, 3), np.uint8)
+        harness.hb_decode_block(_p(kin), Q, flags, _p(out))
+        assert np.array_equal(out, O.decode_frame(kin, 8, 8, Q, flags)), (it, Q, flags)

@@ -1,0 +1,108 @@
+"""GPU parity of the fused DCT+deadzone kernels (through the C ABI).
+
+Bit-exact against (1) the golden vectors produced by the reference's own
+glue (tests/golden, make_golden.py) and (2) the C oracle on seeded inputs,
+including padding, -x, -p, non-power-of-two and wrapping quantization steps,
+batched frames and full 4K/1080p frames.
+"""
+import numpy as np
+import pytest
+
+from conftest import case_params, golden_cases, load_case
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+D = pytest.importorskip("vcf_amd.dct")
+
+
+@pytest.mark.parametrize("case", golden_cases(), ids=lambda c: c["name"])
+def test_encode_matches_reference_golden(case):
+    z = load_case(case)
+    Q, flags = case_params(case)
+    k = D.encode(z["rgb"], Q, flags)
+    assert k.shape == z["k"].shape
+    assert np.array_equal(k, z["k"])
+
+
+@pytest.mark.parametrize("case", golden_cases(), ids=lambda c: c["name"])
+def test_decode_matches_reference_golden(case):
+    z = load_case(case)
+    Q, flags = case_params(case)
+    out = D.decode(z["k"], case["H"], case["W"], Q, flags)
+    assert np.array_equal(out, z["decoded"])
+
+
+def _rand(shape, seed, kind="rand"):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    if kind == "rand":
+        return rng.integers(0, 256, shape, dtype=np.uint8)
+    if kind == "flat":
+        H, W, _ = shape
+        b = rng.integers(0, 256, ((H + 7) // 8, (W + 7) // 8, 3), dtype=np.uint8)
+        return np.repeat(np.repeat(b, 8, 0), 8, 1)[:H, :W].copy()
+    y, x = np.mgrid[0:shape[0], 0:shape[1]]
+    v = np.stack([128 + 100 * np.sin(x / 13 + c) * np.cos(y / 7 - c) for c in range(3)], -1)
+    v = v + rng.normal(0, 6, shape)
+    return np.clip(np.rint(v), 0, 255).astype(np.uint8)
+
+
+SHAPES = [(8, 8), (16, 2048), (24, 4104), (72, 136), (13, 29), (100, 100), (9, 4097), (264, 320)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("Q,flags", [(32, 0), (7, 0), (1, 0), (32, 1), (32, 2), (5, 3), (64, 2)])
+def test_encode_decode_vs_oracle(shape, Q, flags):
+    H, W = shape
+    rgb = _rand((H, W, 3), seed=H * 7919 + W + Q, kind="smooth" if H % 2 else "rand")
+    k = D.encode(rgb, Q, flags)
+    assert np.array_equal(k, O.encode_frame(rgb, Q, flags))
+    out = D.decode(k, H, W, Q, flags)
+    assert np.array_equal(out, O.decode_frame(k, H, W, Q, flags))
+
+
+def test_flat_blocks_boundary_hazard():
+    """Constant 8x8 blocks: the fp32 DC sits on k boundaries."""
+    rgb = _rand((256, 512, 3), 3, "flat")
+    for Q in (1, 2, 4, 8, 16, 32):
+        assert np.array_equal(D.encode(rgb, Q), O.encode_frame(rgb, Q))
+
+
+def test_batched_frames_equal_single():
+    frames = np.stack([_rand((64, 96, 3), s) for s in range(5)])
+    k = D.encode(frames, 32)
+    for i in range(5):
+        assert np.array_equal(k[i], O.encode_frame(frames[i], 32))
+    out = D.decode(k, 64, 96, 32)
+    for i in range(5):
+        assert np.array_equal(out[i], O.decode_frame(k[i], 64, 96, 32))
+
+
+def test_extreme_wrap_q1():
+    """q=1: |k| > 127 wraps modulo 256 exactly like astype(uint8)."""
+    rgb = (np.indices((64, 64)).sum(0) % 2 * 255).astype(np.uint8)[..., None].repeat(3, 2)
+    k = D.encode(rgb, 1)
+    assert np.array_equal(k, O.encode_frame(rgb, 1))
+    assert np.array_equal(D.decode(k, 64, 64, 1), O.decode_frame(k, 64, 64, 1))
+
+
+@pytest.mark.parametrize("shape", [(1080, 1920), (2160, 3840)])
+def test_full_size_frames(shape):
+    H, W = shape
+    rgb = _rand((H, W, 3), 11, "smooth")
+    k = D.encode(rgb, 32)
+    assert np.array_equal(k, O.encode_frame(rgb, 32))
+    out = D.decode(k, H, W, 32)
+    assert np.array_equal(out, O.decode_frame(k, H, W, 32))
+
+
+def test_zero_frames_and_errors():
+    from vcf_amd.device import DeviceBuffer
+    buf = DeviceBuffer(64)
+    D.encode_device(buf, 0, 8, 8, out=DeviceBuffer(64))   # no-op
+    with pytest.raises(ValueError):
+        D.encode(np.zeros((8, 8), np.uint8))
+    with pytest.raises(NotImplementedError):
+        D.encode(np.zeros((16, 16, 3), np.uint8), 32, block_size=16)
+    with pytest.raises(ValueError):
+        D.decode(np.zeros((8, 8, 3), np.uint8), 8, 8, 40000)

@@ -1,0 +1,54 @@
+"""Build recipe for libvcf_amd.so (hipcc, gfx950) -- used by __graft_entry__.build().
+
+The library is built in-tree (vcf_amd/libvcf_amd.so) so it travels to the GPU
+box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libvcf_amd.so")
+SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip"]
+HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h"]
+ARCH = os.environ.get("VCF_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm is required to build libvcf_amd.so)")
+
+
+def needs_rebuild() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    deps.append(os.path.join(ROOT, "include", "vcf_amd.h"))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_rebuild():
+        return LIB
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17",
+           # bit-exactness: pocketfft's separate multiply and add must not fuse
+           "-ffp-contract=off",
+           "-fPIC", "-shared", "-Wall",
+           "-I", os.path.join(ROOT, "include"), "-I", CSRC,
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force=True, verbose=True)

@@ -1,0 +1,119 @@
+"""ctypes binding of libvcf_amd.so (include/vcf_amd.h).
+
+There is deliberately no CPU fallback: if the HIP library is missing or fails
+to load, every entry point raises.  The oracle under oracle/ is test
+infrastructure and is never imported from here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from . import _build
+
+VCF_OK = 0
+VCF_ERR_INVALID = -1
+VCF_ERR_HIP = -2
+VCF_ERR_UNSUPPORTED = -3
+
+VCF_DCT_NO_SUBBANDS = 1
+VCF_DCT_PERCEPTUAL = 2
+
+
+class VCFError(RuntimeError):
+    """A libvcf_amd call failed (status < 0)."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"[vcf status {status}] {message}")
+        self.status = status
+
+
+class VCFInvalidArgument(VCFError, ValueError):
+    """VCF_ERR_INVALID: the reference raises ValueError in the same cases."""
+
+
+class VCFUnsupported(VCFError, NotImplementedError):
+    pass
+
+
+_P = ctypes.c_void_p
+_SZ = ctypes.c_size_t
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_U32 = ctypes.c_uint32
+_PI32 = ctypes.POINTER(ctypes.c_int32)
+_PI = ctypes.POINTER(ctypes.c_int)
+
+# name -> argtypes (restype is int for all but vcf_last_error)
+SIGNATURES = {
+    "vcf_version": [_PI, _PI],
+    "vcf_device_count": [_PI],
+    "vcf_set_device": [ctypes.c_int],
+    "vcf_get_device": [_PI],
+    "vcf_device_sync": [],
+    "vcf_malloc": [ctypes.POINTER(_P), _SZ],
+    "vcf_free": [_P],
+    "vcf_host_alloc": [ctypes.POINTER(_P), _SZ],
+    "vcf_host_free": [_P],
+    "vcf_memcpy_htod": [_P, _P, _SZ, _P],
+    "vcf_memcpy_dtoh": [_P, _P, _SZ, _P],
+    "vcf_memcpy_dtod": [_P, _P, _SZ, _P],
+    "vcf_memset": [_P, ctypes.c_int, _SZ, _P],
+    "vcf_stream_create": [ctypes.POINTER(_P)],
+    "vcf_stream_destroy": [_P],
+    "vcf_stream_sync": [_P],
+    "vcf_event_create": [ctypes.POINTER(_P)],
+    "vcf_event_destroy": [_P],
+    "vcf_event_record": [_P, _P],
+    "vcf_event_sync": [_P],
+    "vcf_event_elapsed_ms": [_P, _P, ctypes.POINTER(ctypes.c_float)],
+    "vcf_dct_padded_shape": [_I32, _I32, _I32, _PI32, _PI32],
+    "vcf_dct_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dct_dz_decode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib_path() -> str:
+    return os.environ.get("VCF_AMD_LIB", _build.LIB)
+
+
+def lib():
+    """Load (once) and return the ctypes handle.  Raises if it cannot."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            path = lib_path()
+            if not os.path.exists(path):
+                raise ImportError(
+                    f"libvcf_amd.so not found at {path}: build it with "
+                    "`python -m vcf_amd._build` (hipcc, gfx950). There is no CPU fallback.")
+            L = ctypes.CDLL(path)
+            for name, argtypes in SIGNATURES.items():
+                f = getattr(L, name)
+                f.argtypes = argtypes
+                f.restype = ctypes.c_int
+            L.vcf_last_error.argtypes = []
+            L.vcf_last_error.restype = ctypes.c_char_p
+            _lib = L
+    return _lib
+
+
+def check(status: int) -> None:
+    if status == VCF_OK:
+        return
+    msg = lib().vcf_last_error().decode(errors="replace")
+    if status == VCF_ERR_INVALID:
+        raise VCFInvalidArgument(status, msg)
+    if status == VCF_ERR_UNSUPPORTED:
+        raise VCFUnsupported(status, msg)
+    raise VCFError(status, msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args))

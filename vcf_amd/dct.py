@@ -1,0 +1,97 @@
+"""DCT(B=8) + deadzone hot path on the GPU (include/vcf_amd.h vcf_dct_dz_*).
+
+Replaces, in one fused kernel per direction, the numpy/scipy span of
+src/2D-DCT.py encode_fn :276-361 (to the uint8 indices handed to the entropy
+codec) and decode_fn :399-466 (from the entropy decoder's uint8 array to the
+clipped RGB frame).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import VCF_DCT_NO_SUBBANDS, VCF_DCT_PERCEPTUAL, call
+from .device import DeviceBuffer, _h
+
+__all__ = ["padded_shape", "flags_from", "encode_device", "decode_device", "encode", "decode",
+           "VCF_DCT_NO_SUBBANDS", "VCF_DCT_PERCEPTUAL"]
+
+
+def padded_shape(H: int, W: int, block_size: int = 8):
+    hp, wp = ctypes.c_int32(), ctypes.c_int32()
+    call("vcf_dct_padded_shape", H, W, block_size, ctypes.byref(hp), ctypes.byref(wp))
+    return hp.value, wp.value
+
+
+def flags_from(disable_subbands: bool = False, perceptual: bool = False) -> int:
+    return (VCF_DCT_NO_SUBBANDS if disable_subbands else 0) | (VCF_DCT_PERCEPTUAL if perceptual else 0)
+
+
+def encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32, flags: int = 0,
+                  out: DeviceBuffer | None = None, stream=None, block_size: int = 8) -> DeviceBuffer:
+    """Frames resident in HBM -> coefficient frames in HBM (asynchronous on `stream`)."""
+    Hp, Wp = padded_shape(H, W, block_size)
+    if rgb.nbytes < n_frames * H * W * 3:
+        raise ValueError("input buffer too small")
+    if out is None:
+        out = DeviceBuffer(n_frames * Hp * Wp * 3)
+    elif out.nbytes < n_frames * Hp * Wp * 3:
+        raise ValueError("output buffer too small")
+    call("vcf_dct_dz_encode", rgb.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
+    return out
+
+
+def decode_device(k: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32, flags: int = 0,
+                  out: DeviceBuffer | None = None, stream=None, block_size: int = 8) -> DeviceBuffer:
+    Hp, Wp = padded_shape(H, W, block_size)
+    if k.nbytes < n_frames * Hp * Wp * 3:
+        raise ValueError("input buffer too small")
+    if out is None:
+        out = DeviceBuffer(n_frames * H * W * 3)
+    elif out.nbytes < n_frames * H * W * 3:
+        raise ValueError("output buffer too small")
+    call("vcf_dct_dz_decode", k.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
+    return out
+
+
+def _frames(a: np.ndarray, what: str) -> np.ndarray:
+    a = np.asarray(a)
+    if a.dtype != np.uint8:
+        raise TypeError(f"{what} must be uint8, got {a.dtype}")
+    if a.ndim == 3:
+        a = a[None]
+    if a.ndim != 4 or a.shape[3] != 3:
+        raise ValueError("Input image must be a 3D array (height, width, channels).")
+    return np.ascontiguousarray(a)
+
+
+def encode(rgb: np.ndarray, Q: int = 32, flags: int = 0, block_size: int = 8) -> np.ndarray:
+    """Host convenience: HxWx3 (or NxHxWx3) u8 -> HpxWpx3 (NxHpxWpx3) u8 indices."""
+    single = np.asarray(rgb).ndim == 3
+    f = _frames(rgb, "rgb")
+    n, H, W, _ = f.shape
+    Hp, Wp = padded_shape(H, W, block_size)
+    din = DeviceBuffer.from_array(f)
+    dout = encode_device(din, n, H, W, Q, flags, block_size=block_size)
+    res = dout.download(np.empty((n, Hp, Wp, 3), np.uint8))
+    din.free()
+    dout.free()
+    return res[0] if single else res
+
+
+def decode(k: np.ndarray, H: int, W: int, Q: int = 32, flags: int = 0, block_size: int = 8) -> np.ndarray:
+    """Host convenience: HpxWpx3 (or N...) u8 indices -> HxWx3 u8 reconstruction."""
+    single = np.asarray(k).ndim == 3
+    f = _frames(k, "k")
+    n = f.shape[0]
+    Hp, Wp = padded_shape(H, W, block_size)
+    if f.shape[1:3] != (Hp, Wp):
+        raise ValueError(f"index frames {f.shape[1:3]} do not match {(Hp, Wp)} for {H}x{W}")
+    din = DeviceBuffer.from_array(f)
+    dout = decode_device(din, n, H, W, Q, flags, block_size=block_size)
+    res = dout.download(np.empty((n, H, W, 3), np.uint8))
+    din.free()
+    dout.free()
+    return res[0] if single else res
