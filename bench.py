@@ -130,6 +130,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of oracle CPU time for cpu_baseline (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", type=int, default=0, help="encode kernel (0 = automatic)")
     args = ap.parse_args()
 
     world, rank, local, pg = dist_setup(args.gpus)
@@ -148,7 +149,7 @@ def main():
     stream = Stream()
 
     def step():
-        D.encode_device(din, F, H, W, Q, 0, out=dout, stream=stream)
+        D.encode_device(din, F, H, W, Q, 0, out=dout, stream=stream, variant=args.variant)
 
     for _ in range(args.warmup):
         step()

@@ -89,6 +89,16 @@ int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *k_dev,
                       void *stream);
 
+/* Same as vcf_dct_dz_encode with an explicit kernel choice (benchmarking and
+ * tests): 0 = automatic, 1 = lane-per-block tile kernel (the default),
+ * 2 = diagnostic: variant 1's arithmetic with no memory traffic (writes one
+ * word per block, not the coefficients; power-of-two Q only),
+ * 3 = column-per-lane tile kernel (8 lanes per block, LDS transpose).
+ * Variants 1 and 3 produce identical bytes. */
+int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H,
+                              int32_t W, int32_t block_size, int32_t Q, uint32_t flags,
+                              uint8_t *k_dev, void *stream);
+
 /* Inverse: n_frames coefficient frames (Hp x Wp x 3) -> RGB frames (H x W x 3),
  * the padding removed.  1 <= Q <= 32767 (the dequantizer works in int16). */
 int vcf_dct_dz_decode(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,

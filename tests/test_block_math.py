@@ -25,6 +25,8 @@ def harness(tmp_path_factory):
     u8 = ctypes.POINTER(ctypes.c_uint8)
     L.hb_encode_block.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
     L.hb_decode_block.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
+    L.hb_encode_block_bytes.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
+    L.hb_encode_block_cols.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
     return L
 
 
@@ -46,6 +48,11 @@ def test_block_encode_decode_vs_oracle(harness, Q, flags):
         harness.hb_encode_block(_p(blk), Q, flags, _p(k))
         kref = O.encode_frame(blk, Q, flags)
         assert np.array_equal(k, kref), (it, Q, flags)
+        kb = np.empty((8, 8, 3), np.uint8)
+        harness.hb_encode_block_bytes(_p(blk), Q, flags, _p(kb))
+        assert np.array_equal(kb, kref), ("bytes", it, Q, flags)
+        harness.hb_encode_block_cols(_p(blk), Q, flags, _p(kb))
+        assert np.array_equal(kb, kref), ("cols", it, Q, flags)
         # decode arbitrary index blocks too (not only encoder outputs)
         kin = kref if it % 2 else rng.integers(0, 256, (8, 8, 3), dtype=np.uint8)
         out = np.empty((8, 8, 3), np.uint8)

@@ -106,3 +106,22 @@ def test_zero_frames_and_errors():
         D.encode(np.zeros((16, 16, 3), np.uint8), 32, block_size=16)
     with pytest.raises(ValueError):
         D.decode(np.zeros((8, 8, 3), np.uint8), 8, 8, 40000)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 3])
+@pytest.mark.parametrize("Q,flags", [(32, 0), (7, 0), (1, 0), (32, 1), (5, 3), (64, 2)])
+def test_encode_variants_vs_oracle(variant, Q, flags):
+    """Both encode kernels on shapes both support (no padding, W % 32 == 0)."""
+    for H, W in [(8, 32), (64, 128), (40, 96), (136, 2048)]:
+        rgb = _rand((H, W, 3), seed=H + W + Q, kind="rand" if W % 64 else "smooth")
+        k = D.encode(rgb, Q, flags, variant=variant)
+        assert np.array_equal(k, O.encode_frame(rgb, Q, flags)), (H, W)
+    frames = np.stack([_rand((24, 160, 3), s) for s in range(7)])
+    k = D.encode(frames, Q, flags, variant=variant)
+    for i in range(7):
+        assert np.array_equal(k[i], O.encode_frame(frames[i], Q, flags))
+
+
+def test_unknown_variant_rejected():
+    with pytest.raises(ValueError):
+        D.encode(np.zeros((16, 16, 3), np.uint8), 32, variant=99)

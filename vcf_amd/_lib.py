@@ -70,6 +70,7 @@ SIGNATURES = {
     "vcf_event_elapsed_ms": [_P, _P, ctypes.POINTER(ctypes.c_float)],
     "vcf_dct_padded_shape": [_I32, _I32, _I32, _PI32, _PI32],
     "vcf_dct_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dct_dz_encode_variant": [ctypes.c_int, _P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_decode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
 }
 

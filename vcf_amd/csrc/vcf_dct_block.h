@@ -13,15 +13,27 @@
 //   -> dct3_8r on columns then rows (A2) -> * 1/16 -> trunc -> int16
 //   -> to_RGB in int16 (A4) -> +128 -> clip to u8
 #pragma once
+#include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "vcf_dct8.h"
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // An empty asm that makes `x` look redefined: blocks CSE / sinking across it.
 #define VCF_OPAQUE(x) asm volatile("" : "+v"(x))
+// Keep the machine scheduler from interleaving independent phases (it
+// otherwise overlaps all eight column transforms and spills).
+#define VCF_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define VCF_OPAQUE(x) ((void)0)
+#define VCF_SCHED_FENCE() ((void)0)
+#endif
+
+#if defined(__HIPCC__)
+#define VCF_HD_HOST __host__
+#else
+#define VCF_HD_HOST
 #endif
 
 namespace vcf {
@@ -78,39 +90,366 @@ VCF_HD float quant_div(float t, float d)
 #endif
 }
 
-// One channel of one block -> 64 index bytes (k + 128) in (i*8 + j) order.
-template <int C, bool POW2, bool PERC>
-VCF_HD void encode_block_channel(const uint32_t (&raw)[8][6], const float (&qd)[4], uint8_t (&kb)[64])
+// Order the eight 1-D transforms of a pass one after another: `dep` is an
+// output of the previous transform, and the empty asm makes this transform's
+// inputs depend on it.  Without it the compiler overlaps all eight (plus the
+// other channels) for ILP and spills; with it a block channel needs about
+// 64 + 16 registers and the wave scheduler supplies the overlap instead.
+template <typename T>
+VCF_HD void chain8(T (&c)[8], T dep)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]),
+                 "+v"(c[6]), "+v"(c[7]) : "v"(dep));
+#else
+    (void)c;
+    (void)dep;
+#endif
+}
+
+// Order groups of ILP 1-D transforms one after another (see chain8); within
+// a group the ILP transforms are independent, so the compiler interleaves them.
+template <int ILP>
+VCF_HD void chain_group(float (*cols)[8], float dep)
+{
+    if (ILP == 1) {
+        chain8(cols[0], dep);
+    } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(cols[0][0]), "+v"(cols[0][1]), "+v"(cols[0][2]), "+v"(cols[0][3]),
+                     "+v"(cols[0][4]), "+v"(cols[0][5]), "+v"(cols[0][6]), "+v"(cols[0][7]),
+                     "+v"(cols[1][0]), "+v"(cols[1][1]), "+v"(cols[1][2]), "+v"(cols[1][3]),
+                     "+v"(cols[1][4]), "+v"(cols[1][5]), "+v"(cols[1][6]), "+v"(cols[1][7])
+                     : "v"(dep));
+#endif
+        if (ILP == 4) chain_group<2>(cols + 2, cols[1][0]);
+    }
+}
+
+// One channel of one block -> 64 index bytes (k + 128) in (i*8 + j) order,
+// packed four per word (byte n in bits 8*(n&3) of K[n>>2]).
+template <int C, bool POW2, bool PERC, int ILP = 1>
+VCF_HD void encode_block_channel(const uint32_t (&raw)[8][6], const float (&qd)[4], uint32_t (&K)[16])
+{
+    float v[8][8];   // v[y][x]; after the column pass row i holds coefficient row i
+    float dep = qd[0];
+    // axis 0 (columns) first, then axis 1 (rows): dct(dct(b.T).T)
+#pragma unroll
+    for (int x0 = 0; x0 < 8; x0 += ILP) {
+        float col[ILP][8];
+#pragma unroll
+        for (int u = 0; u < ILP; ++u)
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+                col[u][y] = ycocg_scaled<C>(byte_of(raw[y], 3 * (x0 + u)), byte_of(raw[y], 3 * (x0 + u) + 1),
+                                            byte_of(raw[y], 3 * (x0 + u) + 2));
+        // (the asm also hides that these are small integers: LLVM would
+        // otherwise turn the first butterflies into integer adds across columns)
+        chain_group<ILP>(col, dep);
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) dct2_8r(col[u]);
+#pragma unroll
+        for (int u = 0; u < ILP; ++u)
+#pragma unroll
+            for (int y = 0; y < 8; ++y) v[y][x0 + u] = col[u][y];
+        dep = col[ILP - 1][0];
+    }
+#pragma unroll
+    for (int i0 = 0; i0 < 8; i0 += ILP) {
+        chain_group<ILP>(&v[i0], dep);
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) dct2_8r(v[i0 + u]);
+        dep = v[i0 + ILP - 1][0];
+#pragma unroll
+        for (int i = i0; i < i0 + ILP; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float t = v[i][j];
+                if (PERC) t = (float)((double)t * pweight<C>(i * 8 + j));
+                const float q = quant_div<POW2>(t, qd[qexp<C>(i, j) - 3]);
+                const int k = (int)q;   // astype(int32): truncation toward zero
+                const uint32_t b = (uint32_t)(k + 128) & 0xffu;   // += 128, astype(uint8)
+                const int n = i * 8 + j;
+                K[n >> 2] = (n & 3) ? (K[n >> 2] | (b << (8 * (n & 3)))) : b;
+                // pin the finished word here (volatile asms keep program order):
+                // otherwise the quantization is sunk to the word's far-away use
+                // and 64 coefficients stay live through the next channels
+                if ((n & 3) == 3) VCF_OPAQUE(K[n >> 2]);
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Conversion-free variant (the float<->int conversions are quarter-rate on
+// gfx950 and were ~15% of the block's VALU time):
+//   * int -> float: the float with bits 0x4B000000 + n is 2^23 + n exactly,
+//     so (bits(n + magic) - (2^23 + bias)) is n - bias in one full-rate sub;
+//   * float -> byte: trunc(q) + (3*2^22 + 128) lies in [2^23, 2^24) for
+//     |q| < 2^22, where the float's bit pattern is 0x4B000000 + 2^22 + 128 +
+//     trunc(q): its low byte is (trunc(q) + 128) mod 256, exactly
+//     astype(int32) + 128 -> astype(uint8).  The byte is stored straight from
+//     that register.
+// ---------------------------------------------------------------------------
+VCF_HD float bits_as_float(uint32_t u)
+{
+#if defined(__HIPCC__)
+    return __uint_as_float(u);
+#else
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+#endif
+}
+
+VCF_HD uint32_t float_bits(float f)
+{
+#if defined(__HIPCC__)
+    return __float_as_uint(f);
+#else
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+#endif
+}
+
+constexpr uint32_t kMagicI = 0x4B000000u;      // bits of 2^23
+constexpr float kQuantMagic = 12583040.0f;     // 3*2^22 + 128
+
+// 4Y, 2Co, 4Cg of (R-128, G-128, B-128) as floats, without a conversion
+template <int C>
+VCF_HD float ycocg_magic(uint32_t r, uint32_t g, uint32_t b)
+{
+    if (C == 0) return bits_as_float(kMagicI + r + 2 * g + b) - (8388608.0f + 512.0f);
+    if (C == 1) return bits_as_float(kMagicI + 256u + r - b) - (8388608.0f + 256.0f);
+    return bits_as_float(kMagicI + 512u + 2 * g - r - b) - (8388608.0f + 512.0f);
+}
+
+VCF_HD float trunc_f(float x)
+{
+#if defined(__HIPCC__)
+    return __builtin_truncf(x);
+#else
+    return truncf(x);
+#endif
+}
+
+// One channel of one block; sink(i, j, word) receives each coefficient's
+// index byte in the low 8 bits of `word`, row by row as the rows finish.
+// ILP transforms of a pass are issued as one group (see chain_group): enough
+// independent work per wave to cover the VALU dependency latency.
+template <int C, bool POW2, bool PERC, int ILP = 1, typename Sink>
+VCF_HD void encode_block_channel_bytes(const uint32_t (&raw)[8][6], const float (&qd)[4], Sink &&sink)
 {
     float v[8][8];
+    float dep = qd[0];
 #pragma unroll
-    for (int y = 0; y < 8; ++y)
+    for (int x0 = 0; x0 < 8; x0 += ILP) {
+        float col[ILP][8];
 #pragma unroll
-        for (int x = 0; x < 8; ++x)
-            v[y][x] = ycocg_scaled<C>(byte_of(raw[y], 3 * x), byte_of(raw[y], 3 * x + 1),
-                                      byte_of(raw[y], 3 * x + 2));
-    // axis 0 (columns) first, then axis 1 (rows): dct(dct(b.T).T)
+        for (int u = 0; u < ILP; ++u)
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+                col[u][y] = ycocg_magic<C>(byte_of(raw[y], 3 * (x0 + u)), byte_of(raw[y], 3 * (x0 + u) + 1),
+                                           byte_of(raw[y], 3 * (x0 + u) + 2));
+        chain_group<ILP>(col, dep);
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) dct2_8r(col[u]);
+#pragma unroll
+        for (int u = 0; u < ILP; ++u)
+#pragma unroll
+            for (int y = 0; y < 8; ++y) v[y][x0 + u] = col[u][y];
+        dep = col[ILP - 1][0];
+    }
+#pragma unroll
+    for (int i0 = 0; i0 < 8; i0 += ILP) {
+        chain_group<ILP>(&v[i0], dep);
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) dct2_8r(v[i0 + u]);
+        dep = v[i0 + ILP - 1][0];
+#pragma unroll
+        for (int i = i0; i < i0 + ILP; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float t = v[i][j];
+                if (PERC) t = (float)((double)t * pweight<C>(i * 8 + j));
+                const float q = quant_div<POW2>(t, qd[qexp<C>(i, j) - 3]);
+                sink(i, j, float_bits(trunc_f(q) + kQuantMagic));
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fetch-lean encode body (v6).  The tile kernel is bound by instruction fetch
+// (SQC busy ~100 %, no misses) at ~5.7 code bytes per instruction, so:
+//   * every constant (pocketfft twiddles, quantizer multipliers, magics, dot
+//     weights) comes from a kernel-argument struct, i.e. an SGPR operand
+//     instead of a 32-bit literal: the DCT's multiplies stay 4-byte VOP2;
+//   * YCoCg is one or two v_dot4 of the signed bytes (RGB - 128) per sample
+//     (the raw words are XORed with 0x80808080 once), accumulated onto
+//     2^23 + bias and turned into a float by one subtraction (see above).
+// ---------------------------------------------------------------------------
+struct EncConsts {
+    float tw[7];      // pocketfft DCT-II twiddles (fp32)
+    float hf;         // rfft8 twiddle = sqrt2/2 (fp32)
+    float hfx2, tw3x2; // 2*hf, 2*tw[3] (exact): column pass of the column-per-lane kernel
+    float qd[4];      // quantizer divisors Q*2^e or, for power-of-two Q, 2^-e/Q
+    float qmagic;     // 3*2^22 + 128
+    float csub[3];    // 2^23 + 1024 per channel (what the dot accumulator's float is offset by)
+    uint32_t cinit;   // bits of 2^23 + 1024: the dot accumulator's start value
+    uint32_t w[3][6]; // per channel: dot weights of the six byte patterns of a 24-byte row
+};
+
+#define VCF_K_TW(k, i) (k).tw[i]
+
+// DCT-II of dct2_8r with the constants taken from K (bit-identical ops)
+VCF_HD void dct2_8k(float (&c)[8], const EncConsts &K)
+{
+    const float x1 = c[1] + c[2], x2 = c[2] - c[1];
+    const float x3 = c[3] + c[4], x7 = c[3] - c[4];
+    const float x5 = c[5] + c[6], x6 = c[6] - c[5];
+    const float a0 = c[0] + c[7], a4 = c[0] - c[7];
+    const float a1 = x1 + x5, tr2 = x1 - x5;
+    const float ti2 = x2 + x6, a2 = x2 - x6;
+    const float a6 = K.hf * ti2 + K.hf * tr2;
+    const float a5 = K.hf * tr2 - K.hf * ti2;
+    const float T2 = a0 + x3, T1 = a0 - x3;
+    const float r0 = T2 + a1, r4 = T2 - a1, r6 = T1 + a2, r2 = T1 - a2;
+    const float U2 = a4 + x7, U1 = a4 - x7;
+    const float r1 = U2 + a5, r5 = U2 - a5, r7 = U1 + a6, r3 = U1 - a6;
+    float t1, t2;
+    t1 = K.tw[0] * r7 + K.tw[6] * r1; t2 = K.tw[0] * r1 - K.tw[6] * r7;
+    c[1] = t1 + t2; c[7] = t1 - t2;
+    t1 = K.tw[1] * r6 + K.tw[5] * r2; t2 = K.tw[1] * r2 - K.tw[5] * r6;
+    c[2] = t1 + t2; c[6] = t1 - t2;
+    t1 = K.tw[2] * r5 + K.tw[4] * r3; t2 = K.tw[2] * r3 - K.tw[4] * r5;
+    c[3] = t1 + t2; c[5] = t1 - t2;
+    c[4] = r4 * K.tw[3];
+    c[0] = r0 * K.hf;
+}
+
+// Column pass of the column-per-lane kernel: dct2_8k with outputs 0 and 4
+// doubled (2*hf, 2*tw3 are exact), so all eight outputs carry the scale 1/4.
+VCF_HD void dct2_8k_colpass(float (&c)[8], const EncConsts &K)
+{
+    const float x1 = c[1] + c[2], x2 = c[2] - c[1];
+    const float x3 = c[3] + c[4], x7 = c[3] - c[4];
+    const float x5 = c[5] + c[6], x6 = c[6] - c[5];
+    const float a0 = c[0] + c[7], a4 = c[0] - c[7];
+    const float a1 = x1 + x5, tr2 = x1 - x5;
+    const float ti2 = x2 + x6, a2 = x2 - x6;
+    const float a6 = K.hf * ti2 + K.hf * tr2;
+    const float a5 = K.hf * tr2 - K.hf * ti2;
+    const float T2 = a0 + x3, T1 = a0 - x3;
+    const float r0 = T2 + a1, r4 = T2 - a1, r6 = T1 + a2, r2 = T1 - a2;
+    const float U2 = a4 + x7, U1 = a4 - x7;
+    const float r1 = U2 + a5, r5 = U2 - a5, r7 = U1 + a6, r3 = U1 - a6;
+    float t1, t2;
+    t1 = K.tw[0] * r7 + K.tw[6] * r1; t2 = K.tw[0] * r1 - K.tw[6] * r7;
+    c[1] = t1 + t2; c[7] = t1 - t2;
+    t1 = K.tw[1] * r6 + K.tw[5] * r2; t2 = K.tw[1] * r2 - K.tw[5] * r6;
+    c[2] = t1 + t2; c[6] = t1 - t2;
+    t1 = K.tw[2] * r5 + K.tw[4] * r3; t2 = K.tw[2] * r3 - K.tw[4] * r5;
+    c[3] = t1 + t2; c[5] = t1 - t2;
+    c[4] = r4 * K.tw3x2;
+    c[0] = r0 * K.hfx2;
+}
+
+// -p weight with a runtime table index (column-per-lane kernel: row = lane)
+VCF_HD double pweight_rt(int C, int n)
+{
+    return C == 0 ? (double)kYQ[n] / 121.0 : (double)kCQ[n] / 99.0;
+}
+
+VCF_HD int sdot4(uint32_t a, uint32_t b, int c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+#else
+    int s = c;
+    for (int k = 0; k < 4; ++k) s += (int)(int8_t)(a >> (8 * k)) * (int)(int8_t)(b >> (8 * k));
+    return s;
+#endif
+}
+
+// Weights of channel C (4Y = R'+2G'+B', 2Co = R'-B', 4Cg = -R'+2G'-B') laid
+// on the six byte patterns of a row: pixel p occupies bytes 3p..3p+2.
+VCF_HD_HOST inline void make_enc_consts(EncConsts &K, int Q)
+{
+    K.tw[0] = VCF_TWF0; K.tw[1] = VCF_TWF1; K.tw[2] = VCF_TWF2; K.tw[3] = VCF_TWF3;
+    K.tw[4] = VCF_TWF4; K.tw[5] = VCF_TWF5; K.tw[6] = VCF_TWF6; K.hf = VCF_HF;
+    K.hfx2 = 2.0f * VCF_HF;
+    K.tw3x2 = 2.0f * VCF_TWF3;
+    const bool pow2 = (Q & (Q - 1)) == 0;
+    for (int e = 0; e < 4; ++e) {
+        const double D = (double)Q * (double)(1 << (e + 3));
+        K.qd[e] = pow2 ? (float)(1.0 / D) : (float)D;
+    }
+    K.qmagic = 12583040.0f;
+    K.cinit = 0x4B000000u + 1024u;
+    for (int c = 0; c < 3; ++c) K.csub[c] = 8388608.0f + 1024.0f;
+    const int wt[3][3] = {{1, 2, 1}, {1, 0, -1}, {-1, 2, -1}};
+    for (int c = 0; c < 3; ++c) {
+        auto wb = [&](int comp) { return (uint32_t)(uint8_t)(int8_t)wt[c][comp]; };
+        // A=[R,G,B,0] B1=[0,0,0,R] B2=[G,B,0,0] C1=[0,0,R,G] C2=[B,0,0,0] D=[0,R,G,B]
+        K.w[c][0] = wb(0) | (wb(1) << 8) | (wb(2) << 16);
+        K.w[c][1] = wb(0) << 24;
+        K.w[c][2] = wb(1) | (wb(2) << 8);
+        K.w[c][3] = (wb(0) << 16) | (wb(1) << 24);
+        K.w[c][4] = wb(2);
+        K.w[c][5] = (wb(0) << 8) | (wb(1) << 16) | (wb(2) << 24);
+    }
+}
+
+// channel-C value of pixel x of a row whose six words hold the signed bytes
+// (R-128, G-128, B-128): 4Y, 2Co or 4Cg as an exact float
+template <int C>
+VCF_HD float ycocg_dot(const uint32_t (&row)[6], int x, const EncConsts &K)
+{
+    const int q = x >> 2, p = x & 3;   // pixels 4q..4q+3 live in words 3q..3q+2
+    int acc;
+    if (p == 0) acc = sdot4(row[3 * q], K.w[C][0], (int)K.cinit);
+    else if (p == 1) acc = sdot4(row[3 * q + 1], K.w[C][2], sdot4(row[3 * q], K.w[C][1], (int)K.cinit));
+    else if (p == 2) acc = sdot4(row[3 * q + 2], K.w[C][4], sdot4(row[3 * q + 1], K.w[C][3], (int)K.cinit));
+    else acc = sdot4(row[3 * q + 2], K.w[C][5], (int)K.cinit);
+    return bits_as_float((uint32_t)acc) - K.csub[C];
+}
+
+// v6 channel body: columns then rows, sink(i, j, word) as in
+// encode_block_channel_bytes; raw holds the signed bytes (raw ^ 0x80808080).
+template <int C, bool POW2, bool PERC, typename Sink>
+VCF_HD void encode_block_channel_v6(const uint32_t (&raw)[8][6], const EncConsts &K, Sink &&sink)
+{
+    float v[8][8];
+    float dep = K.qd[0];
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
         float col[8];
 #pragma unroll
-        for (int y = 0; y < 8; ++y) col[y] = v[y][x];
-        dct2_8r(col);
+        for (int y = 0; y < 8; ++y) col[y] = ycocg_dot<C>(raw[y], x, K);
+        chain8(col, dep);
+        dct2_8k(col, K);
 #pragma unroll
         for (int y = 0; y < 8; ++y) v[y][x] = col[y];
+        dep = col[0];
     }
 #pragma unroll
-    for (int y = 0; y < 8; ++y) dct2_8r(v[y]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
+        chain8(v[i], dep);
+        dct2_8k(v[i], K);
+        dep = v[i][0];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float t = v[i][j];
             if (PERC) t = (float)((double)t * pweight<C>(i * 8 + j));
-            const float q = quant_div<POW2>(t, qd[qexp<C>(i, j) - 3]);
-            const int k = (int)q;   // astype(int32): truncation toward zero
-            kb[i * 8 + j] = (uint8_t)(k + 128);
+            const float q = quant_div<POW2>(t, K.qd[qexp<C>(i, j) - 3]);
+            sink(i, j, float_bits(trunc_f(q) + K.qmagic));
         }
+    }
+}
+
+VCF_HD uint32_t byte_at(const uint32_t (&K)[16], int n)
+{
+    return (K[n >> 2] >> (8 * (n & 3))) & 0xffu;
 }
 
 // One channel of one block: 64 index bytes in (i*8 + j) order -> 64 int16

@@ -4,22 +4,27 @@
 // What the kernels compute is src/2D-DCT.py encode_fn :276-361 and decode_fn
 // :399-466 of the reference (see include/vcf_amd.h for the line map), with
 // the upstream-package semantics A1-A5 of SURVEY.md Appendix A, bit-exact to
-// oracle/vcf_oracle.c.
+// oracle/vcf_oracle.c.  The per-block arithmetic lives in vcf_dct_block.h
+// (host-testable); this file only moves memory around it.
 //
 // Layout and mapping:
-//   * a workgroup of 256 lanes owns one block row (8 pixel rows) x 256
-//     consecutive 8x8 blocks; lane = block.  The 192 input bytes of a block
-//     sit in 48 VGPRs; each YCoCg channel is built, transformed (column pass,
-//     then row pass, dct2_8r), quantized and dropped as bytes into an LDS
-//     image laid out exactly like the output (64 subband runs of 768 B);
-//   * the LDS image leaves with 16-byte coalesced stores: for a full tile
-//     every (i, j) subband run is 768 contiguous bytes of the output frame;
-//   * decode mirrors it: coalesced 16-byte loads of the 64 runs into LDS,
-//     lane-per-block fp64 inverse transform (dct3_8r), int16 YCoCg->RGB,
-//     RGB rows written straight from registers.
-// No MFMA: the transforms must follow pocketfft's rounding sequence exactly.
+//   * encode variant 1 (default): a workgroup of 256 lanes owns one block row
+//     (8 pixel rows) x 256 consecutive 8x8 blocks; lane = block.  The 192
+//     input bytes of a block sit in 48 VGPRs; each YCoCg channel is built,
+//     transformed (column pass, then row pass), quantized, and every index
+//     byte is dropped from its register into an LDS image laid out exactly
+//     like the output, which leaves with 16-byte coalesced stores (for a full
+//     tile every (i, j) subband run is 768 contiguous bytes of the frame);
+//   * encode variant 3: column-per-lane (8 lanes per block, LDS transpose
+//     between the passes); cheaper arithmetic, weaker memory overlap;
+//   * decode mirrors variant 1: coalesced 16-byte loads of the runs into LDS,
+//     lane-per-block fp64 inverse transform, int16 YCoCg->RGB, RGB rows
+//     written straight from registers.
+// The encode is VALU-issue bound (profiles/).  No MFMA: the
+// transforms must follow pocketfft's rounding sequence exactly.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "vcf_amd.h"
@@ -33,13 +38,13 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kTile = 256;                 // blocks (= lanes) per workgroup
-constexpr int kSegBytes = kTile * 3;       // one (i, j) subband run of a full tile
+constexpr int kTile = 256;                   // blocks (= lanes) per workgroup
+constexpr int kSegBytes = kTile * 3;         // one (i, j) subband run of a full tile
 constexpr int kStageBytes = 64 * kSegBytes;  // 48 KiB LDS image
 
 struct Geom {
     int H, W, Hp, Wp, top, left, nbx, nby, tiles_per_row;
-    long long in_stride, out_stride;   // bytes per frame (input, output)
+    long long in_stride, out_stride;   // bytes per frame (RGB, coefficients)
     int vec;                           // 16-B path valid for the coefficient frames
 };
 
@@ -87,32 +92,81 @@ __device__ __forceinline__ void move_runs(const Geom &g, uint8_t *stage, uint8_t
     }
 }
 
-__device__ __forceinline__ void opaque(uint32_t (&raw)[8][6])
+// Make raw[] look redefined *after* `dep` exists, so a channel's byte
+// extractions can neither be CSE'd with the previous channel's nor hoisted
+// above it (either keeps 2-3 channels' inputs live at once and spills).
+__device__ __forceinline__ void opaque(uint32_t (&raw)[8][6], uint32_t dep)
 {
 #pragma unroll
     for (int y = 0; y < 8; ++y)
 #pragma unroll
-        for (int w = 0; w < 6; ++w) VCF_OPAQUE(raw[y][w]);
+        for (int w = 0; w < 6; ++w) asm volatile("" : "+v"(raw[y][w]) : "v"(dep));
 }
 
-template <int C, bool POW2, bool SUB, bool PERC>
-__device__ __forceinline__ void encode_channel(const uint32_t (&raw)[8][6], const float (&qd)[4],
-                                               uint8_t *stage, int tid)
+// The 192 bytes of block (by, bx), row y in raw[y][0..5] (little-endian);
+// the padding (2D-DCT.py:187-229) reads as zero bytes like the reference's.
+template <bool PAD>
+__device__ __forceinline__ void load_block(const Geom &g, const uint8_t *src, int by, int bx,
+                                           uint32_t (&raw)[8][6])
 {
-    uint8_t kb[64];
-    encode_block_channel<C, POW2, PERC>(raw, qd, kb);
+    if (!PAD) {
 #pragma unroll
-    for (int n = 0; n < 64; ++n) {
-        const int i = n >> 3, j = n & 7;
-        if (SUB) stage[n * kSegBytes + tid * 3 + C] = kb[n];
-        else stage[i * (kTile * 24) + tid * 24 + j * 3 + C] = kb[n];
+        for (int y = 0; y < 8; ++y) {
+            const u32x2 *p = reinterpret_cast<const u32x2 *>(
+                src + ((long long)(by * 8 + y) * g.W + bx * 8) * 3);
+            const u32x2 a = __builtin_nontemporal_load(p);
+            const u32x2 b = __builtin_nontemporal_load(p + 1);
+            const u32x2 c = __builtin_nontemporal_load(p + 2);
+            raw[y][0] = a.x; raw[y][1] = a.y; raw[y][2] = b.x;
+            raw[y][3] = b.y; raw[y][4] = c.x; raw[y][5] = c.y;
+        }
+    } else {
+#pragma unroll
+        for (int y = 0; y < 8; ++y) {
+            const int sy = by * 8 + y - g.top;
+#pragma unroll
+            for (int w = 0; w < 6; ++w) raw[y][w] = 0;
+#pragma unroll
+            for (int n = 0; n < 24; ++n) {
+                const int sx = bx * 8 + n / 3 - g.left;
+                uint32_t b = 0;
+                if (sy >= 0 && sy < g.H && sx >= 0 && sx < g.W)
+                    b = src[((long long)sy * g.W + sx) * 3 + n % 3];
+                raw[y][n >> 2] |= b << ((n & 3) * 8);
+            }
+        }
     }
+}
+
+template <bool POW2, bool SUB, bool PERC>
+__device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncConsts &K,
+                                             uint8_t *stage, int tid)
+{
+    // each index byte goes from the low byte of its register straight into
+    // the LDS image of the output (no conversion, no packing)
+    auto s0 = [&](int i, int j, uint32_t w) {
+        if (SUB) stage[(i * 8 + j) * kSegBytes + tid * 3 + 0] = (uint8_t)w;
+        else stage[i * (kTile * 24) + tid * 24 + j * 3 + 0] = (uint8_t)w;
+    };
+    auto s1 = [&](int i, int j, uint32_t w) {
+        if (SUB) stage[(i * 8 + j) * kSegBytes + tid * 3 + 1] = (uint8_t)w;
+        else stage[i * (kTile * 24) + tid * 24 + j * 3 + 1] = (uint8_t)w;
+    };
+    auto s2 = [&](int i, int j, uint32_t w) {
+        if (SUB) stage[(i * 8 + j) * kSegBytes + tid * 3 + 2] = (uint8_t)w;
+        else stage[i * (kTile * 24) + tid * 24 + j * 3 + 2] = (uint8_t)w;
+    };
+    encode_block_channel_bytes<0, POW2, PERC>(raw, K.qd, s0);
+    opaque(raw, (uint32_t)tid);
+    encode_block_channel_bytes<1, POW2, PERC>(raw, K.qd, s1);
+    opaque(raw, (uint32_t)tid);
+    encode_block_channel_bytes<2, POW2, PERC>(raw, K.qd, s2);
 }
 
 template <bool POW2, bool SUB, bool PERC, bool PAD>
 __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
                                                                  uint8_t *__restrict__ kout, Geom g,
-                                                                 float4 qd4)
+                                                                 EncConsts K)
 {
     __shared__ __attribute__((aligned(16))) uint8_t stage[kStageBytes];
     const int tid = threadIdx.x;
@@ -120,51 +174,188 @@ __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_kernel(const uint8_t *
     const int by = blockIdx.x / g.tiles_per_row;
     const int bx0 = (blockIdx.x - by * g.tiles_per_row) * kTile;
     const int nvalid = min(kTile, g.nbx - bx0);
-    const int bx = bx0 + tid;
-    const uint8_t *src = rgb + frame * g.in_stride;
-    const float qd[4] = {qd4.x, qd4.y, qd4.z, qd4.w};
-
     if (tid < nvalid) {
         uint32_t raw[8][6];
-        if (!PAD) {
-#pragma unroll
-            for (int y = 0; y < 8; ++y) {
-                const u32x2 *p = reinterpret_cast<const u32x2 *>(
-                    src + ((long long)(by * 8 + y) * g.W + bx * 8) * 3);
-                const u32x2 a = __builtin_nontemporal_load(p);
-                const u32x2 b = __builtin_nontemporal_load(p + 1);
-                const u32x2 c = __builtin_nontemporal_load(p + 2);
-                raw[y][0] = a.x; raw[y][1] = a.y; raw[y][2] = b.x;
-                raw[y][3] = b.y; raw[y][4] = c.x; raw[y][5] = c.y;
-            }
-        } else {
-            // zero padding, centred (2D-DCT.py:187-229)
-#pragma unroll
-            for (int y = 0; y < 8; ++y) {
-                const int sy = by * 8 + y - g.top;
-#pragma unroll
-                for (int w = 0; w < 6; ++w) raw[y][w] = 0;
-#pragma unroll
-                for (int n = 0; n < 24; ++n) {
-                    const int sx = bx * 8 + n / 3 - g.left;
-                    uint32_t b = 0;
-                    if (sy >= 0 && sy < g.H && sx >= 0 && sx < g.W)
-                        b = src[((long long)sy * g.W + sx) * 3 + n % 3];
-                    raw[y][n >> 2] |= b << ((n & 3) * 8);
-                }
-            }
-        }
-        // Keep the three channels' live ranges apart: the empty asm makes raw[]
-        // look redefined, so the 192 byte extractions are not CSE'd across
-        // channels (that alone kept 192 values live and spilled).
-        encode_channel<0, POW2, SUB, PERC>(raw, qd, stage, tid);
-        opaque(raw);
-        encode_channel<1, POW2, SUB, PERC>(raw, qd, stage, tid);
-        opaque(raw);
-        encode_channel<2, POW2, SUB, PERC>(raw, qd, stage, tid);
+        load_block<PAD>(g, rgb + frame * g.in_stride, by, bx0 + tid, raw);
+        encode_block<POW2, SUB, PERC>(raw, K, stage, tid);
     }
     __syncthreads();
     move_runs<SUB, true>(g, stage, kout + frame * g.out_stride, by, bx0, nvalid);
+}
+
+// Diagnostic (encode variant 2): the same body with no memory traffic at all
+// -- raw synthesised from the lane id, one word stored per lane -- to split
+// kernel time into arithmetic and memory (scripts/bench_variants.py).
+__global__ __launch_bounds__(kTile, 2) void dct_dz_encode_diag(uint8_t *__restrict__ kout, Geom g,
+                                                               EncConsts K, long long nblocks)
+{
+    const long long gid = (long long)blockIdx.x * kTile + threadIdx.x;
+    if (gid >= nblocks) return;
+    uint32_t raw[8][6];
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+#pragma unroll
+        for (int w = 0; w < 6; ++w) raw[y][w] = (uint32_t)(gid * 2654435761u) ^ (y * 0x01010101u * (w + 1));
+    uint32_t acc = 0;
+    auto sink = [&](int i, int j, uint32_t w) { acc += w << ((i + j) & 7); };
+    encode_block_channel_bytes<0, true, false>(raw, K.qd, sink);
+    opaque(raw, acc);
+    encode_block_channel_bytes<1, true, false>(raw, K.qd, sink);
+    opaque(raw, acc);
+    encode_block_channel_bytes<2, true, false>(raw, K.qd, sink);
+    reinterpret_cast<uint32_t *>(kout)[gid] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// Column-per-lane encode (variant 3).  Lane-per-block needs ~120-165 VGPRs
+// (48 for the block's bytes, 64 coefficients), i.e. 3 waves per SIMD, and a
+// gfx950 SIMD needs >= 8 waves to issue a full-rate VALU op every ~2.3 cycles
+// (one wave alone: every ~6.5; scripts/microbench).  Here 8 lanes share a
+// block: lane x of a block loads pixel column x, runs that column's DCT-II,
+// the 8 lanes transpose through LDS (same wave: no barrier), lane x then runs
+// coefficient row x, quantizes it and drops its 8 index bytes into the
+// workgroup's LDS image of the output, which leaves with coalesced stores.
+// The column pass folds the factor 2 of outputs 0 and 4 into its last
+// multiplications (2*hf, 2*tw3; exact), so every row is at the same scale and
+// the quantizer divisor depends on (channel, j) only.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wave_lds_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int TB>
+struct ColsSmem {
+    float tr[TB][8][9];       // per-block 8x8 transpose tile, pitch 9 (bank-conflict free)
+    uint8_t stage[64 * TB * 3 + 8 * 32];
+};
+
+// Offset of output run `seg` in the LDS image.  Lanes x = 0..7 of a block
+// write runs 8 apart (SUB) or rows 1 apart (-x); runs of TB*3 = 384 bytes
+// would put all eight in one bank, so every group of 8 runs (every row) is
+// shifted by 32 bytes -- 8 banks -- keeping the 16-byte alignment.
+template <int TB, bool SUB>
+__device__ __forceinline__ int cols_stage_off(int seg)
+{
+    return SUB ? seg * (TB * 3) + (seg >> 3) * 32 : seg * (TB * 24) + seg * 32;
+}
+
+template <int TB, bool POW2, bool SUB, bool PERC, bool PAD>
+__global__ __launch_bounds__(TB * 8) void dct_dz_encode_cols(const uint8_t *__restrict__ rgb,
+                                                              uint8_t *__restrict__ kout, Geom g,
+                                                              EncConsts K, int tiles_per_row)
+{
+    __shared__ __attribute__((aligned(16))) ColsSmem<TB> sm;
+    const int tid = threadIdx.x;
+    const int lb = tid >> 3, x = tid & 7;
+    const int by = blockIdx.x / tiles_per_row;
+    const int bx0 = (blockIdx.x - by * tiles_per_row) * TB;
+    const int nvalid = min(TB, g.nbx - bx0);
+    const int bx = bx0 + lb;
+    // frames are < 2 GiB (check_args): per-lane offsets stay 32-bit, the
+    // frame bases are wave-uniform (SGPR) 64-bit pointers
+    const uint8_t *src = rgb + blockIdx.y * g.in_stride;
+    uint8_t *dst = kout + blockIdx.y * g.out_stride;
+    if (lb < nvalid) {
+        // the 3 bytes of pixel (y, x), as signed bytes R', G', B' in the low 24 bits
+        uint32_t px[8];
+        if (!PAD) {
+            const int o = 3 * x;
+            const uint32_t row_bytes = (uint32_t)g.W * 3;
+            uint32_t off = (uint32_t)(by * 8) * row_bytes + (uint32_t)bx * 24 + (o & ~3);
+            uint32_t lo[8], hi[8];
+#pragma unroll
+            for (int y = 0; y < 8; ++y, off += row_bytes) {
+                const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(src + off));
+                lo[y] = v.x;
+                hi[y] = v.y;
+            }
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+                px[y] = __builtin_amdgcn_alignbyte(hi[y], lo[y], (uint32_t)(o & 3)) ^ 0x80808080u;
+        } else {
+            const int sx = bx * 8 + x - g.left;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) {
+                const int sy = by * 8 + y - g.top;
+                uint32_t v = 0;
+                if (sy >= 0 && sy < g.H && sx >= 0 && sx < g.W) {
+                    const uint8_t *p = src + ((uint32_t)sy * (uint32_t)g.W + (uint32_t)sx) * 3;
+                    v = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+                }
+                px[y] = v ^ 0x80808080u;
+            }
+        }
+        float (*tr)[9] = sm.tr[lb];
+#pragma unroll
+        for (int C = 0; C < 3; ++C) {
+            float col[8];
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+                col[y] = bits_as_float((uint32_t)sdot4(px[y], K.w[C][0], (int)K.cinit)) - K.csub[C];
+            dct2_8k_colpass(col, K);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) tr[i][x] = col[i];
+            // the 8 lanes of a block are one wave, whose LDS operations
+            // execute in order: only the compiler must not move the reads
+            // above the other lanes' writes (nor the next channel's writes
+            // above these reads)
+            wave_lds_fence();
+            float row[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) row[j] = tr[x][j];
+            wave_lds_fence();
+            dct2_8k(row, K);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float t = row[j];
+                if (PERC) t = (float)((double)t * pweight_rt(C, x * 8 + j));
+                // divisor Q * chs * 4 / s_j = Q * 2^e, e = log2(chs) + 2 + inv(j)
+                const int e = (C == 1 ? 1 : 2) + 2 + dct2_inv_scale_log2(j);
+                const float q = quant_div<POW2>(t, K.qd[e - 3]);
+                const uint8_t b = (uint8_t)float_bits(trunc_f(q) + K.qmagic);
+                if (SUB) sm.stage[cols_stage_off<TB, true>(x * 8 + j) + lb * 3 + C] = b;
+                else sm.stage[cols_stage_off<TB, false>(x) + lb * 24 + j * 3 + C] = b;
+            }
+        }
+    }
+    __syncthreads();
+    // copy the LDS image out: 64 runs of 3*nvalid bytes (or 8 rows of 24*nvalid)
+    constexpr int nseg = SUB ? 64 : 8;
+    auto seg_off = [&](int seg) -> uint32_t {
+        return (uint32_t)(SUB ? seg_offset_sub(g, by, bx0, seg) : seg_offset_nosub(g, by, bx0, seg));
+    };
+    if (g.vec && nvalid == TB && (TB * 3) % 16 == 0) {
+        // full tile: compile-time chunk geometry
+        constexpr int cps = (SUB ? 3 * TB : 24 * TB) / 16, total = nseg * cps;
+#pragma unroll
+        for (int q0 = 0; q0 < total; q0 += TB * 8) {
+            const int q = q0 + tid;
+            if (total % (TB * 8) == 0 || q < total) {
+                const int seg = q / cps, off = (q - seg * cps) << 4;
+                __builtin_nontemporal_store(
+                    *reinterpret_cast<const u32x4 *>(sm.stage + cols_stage_off<TB, SUB>(seg) + off),
+                    reinterpret_cast<u32x4 *>(dst + seg_off(seg) + off));
+            }
+        }
+    } else if (g.vec && (TB * 3) % 16 == 0) {
+        const int cps = (SUB ? 3 * nvalid : 24 * nvalid) >> 4, total = nseg * cps;
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+        for (int q = tid; q < total; q += TB * 8) {
+            const int seg = q / cps, off = (q - seg * cps) << 4;
+            __builtin_nontemporal_store(
+                *reinterpret_cast<const u32x4 *>(sm.stage + cols_stage_off<TB, SUB>(seg) + off),
+                reinterpret_cast<u32x4 *>(dst + seg_off(seg) + off));
+        }
+    } else {
+        const int seg_len = SUB ? 3 * nvalid : 24 * nvalid, total = nseg * seg_len;
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+        for (int q = tid; q < total; q += TB * 8) {
+            const int seg = q / seg_len, off = q - seg * seg_len;
+            dst[seg_off(seg) + off] = sm.stage[cols_stage_off<TB, SUB>(seg) + off];
+        }
+    }
 }
 
 template <int C, bool SUB, bool PERC>
@@ -239,7 +430,35 @@ __global__ __launch_bounds__(kTile, 2) void dct_dz_decode_kernel(const uint8_t *
     }
 }
 
-int make_geom(int32_t H, int32_t W, Geom &g)
+template <int TB>
+int launch_cols(const uint8_t *rgb_dev, int64_t n_frames, uint8_t *k_dev, const Geom &g,
+                const EncConsts &K, bool pow2, bool sub, bool perc, bool pad, void *stream)
+{
+    const int tpr = (g.nbx + TB - 1) / TB;
+    for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
+        const dim3 grid(tpr * g.nby, (unsigned)std::min<int64_t>(65535, n_frames - f0));
+        const uint8_t *in = rgb_dev + f0 * g.in_stride;
+        uint8_t *out = k_dev + f0 * g.out_stride;
+#define VCF_ENC7(P2, SB, PC, PD) \
+        if (pow2 == P2 && sub == SB && perc == PC && pad == PD) \
+            hipLaunchKernelGGL((dct_dz_encode_cols<TB, P2, SB, PC, PD>), grid, dim3(TB * 8), 0, \
+                               (hipStream_t)stream, in, out, g, K, tpr);
+        VCF_ENC7(true, true, false, false) else VCF_ENC7(true, true, false, true)
+        else VCF_ENC7(true, true, true, false) else VCF_ENC7(true, true, true, true)
+        else VCF_ENC7(true, false, false, false) else VCF_ENC7(true, false, false, true)
+        else VCF_ENC7(true, false, true, false) else VCF_ENC7(true, false, true, true)
+        else VCF_ENC7(false, true, false, false) else VCF_ENC7(false, true, false, true)
+        else VCF_ENC7(false, true, true, false) else VCF_ENC7(false, true, true, true)
+        else VCF_ENC7(false, false, false, false) else VCF_ENC7(false, false, false, true)
+        else VCF_ENC7(false, false, true, false) else VCF_ENC7(false, false, true, true)
+#undef VCF_ENC7
+        const int rc = hip_check(hipGetLastError(), "dct_dz_encode_cols launch");
+        if (rc != VCF_OK) return rc;
+    }
+    return VCF_OK;
+}
+
+void make_geom(int32_t H, int32_t W, Geom &g)
 {
     g.H = H;
     g.W = W;
@@ -255,7 +474,6 @@ int make_geom(int32_t H, int32_t W, Geom &g)
     // every subband run starts 16-B aligned and spans whole 16-B chunks iff
     // nbx % 16 == 0 (then Wp*3, nbx*3, 768 and the frame size are multiples of 16)
     g.vec = (g.nbx % 16 == 0) ? 1 : 0;
-    return VCF_OK;
 }
 
 int check_args(const void *a, const void *b, int64_t n_frames, int32_t H, int32_t W,
@@ -270,9 +488,13 @@ int check_args(const void *a, const void *b, int64_t n_frames, int32_t H, int32_
                          block_size);
     if (Q < 1 || (decode && Q > 32767))
         return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
+    // the fp32 divisor Q*2^6 must be exact for a general (non power-of-two) Q
+    if (!decode && (Q & (Q - 1)) != 0 && Q > (1 << 18))
+        return set_error(VCF_ERR_UNSUPPORTED, "quantization step %d too large", Q);
     if (flags & ~(VCF_DCT_NO_SUBBANDS | VCF_DCT_PERCEPTUAL))
         return set_error(VCF_ERR_INVALID, "unknown flags 0x%x", flags);
-    if ((long long)H * W > (1LL << 31) / 3)
+    // the kernels address within a frame with 32-bit offsets
+    if ((long long)((H + 7) & ~7) * ((W + 7) & ~7) * 3 >= (1LL << 31))
         return set_error(VCF_ERR_INVALID, "frame too large");
     return VCF_OK;
 }
@@ -286,7 +508,7 @@ using namespace vcf;
     if (pow2 == P2 && sub == SB && perc == PC && pad == PD)                               \
         hipLaunchKernelGGL((dct_dz_encode_kernel<P2, SB, PC, PD>), grid, dim3(kTile), 0,  \
                            (hipStream_t)stream, rgb_dev + f0 * g.in_stride,               \
-                           k_dev + f0 * g.out_stride, g, qd4);
+                           k_dev + f0 * g.out_stride, g, K);
 
 #define VCF_DEC_CASE(SB, PC, PD)                                                          \
     if (sub == SB && perc == PC && pad == PD)                                             \
@@ -309,8 +531,16 @@ int vcf_dct_padded_shape(int32_t H, int32_t W, int32_t block_size, int32_t *Hp, 
 int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *k_dev, void *stream)
 {
+    return vcf_dct_dz_encode_variant(0, rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, stream);
+}
+
+int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H,
+                              int32_t W, int32_t block_size, int32_t Q, uint32_t flags,
+                              uint8_t *k_dev, void *stream)
+{
     int rc = check_args(rgb_dev, k_dev, n_frames, H, W, block_size, Q, flags, false);
     if (rc != VCF_OK) return rc;
+    if (variant < 0 || variant > 3) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -318,13 +548,16 @@ int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
     const bool sub = !(flags & VCF_DCT_NO_SUBBANDS);
     const bool perc = (flags & VCF_DCT_PERCEPTUAL) != 0;
     const bool pad = (g.Hp != H) || (g.Wp != W);
-    // divisors Q*2^e (e = 3..6) or, for a power-of-two Q, their exact reciprocals
-    float d[4];
-    for (int e = 0; e < 4; ++e) {
-        const double D = (double)Q * (double)(1 << (e + 3));
-        d[e] = pow2 ? (float)(1.0 / D) : (float)D;
+    EncConsts K;
+    make_enc_consts(K, Q);
+    if (variant == 2) {
+        if (!pow2) return set_error(VCF_ERR_INVALID, "diagnostic variant needs a power-of-two Q");
+        const long long nblocks = (long long)n_frames * g.nbx * g.nby;
+        hipLaunchKernelGGL(dct_dz_encode_diag, dim3((unsigned)((nblocks + kTile - 1) / kTile)), dim3(kTile),
+                           0, (hipStream_t)stream, k_dev, g, K, nblocks);
+        return hip_check(hipGetLastError(), "dct_dz_encode_diag launch");
     }
-    const float4 qd4 = make_float4(d[0], d[1], d[2], d[3]);
+    if (variant == 3) return launch_cols<128>(rgb_dev, n_frames, k_dev, g, K, pow2, sub, perc, pad, stream);
     for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
         const dim3 grid(g.tiles_per_row * g.nby, (unsigned)std::min<int64_t>(65535, n_frames - f0));
         VCF_ENC_CASE(true, true, false, false) else VCF_ENC_CASE(true, true, false, true)

@@ -30,8 +30,11 @@ def flags_from(disable_subbands: bool = False, perceptual: bool = False) -> int:
 
 
 def encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32, flags: int = 0,
-                  out: DeviceBuffer | None = None, stream=None, block_size: int = 8) -> DeviceBuffer:
-    """Frames resident in HBM -> coefficient frames in HBM (asynchronous on `stream`)."""
+                  out: DeviceBuffer | None = None, stream=None, block_size: int = 8,
+                  variant: int = 0) -> DeviceBuffer:
+    """Frames resident in HBM -> coefficient frames in HBM (asynchronous on `stream`).
+
+    variant: 0 automatic, 1 LDS-staged tile kernel, 2 register kernel (see vcf_amd.h)."""
     Hp, Wp = padded_shape(H, W, block_size)
     if rgb.nbytes < n_frames * H * W * 3:
         raise ValueError("input buffer too small")
@@ -39,7 +42,8 @@ def encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32,
         out = DeviceBuffer(n_frames * Hp * Wp * 3)
     elif out.nbytes < n_frames * Hp * Wp * 3:
         raise ValueError("output buffer too small")
-    call("vcf_dct_dz_encode", rgb.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
+    call("vcf_dct_dz_encode_variant", variant, rgb.ptr, n_frames, H, W, block_size, int(Q), flags,
+         out.ptr, _h(stream))
     return out
 
 
@@ -67,14 +71,15 @@ def _frames(a: np.ndarray, what: str) -> np.ndarray:
     return np.ascontiguousarray(a)
 
 
-def encode(rgb: np.ndarray, Q: int = 32, flags: int = 0, block_size: int = 8) -> np.ndarray:
+def encode(rgb: np.ndarray, Q: int = 32, flags: int = 0, block_size: int = 8,
+           variant: int = 0) -> np.ndarray:
     """Host convenience: HxWx3 (or NxHxWx3) u8 -> HpxWpx3 (NxHpxWpx3) u8 indices."""
     single = np.asarray(rgb).ndim == 3
     f = _frames(rgb, "rgb")
     n, H, W, _ = f.shape
     Hp, Wp = padded_shape(H, W, block_size)
     din = DeviceBuffer.from_array(f)
-    dout = encode_device(din, n, H, W, Q, flags, block_size=block_size)
+    dout = encode_device(din, n, H, W, Q, flags, block_size=block_size, variant=variant)
     res = dout.download(np.empty((n, Hp, Wp, 3), np.uint8))
     din.free()
     dout.free()
