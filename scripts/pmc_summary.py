@@ -3,6 +3,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -12,7 +13,8 @@ for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), rec
     with open(f) as fh:
         for row in csv.DictReader(fh):
             name = row.get("Kernel_Name", "?")
-            short = name.split("(")[0].split("::")[-1]
+            m = re.search(r"(\w+)<[^()]*>\(", name) or re.search(r"(\w+)\(", name)
+            short = m.group(1) if m else name
             acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
 res = {}
 for k, d in acc.items():
