@@ -1,0 +1,93 @@
+"""The C-ABI library without a GPU: it builds, loads, and exports exactly what
+include/*.h declares; argument validation runs on the host and reports the
+reference's errors (2D-DCT.py:199-200 raises ValueError for ndim != 3).
+No compute entry point is called with real buffers here."""
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+import vcf_amd._lib as L
+
+
+def _declared():
+    names = []
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names += re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s]*?[\s*](vcf_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_library_builds_and_loads():
+    lib = L.lib()
+    assert os.path.exists(L.lib_path())
+    major, minor = ctypes.c_int(), ctypes.c_int()
+    assert lib.vcf_version(ctypes.byref(major), ctypes.byref(minor)) == 0
+    assert major.value >= 0 and minor.value >= 0
+
+
+def test_every_declared_symbol_is_exported():
+    lib = L.lib()
+    names = _declared()
+    assert len(names) >= 25, names
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_the_header():
+    """Every declared entry point has argtypes in vcf_amd/_lib.py, and no extra."""
+    declared = set(_declared()) - {"vcf_last_error"}
+    assert declared == set(L.SIGNATURES), (declared ^ set(L.SIGNATURES))
+
+
+def test_padded_shape_is_host_only():
+    Hp, Wp = ctypes.c_int32(), ctypes.c_int32()
+    lib = L.lib()
+    assert lib.vcf_dct_padded_shape(61, 77, 8, ctypes.byref(Hp), ctypes.byref(Wp)) == 0
+    assert (Hp.value, Wp.value) == (64, 80)
+    assert lib.vcf_dct_padded_shape(0, 77, 8, ctypes.byref(Hp), ctypes.byref(Wp)) == L.VCF_ERR_INVALID
+
+
+@pytest.mark.parametrize("args,status", [
+    (dict(H=0), L.VCF_ERR_INVALID),              # not an image
+    (dict(block_size=16), L.VCF_ERR_UNSUPPORTED),  # -B 16 not on the HIP path
+    (dict(Q=0), L.VCF_ERR_INVALID),
+    (dict(flags=8), L.VCF_ERR_INVALID),
+    (dict(n_frames=-1), L.VCF_ERR_INVALID),
+])
+def test_argument_errors_before_any_device_work(args, status):
+    """check_args() rejects bad calls before touching HIP (null device
+    pointers would otherwise fault)."""
+    a = dict(n_frames=1, H=8, W=8, block_size=8, Q=32, flags=0)
+    a.update(args)
+    dummy = ctypes.c_void_p(16)   # never dereferenced: validation fails first
+    rc = L.lib().vcf_dct_dz_encode(dummy, a["n_frames"], a["H"], a["W"], a["block_size"], a["Q"],
+                                   a["flags"], dummy, None)
+    assert rc == status
+    assert L.lib().vcf_last_error()  # a message is recorded
+
+
+def test_null_buffers_rejected():
+    rc = L.lib().vcf_dct_dz_decode(None, 1, 8, 8, 8, 32, 0, None, None)
+    assert rc == L.VCF_ERR_INVALID
+
+
+def test_status_mapping():
+    with pytest.raises(ValueError):
+        L.check(L.VCF_ERR_INVALID)
+    with pytest.raises(NotImplementedError):
+        L.check(L.VCF_ERR_UNSUPPORTED)
+    with pytest.raises(RuntimeError):
+        L.check(L.VCF_ERR_HIP)
+
+
+def test_product_never_imports_the_oracle():
+    """vcf_amd/ has no path to oracle/ (no CPU fallback)."""
+    for p in glob.glob(os.path.join(ROOT, "vcf_amd", "**", "*.py"), recursive=True):
+        src = open(p).read()
+        assert "oracle" not in re.sub(r"#.*|\"\"\".*?\"\"\"", "", src, flags=re.S), p
