@@ -48,6 +48,13 @@ extern "C" {
 #define VCF_ERR_HIP (-2)         /* HIP runtime failure                    */
 #define VCF_ERR_UNSUPPORTED (-3) /* option not implemented on this path    */
 
+/* element types of the stand-alone quantizer */
+#define VCF_DTYPE_F32 0
+#define VCF_DTYPE_F64 1
+#define VCF_DTYPE_I16 2
+#define VCF_DTYPE_I32 3
+#define VCF_DTYPE_U8 4
+
 /* flags of the DCT path */
 #define VCF_DCT_NO_SUBBANDS 1u   /* -x, --disable_subbands  (2D-DCT.py:40)  */
 #define VCF_DCT_PERCEPTUAL 2u    /* -p, --perceptual_quantization (:38)    */
@@ -104,6 +111,19 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
 int vcf_dct_dz_decode(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev,
                       void *stream);
+
+/* ---- deadzone quantizer plug-in (deadzone.py:95-117, assumption A5) ---------- */
+
+/* k[i] = (int32)(x[i] / Q), truncation toward zero; the division is float32
+ * for VCF_DTYPE_F32 input and float64 for every other input type (numpy true
+ * division).  Replaces deadzone.CoDec.quantize_fn (deadzone.py:95-102). */
+int vcf_deadzone_quantize(const void *x_dev, int32_t x_dtype, int64_t n, int32_t Q, int32_t *k_dev,
+                          void *stream);
+
+/* y[i] = Q * k[i] in k's type (VCF_DTYPE_I16 or VCF_DTYPE_I32), wrapping.
+ * Replaces deadzone.CoDec.dequantize_fn (deadzone.py:107-117). */
+int vcf_deadzone_dequantize(const void *k_dev, int32_t k_dtype, int64_t n, int32_t Q, void *y_dev,
+                            void *stream);
 
 #ifdef __cplusplus
 }

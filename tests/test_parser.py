@@ -1,0 +1,49 @@
+"""The CLI surface: Namespaces equal to the ones the reference prints
+(notebooks/III.ipynb cells 8 and 13), and the codec's option checks."""
+import pytest
+
+from vcf_amd.codec import parser as P
+
+
+def _ns(p, argv):
+    d = vars(P.parse(p, argv))
+    d.pop("func")
+    return d
+
+
+def test_iii_encode_namespace_matches_reference():
+    d = _ns(P.iii_parser(), ["encode", "-o", "/tmp/mobile_352x288x30x420x300.mp4"])
+    assert list(d.items()) == [
+        ("debug", False), ("subparser_name", "encode"), ("transform", "2D-DCT"), ("number_of_frames", 20),
+        ("block_size_DCT", 8), ("color_transform", "YCoCg"), ("perceptual_quantization", False),
+        ("Lambda", None), ("disable_subbands", False), ("quantizer", "deadzone"), ("QSS", 32),
+        ("entropy_image_codec", "TIFF"), ("original", "/tmp/mobile_352x288x30x420x300.mp4"),
+        ("encoded", "/tmp/encoded")]
+
+
+def test_iii_decode_namespace_matches_reference():
+    d = _ns(P.iii_parser(), ["decode"])
+    assert list(d.items()) == [
+        ("debug", False), ("subparser_name", "decode"), ("transform", "2D-DCT"), ("number_of_frames", 20),
+        ("block_size_DCT", 8), ("color_transform", "YCoCg"), ("perceptual_quantization", False),
+        ("disable_subbands", False), ("quantizer", "deadzone"), ("QSS", 32), ("filter", "no_filter"),
+        ("entropy_image_codec", "TIFF"), ("encoded", "/tmp/encoded"), ("decoded", "/tmp/decoded.png")]
+
+
+def test_dct_options():
+    d = _ns(P.dct_parser(), ["-g", "encode", "-B", "8", "-p", "-x", "-q", "7", "-c", "TIFF",
+                             "-o", "a.png", "-e", "out"])
+    assert d["debug"] and d["perceptual_quantization"] and d["disable_subbands"]
+    assert d["QSS"] == 7 and d["original"] == "a.png" and d["encoded"] == "out"
+    assert P.int_or_str("12") == 12 and P.int_or_str("x") == "x"
+
+
+def test_unsupported_options_raise():
+    """Options outside the HIP path fail when the codec is built, before any
+    file or device work."""
+    from vcf_amd.codec.dct2d import CoDec
+    p = P.dct_parser()
+    for argv in (["encode", "-B", "16"], ["encode", "-t", "YCrCb"], ["encode", "-a", "LloydMax"],
+                 ["encode", "-L", "1"], ["encode", "-c", "PNG"], ["decode", "-f", "gaussian_blur"]):
+        with pytest.raises(NotImplementedError):
+            CoDec(P.parse(p, argv))

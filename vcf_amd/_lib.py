@@ -17,6 +17,12 @@ VCF_ERR_INVALID = -1
 VCF_ERR_HIP = -2
 VCF_ERR_UNSUPPORTED = -3
 
+VCF_DTYPE_F32 = 0
+VCF_DTYPE_F64 = 1
+VCF_DTYPE_I16 = 2
+VCF_DTYPE_I32 = 3
+VCF_DTYPE_U8 = 4
+
 VCF_DCT_NO_SUBBANDS = 1
 VCF_DCT_PERCEPTUAL = 2
 
@@ -72,6 +78,8 @@ SIGNATURES = {
     "vcf_dct_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_encode_variant": [ctypes.c_int, _P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_decode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],
+    "vcf_deadzone_dequantize": [_P, _I32, _I64, _I32, _P, _P],
 }
 
 _lib = None

@@ -1,0 +1,217 @@
+"""2D-DCT image codec: the drop-in for src/2D-DCT.py's CoDec.
+
+Same constructor (an argparse Namespace, see parser.py), same methods and
+return values (encode_fn/decode_fn -> bytes written; encode/decode with the
+reference's hard-wired default paths; bye), same files ({out}.tif holding
+the k + 128 indices in subband layout, {out}_shape.bin = struct 'iii').  The
+span between reading the image and handing the indices to the entropy codec
+-- 2D-DCT.py:276-361 encode, :399-466 decode -- runs on the GPU through
+libvcf_amd.so (vcf_dct_dz_encode / vcf_dct_dz_decode); there is no CPU
+implementation of it in the product.
+
+Options the HIP path does not implement raise NotImplementedError when the
+codec is constructed (block sizes other than 8 incl. -L, colour transforms
+other than YCoCg, quantizers other than deadzone, filters other than
+no_filter); entropy codecs come from ENTROPY_CODECS.
+"""
+from __future__ import annotations
+
+import logging
+import struct
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from .. import dct as D
+from .eic import CoDec as EICCoDec
+from .tiff import TIFFCodec
+
+ENTROPY_CODECS = {"TIFF": TIFFCodec}
+
+
+def register_entropy_codec(name, cls):
+    ENTROPY_CODECS[name] = cls
+
+
+def _flags(args) -> int:
+    return D.flags_from(bool(getattr(args, "disable_subbands", False)),
+                        bool(getattr(args, "perceptual_quantization", False)))
+
+
+class CoDec(EICCoDec):
+    """2D-DCT.CoDec (2D-DCT.py:50-579) over the YCoCg / deadzone / no_filter /
+    <entropy codec> chain."""
+
+    def __init__(self, args):
+        super().__init__(args)
+        self.block_size = int(getattr(args, "block_size_DCT", 8))
+        ct = getattr(args, "color_transform", "YCoCg")
+        if ct != "YCoCg":
+            raise NotImplementedError(f"color transform {ct!r}: only YCoCg is on the HIP path")
+        quant = getattr(args, "quantizer", "deadzone")
+        if quant != "deadzone":
+            raise NotImplementedError(f"quantizer {quant!r}: only deadzone is on the HIP path")
+        filt = getattr(args, "filter", "no_filter")
+        if not self.encoding and filt != "no_filter":
+            raise NotImplementedError(f"filter {filt!r}: only no_filter is on the HIP path")
+        if self.block_size != 8:
+            raise NotImplementedError(f"block size {self.block_size}: only B=8 is on the HIP path")
+        if self.encoding and getattr(args, "Lambda", None) is not None \
+                and not getattr(args, "perceptual_quantization", False):
+            # 2D-DCT.py:93-101 -> optimize_block_size over B in {2,...,128}
+            raise NotImplementedError("-L (RD-optimized block size) needs B != 8 transforms")
+        ec_name = getattr(args, "entropy_image_codec", "TIFF")
+        if ec_name not in ENTROPY_CODECS:
+            raise NotImplementedError(f"entropy codec {ec_name!r} (have: {sorted(ENTROPY_CODECS)})")
+        self.entropy = ENTROPY_CODECS[ec_name]()
+        self.file_extension = self.entropy.file_extension
+        self.QSS = int(getattr(args, "QSS", 32))
+        self.offset = 128            # 2D-DCT.py:102-105 (quantizer == deadzone)
+        self.flags = _flags(args)
+        self.original_shape = None
+
+    # entropy stage (TIFF.py / CBAAC.py surface)
+    def compress(self, img):
+        return self.entropy.compress(img)
+
+    def decompress(self, codestream):
+        return self.entropy.decompress(codestream)
+
+    # 2D-DCT.py:187-266 semantics, used by callers that pad/crop themselves
+    def pad_and_center_to_multiple_of_block_size(self, img):
+        if img.ndim != 3:
+            raise ValueError("Input image must be a 3D array (height, width, channels).")
+        self.original_shape = img.shape
+        H, W = img.shape[:2]
+        Hp, Wp = D.padded_shape(H, W, self.block_size)
+        t, l = (Hp - H) // 2, (Wp - W) // 2
+        return np.pad(img, ((t, Hp - H - t), (l, Wp - W - l), (0, 0)), mode="constant")
+
+    def remove_padding(self, padded_img):
+        if padded_img.ndim != 3:
+            raise ValueError("Padded image must be a 3D array (height, width, channels).")
+        if self.original_shape is None:
+            raise ValueError("Original shape is not set. Pad the image first.")
+        H, W = self.original_shape[:2]
+        t = (padded_img.shape[0] - H) // 2
+        l = (padded_img.shape[1] - W) // 2
+        return padded_img[t:t + H, l:l + W, :]
+
+    # ---- the hot path -------------------------------------------------------
+    def _check_frame(self, img):
+        if img.ndim != 3:
+            raise ValueError("Input image must be a 3D array (height, width, channels).")
+        if img.dtype != np.uint8 or img.shape[2] != 3:
+            raise NotImplementedError(f"{img.dtype} x{img.shape[2]} images: the HIP path takes u8 RGB")
+
+    def encode_indices(self, img: np.ndarray) -> np.ndarray:
+        """2D-DCT.py:276-361 on the GPU: u8 RGB -> u8 indices (k + 128, wrapped)."""
+        self._check_frame(img)
+        self.original_shape = img.shape
+        return D.encode(img, self.QSS, self.flags, self.block_size)
+
+    def decode_indices(self, k: np.ndarray, shape) -> np.ndarray:
+        """2D-DCT.py:399-466 on the GPU: u8 indices -> u8 RGB (padding removed)."""
+        H, W = int(shape[0]), int(shape[1])
+        return D.decode(np.ascontiguousarray(k, dtype=np.uint8), H, W, self.QSS, self.flags,
+                        self.block_size)
+
+    def encode_fn(self, in_fn, out_fn):
+        img = self.encode_read_fn(in_fn)
+        k = self.encode_indices(img)
+        with open(f"{out_fn}_shape.bin", "wb") as f:
+            f.write(struct.pack("iii", *self.original_shape))
+        return self.encode_write_fn(self.compress(k), out_fn)
+
+    def encode(self, in_fn="/tmp/original.png", out_fn="/tmp/encoded"):
+        # 2D-DCT.py:374-375: the reference's encode() ignores -o/-e
+        return self.encode_fn(in_fn, out_fn)
+
+    def decode_fn(self, in_fn, out_fn):
+        codestream = self.decode_read_fn(in_fn)
+        with open(f"{in_fn}_shape.bin", "rb") as f:
+            self.original_shape = struct.unpack("iii", f.read(12))
+        k = self.decompress(codestream)
+        y = self.decode_indices(k, self.original_shape)
+        return self.decode_write_fn(y, out_fn)
+
+    def decode(self, in_fn="/tmp/encoded", out_fn="/tmp/decoded.png"):
+        return self.decode_fn(in_fn, out_fn)
+
+    # ---- batched frames (III runner): one launch per batch of equal shapes --
+    def encode_fns(self, pairs, batch: int = 64, io_threads: int = 8):
+        """encode_fn over (in_fn, out_fn) pairs; returns the bytes written per
+        frame.  Frames of equal shape share one GPU launch; PNG decode and
+        TIFF deflate run on a host thread pool."""
+        pairs = list(pairs)
+        sizes = [0] * len(pairs)
+        with ThreadPoolExecutor(max_workers=io_threads) as pool:
+            for b0 in range(0, len(pairs), batch):
+                chunk = pairs[b0:b0 + batch]
+                imgs = list(pool.map(lambda p: self.encode_read_fn(p[0]), chunk))
+                for img in imgs:
+                    self._check_frame(img)
+                groups = {}
+                for i, img in enumerate(imgs):
+                    groups.setdefault(img.shape, []).append(i)
+                ks = [None] * len(chunk)
+                for shape, idx in groups.items():
+                    out = D.encode(np.stack([imgs[i] for i in idx]), self.QSS, self.flags, self.block_size)
+                    for j, i in enumerate(idx):
+                        ks[i] = out[j]
+
+                def _write(i):
+                    out_fn = chunk[i][1]
+                    with open(f"{out_fn}_shape.bin", "wb") as f:
+                        f.write(struct.pack("iii", *imgs[i].shape))
+                    return self.encode_write_fn(self.compress(ks[i]), out_fn)
+
+                for i, s in enumerate(pool.map(_write, range(len(chunk)))):
+                    sizes[b0 + i] = s
+        if pairs:
+            self.original_shape = imgs[-1].shape
+        return sizes
+
+    def decode_fns(self, pairs, batch: int = 64, io_threads: int = 8):
+        """decode_fn over (in_fn, out_fn) pairs, batched like encode_fns."""
+        pairs = list(pairs)
+        sizes = [0] * len(pairs)
+        with ThreadPoolExecutor(max_workers=io_threads) as pool:
+            for b0 in range(0, len(pairs), batch):
+                chunk = pairs[b0:b0 + batch]
+
+                def _read(p):
+                    cs = self.decode_read_fn(p[0])
+                    with open(f"{p[0]}_shape.bin", "rb") as f:
+                        shp = struct.unpack("iii", f.read(12))
+                    return self.decompress(cs), shp
+
+                got = list(pool.map(_read, chunk))
+                groups = {}
+                for i, (k, shp) in enumerate(got):
+                    groups.setdefault(tuple(shp), []).append(i)
+                ys = [None] * len(chunk)
+                for shp, idx in groups.items():
+                    out = D.decode(np.stack([got[i][0] for i in idx]), shp[0], shp[1], self.QSS,
+                                   self.flags, self.block_size)
+                    for j, i in enumerate(idx):
+                        ys[i] = out[j]
+                for i, s in enumerate(pool.map(lambda i: self.decode_write_fn(ys[i], chunk[i][1]),
+                                               range(len(chunk)))):
+                    sizes[b0 + i] = s
+        return sizes
+
+    # ---- quantizer surface (deadzone.py:95-124) -----------------------------
+    def quantize_decom(self, decom):
+        return self.quantize(decom)
+
+    def dequantize_decom(self, decom_k):
+        return self.dequantize(decom_k)
+
+    def quantize(self, img, fn="/tmp/encoded"):
+        from .. import quant
+        return quant.deadzone_quantize(img, self.QSS)
+
+    def dequantize(self, k, fn="/tmp/encoded"):
+        from .. import quant
+        return quant.deadzone_dequantize(k, self.QSS)

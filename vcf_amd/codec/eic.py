@@ -1,0 +1,95 @@
+"""Shared I/O of the entropy image codecs: src/entropy_image_coding.py.
+
+CoDec.encode_read_fn (:51-65) reads an image file into an H x W x 3 uint8
+RGB array; encode_write_fn (:70-79) writes a code-stream as fn +
+file_extension; decode_read_fn (:91-96) reads it back; decode_write_fn
+(:101-112) writes the decoded image.  The reference reads PNGs with OpenCV
+(IMREAD_UNCHANGED + BGR2RGB) and writes them with skimage.io.imsave; here
+PIL does both (assumption A9: lossless 8-bit RGB PNG decode is the same
+array either way; the PNG bytes written by decode_write_fn may differ from
+skimage's encoder, the pixels do not).
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+import numpy as np
+
+
+def read_image(fn: str) -> tuple[np.ndarray, int]:
+    """(H x W x 3 uint8 RGB array, bytes on disk)."""
+    from PIL import Image
+    size = os.path.getsize(fn)
+    with Image.open(fn) as im:
+        if im.mode in ("RGB", "RGBA", "P", "PA", "CMYK", "YCbCr"):
+            img = np.asarray(im.convert("RGB"))
+        elif im.mode in ("I;16", "I;16B", "I"):
+            img = np.asarray(im)     # 16-bit: kept as is (the HIP path rejects it)
+        else:
+            img = np.asarray(im)
+    return np.ascontiguousarray(img), size
+
+
+def write_image(fn: str, img: np.ndarray) -> int:
+    from PIL import Image
+    Image.fromarray(np.ascontiguousarray(img)).save(fn)
+    return os.path.getsize(fn)
+
+
+class CoDec:
+    """entropy_image_coding.CoDec (:32-121), with the entropy stage injected."""
+
+    file_extension = ""
+
+    def __init__(self, args):
+        logging.debug(f"trace args={args}")
+        self.args = args
+        self.encoding = getattr(args, "subparser_name", "encode") == "encode"
+        self.total_input_size = 0
+        self.total_output_size = 0
+
+    def bye(self):
+        logging.info(f"Input bytes = {self.total_input_size}")
+        logging.info(f"Output bytes = {self.total_output_size}")
+
+    def encode_read_fn(self, fn):
+        img, input_size = read_image(fn)
+        self.total_input_size += input_size
+        logging.debug(f"Read {input_size} bytes from {fn} with shape {img.shape} and type={img.dtype}")
+        self.img_shape = img.shape
+        return img
+
+    def encode_read(self, fn="/tmp/original.png"):
+        return self.encode_read_fn(fn)
+
+    def encode_write_fn(self, codestream, fn):
+        codestream.seek(0)
+        with open(fn + self.file_extension, "wb") as f:
+            f.write(codestream.read())
+        output_size = os.path.getsize(fn + self.file_extension)
+        self.total_output_size += output_size
+        logging.info(f"Written {output_size} bytes in {fn + self.file_extension}")
+        return output_size
+
+    def encode_write(self, codestream, fn="/tmp/encoded"):
+        return self.encode_write_fn(codestream, fn)
+
+    def decode_read_fn(self, fn):
+        input_size = os.path.getsize(fn + self.file_extension)
+        self.total_input_size += input_size
+        with open(fn + self.file_extension, "rb") as f:
+            return f.read()
+
+    def decode_read(self, fn="/tmp/encoded"):
+        return self.decode_read_fn(fn)
+
+    def decode_write_fn(self, img, fn):
+        output_size = write_image(fn, img)
+        self.img_shape = img.shape
+        self.total_output_size += output_size
+        logging.debug(f"Written {output_size} bytes in {fn} with shape {img.shape} and type {img.dtype}")
+        return output_size
+
+    def decode_write(self, img, fn="/tmp/decoded.png"):
+        return self.decode_write_fn(img, fn)

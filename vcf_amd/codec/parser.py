@@ -1,0 +1,164 @@
+"""Command-line surface of the reference, built explicitly.
+
+The reference assembles its argparse parser from import side effects: every
+module in the codec chain adds its options to the shared `parser.parser`
+(src/parser.py:61-81) and then imports the next module named by an option
+(2D-DCT.py -> YCoCg.py -> deadzone.py -> no_filter.py -> TIFF.py ->
+entropy_image_coding.py).  Here the same options -- names, flags, defaults,
+help -- are added by plain functions, so a Namespace from this parser has
+exactly the attributes the reference's CoDec classes read (the Namespaces
+printed in notebooks/III.ipynb cells 8 and 13).
+"""
+from __future__ import annotations
+
+import argparse
+
+# defaults (module constants of the reference)
+ORIGINAL = "/tmp/original.png"          # entropy_image_coding.py:19
+ENCODED = "/tmp/encoded"                # :20 (extension decided at run time)
+DECODED = "/tmp/decoded.png"            # :22
+DEFAULT_BLOCK_SIZE = 8                  # 2D-DCT.py:27
+DEFAULT_CT = "YCoCg"                    # :28
+DEFAULT_QUANTIZER = "deadzone"          # YCoCg.py:15
+DEFAULT_QSS = 32                        # deadzone.py:23
+DEFAULT_FILTER = "no_filter"            # deadzone.py:26
+DEFAULT_EIC = "TIFF"                    # no_filter.py:11
+DEFAULT_TRANSFORM = "2D-DCT"            # video_coding.py:33
+N_FRAMES = 20                           # video_coding.py:31
+DEFAULT_LEVELS = 5                      # 2D-DWT.py
+DEFAULT_WAVELET = "db5"                 # 2D-DWT.py:23
+
+
+def int_or_str(text):
+    """src/parser.py:4-9."""
+    try:
+        return int(text)
+    except ValueError:
+        return text
+
+
+def _encode(codec):
+    return codec.encode()
+
+
+def _decode(codec):
+    return codec.decode()
+
+
+class CustomArgumentParser(argparse.ArgumentParser):
+    """src/parser.py:17-28: print the message and exit with the status."""
+
+    def exit(self, status=0, message=None):
+        if message:
+            self._print_message(message, None)
+        raise SystemExit(status)
+
+
+def base_parser(description: str | None = None):
+    """src/parser.py:63-81: -g and the encode/decode subcommands."""
+    p = CustomArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter,
+                             exit_on_error=False, description=description)
+    p.add_argument("-g", "--debug", action="store_true", help="Output debug information")
+    sub = p.add_subparsers(help="You must specify one of the following subcomands:",
+                           dest="subparser_name")
+    enc = sub.add_parser("encode", help="Compress data")
+    dec = sub.add_parser("decode", help="Uncompress data")
+    enc.set_defaults(func=_encode)
+    dec.set_defaults(func=_decode)
+    return p, enc, dec
+
+
+def add_eic(enc, dec):
+    """entropy_image_coding.py:25-30."""
+    enc.add_argument("-o", "--original", type=int_or_str,
+                     help=f"Input image (default: {ORIGINAL})", default=ORIGINAL)
+    enc.add_argument("-e", "--encoded", type=int_or_str,
+                     help=f"Output image (default: {ENCODED})", default=f"{ENCODED}")
+    dec.add_argument("-e", "--encoded", type=int_or_str,
+                     help=f"Input code-stream (default: {ENCODED})", default=f"{ENCODED}")
+    dec.add_argument("-d", "--decoded", type=int_or_str,
+                     help=f"Output image (default: {DECODED})", default=f"{DECODED}")
+
+
+def add_filter(enc, dec):
+    """no_filter.py:14-17 (entropy codec choice lives in the filter module)."""
+    enc.add_argument("-c", "--entropy_image_codec",
+                     help=f"Entropy Image Codec (default: {DEFAULT_EIC})", default=DEFAULT_EIC)
+    dec.add_argument("-c", "--entropy_image_codec",
+                     help=f"Entropy Image Codec (default: {DEFAULT_EIC})", default=DEFAULT_EIC)
+
+
+def add_deadzone(enc, dec):
+    """deadzone.py:32-35."""
+    enc.add_argument("-q", "--QSS", type=int_or_str,
+                     help=f"Quantization step size (default: {DEFAULT_QSS})", default=DEFAULT_QSS)
+    dec.add_argument("-q", "--QSS", type=int_or_str,
+                     help=f"Quantization step size (default: {DEFAULT_QSS})", default=DEFAULT_QSS)
+    dec.add_argument("-f", "--filter", type=int_or_str,
+                     help=f"Denoising filter (default: {DEFAULT_FILTER})", default=DEFAULT_FILTER)
+
+
+def add_ycocg(enc, dec):
+    """YCoCg.py:17-19."""
+    enc.add_argument("-a", "--quantizer", help=f"Quantizer (default: {DEFAULT_QUANTIZER})",
+                     default=DEFAULT_QUANTIZER)
+    dec.add_argument("-a", "--quantizer", help=f"Quantizer (default: {DEFAULT_QUANTIZER})",
+                     default=DEFAULT_QUANTIZER)
+
+
+def add_dct(enc, dec):
+    """2D-DCT.py:34-45."""
+    for p, what in ((enc, "quantization"), (dec, "dequantization")):
+        p.add_argument("-B", "--block_size_DCT", type=int_or_str,
+                       help=f"Block size (default: {DEFAULT_BLOCK_SIZE})", default=DEFAULT_BLOCK_SIZE)
+        p.add_argument("-t", "--color_transform", type=int_or_str,
+                       help=f"Color transform (default: \"{DEFAULT_CT}\")", default=DEFAULT_CT)
+        p.add_argument("-p", "--perceptual_quantization", action="store_true",
+                       help=f"Use perceptual {what} (default: \"False\")", default=False)
+        if p is enc:
+            p.add_argument("-L", "--Lambda", type=int_or_str,
+                           help="Relative weight between the rate and the distortion. If provided "
+                                "(float), the block size is RD-optimized between {2**i; i=1,2,3,4,5,6,7}. "
+                                "For example, if Lambda=1.0, then the rate and the distortion have the "
+                                "same weight.")
+        p.add_argument("-x", "--disable_subbands", action="store_true",
+                       help="Disable the coefficients reordering in subbands (default: \"False\")",
+                       default=False)
+
+
+def add_iii(enc, dec):
+    """III.py:23-33."""
+    for p, what in ((enc, "encode"), (dec, "decode")):
+        p.add_argument("-T", "--transform", type=str,
+                       help=f"2D-transform, default: {DEFAULT_TRANSFORM}", default=DEFAULT_TRANSFORM)
+        p.add_argument("-N", "--number_of_frames", type=int_or_str,
+                       help=f"Number of frames to {what} (default: {N_FRAMES})", default=f"{N_FRAMES}")
+
+
+def dct_parser(description: str = "Exploiting spatial redundancy with the 2D Discrete Cosine "
+                                  "Transform of constant block size."):
+    """The parser `python 2D-DCT.py ...` ends up with (default codec chain)."""
+    p, enc, dec = base_parser(description)
+    add_dct(enc, dec)
+    add_ycocg(enc, dec)
+    add_deadzone(enc, dec)
+    add_filter(enc, dec)
+    add_eic(enc, dec)
+    return p
+
+
+def iii_parser(description: str = "III coding: runs a 2D image codec for each image of a sequence."):
+    """`python III.py ...` (III.py + the default 2D-DCT chain it imports)."""
+    p, enc, dec = base_parser(description)
+    add_iii(enc, dec)
+    add_dct(enc, dec)
+    add_ycocg(enc, dec)
+    add_deadzone(enc, dec)
+    add_filter(enc, dec)
+    add_eic(enc, dec)
+    return p
+
+
+def parse(parser, argv=None):
+    """parser.parse_known_args()[0] as main.py:9 does."""
+    return parser.parse_known_args(argv)[0]
