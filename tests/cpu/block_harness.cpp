@@ -2,6 +2,8 @@
 // for CPU-only parity tests against the oracle (tests/test_block_math.py).
 #include <string.h>
 
+#include <type_traits>
+
 #include "vcf_dct_block.h"
 
 using namespace vcf;
@@ -124,4 +126,30 @@ extern "C" void hb_encode_block_cols(const uint8_t *rgb, int Q, unsigned flags, 
     const bool perc = flags & 2;
     if (pow2) perc ? enc_cols<true, true>(rgb, K, k) : enc_cols<true, false>(rgb, K, k);
     else perc ? enc_cols<false, true>(rgb, K, k) : enc_cols<false, false>(rgb, K, k);
+}
+
+// Folded-quantizer body of encode variants 1/2: the sink gets the low byte of
+// k; the kernel's copy-out adds 128 by XOR 0x80.
+extern "C" void hb_encode_block_fold(const uint8_t *rgb, int Q, unsigned flags, uint8_t *k)
+{
+    uint32_t raw[8][6];
+    memcpy(raw, rgb, 192);
+    EncConsts K;
+    make_enc_consts(K, Q);
+    const bool pow2 = (Q & (Q - 1)) == 0;
+    const FinalK rowk = pow2 ? row_final_k(Q) : final_k(1.0f, 1.0f);
+    const bool perc = flags & 2;
+    auto run = [&](auto pw2, auto pc) {
+        constexpr bool P2 = decltype(pw2)::value, PC = decltype(pc)::value;
+        auto s0 = [&](int i, int j, uint32_t w) { k[(i * 8 + j) * 3 + 0] = (uint8_t)(w ^ 0x80u); };
+        auto s1 = [&](int i, int j, uint32_t w) { k[(i * 8 + j) * 3 + 1] = (uint8_t)(w ^ 0x80u); };
+        auto s2 = [&](int i, int j, uint32_t w) { k[(i * 8 + j) * 3 + 2] = (uint8_t)(w ^ 0x80u); };
+        encode_block_channel_fold<0, P2, PC>(raw, rowk, K.qd, s0);
+        encode_block_channel_fold<1, P2, PC>(raw, rowk, K.qd, s1);
+        encode_block_channel_fold<2, P2, PC>(raw, rowk, K.qd, s2);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    if (pow2) perc ? run(T{}, T{}) : run(T{}, F{});
+    else perc ? run(F{}, T{}) : run(F{}, F{});
 }

@@ -27,6 +27,7 @@ def harness(tmp_path_factory):
     L.hb_decode_block.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
     L.hb_encode_block_bytes.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
     L.hb_encode_block_cols.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
+    L.hb_encode_block_fold.argtypes = [u8, ctypes.c_int, ctypes.c_uint, u8]
     return L
 
 
@@ -34,7 +35,7 @@ def _p(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
 
 
-@pytest.mark.parametrize("Q,flags", [(32, 0), (7, 0), (1, 0), (64, 2), (5, 2), (3, 0), (1024, 0)])
+@pytest.mark.parametrize("Q,flags", [(32, 0), (7, 0), (1, 0), (64, 2), (5, 2), (3, 0), (1024, 0), (2, 2), (1 << 20, 0), (1 << 30, 2)])
 def test_block_encode_decode_vs_oracle(harness, Q, flags):
     rng = np.random.Generator(np.random.PCG64(Q * 10 + flags))
     for it in range(300):
@@ -53,6 +54,10 @@ def test_block_encode_decode_vs_oracle(harness, Q, flags):
         assert np.array_equal(kb, kref), ("bytes", it, Q, flags)
         harness.hb_encode_block_cols(_p(blk), Q, flags, _p(kb))
         assert np.array_equal(kb, kref), ("cols", it, Q, flags)
+        harness.hb_encode_block_fold(_p(blk), Q, flags, _p(kb))
+        assert np.array_equal(kb, kref), ("fold", it, Q, flags)
+        if Q > 32767:
+            continue   # decode is int16 (A5): not defined past Q = 32767
         # decode arbitrary index blocks too (not only encoder outputs)
         kin = kref if it % 2 else rng.integers(0, 256, (8, 8, 3), dtype=np.uint8)
         out = np.empty((8, 8, 3), np.uint8)

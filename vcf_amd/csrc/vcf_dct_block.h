@@ -447,6 +447,215 @@ VCF_HD void encode_block_channel_v6(const uint32_t (&raw)[8][6], const EncConsts
     }
 }
 
+// ---------------------------------------------------------------------------
+// "Folded" channel body (encode variants 1 and 2).  For a power-of-two Q the
+// quantizer divisor Q * 2^e, e = chs + inv(i) + inv(j), is a power of two,
+// and every DCT output leaves its pass through one final multiplication
+// (t1 +- t2 with t = tw*r +- tw*r, or r*tw3, r*hf), so the division folds
+// into those final constants exactly: the column pass's by 2^-(chs+inv(i))
+// (compile-time literals), the row pass's by 2^-(inv(j)+log2 Q) (kernel
+// arguments -> SGPR operands).  The row pass then yields x / Q / 2^e itself;
+// one v_cvt_i32_f32 (truncation toward zero = astype(int32)) gives k, whose
+// low byte goes to the sink; the +128 of 2D-DCT.py:348 is applied later to
+// whole words (XOR 0x80 per byte == +128 mod 256).  Non-power-of-two Q keeps
+// the unscaled transforms and a correctly rounded division.
+// ---------------------------------------------------------------------------
+struct FinalK {
+    float p0a, p0b;   // tw0, tw6 -> outputs 1, 7
+    float p1a, p1b;   // tw1, tw5 -> outputs 2, 6
+    float p2a, p2b;   // tw2, tw4 -> outputs 3, 5
+    float s4, s0;     // tw3 -> output 4, hf -> output 0
+};
+
+VCF_HD constexpr FinalK final_k(float pair_scale, float single_scale)
+{
+    return FinalK{VCF_TWF0 * pair_scale, VCF_TWF6 * pair_scale, VCF_TWF1 * pair_scale, VCF_TWF5 * pair_scale,
+                  VCF_TWF2 * pair_scale, VCF_TWF4 * pair_scale, VCF_TWF3 * single_scale, VCF_HF * single_scale};
+}
+
+// dct2_8r with caller-chosen final multipliers (see above)
+VCF_HD void dct2_8f(float (&c)[8], const FinalK &k)
+{
+    const float x1 = c[1] + c[2], x2 = c[2] - c[1];
+    const float x3 = c[3] + c[4], x7 = c[3] - c[4];
+    const float x5 = c[5] + c[6], x6 = c[6] - c[5];
+    const float a0 = c[0] + c[7], a4 = c[0] - c[7];
+    const float a1 = x1 + x5, tr2 = x1 - x5;
+    const float ti2 = x2 + x6, a2 = x2 - x6;
+    const float a6 = VCF_HF * ti2 + VCF_HF * tr2;
+    const float a5 = VCF_HF * tr2 - VCF_HF * ti2;
+    const float T2 = a0 + x3, T1 = a0 - x3;
+    const float r0 = T2 + a1, r4 = T2 - a1, r6 = T1 + a2, r2 = T1 - a2;
+    const float U2 = a4 + x7, U1 = a4 - x7;
+    const float r1 = U2 + a5, r5 = U2 - a5, r7 = U1 + a6, r3 = U1 - a6;
+    float t1, t2;
+    t1 = k.p0a * r7 + k.p0b * r1; t2 = k.p0a * r1 - k.p0b * r7;
+    c[1] = t1 + t2; c[7] = t1 - t2;
+    t1 = k.p1a * r6 + k.p1b * r2; t2 = k.p1a * r2 - k.p1b * r6;
+    c[2] = t1 + t2; c[6] = t1 - t2;
+    t1 = k.p2a * r5 + k.p2b * r3; t2 = k.p2a * r3 - k.p2b * r5;
+    c[3] = t1 + t2; c[5] = t1 - t2;
+    c[4] = r4 * k.s4;
+    c[0] = r0 * k.s0;
+}
+
+VCF_HD int cvt_trunc_i32(float q)
+{
+    return (int)q;   // v_cvt_i32_f32: rounds toward zero, like astype(int32)
+}
+
+// Row-pass final constants for a power-of-two Q (kernel argument).
+VCF_HD_HOST inline FinalK row_final_k(int Q)
+{
+    int l = 0;
+    while ((1 << l) < Q) ++l;
+    const float s = 1.0f / (float)(1u << l);   // exact
+    return final_k(0.25f * s, 0.5f * s);       // 2^-(inv(j) + log2 Q)
+}
+
+// ---- YCoCg straight from the packed bytes with SDWA byte operands --------
+// A VOP2 SDWA instruction reads any byte of either source register as a
+// zero-extended operand, so byte extraction costs nothing:
+//   4Y  bits = magic + r + b + 2g : lshl_sdwa(2g), add_sdwa(r + b), add3  (3)
+//   2Co bits = magic + r - b      : add_sdwa(magic + r), sub_sdwa(.. - b) (2)
+//   4Cg bits = magic - (r+b) + 2g : add_sdwa(r + b), sub, add_sdwa(+g) x2 (4)
+// each followed by one float subtraction of the magic (2^23 + centring),
+// 12 VALU per pixel where the generic byte code needs about 17.
+template <int SEL>
+VCF_HD uint32_t byte_sel(uint32_t w)
+{
+    return (w >> (8 * SEL)) & 0xffu;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define VCF_SDWA_BODY(OP, S0, S1)                                                                    \
+    asm(OP " %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:" S0 " src1_sel:" S1          \
+        : "=v"(r) : "v"(a), "v"(b))
+#define VCF_SDWA_SEL(OP, S0)                                                                         \
+    if (B1 == 0) VCF_SDWA_BODY(OP, S0, "BYTE_0");                                                    \
+    else if (B1 == 1) VCF_SDWA_BODY(OP, S0, "BYTE_1");                                               \
+    else if (B1 == 2) VCF_SDWA_BODY(OP, S0, "BYTE_2");                                               \
+    else VCF_SDWA_BODY(OP, S0, "BYTE_3");
+#define VCF_SDWA_FN(OP)                                                                              \
+    uint32_t r;                                                                                      \
+    if (B0 < 0) { VCF_SDWA_SEL(OP, "DWORD") }                                                        \
+    else if (B0 == 0) { VCF_SDWA_SEL(OP, "BYTE_0") }                                                 \
+    else if (B0 == 1) { VCF_SDWA_SEL(OP, "BYTE_1") }                                                 \
+    else if (B0 == 2) { VCF_SDWA_SEL(OP, "BYTE_2") }                                                 \
+    else { VCF_SDWA_SEL(OP, "BYTE_3") }                                                              \
+    return r;
+#endif
+
+// a[B0] + b[B1]; B0 < 0 takes all of a
+template <int B0, int B1>
+VCF_HD uint32_t add_sdwa(uint32_t a, uint32_t b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    VCF_SDWA_FN("v_add_u32_sdwa")
+#else
+    return (B0 < 0 ? a : byte_sel<(B0 < 0 ? 0 : B0)>(a)) + byte_sel<B1>(b);
+#endif
+}
+
+// a[B0] - b[B1]
+template <int B0, int B1>
+VCF_HD uint32_t sub_sdwa(uint32_t a, uint32_t b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    VCF_SDWA_FN("v_sub_u32_sdwa")
+#else
+    return (B0 < 0 ? a : byte_sel<(B0 < 0 ? 0 : B0)>(a)) - byte_sel<B1>(b);
+#endif
+}
+
+// b[B1] << 1  (src0 is the shift count)
+template <int B1>
+VCF_HD uint32_t twice_byte(uint32_t b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    constexpr int B0 = -1;
+    const uint32_t a = 1;
+    VCF_SDWA_FN("v_lshlrev_b32_sdwa")
+#else
+    return byte_sel<B1>(b) << 1;
+#endif
+}
+
+// channel C of pixel x of a 24-byte row, scaled (4Y, 2Co, 4Cg) and centred
+template <int C, int X>
+VCF_HD float ycocg_sdwa(const uint32_t (&row)[6], uint32_t magic)
+{
+    constexpr int nr = 3 * X, ng = 3 * X + 1, nb = 3 * X + 2;
+    const uint32_t wr = row[nr >> 2], wg = row[ng >> 2], wb = row[nb >> 2];
+    if (C == 0) {
+        const uint32_t rb = add_sdwa<nr & 3, nb & 3>(wr, wb);
+        return bits_as_float(rb + twice_byte<ng & 3>(wg) + magic) - (8388608.0f + 512.0f);
+    }
+    if (C == 1) {
+        const uint32_t t = add_sdwa<-1, nr & 3>(magic, wr);
+        return bits_as_float(sub_sdwa<-1, nb & 3>(t, wb)) - (8388608.0f + 256.0f);
+    }
+    const uint32_t rb = add_sdwa<nr & 3, nb & 3>(wr, wb);
+    const uint32_t t = add_sdwa<-1, ng & 3>(magic - rb, wg);
+    return bits_as_float(add_sdwa<-1, ng & 3>(t, wg)) - (8388608.0f + 512.0f);
+}
+
+// the per-channel magic word: 2^23's bits plus the offset that keeps the
+// integer non-negative (Co: r - b >= -255; Cg: 2g - r - b >= -510)
+template <int C>
+VCF_HD constexpr uint32_t ycocg_magic_word()
+{
+    return C == 0 ? kMagicI : C == 1 ? kMagicI + 256u : kMagicI + 512u;
+}
+
+template <int C, int X, bool SDWA>
+VCF_HD void fold_columns(const uint32_t (&raw)[8][6], uint32_t magic, const FinalK &colk, float (&v)[8][8],
+                         float &dep)
+{
+    if constexpr (X < 8) {
+        float col[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+            col[y] = SDWA ? ycocg_sdwa<C, X>(raw[y], magic)
+                          : ycocg_magic<C>(byte_of(raw[y], 3 * X), byte_of(raw[y], 3 * X + 1),
+                                           byte_of(raw[y], 3 * X + 2));
+        chain8(col, dep);
+        dct2_8f(col, colk);
+#pragma unroll
+        for (int y = 0; y < 8; ++y) v[y][X] = col[y];
+        dep = col[0];
+        fold_columns<C, X + 1, SDWA>(raw, magic, colk, v, dep);
+    }
+}
+
+template <int C, bool POW2, bool PERC, bool SDWA = false, typename Sink>
+VCF_HD void encode_block_channel_fold(const uint32_t (&raw)[8][6], const FinalK &rowk, const float (&qd)[4],
+                                      Sink &&sink)
+{
+    // column pass: 2^-(chs + inv(i)), chs = log2 of the channel scale (4Y, 2Co, 4Cg)
+    constexpr float cs = C == 1 ? 0.5f : 0.25f;
+    constexpr FinalK colk = POW2 ? final_k(cs * 0.25f, cs * 0.5f) : final_k(1.0f, 1.0f);
+    float v[8][8];
+    float dep = qd[0];
+    uint32_t magic = ycocg_magic_word<C>();
+    VCF_OPAQUE(magic);   // one VGPR, not a literal per use
+    fold_columns<C, 0, SDWA>(raw, magic, colk, v, dep);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        chain8(v[i], dep);
+        if (POW2) dct2_8f(v[i], rowk);
+        else dct2_8r(v[i]);
+        dep = v[i][0];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float t = v[i][j];
+            if (PERC) t = (float)((double)t * pweight<C>(i * 8 + j));
+            const float q = POW2 ? t : quant_div<false>(t, qd[qexp<C>(i, j) - 3]);
+            sink(i, j, (uint32_t)cvt_trunc_i32(q));
+        }
+    }
+}
+
 VCF_HD uint32_t byte_at(const uint32_t (&K)[16], int n)
 {
     return (K[n >> 2] >> (8 * (n & 3))) & 0xffu;

@@ -59,7 +59,9 @@ __device__ __forceinline__ long long seg_offset_nosub(const Geom &g, int by, int
     return ((long long)(by * 8 + i) * g.Wp + (long long)bx0 * 8) * 3;
 }
 
-// Copy the LDS image <-> the coefficient frame.  TO_GLOBAL selects direction.
+// Copy the LDS image <-> the coefficient frame.  TO_GLOBAL selects direction;
+// on the way out every byte is XORed with 0x80: the encode stages the low
+// byte of k, and (k ^ 0x80) & 0xff == (k + 128) mod 256 (2D-DCT.py:348,361).
 template <bool SUB, bool TO_GLOBAL>
 __device__ __forceinline__ void move_runs(const Geom &g, uint8_t *stage, uint8_t *frame, int by,
                                           int bx0, int nvalid)
@@ -77,7 +79,7 @@ __device__ __forceinline__ void move_runs(const Geom &g, uint8_t *stage, uint8_t
             const long long go = (SUB ? seg_offset_sub(g, by, bx0, seg) : seg_offset_nosub(g, by, bx0, seg)) + off;
             u32x4 *lp = reinterpret_cast<u32x4 *>(stage + seg * lds_stride + off);
             u32x4 *gp = reinterpret_cast<u32x4 *>(frame + go);
-            if (TO_GLOBAL) __builtin_nontemporal_store(*lp, gp);
+            if (TO_GLOBAL) __builtin_nontemporal_store(*lp ^ 0x80808080u, gp);   // k -> k + 128
             else *lp = __builtin_nontemporal_load(gp);
         }
     } else {
@@ -86,7 +88,7 @@ __device__ __forceinline__ void move_runs(const Geom &g, uint8_t *stage, uint8_t
             const int seg = q / seg_len;
             const int off = q - seg * seg_len;
             const long long go = (SUB ? seg_offset_sub(g, by, bx0, seg) : seg_offset_nosub(g, by, bx0, seg)) + off;
-            if (TO_GLOBAL) frame[go] = stage[seg * lds_stride + off];
+            if (TO_GLOBAL) frame[go] = stage[seg * lds_stride + off] ^ 0x80;
             else stage[seg * lds_stride + off] = frame[go];
         }
     }
@@ -138,8 +140,8 @@ __device__ __forceinline__ void load_block(const Geom &g, const uint8_t *src, in
     }
 }
 
-template <bool POW2, bool SUB, bool PERC>
-__device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncConsts &K,
+template <bool POW2, bool SUB, bool PERC, bool SDWA>
+__device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncConsts &K, const FinalK &rowk,
                                              uint8_t *stage, int tid)
 {
     // each index byte goes from the low byte of its register straight into
@@ -156,17 +158,17 @@ __device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncCon
         if (SUB) stage[(i * 8 + j) * kSegBytes + tid * 3 + 2] = (uint8_t)w;
         else stage[i * (kTile * 24) + tid * 24 + j * 3 + 2] = (uint8_t)w;
     };
-    encode_block_channel_bytes<0, POW2, PERC>(raw, K.qd, s0);
+    encode_block_channel_fold<0, POW2, PERC, SDWA>(raw, rowk, K.qd, s0);
     opaque(raw, (uint32_t)tid);
-    encode_block_channel_bytes<1, POW2, PERC>(raw, K.qd, s1);
+    encode_block_channel_fold<1, POW2, PERC, SDWA>(raw, rowk, K.qd, s1);
     opaque(raw, (uint32_t)tid);
-    encode_block_channel_bytes<2, POW2, PERC>(raw, K.qd, s2);
+    encode_block_channel_fold<2, POW2, PERC, SDWA>(raw, rowk, K.qd, s2);
 }
 
-template <bool POW2, bool SUB, bool PERC, bool PAD>
+template <bool POW2, bool SUB, bool PERC, bool PAD, bool SDWA = false>
 __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
                                                                  uint8_t *__restrict__ kout, Geom g,
-                                                                 EncConsts K)
+                                                                 EncConsts K, FinalK rowk)
 {
     __shared__ __attribute__((aligned(16))) uint8_t stage[kStageBytes];
     const int tid = threadIdx.x;
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_kernel(const uint8_t *
     if (tid < nvalid) {
         uint32_t raw[8][6];
         load_block<PAD>(g, rgb + frame * g.in_stride, by, bx0 + tid, raw);
-        encode_block<POW2, SUB, PERC>(raw, K, stage, tid);
+        encode_block<POW2, SUB, PERC, SDWA>(raw, K, rowk, stage, tid);
     }
     __syncthreads();
     move_runs<SUB, true>(g, stage, kout + frame * g.out_stride, by, bx0, nvalid);
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_kernel(const uint8_t *
 // -- raw synthesised from the lane id, one word stored per lane -- to split
 // kernel time into arithmetic and memory (scripts/bench_variants.py).
 __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_diag(uint8_t *__restrict__ kout, Geom g,
-                                                               EncConsts K, long long nblocks)
+                                                               EncConsts K, FinalK rowk, long long nblocks)
 {
     const long long gid = (long long)blockIdx.x * kTile + threadIdx.x;
     if (gid >= nblocks) return;
@@ -198,11 +200,11 @@ __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_diag(uint8_t *__restri
         for (int w = 0; w < 6; ++w) raw[y][w] = (uint32_t)(gid * 2654435761u) ^ (y * 0x01010101u * (w + 1));
     uint32_t acc = 0;
     auto sink = [&](int i, int j, uint32_t w) { acc += w << ((i + j) & 7); };
-    encode_block_channel_bytes<0, true, false>(raw, K.qd, sink);
+    encode_block_channel_fold<0, true, false>(raw, rowk, K.qd, sink);
     opaque(raw, acc);
-    encode_block_channel_bytes<1, true, false>(raw, K.qd, sink);
+    encode_block_channel_fold<1, true, false>(raw, rowk, K.qd, sink);
     opaque(raw, acc);
-    encode_block_channel_bytes<2, true, false>(raw, K.qd, sink);
+    encode_block_channel_fold<2, true, false>(raw, rowk, K.qd, sink);
     reinterpret_cast<uint32_t *>(kout)[gid] = acc;
 }
 
@@ -508,7 +510,7 @@ using namespace vcf;
     if (pow2 == P2 && sub == SB && perc == PC && pad == PD)                               \
         hipLaunchKernelGGL((dct_dz_encode_kernel<P2, SB, PC, PD>), grid, dim3(kTile), 0,  \
                            (hipStream_t)stream, rgb_dev + f0 * g.in_stride,               \
-                           k_dev + f0 * g.out_stride, g, K);
+                           k_dev + f0 * g.out_stride, g, K, rowk);
 
 #define VCF_DEC_CASE(SB, PC, PD)                                                          \
     if (sub == SB && perc == PC && pad == PD)                                             \
@@ -540,7 +542,7 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
 {
     int rc = check_args(rgb_dev, k_dev, n_frames, H, W, block_size, Q, flags, false);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 3) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
+    if (variant < 0 || variant > 4) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -550,12 +552,22 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
     const bool pad = (g.Hp != H) || (g.Wp != W);
     EncConsts K;
     make_enc_consts(K, Q);
+    const FinalK rowk = pow2 ? row_final_k(Q) : final_k(1.0f, 1.0f);
     if (variant == 2) {
         if (!pow2) return set_error(VCF_ERR_INVALID, "diagnostic variant needs a power-of-two Q");
         const long long nblocks = (long long)n_frames * g.nbx * g.nby;
         hipLaunchKernelGGL(dct_dz_encode_diag, dim3((unsigned)((nblocks + kTile - 1) / kTile)), dim3(kTile),
-                           0, (hipStream_t)stream, k_dev, g, K, nblocks);
+                           0, (hipStream_t)stream, k_dev, g, K, rowk, nblocks);
         return hip_check(hipGetLastError(), "dct_dz_encode_diag launch");
+    }
+    if (variant == 4) {   // experiment: SDWA colour conversion (default flags, aligned, pow2 Q)
+        if (!(pow2 && sub && !perc && !pad)) return set_error(VCF_ERR_INVALID, "variant 4: pow2 Q, aligned, default flags");
+        for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
+            const dim3 grid(g.tiles_per_row * g.nby, (unsigned)std::min<int64_t>(65535, n_frames - f0));
+            hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true>), grid, dim3(kTile), 0,
+                               (hipStream_t)stream, rgb_dev + f0 * g.in_stride, k_dev + f0 * g.out_stride, g, K, rowk);
+        }
+        return hip_check(hipGetLastError(), "variant 4 launch");
     }
     if (variant == 3) return launch_cols<128>(rgb_dev, n_frames, k_dev, g, K, pow2, sub, perc, pad, stream);
     for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
