@@ -31,8 +31,10 @@ for v in variants[1:]:
     print(f"variant {v} == variant {variants[0]}: {np.array_equal(o, ref)}", flush=True)
 res = {v: [] for v in variants}
 e0, e1 = Event(), Event()
-for rnd in range(8):
-    for v in variants:
+ROUNDS = int(os.environ.get("ROUNDS", "16"))
+for rnd in range(ROUNDS):
+    order = variants if rnd % 2 == 0 else variants[::-1]   # ABBA: cancel position effects
+    for v in order:
         e0.record(s)
         for _ in range(10):
             D.encode_device(din, F, H, W, Q, out=outs[v], stream=s, variant=v)
@@ -40,8 +42,10 @@ for rnd in range(8):
         s.synchronize()
         res[v].append(e0.elapsed_ms(e1) / 10)
 alg = F * (H * W * 3 + Hp * Wp * 3)
+base = np.array(res[variants[0]])
 for v in variants:
     t = np.median(res[v])
+    ratio = np.median(np.array(res[v]) / base)
     print(f"variant {v}: median {t:.4f} ms/launch (min {min(res[v]):.4f}) -> "
           f"{alg / t / 1e6:.0f} GB/s ({alg / t / 1e6 / 8000:.1%} of 8 TB/s), "
-          f"{F * H * W / t / 1e3:.0f} Mpix/s", flush=True)
+          f"{F * H * W / t / 1e3:.0f} Mpix/s; per-round ratio to {variants[0]}: {ratio:.4f}", flush=True)

@@ -122,6 +122,14 @@ def test_encode_variants_vs_oracle(variant, Q, flags):
         assert np.array_equal(k[i], O.encode_frame(frames[i], Q, flags))
 
 
+@pytest.mark.parametrize("Q", [1, 32, 256])
+def test_encode_variant4_generic_colour(Q):
+    """The A/B reference kernel (generic colour code) equals the oracle too."""
+    for H, W in [(8, 32), (64, 128), (136, 2048)]:
+        rgb = _rand((H, W, 3), seed=H * W + Q)
+        assert np.array_equal(D.encode(rgb, Q, 0, variant=4), O.encode_frame(rgb, Q, 0)), (H, W)
+
+
 def test_unknown_variant_rejected():
     with pytest.raises(ValueError):
         D.encode(np.zeros((16, 16, 3), np.uint8), 32, variant=99)

@@ -44,6 +44,7 @@ constexpr int kStageBytes = 64 * kSegBytes;  // 48 KiB LDS image
 
 struct Geom {
     int H, W, Hp, Wp, top, left, nbx, nby, tiles_per_row;
+    int nblocks, tiles_per_frame;      // raster tiles: kTile consecutive blocks of a frame
     long long in_stride, out_stride;   // bytes per frame (RGB, coefficients)
     int vec;                           // 16-B path valid for the coefficient frames
 };
@@ -59,35 +60,65 @@ __device__ __forceinline__ long long seg_offset_nosub(const Geom &g, int by, int
     return ((long long)(by * 8 + i) * g.Wp + (long long)bx0 * 8) * 3;
 }
 
-// Copy the LDS image <-> the coefficient frame.  TO_GLOBAL selects direction;
-// on the way out every byte is XORed with 0x80: the encode stages the low
-// byte of k, and (k ^ 0x80) & 0xff == (k + 128) mod 256 (2D-DCT.py:348,361).
-template <bool SUB, bool TO_GLOBAL>
-__device__ __forceinline__ void move_runs(const Geom &g, uint8_t *stage, uint8_t *frame, int by,
-                                          int bx0, int nvalid)
+// Raster tiles (encode variants 1/4, decode): a tile is kTile consecutive
+// blocks of a frame in raster order and may wrap into the next block rows, so
+// only a frame's last tile is partial.  Each lane publishes where its block's
+// bytes start in the frame (`rowbase`: (by*Wp + bx)*3, or (by*8*Wp + bx*8)*3
+// for -x); output run `seg` of the LDS image then maps to rowbase[block] +
+// segment base.  With nbx % 16 == 0 block-row ends fall on 16-block
+// boundaries of the tile, so a 16-byte chunk never straddles one.
+__device__ __forceinline__ void tile_block(const Geom &g, int n, int &by, int &bx)
 {
-    const int nseg = SUB ? 64 : 8;
-    const int seg_len = SUB ? 3 * nvalid : 24 * nvalid;
-    const int lds_stride = SUB ? kSegBytes : kTile * 24;
+    by = n / g.nbx;
+    bx = n - by * g.nbx;
+}
+
+template <bool SUB>
+__device__ __forceinline__ uint32_t block_rowbase(const Geom &g, int by, int bx)
+{
+    return SUB ? ((uint32_t)by * (uint32_t)g.Wp + (uint32_t)bx) * 3u
+               : ((uint32_t)by * 8u * (uint32_t)g.Wp + (uint32_t)bx * 8u) * 3u;
+}
+
+template <bool SUB>
+__device__ __forceinline__ uint32_t seg_base(const Geom &g, int seg)
+{
+    if (!SUB) return (uint32_t)seg * (uint32_t)g.Wp * 3u;
+    const uint32_t i = seg >> 3, j = seg & 7;
+    return (i * (uint32_t)g.nby * (uint32_t)g.Wp + j * (uint32_t)g.nbx) * 3u;
+}
+
+template <bool SUB, bool TO_GLOBAL>
+__device__ __forceinline__ void move_runs_tab(const Geom &g, uint8_t *stage, const uint32_t *rowbase,
+                                              uint8_t *frame, int nvalid)
+{
+    constexpr int nseg = SUB ? 64 : 8;
+    constexpr int bpb = SUB ? 3 : 24;                  // bytes per block in a run
+    constexpr int lds_stride = SUB ? kSegBytes : kTile * 24;
     const int tid = threadIdx.x;
     if (g.vec) {
-        const int cps = seg_len >> 4;
+        const int cps = (nvalid * bpb) >> 4;           // nvalid is a multiple of 16
+        // stage bytes are the low bytes of k: XOR 0x80 == +128 mod 256 (2D-DCT.py:348,361)
         const int total = nseg * cps;
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
         for (int q = tid; q < total; q += kTile) {
             const int seg = q / cps;
             const int off = (q - seg * cps) << 4;
-            const long long go = (SUB ? seg_offset_sub(g, by, bx0, seg) : seg_offset_nosub(g, by, bx0, seg)) + off;
+            const int blk = off / bpb;
+            const uint32_t go = rowbase[blk] + seg_base<SUB>(g, seg) + (uint32_t)(off - blk * bpb);
             u32x4 *lp = reinterpret_cast<u32x4 *>(stage + seg * lds_stride + off);
             u32x4 *gp = reinterpret_cast<u32x4 *>(frame + go);
             if (TO_GLOBAL) __builtin_nontemporal_store(*lp ^ 0x80808080u, gp);   // k -> k + 128
             else *lp = __builtin_nontemporal_load(gp);
         }
     } else {
-        const int total = nseg * seg_len;
+        const int seg_len = nvalid * bpb, total = nseg * seg_len;
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
         for (int q = tid; q < total; q += kTile) {
             const int seg = q / seg_len;
             const int off = q - seg * seg_len;
-            const long long go = (SUB ? seg_offset_sub(g, by, bx0, seg) : seg_offset_nosub(g, by, bx0, seg)) + off;
+            const int blk = off / bpb;
+            const uint32_t go = rowbase[blk] + seg_base<SUB>(g, seg) + (uint32_t)(off - blk * bpb);
             if (TO_GLOBAL) frame[go] = stage[seg * lds_stride + off] ^ 0x80;
             else stage[seg * lds_stride + off] = frame[go];
         }
@@ -165,24 +196,27 @@ __device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncCon
     encode_block_channel_fold<2, POW2, PERC, SDWA>(raw, rowk, K.qd, s2);
 }
 
-template <bool POW2, bool SUB, bool PERC, bool PAD, bool SDWA = false>
+template <bool POW2, bool SUB, bool PERC, bool PAD, bool SDWA = true>
 __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
                                                                  uint8_t *__restrict__ kout, Geom g,
                                                                  EncConsts K, FinalK rowk)
 {
     __shared__ __attribute__((aligned(16))) uint8_t stage[kStageBytes];
+    __shared__ uint32_t rowbase[kTile];
     const int tid = threadIdx.x;
     const long long frame = blockIdx.y;
-    const int by = blockIdx.x / g.tiles_per_row;
-    const int bx0 = (blockIdx.x - by * g.tiles_per_row) * kTile;
-    const int nvalid = min(kTile, g.nbx - bx0);
+    const int n0 = blockIdx.x * kTile;
+    const int nvalid = min(kTile, g.nblocks - n0);
     if (tid < nvalid) {
+        int by, bx;
+        tile_block(g, n0 + tid, by, bx);
+        rowbase[tid] = block_rowbase<SUB>(g, by, bx);
         uint32_t raw[8][6];
-        load_block<PAD>(g, rgb + frame * g.in_stride, by, bx0 + tid, raw);
+        load_block<PAD>(g, rgb + frame * g.in_stride, by, bx, raw);
         encode_block<POW2, SUB, PERC, SDWA>(raw, K, rowk, stage, tid);
     }
     __syncthreads();
-    move_runs<SUB, true>(g, stage, kout + frame * g.out_stride, by, bx0, nvalid);
+    move_runs_tab<SUB, true>(g, stage, rowbase, kout + frame * g.out_stride, nvalid);
 }
 
 // Diagnostic (encode variant 2): the same body with no memory traffic at all
@@ -200,11 +234,11 @@ __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_diag(uint8_t *__restri
         for (int w = 0; w < 6; ++w) raw[y][w] = (uint32_t)(gid * 2654435761u) ^ (y * 0x01010101u * (w + 1));
     uint32_t acc = 0;
     auto sink = [&](int i, int j, uint32_t w) { acc += w << ((i + j) & 7); };
-    encode_block_channel_fold<0, true, false>(raw, rowk, K.qd, sink);
+    encode_block_channel_fold<0, true, false, true>(raw, rowk, K.qd, sink);
     opaque(raw, acc);
-    encode_block_channel_fold<1, true, false>(raw, rowk, K.qd, sink);
+    encode_block_channel_fold<1, true, false, true>(raw, rowk, K.qd, sink);
     opaque(raw, acc);
-    encode_block_channel_fold<2, true, false>(raw, rowk, K.qd, sink);
+    encode_block_channel_fold<2, true, false, true>(raw, rowk, K.qd, sink);
     reinterpret_cast<uint32_t *>(kout)[gid] = acc;
 }
 
@@ -379,14 +413,18 @@ __global__ __launch_bounds__(kTile, 2) void dct_dz_decode_kernel(const uint8_t *
                                                                  int Q)
 {
     __shared__ __attribute__((aligned(16))) uint8_t stage[kStageBytes];
+    __shared__ uint32_t rowbase[kTile];
     const int tid = threadIdx.x;
     const long long frame = blockIdx.y;
-    const int by = blockIdx.x / g.tiles_per_row;
-    const int bx0 = (blockIdx.x - by * g.tiles_per_row) * kTile;
-    const int nvalid = min(kTile, g.nbx - bx0);
-    const int bx = bx0 + tid;
-    move_runs<SUB, false>(g, stage, const_cast<uint8_t *>(kin) + frame * g.out_stride, by, bx0,
-                          nvalid);
+    const int n0 = blockIdx.x * kTile;
+    const int nvalid = min(kTile, g.nblocks - n0);
+    int by = 0, bx = 0;
+    if (tid < nvalid) {
+        tile_block(g, n0 + tid, by, bx);
+        rowbase[tid] = block_rowbase<SUB>(g, by, bx);
+    }
+    __syncthreads();
+    move_runs_tab<SUB, false>(g, stage, rowbase, const_cast<uint8_t *>(kin) + frame * g.out_stride, nvalid);
     __syncthreads();
     if (tid >= nvalid) return;
 
@@ -471,6 +509,8 @@ void make_geom(int32_t H, int32_t W, Geom &g)
     g.nbx = g.Wp / 8;
     g.nby = g.Hp / 8;
     g.tiles_per_row = (g.nbx + kTile - 1) / kTile;
+    g.nblocks = g.nbx * g.nby;
+    g.tiles_per_frame = (g.nblocks + kTile - 1) / kTile;
     g.in_stride = (long long)H * W * 3;
     g.out_stride = (long long)g.Hp * g.Wp * 3;
     // every subband run starts 16-B aligned and spans whole 16-B chunks iff
@@ -560,18 +600,18 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                            0, (hipStream_t)stream, k_dev, g, K, rowk, nblocks);
         return hip_check(hipGetLastError(), "dct_dz_encode_diag launch");
     }
-    if (variant == 4) {   // experiment: SDWA colour conversion (default flags, aligned, pow2 Q)
+    if (variant == 4) {   // A/B reference: variant 1 with generic byte code for the colour conversion
         if (!(pow2 && sub && !perc && !pad)) return set_error(VCF_ERR_INVALID, "variant 4: pow2 Q, aligned, default flags");
         for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
-            const dim3 grid(g.tiles_per_row * g.nby, (unsigned)std::min<int64_t>(65535, n_frames - f0));
-            hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true>), grid, dim3(kTile), 0,
+            const dim3 grid(g.tiles_per_frame, (unsigned)std::min<int64_t>(65535, n_frames - f0));
+            hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, false>), grid, dim3(kTile), 0,
                                (hipStream_t)stream, rgb_dev + f0 * g.in_stride, k_dev + f0 * g.out_stride, g, K, rowk);
         }
         return hip_check(hipGetLastError(), "variant 4 launch");
     }
     if (variant == 3) return launch_cols<128>(rgb_dev, n_frames, k_dev, g, K, pow2, sub, perc, pad, stream);
     for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
-        const dim3 grid(g.tiles_per_row * g.nby, (unsigned)std::min<int64_t>(65535, n_frames - f0));
+        const dim3 grid(g.tiles_per_frame, (unsigned)std::min<int64_t>(65535, n_frames - f0));
         VCF_ENC_CASE(true, true, false, false) else VCF_ENC_CASE(true, true, false, true)
         else VCF_ENC_CASE(true, true, true, false) else VCF_ENC_CASE(true, true, true, true)
         else VCF_ENC_CASE(true, false, false, false) else VCF_ENC_CASE(true, false, false, true)
@@ -598,7 +638,7 @@ int vcf_dct_dz_decode(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t
     const bool perc = (flags & VCF_DCT_PERCEPTUAL) != 0;
     const bool pad = (g.Hp != H) || (g.Wp != W);
     for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
-        const dim3 grid(g.tiles_per_row * g.nby, (unsigned)std::min<int64_t>(65535, n_frames - f0));
+        const dim3 grid(g.tiles_per_frame, (unsigned)std::min<int64_t>(65535, n_frames - f0));
         VCF_DEC_CASE(true, false, false) else VCF_DEC_CASE(true, false, true)
         else VCF_DEC_CASE(true, true, false) else VCF_DEC_CASE(true, true, true)
         else VCF_DEC_CASE(false, false, false) else VCF_DEC_CASE(false, false, true)
