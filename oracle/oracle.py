@@ -34,9 +34,8 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH) or (
-            os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "vcf_oracle.c"))
-        ):
+        srcs = [os.path.join(HERE, "vcf_oracle.c"), os.path.join(HERE, "vcf_dwt_oracle.cpp")]
+        if not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(f) for f in srcs):
             build()
         L = ctypes.CDLL(LIB_PATH)
         u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -52,6 +51,18 @@ def lib():
             getattr(L, n).argtypes = [dp]
         L.vcfo_pocketfft_consts.argtypes = [fp, dp, fp, dp, fp, dp]
         L.vcfo_perceptual_weights.argtypes = [dp]
+        # 2D-DWT path (vcf_dwt_oracle.cpp)
+        ip = ctypes.POINTER(ctypes.c_int)
+        u16p = ctypes.POINTER(ctypes.c_uint16)
+        L.vcfo_wavelet_index.argtypes = [ctypes.c_char_p]
+        L.vcfo_wavelet_len.argtypes = [ctypes.c_int]
+        L.vcfo_dwt_shapes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ip]
+        L.vcfo_wavedec2.argtypes = [dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]
+        L.vcfo_waverec2.argtypes = [dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]
+        L.vcfo_dwt_dz_encode.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, u16p, u8p]
+        L.vcfo_dwt_dz_decode.argtypes = [u16p, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, u8p]
         _lib = L
     return _lib
 
@@ -139,3 +150,101 @@ def perceptual_weights() -> np.ndarray:
 # --------------------------------------------------------------------------
 def encode_frames(frames: np.ndarray, Q: int = 32, flags: int = 0) -> np.ndarray:
     return np.stack([encode_frame(f, Q, flags) for f in frames])
+
+
+# --------------------------------------------------------------------------
+# 2D-DWT path (src/2D-DWT.py encode_fn :57-78, decode_fn :80-101)
+# --------------------------------------------------------------------------
+def wavelet_index(name: str) -> int:
+    i = lib().vcfo_wavelet_index(name.encode())
+    if i < 0:
+        raise ValueError(f"unknown wavelet {name!r}")
+    return i
+
+
+def dwt_shapes(H: int, W: int, levels: int):
+    """[(h_l, w_l) for l = 1..levels] (mode 'per': ceil halving)."""
+    hs = (ctypes.c_int * levels)()
+    ws = (ctypes.c_int * levels)()
+    lib().vcfo_dwt_shapes(H, W, levels, hs, ws)
+    return list(zip(hs[:], ws[:]))
+
+
+def subband_names(levels: int):
+    """File order of write_decom_fn (2D-DWT.py:162-200)."""
+    return [f"LL_{levels}"] + [f"{s}_{r}" for r in range(levels, 0, -1) for s in ("LH", "HL", "HH")]
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _coeff_count(H, W, levels):
+    sh = dwt_shapes(H, W, levels)
+    return sh[-1][0] * sh[-1][1] + sum(3 * h * w for h, w in sh)
+
+
+def wavedec2(x: np.ndarray, wavelet: str, levels: int):
+    """pywt.wavedec2(x, wavelet, mode='per', level=levels) as [cA, (cH, cV, cD), ...]."""
+    x = np.ascontiguousarray(x, np.float64)
+    H, W = x.shape
+    flat = np.empty(_coeff_count(H, W, levels))
+    rc = lib().vcfo_wavedec2(_dp(x), H, W, wavelet_index(wavelet), levels, _dp(flat))
+    if rc != 0:
+        raise RuntimeError("oracle wavedec2 failed")
+    sh = dwt_shapes(H, W, levels)
+    h, w = sh[-1]
+    out = [flat[:h * w].reshape(h, w)]
+    off = h * w
+    for r in range(levels, 0, -1):
+        h, w = sh[r - 1]
+        out.append(tuple(flat[off + k * h * w:off + (k + 1) * h * w].reshape(h, w) for k in range(3)))
+        off += 3 * h * w
+    return out
+
+
+def waverec2(coeffs, wavelet: str, H: int, W: int):
+    """pywt.waverec2(coeffs, wavelet, mode='per') for a plane of H x W."""
+    levels = len(coeffs) - 1
+    flat = np.concatenate([np.ravel(coeffs[0])] + [np.ravel(b) for r in coeffs[1:] for b in r]).astype(np.float64)
+    sh = dwt_shapes(H, W, levels)
+    out = np.empty((2 * sh[0][0], 2 * sh[0][1]))
+    rc = lib().vcfo_waverec2(_dp(flat), H, W, wavelet_index(wavelet), levels, _dp(out))
+    if rc != 0:
+        raise RuntimeError("oracle waverec2 failed")
+    return out
+
+
+def dwt_encode_frame(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32):
+    """u8 RGB -> {subband name: u16 (LL) / u8 (details) H_l x W_l x 3}."""
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    H, W = rgb.shape[:2]
+    sh = dwt_shapes(H, W, levels)
+    LL = np.empty((sh[-1][0], sh[-1][1], 3), np.uint16)
+    det = np.empty(3 * sum(3 * h * w for h, w in sh), np.uint8)
+    rc = lib().vcfo_dwt_dz_encode(_u8(rgb), H, W, wavelet_index(wavelet), levels, int(Q),
+                                  LL.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), _u8(det))
+    if rc != 0:
+        raise RuntimeError("oracle dwt encode failed")
+    out = {f"LL_{levels}": LL}
+    off = 0
+    for r in range(levels, 0, -1):
+        h, w = sh[r - 1]
+        for s in ("LH", "HL", "HH"):
+            out[f"{s}_{r}"] = det[off:off + 3 * h * w].reshape(h, w, 3)
+            off += 3 * h * w
+    return out
+
+
+def dwt_decode_frame(subbands, H: int, W: int, wavelet: str = "db5", levels: int = 5, Q: int = 32):
+    """{subband: indices} -> u8 RGB (2*ceil(H/2) x 2*ceil(W/2) x 3, like pywt.waverec2)."""
+    sh = dwt_shapes(H, W, levels)
+    LL = np.ascontiguousarray(subbands[f"LL_{levels}"], np.uint16)
+    det = np.concatenate([np.ravel(np.ascontiguousarray(subbands[f"{s}_{r}"], np.uint8))
+                          for r in range(levels, 0, -1) for s in ("LH", "HL", "HH")])
+    out = np.empty((2 * sh[0][0], 2 * sh[0][1], 3), np.uint8)
+    rc = lib().vcfo_dwt_dz_decode(LL.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), _u8(det), H, W,
+                                  wavelet_index(wavelet), levels, int(Q), _u8(out))
+    if rc != 0:
+        raise RuntimeError("oracle dwt decode failed")
+    return out
