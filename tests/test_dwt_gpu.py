@@ -1,0 +1,62 @@
+"""2D-DWT + deadzone on the GPU against the reference's files (tests/golden/
+dwt_*.npz, made by src/2D-DWT.py) and the oracle, bit for bit."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+_MAN = json.load(open(os.path.join(GOLDEN, "manifest_dwt.json")))
+
+
+def _params(case):
+    fl = case["flags"]
+    w = fl[fl.index("-w") + 1] if "-w" in fl else "db5"
+    Q = int(fl[fl.index("-q") + 1]) if "-q" in fl else 32
+    return w, case["levels"], Q
+
+
+@pytest.mark.parametrize("case", _MAN["cases"], ids=lambda c: c["name"])
+def test_dwt_encode_decode_vs_reference(case):
+    import vcf_amd.dwt as DW
+    d = np.load(os.path.join(GOLDEN, f"dwt_{case['name']}.npz"))
+    w, L, Q = _params(case)
+    sb = DW.encode(d["rgb"], w, L, Q)[0]
+    for name in case["subbands"]:
+        assert np.array_equal(sb[name], d[name]), name
+    out = DW.decode({n: d[n] for n in case["subbands"]}, case["H"], case["W"], w, L, Q)
+    assert np.array_equal(out, d["decoded"])
+
+
+@pytest.mark.parametrize("wavelet", ["db5", "bior4.4", "haar", "sym4", "coif2", "db10"])
+@pytest.mark.parametrize("H,W,L,Q", [(96, 128, 3, 32), (67, 45, 2, 7), (256, 160, 5, 16), (8, 10, 1, 1)])
+def test_dwt_vs_oracle(wavelet, H, W, L, Q):
+    import vcf_amd.dwt as DW
+    shapes = O.dwt_shapes(H, W, L)
+    rng = np.random.Generator(np.random.PCG64(H * W + L))
+    frames = rng.integers(0, 256, (2, H, W, 3), dtype=np.uint8)
+    got = DW.encode(frames, wavelet, L, Q)
+    for f in range(2):
+        ref = O.dwt_encode_frame(frames[f], wavelet, L, Q)
+        for name, arr in ref.items():
+            assert np.array_equal(got[f][name], arr), (f, name)
+    half = O.lib().vcfo_wavelet_len(O.wavelet_index(wavelet)) // 2
+    if min(shapes[-1]) < half:
+        with pytest.raises(NotImplementedError):
+            DW.decode(got[0], H, W, wavelet, L, Q)
+        return
+    out = DW.decode(got, H, W, wavelet, L, Q)
+    for f in range(2):
+        assert np.array_equal(out[f], O.dwt_decode_frame(got[f], H, W, wavelet, L, Q))
+
+
+def test_dwt_errors():
+    import vcf_amd.dwt as DW
+    with pytest.raises(ValueError):
+        DW.wavelet_index("nope")
+    with pytest.raises(ValueError):
+        DW.encode(np.zeros((8, 8, 3), np.uint8), "db5", 0, 32)

@@ -1,0 +1,99 @@
+"""2D-DWT + deadzone on the GPU (src/2D-DWT.py encode_fn :57-78 up to the
+TIFF writer, decode_fn :80-101 after the TIFF reader), through
+libvcf_amd.so (vcf_dwt_dz_encode / vcf_dwt_dz_decode).  No CPU path."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+from .device import DeviceBuffer
+
+
+def wavelet_index(name: str) -> int:
+    i = ctypes.c_int32()
+    L.call("vcf_wavelet_index", str(name).encode(), ctypes.byref(i))
+    return i.value
+
+
+def layout(H: int, W: int, levels: int):
+    """([(h_l, w_l) for l = 1..levels], packed bytes per frame, workspace bytes per frame)."""
+    hs = (ctypes.c_int32 * levels)()
+    ws = (ctypes.c_int32 * levels)()
+    pb, wb = ctypes.c_int64(), ctypes.c_int64()
+    L.call("vcf_dwt_layout", H, W, levels, hs, ws, ctypes.byref(pb), ctypes.byref(wb))
+    return list(zip(hs[:], ws[:])), pb.value, wb.value
+
+
+def subband_names(levels: int):
+    """File order of write_decom_fn (2D-DWT.py:162-200)."""
+    return [f"LL_{levels}"] + [f"{s}_{r}" for r in range(levels, 0, -1) for s in ("LH", "HL", "HH")]
+
+
+def unpack(packed: np.ndarray, H: int, W: int, levels: int):
+    """Packed bytes of one frame -> {name: u16 LL / u8 detail array (h x w x 3)}."""
+    shapes, _, _ = layout(H, W, levels)
+    h, w = shapes[-1]
+    out = {f"LL_{levels}": packed[:h * w * 6].view(np.uint16).reshape(h, w, 3)}
+    off = h * w * 6
+    for r in range(levels, 0, -1):
+        h, w = shapes[r - 1]
+        for s in ("LH", "HL", "HH"):
+            out[f"{s}_{r}"] = packed[off:off + h * w * 3].reshape(h, w, 3)
+            off += h * w * 3
+    return out
+
+
+def pack(subbands, H: int, W: int, levels: int) -> np.ndarray:
+    parts = [np.ascontiguousarray(subbands[f"LL_{levels}"], np.uint16).view(np.uint8).ravel()]
+    for r in range(levels, 0, -1):
+        for s in ("LH", "HL", "HH"):
+            parts.append(np.ascontiguousarray(subbands[f"{s}_{r}"], np.uint8).ravel())
+    return np.concatenate(parts)
+
+
+def _frames(a, what):
+    a = np.asarray(a)
+    if a.ndim == 3:
+        a = a[None]
+    if a.ndim != 4 or a.shape[-1] != 3 or a.dtype != np.uint8:
+        raise ValueError(f"{what}: expected (N,) H x W x 3 uint8")
+    return np.ascontiguousarray(a)
+
+
+def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32):
+    """HxWx3 u8 (or N of them) -> list of {subband name: indices} per frame."""
+    f = _frames(rgb, "rgb")
+    n, H, W, _ = f.shape
+    _, pb, wb = layout(H, W, levels)
+    din, dout, dws = DeviceBuffer.from_array(f), DeviceBuffer(n * pb), DeviceBuffer(n * wb)
+    try:
+        L.call("vcf_dwt_dz_encode", din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q), dout.ptr, dws.ptr,
+               None)
+        packed = dout.download(np.empty((n, pb), np.uint8))
+    finally:
+        din.free()
+        dout.free()
+        dws.free()
+    return [unpack(packed[i], H, W, levels) for i in range(n)]
+
+
+def decode(subbands, H: int, W: int, wavelet: str = "db5", levels: int = 5, Q: int = 32) -> np.ndarray:
+    """{name: indices} (or a list of them) -> u8 RGB (2*ceil(H/2) x 2*ceil(W/2) x 3 each)."""
+    single = isinstance(subbands, dict)
+    sets = [subbands] if single else list(subbands)
+    shapes, pb, wb = layout(H, W, levels)
+    packed = np.stack([pack(s, H, W, levels) for s in sets])
+    n = len(sets)
+    Ho, Wo = 2 * shapes[0][0], 2 * shapes[0][1]
+    din, dout, dws = DeviceBuffer.from_array(packed), DeviceBuffer(n * Ho * Wo * 3), DeviceBuffer(n * wb)
+    try:
+        L.call("vcf_dwt_dz_decode", din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q), dout.ptr, dws.ptr,
+               None)
+        out = dout.download(np.empty((n, Ho, Wo, 3), np.uint8))
+    finally:
+        din.free()
+        dout.free()
+        dws.free()
+    return out[0] if single else out
