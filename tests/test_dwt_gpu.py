@@ -60,3 +60,48 @@ def test_dwt_errors():
         DW.wavelet_index("nope")
     with pytest.raises(ValueError):
         DW.encode(np.zeros((8, 8, 3), np.uint8), "db5", 0, 32)
+
+
+@pytest.mark.parametrize("case", _MAN["cases"][:5], ids=lambda c: c["name"])
+def test_dwt_codec_files(tmp_path, case):
+    """encode_fn writes the reference's subband files; decode_fn of the
+    reference's files gives its decoded frame."""
+    from PIL import Image
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec.dwt2d import CoDec
+    from vcf_amd.codec.tiff import imread_bytes, imwrite_bytes
+    d = np.load(os.path.join(GOLDEN, f"dwt_{case['name']}.npz"))
+    src = str(tmp_path / "in.png")
+    Image.fromarray(d["rgb"]).save(src)
+    enc = str(tmp_path / "enc")
+    c = CoDec(P.parse(P.dwt_parser(), ["encode"] + case["flags"]))
+    n = c.encode_fn(src, enc)
+    assert n == case["encode_bytes"]
+    L = case["levels"]
+    assert open(f"{enc}_LL_{L}.tif", "rb").read() == bytes(d["tif_LL"])
+    for name in case["subbands"]:
+        assert np.array_equal(imread_bytes(open(f"{enc}_{name}.tif", "rb").read()), d[name]), name
+    ref = str(tmp_path / "ref")
+    for name in case["subbands"]:
+        with open(f"{ref}_{name}.tif", "wb") as f:
+            f.write(imwrite_bytes(d[name]))
+    out = str(tmp_path / "out.png")
+    CoDec(P.parse(P.dwt_parser(), ["decode"] + case["flags"])).decode_fn(ref, out)
+    assert np.array_equal(np.asarray(Image.open(out)), d["decoded"])
+
+
+def test_cli_2d_dwt(tmp_path):
+    import subprocess
+    import sys
+    from PIL import Image
+    from conftest import ROOT
+    rgb = np.random.Generator(np.random.PCG64(3)).integers(0, 256, (48, 64, 3), dtype=np.uint8)
+    src, enc, dec = str(tmp_path / "o.png"), str(tmp_path / "e"), str(tmp_path / "d.png")
+    Image.fromarray(rgb).save(src)
+    for argv in (["encode", "-l", "2", "-w", "bior4.4", "-o", src, "-e", enc],
+                 ["decode", "-l", "2", "-w", "bior4.4", "-e", enc, "-d", dec]):
+        r = subprocess.run([sys.executable, "vcf_amd/cli/2D-DWT.py"] + argv, cwd=ROOT, capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+    sb = O.dwt_encode_frame(rgb, "bior4.4", 2, 32)
+    assert np.array_equal(np.asarray(Image.open(dec)), O.dwt_decode_frame(sb, 48, 64, "bior4.4", 2, 32))

@@ -47,3 +47,13 @@ def test_unsupported_options_raise():
                  ["encode", "-L", "1"], ["encode", "-c", "PNG"], ["decode", "-f", "gaussian_blur"]):
         with pytest.raises(NotImplementedError):
             CoDec(P.parse(p, argv))
+
+
+def test_dwt_options():
+    d = _ns(P.dwt_parser(), ["encode", "-l", "3", "-w", "bior4.4", "-q", "16"])
+    assert d["levels"] == 3 and d["wavelet"] == "bior4.4" and d["QSS"] == 16
+    assert d["color_transform"] == "YCoCg" and d["quantizer"] == "deadzone"
+    d = _ns(P.dwt_parser(), ["decode"])
+    assert d["levels"] == 5 and d["wavelet"] == "db5" and d["filter"] == "no_filter"
+    d = _ns(P.iii_parser(transform="2D-DWT"), ["encode", "-T", "2D-DWT", "-l", "2"])
+    assert d["transform"] == "2D-DWT" and d["levels"] == 2

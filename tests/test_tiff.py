@@ -66,3 +66,18 @@ def test_tiff_uint16_and_codec_surface():
     assert c.file_extension == ".tif"
     with pytest.raises(AssertionError):
         c.compress(a.astype(np.float32))
+
+
+def _dwt_cases():
+    import json
+    return json.load(open(os.path.join(GOLDEN, "manifest_dwt.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", _dwt_cases(), ids=lambda c: c["name"])
+def test_tiff_dwt_subband_files_equal_reference(case):
+    """2D-DWT.py:162-200 writes LL as uint16 and details as uint8 TIFFs."""
+    d = np.load(os.path.join(GOLDEN, f"dwt_{case['name']}.npz"))
+    L = case["levels"]
+    assert imwrite_bytes(d[f"LL_{L}"]) == bytes(d["tif_LL"])
+    assert imwrite_bytes(d["HH_1"]) == bytes(d["tif_HH_1"])
+    assert np.array_equal(imread_bytes(bytes(d["tif_LL"])), d[f"LL_{L}"])

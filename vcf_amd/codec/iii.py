@@ -35,7 +35,10 @@ def transform_codec(args):
     if name == "2D-DCT":
         from .dct2d import CoDec
         return CoDec(args)
-    raise NotImplementedError(f"transform {name!r}: only 2D-DCT is on the HIP path")
+    if name == "2D-DWT":
+        from .dwt2d import CoDec
+        return CoDec(args)
+    raise NotImplementedError(f"transform {name!r}: 2D-DCT and 2D-DWT are on the HIP path")
 
 
 def _frame_inputs(original: str, n: int):

@@ -126,6 +126,17 @@ def add_dct(enc, dec):
                        default=False)
 
 
+def add_dwt(enc, dec):
+    """2D-DWT.py:25-31."""
+    for p in (enc, dec):
+        p.add_argument("-l", "--levels", type=int_or_str,
+                       help=f"Number of decomposition levels (default: {DEFAULT_LEVELS})", default=DEFAULT_LEVELS)
+        p.add_argument("-w", "--wavelet", type=int_or_str,
+                       help=f"Wavelet name (default: \"{DEFAULT_WAVELET}\")", default=DEFAULT_WAVELET)
+        p.add_argument("-t", "--color_transform", type=int_or_str,
+                       help=f"Color transform (default: \"{DEFAULT_CT}\")", default=DEFAULT_CT)
+
+
 def add_iii(enc, dec):
     """III.py:23-33."""
     for p, what in ((enc, "encode"), (dec, "decode")):
@@ -147,11 +158,27 @@ def dct_parser(description: str = "Exploiting spatial redundancy with the 2D Dis
     return p
 
 
-def iii_parser(description: str = "III coding: runs a 2D image codec for each image of a sequence."):
-    """`python III.py ...` (III.py + the default 2D-DCT chain it imports)."""
+def dwt_parser(description: str = "Exploiting spatial redundancy with the 2D dyadic Discrete Wavelet "
+                                  "Transform."):
+    """`python 2D-DWT.py ...` (2D-DWT.py -> YCoCg.py -> deadzone.py -> no_filter.py -> TIFF.py)."""
+    p, enc, dec = base_parser(description)
+    add_dwt(enc, dec)
+    add_ycocg(enc, dec)
+    add_deadzone(enc, dec)
+    add_filter(enc, dec)
+    add_eic(enc, dec)
+    return p
+
+
+def iii_parser(description: str = "III coding: runs a 2D image codec for each image of a sequence.",
+               transform: str = "2D-DCT"):
+    """`python III.py ...` (III.py + the chain of the 2D codec it imports)."""
     p, enc, dec = base_parser(description)
     add_iii(enc, dec)
-    add_dct(enc, dec)
+    if transform == "2D-DWT":
+        add_dwt(enc, dec)
+    else:
+        add_dct(enc, dec)
     add_ycocg(enc, dec)
     add_deadzone(enc, dec)
     add_filter(enc, dec)
