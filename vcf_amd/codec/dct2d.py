@@ -26,7 +26,13 @@ from .. import dct as D
 from .eic import CoDec as EICCoDec
 from .tiff import TIFFCodec
 
-ENTROPY_CODECS = {"TIFF": TIFFCodec}
+
+def _cbaac(args=None):
+    from ..cbaac import CBAACCodec
+    return CBAACCodec(getattr(args, "order", 0) if args is not None else 0)
+
+
+ENTROPY_CODECS = {"TIFF": TIFFCodec, "CBAAC": _cbaac}
 
 
 def register_entropy_codec(name, cls):
@@ -63,7 +69,8 @@ class CoDec(EICCoDec):
         ec_name = getattr(args, "entropy_image_codec", "TIFF")
         if ec_name not in ENTROPY_CODECS:
             raise NotImplementedError(f"entropy codec {ec_name!r} (have: {sorted(ENTROPY_CODECS)})")
-        self.entropy = ENTROPY_CODECS[ec_name]()
+        maker = ENTROPY_CODECS[ec_name]
+        self.entropy = maker(args) if maker is _cbaac else maker()
         self.file_extension = self.entropy.file_extension
         self.QSS = int(getattr(args, "QSS", 32))
         self.offset = 128            # 2D-DCT.py:102-105 (quantizer == deadzone)

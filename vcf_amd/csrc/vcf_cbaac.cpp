@@ -1,0 +1,287 @@
+// vcf_cbaac.cpp -- context-based adaptive arithmetic coding (src/CBAAC.py),
+// native host code, and the vcf_cbaac_* entry points of the C ABI.
+//
+// The model is the reference's, exactly (pinned against traces of its own
+// classes, tests/golden/make_golden_cbaac.py):
+//   AdaptiveModel (CBAAC.py:17-47): 256 frequencies initialised to 1;
+//     update(s): freqs[s] += 1, and if the total *before* that increment is
+//     >= 16384, every frequency becomes (f >> 1) + 1; get_range(s) =
+//     (cum[s], cum[s+1], total).
+//   ContextManager (:49-69): one model per distinct tuple of the previous
+//     `order` symbols (history starts as `order` zeros), created on first use.
+// The arithmetic coder (package arithmetic_coding, not vendored) is
+// assumption A8 of SURVEY.md: a 32-bit Witten-Neal-Cleary integer coder
+// with pending (underflow) bits, bits emitted MSB-first into bytes
+// (bitarray endian='big', zero padded), flush = one more pending bit and a
+// disambiguating bit.  The decoder reads zeros past the end.
+//
+// The coder is inherently serial (every symbol's interval depends on all
+// previous ones), so this is host code; prefix sums are a Fenwick tree
+// (log2 256 = 8 steps per symbol instead of the reference's 256-entry
+// cumulative rebuild), rebuilt only when the model rescales.
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+#include "vcf_amd.h"
+#include "vcf_internal.h"
+
+namespace vcf {
+namespace {
+
+constexpr int kSymbols = 256;
+constexpr uint32_t kMaxFreq = 16384;   // AdaptiveModel(max_freq=16384)
+
+struct Model {
+    uint32_t freq[kSymbols];
+    uint32_t tree[kSymbols + 1];   // Fenwick tree over freq (1-based)
+    uint32_t total;
+
+    Model() { reset(); }
+    void reset()
+    {
+        for (int i = 0; i < kSymbols; ++i) freq[i] = 1;
+        rebuild();
+    }
+    void rebuild()
+    {
+        total = 0;
+        for (int i = 1; i <= kSymbols; ++i) tree[i] = 0;
+        for (int i = 0; i < kSymbols; ++i) {
+            total += freq[i];
+            for (int k = i + 1; k <= kSymbols; k += k & -k) tree[k] += freq[i];
+        }
+    }
+    uint32_t cum(int s) const   // sum of freq[0..s)
+    {
+        uint32_t r = 0;
+        for (int k = s; k > 0; k -= k & -k) r += tree[k];
+        return r;
+    }
+    void update(int s)
+    {
+        const uint32_t stale = total;   // CBAAC.py:34: tests self.total before recomputing
+        ++freq[s];
+        if (stale >= kMaxFreq) {
+            for (int i = 0; i < kSymbols; ++i) freq[i] = (freq[i] >> 1) + 1;
+            rebuild();
+        } else {
+            for (int k = s + 1; k <= kSymbols; k += k & -k) ++tree[k];
+            ++total;
+        }
+    }
+    // largest s with cum(s) <= v (v < total): CBAAC.py get_symbol_from_scaled_value
+    int find(uint32_t v, uint32_t &lo) const
+    {
+        int pos = 0;
+        uint32_t acc = 0;
+        for (int step = kSymbols; step > 0; step >>= 1) {
+            const int nxt = pos + step;
+            if (nxt <= kSymbols && acc + tree[nxt] <= v) {
+                pos = nxt;
+                acc += tree[nxt];
+            }
+        }
+        lo = acc;
+        return pos;   // symbol index (0-based) whose range contains v
+    }
+};
+
+class Contexts {
+  public:
+    explicit Contexts(int order) : order_(order)
+    {
+        if (order_ <= 1) flat_.resize(order_ == 0 ? 1 : kSymbols);
+    }
+    Model &get(uint64_t key)
+    {
+        if (order_ <= 1) return flat_[key];
+        auto it = map_.find(key);
+        if (it == map_.end()) it = map_.emplace(key, std::unique_ptr<Model>(new Model())).first;
+        return *it->second;
+    }
+    uint64_t push(uint64_t key, int s) const
+    {
+        if (order_ == 0) return 0;
+        const uint64_t mask = order_ >= 8 ? ~0ULL : ((1ULL << (8 * order_)) - 1);
+        return ((key << 8) | (uint64_t)s) & mask;
+    }
+
+  private:
+    int order_;
+    std::vector<Model> flat_;
+    std::unordered_map<uint64_t, std::unique_ptr<Model>> map_;
+};
+
+constexpr uint32_t kHalf = 0x80000000u, kQ1 = 0x40000000u, kQ3 = 0xC0000000u;
+
+struct BitWriter {
+    uint8_t *buf;
+    int64_t cap, nbits = 0;
+    bool overflow = false;
+    void put(int b)
+    {
+        const int64_t byte = nbits >> 3;
+        if (byte >= cap) {
+            overflow = true;
+            return;
+        }
+        if ((nbits & 7) == 0) buf[byte] = 0;
+        if (b) buf[byte] |= (uint8_t)(0x80u >> (nbits & 7));
+        ++nbits;
+    }
+};
+
+struct BitReader {
+    const uint8_t *buf;
+    int64_t nbits, pos = 0;
+    int get()
+    {
+        if (pos >= nbits) {
+            ++pos;
+            return 0;
+        }
+        const int b = (buf[pos >> 3] >> (7 - (pos & 7))) & 1;
+        ++pos;
+        return b;
+    }
+};
+
+}  // namespace
+}  // namespace vcf
+
+using namespace vcf;
+
+extern "C" {
+
+int64_t vcf_cbaac_bound(int64_t n_symbols)
+{
+    // each symbol narrows the interval by at most total/1 <= 2^15 -> <= 17 bits incl. carry-over
+    return n_symbols < 0 ? 0 : (n_symbols * 17 + 7) / 8 + 16;
+}
+
+int vcf_cbaac_encode(const uint8_t *symbols, int64_t n, int32_t order, uint8_t *out, int64_t out_capacity,
+                     int64_t *out_bytes, int64_t *out_bits)
+{
+    if (n < 0 || order < 0 || order > 8) return set_error(VCF_ERR_INVALID, "bad n or order (0..8)");
+    if ((n > 0 && !symbols) || !out || !out_bytes) return set_error(VCF_ERR_INVALID, "null buffer");
+    try {
+        Contexts ctx(order);
+        BitWriter bw{out, out_capacity};
+        uint32_t low = 0, high = 0xFFFFFFFFu;
+        uint64_t pending = 0, key = 0;
+        auto emit = [&](int b) {
+            bw.put(b);
+            for (; pending; --pending) bw.put(!b);
+        };
+        for (int64_t i = 0; i < n; ++i) {
+            const int s = symbols[i];
+            Model &m = ctx.get(key);
+            const uint32_t lo = m.cum(s), hi = lo + m.freq[s], tot = m.total;
+            const uint64_t range = (uint64_t)(high - low) + 1;
+            high = low + (uint32_t)((range * hi) / tot - 1);
+            low = low + (uint32_t)((range * lo) / tot);
+            for (;;) {
+                if (high < kHalf) {
+                    emit(0);
+                } else if (low >= kHalf) {
+                    emit(1);
+                    low -= kHalf;
+                    high -= kHalf;
+                } else if (low >= kQ1 && high < kQ3) {
+                    ++pending;
+                    low -= kQ1;
+                    high -= kQ1;
+                } else {
+                    break;
+                }
+                low <<= 1;
+                high = (high << 1) | 1u;
+            }
+            m.update(s);
+            key = ctx.push(key, s);
+            if (bw.overflow) return set_error(VCF_ERR_INVALID, "output buffer too small");
+        }
+        ++pending;   // flush
+        emit(low < kQ1 ? 0 : 1);
+        if (bw.overflow) return set_error(VCF_ERR_INVALID, "output buffer too small");
+        *out_bytes = (bw.nbits + 7) >> 3;
+        if (out_bits) *out_bits = bw.nbits;
+    } catch (const std::bad_alloc &) {
+        return set_error(VCF_ERR_INVALID, "out of host memory (context order %d)", order);
+    }
+    return VCF_OK;
+}
+
+int vcf_cbaac_decode(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t order, uint8_t *symbols_out)
+{
+    if (n < 0 || nbytes < 0 || order < 0 || order > 8) return set_error(VCF_ERR_INVALID, "bad arguments");
+    if ((n > 0 && !symbols_out) || (nbytes > 0 && !bytes)) return set_error(VCF_ERR_INVALID, "null buffer");
+    try {
+        Contexts ctx(order);
+        BitReader br{bytes, nbytes * 8};
+        uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
+        for (int k = 0; k < 32; ++k) value = (value << 1) | (uint32_t)br.get();
+        uint64_t key = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            Model &m = ctx.get(key);
+            const uint64_t range = (uint64_t)(high - low) + 1;
+            const uint32_t tot = m.total;
+            const uint64_t scaled = (((uint64_t)(value - low) + 1) * tot - 1) / range;
+            uint32_t lo;
+            const int s = m.find((uint32_t)scaled, lo);
+            const uint32_t hi = lo + m.freq[s];
+            high = low + (uint32_t)((range * hi) / tot - 1);
+            low = low + (uint32_t)((range * lo) / tot);
+            for (;;) {
+                if (high < kHalf) {
+                } else if (low >= kHalf) {
+                    low -= kHalf;
+                    high -= kHalf;
+                    value -= kHalf;
+                } else if (low >= kQ1 && high < kQ3) {
+                    low -= kQ1;
+                    high -= kQ1;
+                    value -= kQ1;
+                } else {
+                    break;
+                }
+                low <<= 1;
+                high = (high << 1) | 1u;
+                value = (value << 1) | (uint32_t)br.get();
+            }
+            symbols_out[i] = (uint8_t)s;
+            m.update(s);
+            key = ctx.push(key, s);
+        }
+    } catch (const std::bad_alloc &) {
+        return set_error(VCF_ERR_INVALID, "out of host memory (context order %d)", order);
+    }
+    return VCF_OK;
+}
+
+// The model alone, for parity tests: (low, high, total) handed to the coder
+// for every symbol (what CBAAC.py's _encode passes to encode_symbol).
+int vcf_cbaac_model_trace(const uint8_t *symbols, int64_t n, int32_t order, int32_t *triples)
+{
+    if (n < 0 || order < 0 || order > 8) return set_error(VCF_ERR_INVALID, "bad n or order");
+    if (n > 0 && (!symbols || !triples)) return set_error(VCF_ERR_INVALID, "null buffer");
+    Contexts ctx(order);
+    uint64_t key = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int s = symbols[i];
+        Model &m = ctx.get(key);
+        const uint32_t lo = m.cum(s);
+        triples[3 * i] = (int32_t)lo;
+        triples[3 * i + 1] = (int32_t)(lo + m.freq[s]);
+        triples[3 * i + 2] = (int32_t)m.total;
+        m.update(s);
+        key = ctx.push(key, s);
+    }
+    return VCF_OK;
+}
+
+}  // extern "C"
