@@ -137,3 +137,23 @@ def test_cli_iii_sequence(tmp_path):
         k = O.encode_frame(f, 32, 0)
         got = np.asarray(Image.open(f"/tmp/decoded_{i:04d}.png"))
         assert np.array_equal(got, O.decode_frame(k, 40, 56, 32, 0))
+
+
+@pytest.mark.parametrize("ec,ext", [("CBAAC", ".adpt_arith"), ("CBAHC", ".huf")])
+def test_dct_codec_with_context_coders(tmp_path, monkeypatch, ec, ext):
+    """2D-DCT -c CBAAC / -c CBAHC (config C2's entropy stage): the indices the
+    entropy decoder returns are the encoder's, so decode equals the oracle."""
+    from oracle import oracle as O
+    from vcf_amd.codec.dct2d import CoDec
+    monkeypatch.chdir(tmp_path)
+    rgb = np.random.Generator(np.random.PCG64(5)).integers(0, 256, (40, 48, 3), dtype=np.uint8)
+    src = _png(tmp_path / "o.png", rgb)
+    enc = str(tmp_path / "enc")
+    c = CoDec(_args("encode", ["-c", ec]))
+    assert c.file_extension == ext
+    c.encode_fn(src, enc)
+    assert os.path.exists(enc + ext)
+    dec = str(tmp_path / "d.png")
+    CoDec(_args("decode", ["-c", ec])).decode_fn(enc, dec)
+    k = O.encode_frame(rgb, 32, 0)
+    assert np.array_equal(np.asarray(Image.open(dec)), O.decode_frame(k, 40, 48, 32, 0))

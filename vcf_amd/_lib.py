@@ -51,7 +51,7 @@ _U32 = ctypes.c_uint32
 _PI32 = ctypes.POINTER(ctypes.c_int32)
 _PI = ctypes.POINTER(ctypes.c_int)
 
-# name -> argtypes (restype is int for all but vcf_last_error and vcf_cbaac_bound)
+# name -> argtypes (restype is int for all but vcf_last_error and the *_bound functions)
 SIGNATURES = {
     "vcf_version": [_PI, _PI],
     "vcf_device_count": [_PI],
@@ -86,6 +86,9 @@ SIGNATURES = {
     "vcf_cbaac_encode": [_P, _I64, _I32, _P, _I64, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     "vcf_cbaac_decode": [_P, _I64, _I64, _I32, _P],
     "vcf_cbaac_model_trace": [_P, _I64, _I32, _P],
+    "vcf_cbahc_bound": [_I64],
+    "vcf_cbahc_encode": [_P, _I64, _I32, _P, _I64, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
+    "vcf_cbahc_decode": [_P, _I64, _I64, _I32, _P],
     "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],
     "vcf_deadzone_dequantize": [_P, _I32, _I64, _I32, _P, _P],
 }
@@ -118,6 +121,7 @@ def lib():
             L.vcf_last_error.argtypes = []
             L.vcf_last_error.restype = ctypes.c_char_p
             L.vcf_cbaac_bound.restype = ctypes.c_int64
+            L.vcf_cbahc_bound.restype = ctypes.c_int64
             _lib = L
     return _lib
 

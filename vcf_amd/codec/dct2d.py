@@ -32,7 +32,12 @@ def _cbaac(args=None):
     return CBAACCodec(getattr(args, "order", 0) if args is not None else 0)
 
 
-ENTROPY_CODECS = {"TIFF": TIFFCodec, "CBAAC": _cbaac}
+def _cbahc(args=None):
+    from ..cbahc import CBAHCCodec
+    return CBAHCCodec(getattr(args, "order", 0) if args is not None else 0)
+
+
+ENTROPY_CODECS = {"TIFF": TIFFCodec, "CBAAC": _cbaac, "CBAHC": _cbahc}
 
 
 def register_entropy_codec(name, cls):
@@ -70,7 +75,7 @@ class CoDec(EICCoDec):
         if ec_name not in ENTROPY_CODECS:
             raise NotImplementedError(f"entropy codec {ec_name!r} (have: {sorted(ENTROPY_CODECS)})")
         maker = ENTROPY_CODECS[ec_name]
-        self.entropy = maker(args) if maker is _cbaac else maker()
+        self.entropy = maker(args) if maker in (_cbaac, _cbahc) else maker()
         self.file_extension = self.entropy.file_extension
         self.QSS = int(getattr(args, "QSS", 32))
         self.offset = 128            # 2D-DCT.py:102-105 (quantizer == deadzone)
