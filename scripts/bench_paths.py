@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Secondary measurements (one JSON line each), beside bench.py's headline:
+
+  dwt_encode / dwt_decode  4K 2D-DWT l=5 bior4.4 + deadzone (config C3), frames resident in HBM
+  dct_decode               4K DCT+deadzone decode (64 frames resident)
+  dct_encode_pcie          4K encode incl. host->device and device->host copies (pinned buffers)
+  cbaac / cbahc            host entropy coders on a 1080p k-array (config C2), symbols/s
+
+Usage: python scripts/bench_paths.py [--only name,name]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+
+import bench
+import vcf_amd._lib as L
+from vcf_amd.device import DeviceBuffer, Event, Stream, set_device
+
+HBM = 8000.0
+
+
+def timed(stream, fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    stream.synchronize()
+    e0, e1 = Event(), Event()
+    e0.record(stream)
+    for _ in range(steps):
+        fn()
+    e1.record(stream)
+    stream.synchronize()
+    return e0.elapsed_ms(e1) / steps
+
+
+def dwt(args):
+    import vcf_amd.dwt as DW
+    H, W, F, L_, Q = 2160, 3840, 8, 5, 32
+    w = DW.wavelet_index("bior4.4")
+    shapes, pb, wb = DW.layout(H, W, L_)
+    frames = np.stack([bench.synth_frame(H, W, s) for s in range(F)])
+    din, dpk, dws = DeviceBuffer.from_array(frames), DeviceBuffer(F * pb), DeviceBuffer(F * wb)
+    Ho, Wo = 2 * shapes[0][0], 2 * shapes[0][1]
+    dout = DeviceBuffer(F * Ho * Wo * 3)
+    s = Stream()
+    enc = lambda: L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, L_, Q, dpk.ptr, dws.ptr, s.handle)
+    dec = lambda: L.call("vcf_dwt_dz_decode", dpk.ptr, F, H, W, w, L_, Q, dout.ptr, dws.ptr, s.handle)
+    te = timed(s, enc, args.steps, 2)
+    td = timed(s, dec, args.steps, 2)
+    px = F * H * W
+    for name, t, alg in (("dwt_encode", te, F * (H * W * 3 + pb)), ("dwt_decode", td, F * (pb + Ho * Wo * 3))):
+        print(json.dumps({"metric": f"Mpixels/s {name} 4K l=5 bior4.4 Q=32", "value": round(px / t / 1e3, 1),
+                          "unit": "Mpixels/s", "ms_per_launch": round(t, 3), "frames_per_launch": F,
+                          "alg_GBps": round(alg / t / 1e6, 1), "frac_hbm_alg": round(alg / t / 1e6 / HBM, 4),
+                          "note": "fp64 separable passes through a workspace (traffic >> algorithmic)"}), flush=True)
+
+
+def dct_decode(args):
+    import vcf_amd.dct as D
+    H, W, F, Q = 2160, 3840, 64, 32
+    Hp, Wp = D.padded_shape(H, W)
+    frames = [bench.synth_frame(H, W, s) for s in range(4)]
+    din = DeviceBuffer(F * H * W * 3)
+    for f in range(F):
+        din.upload(frames[f % 4], offset=f * H * W * 3)
+    dk, dout = DeviceBuffer(F * Hp * Wp * 3), DeviceBuffer(F * H * W * 3)
+    s = Stream()
+    D.encode_device(din, F, H, W, Q, out=dk, stream=s)
+    t = timed(s, lambda: D.decode_device(dk, F, H, W, Q, out=dout, stream=s), args.steps, 3)
+    alg = F * (Hp * Wp * 3 + H * W * 3)
+    print(json.dumps({"metric": "Mpixels/s dct_decode 4K Q=32", "value": round(F * H * W / t / 1e3, 1),
+                      "unit": "Mpixels/s", "ms_per_launch": round(t, 4), "frames_per_launch": F,
+                      "alg_GBps": round(alg / t / 1e6, 1), "frac_hbm": round(alg / t / 1e6 / HBM, 4)}), flush=True)
+
+
+def dct_encode_pcie(args):
+    """Host frames in pinned memory -> HBM -> encode -> host, one stream, F frames per step."""
+    import vcf_amd.dct as D
+    H, W, F, Q = 2160, 3840, 16, 32
+    Hp, Wp = D.padded_shape(H, W)
+    nin, nout = F * H * W * 3, F * Hp * Wp * 3
+    hin, hout = ctypes.c_void_p(), ctypes.c_void_p()
+    L.call("vcf_host_alloc", ctypes.byref(hin), nin)
+    L.call("vcf_host_alloc", ctypes.byref(hout), nout)
+    src = np.ctypeslib.as_array((ctypes.c_uint8 * nin).from_address(hin.value))
+    src[:] = np.tile(bench.synth_frame(H, W, 0).ravel(), F)
+    din, dout = DeviceBuffer(nin), DeviceBuffer(nout)
+    s = Stream()
+
+    def step():
+        L.call("vcf_memcpy_htod", din.ptr, hin, nin, s.handle)
+        D.encode_device(din, F, H, W, Q, out=dout, stream=s)
+        L.call("vcf_memcpy_dtoh", hout, dout.ptr, nout, s.handle)
+
+    t = timed(s, step, args.steps, 2)
+    print(json.dumps({"metric": "Mpixels/s dct_encode 4K incl. H2D+D2H (pinned, one stream)",
+                      "value": round(F * H * W / t / 1e3, 1), "unit": "Mpixels/s", "ms_per_step": round(t, 3),
+                      "frames_per_step": F, "pcie_GBps": round((nin + nout) / t / 1e6, 1)}), flush=True)
+    L.call("vcf_host_free", hin)
+    L.call("vcf_host_free", hout)
+
+
+def entropy(args):
+    from vcf_amd import cbaac, cbahc
+    import vcf_amd.dct as D
+    rgb = bench.synth_frame(1080, 1920, 3)
+    k = D.encode(rgb, 32)          # the 1080p index array config C2 entropy-codes
+    sym = k.ravel()
+    for name, mod in (("cbaac", cbaac), ("cbahc", cbahc)):
+        for order in (0, 1):
+            n = sym.size if name == "cbaac" else min(sym.size, 1 << 20)
+            t0 = time.perf_counter()
+            out = mod.encode_symbols(sym[:n], order)
+            t1 = time.perf_counter()
+            nbytes = len(out) if isinstance(out, bytes) else len(out[0])
+            print(json.dumps({"metric": f"{name} order {order} encode (host, 1 thread)",
+                              "value": round(n / (t1 - t0) / 1e6, 2), "unit": "Msymbols/s",
+                              "symbols": n, "bits_per_symbol": round(8 * nbytes / n, 4),
+                              "sample": "1080p S-smooth frame, DCT+deadzone indices (config C2)"}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--only", default="dwt,dct_decode,dct_encode_pcie,entropy")
+    args = ap.parse_args()
+    set_device(0)
+    for name in args.only.split(","):
+        globals()[name](args)
+
+
+if __name__ == "__main__":
+    main()
