@@ -34,7 +34,7 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(HERE, "vcf_oracle.c"), os.path.join(HERE, "vcf_dwt_oracle.cpp")]
+        srcs = [os.path.join(HERE, f) for f in ("vcf_oracle.c", "vcf_dwt_oracle.cpp", "vcf_ipp_oracle.c")]
         if not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(f) for f in srcs):
             build()
         L = ctypes.CDLL(LIB_PATH)
@@ -63,6 +63,11 @@ def lib():
                                          ctypes.c_int, u16p, u8p]
         L.vcfo_dwt_dz_decode.argtypes = [u16p, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, u8p]
+        # IPP temporal tools (vcf_ipp_oracle.c)
+        L.vcfo_ipp_gray.argtypes = [u8p, ctypes.c_int64, u8p]
+        L.vcfo_ipp_block_match.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, fp]
+        L.vcfo_ipp_mc.argtypes = [u8p, fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p]
         _lib = L
     return _lib
 
@@ -248,3 +253,40 @@ def dwt_decode_frame(subbands, H: int, W: int, wavelet: str = "db5", levels: int
     if rc != 0:
         raise RuntimeError("oracle dwt decode failed")
     return out
+
+
+# ---- IPP (src/IPP_DCT.py; vcf_ipp_oracle.c) ----
+
+def ipp_gray(rgb: np.ndarray) -> np.ndarray:
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    out = np.empty(rgb.shape[:2], np.uint8)
+    lib().vcfo_ipp_gray(_u8(rgb), rgb.shape[0] * rgb.shape[1], _u8(out))
+    return out
+
+
+def ipp_block_matching(ref, cur, bs=16, sr=8, fast=False) -> np.ndarray:
+    ref, cur = np.ascontiguousarray(ref, np.uint8), np.ascontiguousarray(cur, np.uint8)
+    H, W = ref.shape[:2]
+    mv = np.zeros((H // bs, W // bs, 2), np.float32)
+    lib().vcfo_ipp_block_match(_u8(ref), _u8(cur), H, W, bs, sr, int(bool(fast)),
+                               mv.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    return mv
+
+
+def ipp_motion_compensate(frame, mv, bs=16) -> np.ndarray:
+    frame = np.ascontiguousarray(frame, np.uint8)
+    mv = np.ascontiguousarray(mv, np.float32)
+    out = np.empty_like(frame)
+    H, W = frame.shape[:2]
+    lib().vcfo_ipp_mc(_u8(frame), mv.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), H, W, bs, _u8(out))
+    return out
+
+
+def ipp_residual(cur, comp) -> np.ndarray:
+    """IPP_DCT.py:547-551."""
+    return np.clip(cur.astype(np.int16) - comp.astype(np.int16) + 128, 0, 255).astype(np.uint8)
+
+
+def ipp_reconstruct(comp, rec) -> np.ndarray:
+    """IPP_DCT.py:559-561."""
+    return np.clip(comp.astype(np.int16) + rec.astype(np.int16) - 128, 0, 255).astype(np.uint8)

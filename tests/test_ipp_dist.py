@@ -1,0 +1,81 @@
+"""IPP GOP sharding on the CPU: a world_size-2 gloo job encodes its GOPs and
+rank 0 gathers per-frame sizes and motion fields into the metadata; the
+result must equal the single-rank run's.  The GPU tools
+and the spatial codec are replaced by the oracle here -- they are covered by
+tests/test_ipp_gpu.py; this checks the driver around them."""
+import json
+import os
+import socket
+import types
+
+import numpy as np
+
+
+def _frames(n, H=48, W=64, seed=2):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    base = np.kron(rng.integers(0, 256, (H // 4 + 8, W // 4 + 8, 3)), np.ones((4, 4, 1)))
+    return np.stack([np.clip(base[t % 5:t % 5 + H, (2 * t) % 7:(2 * t) % 7 + W], 0, 255).astype(np.uint8)
+                     for t in range(n)])
+
+
+def _codec(prefix, src, n, gop, group=None):
+    from oracle import oracle as O
+    import vcf_amd.codec.ipp as M
+    from vcf_amd.codec import parser as P
+    M.K = types.SimpleNamespace(block_matching=O.ipp_block_matching, motion_compensate=O.ipp_motion_compensate,
+                                residual=O.ipp_residual, reconstruct=O.ipp_reconstruct)
+
+    class StandIn(M.CoDec):
+        def encode_decode_proxy(self, img, frame_type, seq_idx):
+            H, W = img.shape[:2]
+            rec = O.decode_frame(O.encode_frame(img, 32), H, W, 32)
+            return rec, 1000 * (frame_type == "I") + 10 * seq_idx + int(rec.sum() % 7)
+
+    args = P.parse(P.ipp_parser(), ["encode", "-i", src, "-O", prefix, "-N", str(n), "-G", str(gop)])
+    return StandIn(args, group=group)
+
+
+def _worker(rank, world, port, tmp, n, gop, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from vcf_amd.codec import shard
+    try:
+        g = shard.Group("gloo")
+        total = _codec(os.path.join(tmp, "dist", "v"), os.path.join(tmp, "frames.npy"), n, gop, g).encode()
+        q.put((rank, total))
+        g.close()
+    except Exception as e:
+        q.put((rank, "error", repr(e)))
+
+
+def test_ipp_two_ranks_gloo_equals_one_rank(tmp_path):
+    import torch.multiprocessing as mp
+    n, gop, world = 9, 3, 2
+    np.save(tmp_path / "frames.npy", _frames(n))
+    single = _codec(str(tmp_path / "one" / "v"), str(tmp_path / "frames.npy"), n, gop).encode()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), n, gop, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r) for r in (q.get(timeout=180) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] != "error" for r in res.values()), res
+    assert res[1][1] is None
+    m1 = json.load(open(tmp_path / "one" / "v_meta.json"))
+    m2 = json.load(open(tmp_path / "dist" / "v_meta.json"))
+    for k in ("n_frames", "gop_size", "I_info", "P_info", "width", "height"):
+        assert m1[k] == m2[k], k
+    assert len(m1["I_info"]) == 3 and len(m1["P_info"]) == 6 and m1["I_info"][2]["idx"] == 6
+    with np.load(tmp_path / "one" / "v_mv.npz") as a, np.load(tmp_path / "dist" / "v_mv.npz") as b:
+        assert np.array_equal(a["mv_f32"], b["mv_f32"]) and a["mv_f32"].shape == (6, 3, 4, 2)
+    # single run's total includes its own mv.npz size; the P/I sums agree
+    assert single - os.path.getsize(tmp_path / "one" / "v_mv.npz") * 8 == \
+        res[0][1] - os.path.getsize(tmp_path / "dist" / "v_mv.npz") * 8
+    for i in range(n):
+        assert os.path.exists(tmp_path / "dist" / f"v_O_{i:04d}.png")

@@ -13,7 +13,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libvcf_amd.so")
-SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_quant.hip", "vcf_dwt.hip", "vcf_cbaac.cpp", "vcf_cbahc.cpp"]
+SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_quant.hip", "vcf_dwt.hip", "vcf_cbaac.cpp", "vcf_cbahc.cpp", "vcf_ipp.hip"]
 HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h", "vcf_wavelets.h"]
 ARCH = os.environ.get("VCF_OFFLOAD_ARCH", "gfx950")
 

@@ -189,3 +189,50 @@ def iii_parser(description: str = "III coding: runs a 2D image codec for each im
 def parse(parser, argv=None):
     """parser.parse_known_args()[0] as main.py:9 does."""
     return parser.parse_known_args(argv)[0]
+
+
+def add_ipp(enc, dec):
+    """IPP_DCT.py:45-130 (the --st pre-parser and the temporal options)."""
+    for p in (enc, dec):
+        p.add_argument("--st", dest="space_transform", type=str, default="2D-DCT",
+                       help="Spatial transform codec (default: 2D-DCT)")
+    enc.add_argument("-i", "--input", type=str, default=IPP_INPUT, help=f"Input video (default: {IPP_INPUT})")
+    enc.add_argument("-O", "--output", type=str, default=IPP_OUTPUT, help=f"Output prefix (default: {IPP_OUTPUT})")
+    enc.add_argument("-N", "--number_of_frames", type=int, default=IPP_N_FRAMES,
+                     help=f"Number of frames to encode (default: {IPP_N_FRAMES})")
+    enc.add_argument("-G", "--gop_size", type=int, default=IPP_GOP, help=f"GOP size for IPP pattern (default: {IPP_GOP})")
+    enc.add_argument("-M", "--block_size_ME", type=int, default=IPP_BLOCK_ME,
+                     help=f"Motion estimation block size (default: {IPP_BLOCK_ME})")
+    enc.add_argument("-S", "--search_range", type=int, default=IPP_SEARCH,
+                     help=f"Search range in pixels (default: {IPP_SEARCH})")
+    enc.add_argument("--fast", action="store_true", help="Use fast motion estimation (3-step search)")
+    enc.add_argument("--threads", type=int, default=0, help="Number of threads (0=auto, default: 0)")
+    enc.add_argument("-R", "--rdo_lambda", type=float, default=0.0,
+                     help="RDO lambda for IPP block mode decision (default: 0.0)")
+    dec.add_argument("-i", "--input", type=str, default=IPP_OUTPUT, help=f"Input prefix (default: {IPP_OUTPUT})")
+    dec.add_argument("-O", "--output", type=str, default="./ipp_decoded", help="Output prefix (default: ./ipp_decoded)")
+    dec.add_argument("-N", "--number_of_frames", type=int, default=IPP_N_FRAMES,
+                     help=f"Number of frames (default: {IPP_N_FRAMES})")
+    dec.add_argument("-G", "--gop_size", type=int, help="GOP size for IPP pattern")
+    dec.add_argument("-M", "--block_size_ME", type=int, help="Motion estimation block size")
+    dec.add_argument("-S", "--search_range", type=int, help="Search range in pixels")
+
+
+IPP_INPUT = "http://www.hpca.ual.es/~vruiz/videos/mobile_352x288x30x420x300.mp4"   # IPP_DCT.py:36
+IPP_OUTPUT = "./ipp_encoded"
+IPP_N_FRAMES = 30
+IPP_GOP = 10
+IPP_BLOCK_ME = 16
+IPP_SEARCH = 8
+
+
+def ipp_parser(description: str = "IPP hybrid video coding using motion compensation and DCT."):
+    """`python IPP_DCT.py ...` over the default 2D-DCT chain."""
+    p, enc, dec = base_parser(description)
+    add_dct(enc, dec)
+    add_ycocg(enc, dec)
+    add_deadzone(enc, dec)
+    add_filter(enc, dec)
+    add_eic(enc, dec)
+    add_ipp(enc, dec)
+    return p

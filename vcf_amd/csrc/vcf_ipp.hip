@@ -1,0 +1,263 @@
+// vcf_ipp.hip -- the IPP temporal tools of src/IPP_DCT.py on gfx950:
+// luma conversion, block matching (full search and --fast three-step search),
+// motion compensation, residual and reconstruction; vcf_ipp_* of the C ABI.
+//
+// Bit-exact with the reference's own functions (tests/golden/make_golden_ipp.py
+// runs them unmodified):
+//   IPP.block_matching (:344-376): cv2 RGB2GRAY (assumption A10: OpenCV's
+//     8-bit fixed point (4899 R + 9617 G + 1868 B + 8192) >> 14), then per
+//     bs x bs block of the full-block area a motion vector (dx, dy);
+//   _process_block_row full search (:207-246): dy outer, dx inner over
+//     [-S, S], in-bounds candidates only, SAD in int16, the first strict
+//     minimum wins -> argmin of (SAD, scan index);
+//   _three_step_search (:159-204): serial, the centre moves inside the
+//     8-neighbour loop; one wave per block evaluates the candidates in order;
+//   IPP.motion_compensate (:378-395): block copy, out-of-bounds vectors fall
+//     back to the co-located block, outside the full-block area zeros;
+//   residual (:547-551): clip(cur - comp + 128, 0, 255) as uint8;
+//   reconstruction (:559-561, :788-790): clip(comp + rec - 128, 0, 255).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "vcf_amd.h"
+#include "vcf_internal.h"
+
+namespace vcf {
+namespace {
+
+constexpr int kMaxBs = 64;
+constexpr int kMaxSr = 32;
+
+__device__ __forceinline__ uint32_t luma(const uint8_t *p)
+{
+    return (4899u * p[0] + 9617u * p[1] + 1868u * p[2] + 8192u) >> 14;
+}
+
+__global__ __launch_bounds__(256) void ipp_gray_kernel(const uint8_t *__restrict__ rgb, uint8_t *__restrict__ gray,
+                                                       long long npx)
+{
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < npx) gray[p] = (uint8_t)luma(rgb + 3 * p);
+}
+
+// Full search: one workgroup per block; the block and its search window in
+// LDS (window rows/cols clipped to the frame; out-of-frame candidates are
+// skipped exactly as the reference skips them).
+__global__ __launch_bounds__(256) void ipp_full_search_kernel(const uint8_t *__restrict__ ref,
+                                                              const uint8_t *__restrict__ cur, int H, int W,
+                                                              int bs, int sr, float *__restrict__ mv)
+{
+    __shared__ uint8_t cb[kMaxBs * kMaxBs];
+    __shared__ uint8_t win[(kMaxBs + 2 * kMaxSr) * (kMaxBs + 2 * kMaxSr)];
+    __shared__ unsigned long long best[4];
+    const int bx = blockIdx.x, by = blockIdx.y;
+    const int i = by * bs, j = bx * bs;
+    const int ws = bs + 2 * sr;
+    for (int t = threadIdx.x; t < bs * bs; t += blockDim.x) cb[t] = cur[(long long)(i + t / bs) * W + j + t % bs];
+    for (int t = threadIdx.x; t < ws * ws; t += blockDim.x) {
+        const int y = i - sr + t / ws, x = j - sr + t % ws;
+        win[t] = (y >= 0 && y < H && x >= 0 && x < W) ? ref[(long long)y * W + x] : 0;
+    }
+    __syncthreads();
+    const int side = 2 * sr + 1, ncand = side * side;
+    unsigned long long key = ~0ULL;
+    for (int c = threadIdx.x; c < ncand; c += blockDim.x) {
+        const int dy = c / side - sr, dx = c % side - sr;
+        const int ry = i + dy, rx = j + dx;
+        if (ry < 0 || ry + bs > H || rx < 0 || rx + bs > W) continue;
+        uint32_t sad = 0;
+        const uint8_t *w0 = win + (dy + sr) * ws + (dx + sr);
+        for (int y = 0; y < bs; ++y) {
+            const uint8_t *a = cb + y * bs, *b = w0 + y * ws;
+            int x = 0;
+            for (; x + 4 <= bs; x += 4) {
+                const uint32_t av = a[x] | (a[x + 1] << 8) | (a[x + 2] << 16) | ((uint32_t)a[x + 3] << 24);
+                const uint32_t bv = b[x] | (b[x + 1] << 8) | (b[x + 2] << 16) | ((uint32_t)b[x + 3] << 24);
+                sad = __builtin_amdgcn_sad_u8(av, bv, sad);
+            }
+            for (; x < bs; ++x) sad += (uint32_t)abs((int)a[x] - (int)b[x]);
+        }
+        const unsigned long long k = ((unsigned long long)sad << 20) | (unsigned long long)c;
+        key = k < key ? k : key;
+    }
+    // workgroup argmin of (SAD, scan index)
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(key, off, 64);
+        key = o < key ? o : key;
+    }
+    if ((threadIdx.x & 63) == 0) best[threadIdx.x >> 6] = key;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long k = best[0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) k = best[w] < k ? best[w] : k;
+        float dxv = 0.f, dyv = 0.f;   // no valid candidate cannot happen (0,0 is in bounds)
+        if (k != ~0ULL) {
+            const int c = (int)(k & 0xFFFFF);
+            dyv = (float)(c / side - sr);
+            dxv = (float)(c % side - sr);
+        }
+        float *m = mv + ((long long)by * gridDim.x + bx) * 2;
+        m[0] = dxv;
+        m[1] = dyv;
+    }
+}
+
+// SAD of the block at (i, j) against the reference at (ry, rx), one wave
+__device__ uint32_t wave_sad(const uint8_t *cb, const uint8_t *ref, int W, int bs, int ry, int rx)
+{
+    uint32_t s = 0;
+    for (int t = threadIdx.x; t < bs * bs; t += 64) {
+        const int y = t / bs, x = t % bs;
+        s += (uint32_t)abs((int)cb[t] - (int)ref[(long long)(ry + y) * W + rx + x]);
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    return s;
+}
+
+// Three-step search (--fast): one wave per block, the candidates in the
+// reference's order because an improvement moves the centre immediately.
+__global__ __launch_bounds__(64) void ipp_tss_kernel(const uint8_t *__restrict__ ref, const uint8_t *__restrict__ cur,
+                                                     int H, int W, int bs, int sr, float *__restrict__ mv)
+{
+    __shared__ uint8_t cb[kMaxBs * kMaxBs];
+    const int bx = blockIdx.x, by = blockIdx.y;
+    const int i = by * bs, j = bx * bs;
+    for (int t = threadIdx.x; t < bs * bs; t += 64) cb[t] = cur[(long long)(i + t / bs) * W + j + t % bs];
+    __syncthreads();
+    int step = sr / 2, cx = j, cy = i, bxv = 0, byv = 0;
+    uint32_t best = wave_sad(cb, ref, W, bs, i, j);   // the block itself is always in bounds
+    // a candidate may only improve on a finite minimum; the centre check ran, so min is finite
+    while (step >= 1) {
+        bool improved = false;
+        for (int a = -1; a <= 1; ++a)
+            for (int b = -1; b <= 1; ++b) {
+                if (a == 0 && b == 0) continue;
+                const int ry = cy + a * step, rx = cx + b * step;
+                if (ry < 0 || ry + bs > H || rx < 0 || rx + bs > W) continue;
+                const uint32_t s = wave_sad(cb, ref, W, bs, ry, rx);
+                if (s < best) {
+                    best = s;
+                    bxv = rx - j;
+                    byv = ry - i;
+                    cx = rx;
+                    cy = ry;
+                    improved = true;
+                }
+            }
+        step = improved ? (step / 2 > 1 ? step / 2 : 1) : step / 2;
+    }
+    if (threadIdx.x == 0) {
+        float *m = mv + ((long long)by * gridDim.x + bx) * 2;
+        m[0] = (float)bxv;
+        m[1] = (float)byv;
+    }
+}
+
+__global__ __launch_bounds__(256) void ipp_mc_kernel(const uint8_t *__restrict__ ref, const float *__restrict__ mv,
+                                                     int H, int W, int bs, uint8_t *__restrict__ out)
+{
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (long long)H * W) return;
+    const int y = (int)(p / W), x = (int)(p % W);
+    const int nbx = W / bs, nby = H / bs;
+    const int by = y / bs, bx = x / bs;
+    uint8_t *o = out + p * 3;
+    if (by >= nby || bx >= nbx) {   // outside the full-block area: np.zeros_like
+        o[0] = o[1] = o[2] = 0;
+        return;
+    }
+    const float *m = mv + ((long long)by * nbx + bx) * 2;
+    const int i = by * bs, j = bx * bs;
+    int ry = (int)((float)i + m[1]), rx = (int)((float)j + m[0]);   // int(i + mv[1]) on float32
+    if (!(ry >= 0 && ry + bs <= H && rx >= 0 && rx + bs <= W)) {
+        ry = i;
+        rx = j;
+    }
+    const uint8_t *s = ref + ((long long)(ry + (y - i)) * W + rx + (x - j)) * 3;
+    o[0] = s[0];
+    o[1] = s[1];
+    o[2] = s[2];
+}
+
+__global__ __launch_bounds__(256) void ipp_residual_kernel(const uint8_t *__restrict__ cur,
+                                                           const uint8_t *__restrict__ comp, long long n,
+                                                           uint8_t *__restrict__ out)
+{
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int v = (int)cur[p] - (int)comp[p] + 128;
+    out[p] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+__global__ __launch_bounds__(256) void ipp_recon_kernel(const uint8_t *__restrict__ comp,
+                                                        const uint8_t *__restrict__ rec, long long n,
+                                                        uint8_t *__restrict__ out)
+{
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int v = (int)comp[p] + (int)rec[p] - 128;
+    out[p] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+unsigned blocks_for(long long n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+}  // namespace vcf
+
+using namespace vcf;
+
+extern "C" {
+
+int vcf_ipp_block_match(const uint8_t *ref_rgb_dev, const uint8_t *cur_rgb_dev, int32_t H, int32_t W, int32_t bs,
+                        int32_t sr, int32_t fast, float *mv_dev, uint8_t *gray_workspace_dev, void *stream)
+{
+    if (!ref_rgb_dev || !cur_rgb_dev || !mv_dev || !gray_workspace_dev) return set_error(VCF_ERR_INVALID, "null buffer");
+    if (H <= 0 || W <= 0) return set_error(VCF_ERR_INVALID, "bad frame shape");
+    if (bs < 1 || bs > kMaxBs) return set_error(VCF_ERR_UNSUPPORTED, "block size %d (1..%d)", bs, kMaxBs);
+    if (sr < 0 || sr > kMaxSr) return set_error(VCF_ERR_UNSUPPORTED, "search range %d (0..%d)", sr, kMaxSr);
+    const int nbx = W / bs, nby = H / bs;
+    if (nbx == 0 || nby == 0) return VCF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const long long npx = (long long)H * W;
+    uint8_t *rg = gray_workspace_dev, *cg = gray_workspace_dev + npx;
+    hipLaunchKernelGGL(ipp_gray_kernel, dim3(blocks_for(npx)), dim3(256), 0, s, ref_rgb_dev, rg, npx);
+    hipLaunchKernelGGL(ipp_gray_kernel, dim3(blocks_for(npx)), dim3(256), 0, s, cur_rgb_dev, cg, npx);
+    if (fast)
+        hipLaunchKernelGGL(ipp_tss_kernel, dim3(nbx, nby), dim3(64), 0, s, rg, cg, H, W, bs, sr, mv_dev);
+    else
+        hipLaunchKernelGGL(ipp_full_search_kernel, dim3(nbx, nby), dim3(256), 0, s, rg, cg, H, W, bs, sr, mv_dev);
+    return hip_check(hipGetLastError(), "ipp block match launch");
+}
+
+int vcf_ipp_motion_compensate(const uint8_t *ref_rgb_dev, const float *mv_dev, int32_t H, int32_t W, int32_t bs,
+                              uint8_t *out_rgb_dev, void *stream)
+{
+    if (!ref_rgb_dev || !mv_dev || !out_rgb_dev) return set_error(VCF_ERR_INVALID, "null buffer");
+    if (H <= 0 || W <= 0 || bs < 1) return set_error(VCF_ERR_INVALID, "bad arguments");
+    const long long npx = (long long)H * W;
+    hipLaunchKernelGGL(ipp_mc_kernel, dim3(blocks_for(npx)), dim3(256), 0, (hipStream_t)stream, ref_rgb_dev, mv_dev,
+                       H, W, bs, out_rgb_dev);
+    return hip_check(hipGetLastError(), "ipp mc launch");
+}
+
+int vcf_ipp_residual(const uint8_t *cur_dev, const uint8_t *comp_dev, int64_t n, uint8_t *out_dev, void *stream)
+{
+    if (n < 0 || (n > 0 && (!cur_dev || !comp_dev || !out_dev))) return set_error(VCF_ERR_INVALID, "bad arguments");
+    if (n == 0) return VCF_OK;
+    hipLaunchKernelGGL(ipp_residual_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, cur_dev, comp_dev,
+                       (long long)n, out_dev);
+    return hip_check(hipGetLastError(), "ipp residual launch");
+}
+
+int vcf_ipp_reconstruct(const uint8_t *comp_dev, const uint8_t *rec_dev, int64_t n, uint8_t *out_dev, void *stream)
+{
+    if (n < 0 || (n > 0 && (!comp_dev || !rec_dev || !out_dev))) return set_error(VCF_ERR_INVALID, "bad arguments");
+    if (n == 0) return VCF_OK;
+    hipLaunchKernelGGL(ipp_recon_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, comp_dev, rec_dev,
+                       (long long)n, out_dev);
+    return hip_check(hipGetLastError(), "ipp recon launch");
+}
+
+}  // extern "C"
