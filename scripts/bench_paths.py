@@ -48,16 +48,19 @@ def dwt(args):
     Ho, Wo = 2 * shapes[0][0], 2 * shapes[0][1]
     dout = DeviceBuffer(F * Ho * Wo * 3)
     s = Stream()
-    enc = lambda: L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, L_, Q, dpk.ptr, dws.ptr, s.handle)
-    dec = lambda: L.call("vcf_dwt_dz_decode", dpk.ptr, F, H, W, w, L_, Q, dout.ptr, dws.ptr, s.handle)
-    te = timed(s, enc, args.steps, 2)
-    td = timed(s, dec, args.steps, 2)
     px = F * H * W
-    for name, t, alg in (("dwt_encode", te, F * (H * W * 3 + pb)), ("dwt_decode", td, F * (pb + Ho * Wo * 3))):
-        print(json.dumps({"metric": f"Mpixels/s {name} 4K l=5 bior4.4 Q=32", "value": round(px / t / 1e3, 1),
-                          "unit": "Mpixels/s", "ms_per_launch": round(t, 3), "frames_per_launch": F,
-                          "alg_GBps": round(alg / t / 1e6, 1), "frac_hbm_alg": round(alg / t / 1e6 / HBM, 4),
-                          "note": "fp64 separable passes through a workspace (traffic >> algorithmic)"}), flush=True)
+    for variant, vname in ((1, "fused level kernels"), (2, "separable kernels")):
+        enc = lambda: L.call("vcf_dwt_dz_encode_variant", variant, din.ptr, F, H, W, w, L_, Q, dpk.ptr, dws.ptr,
+                             s.handle)
+        dec = lambda: L.call("vcf_dwt_dz_decode_variant", variant, dpk.ptr, F, H, W, w, L_, Q, dout.ptr, dws.ptr,
+                             s.handle)
+        te = timed(s, enc, args.steps, 2)
+        td = timed(s, dec, args.steps, 2)
+        for name, t, alg in (("dwt_encode", te, F * (H * W * 3 + pb)), ("dwt_decode", td, F * (pb + Ho * Wo * 3))):
+            print(json.dumps({"metric": f"Mpixels/s {name} 4K l=5 bior4.4 Q=32", "variant": vname,
+                              "value": round(px / t / 1e3, 1), "unit": "Mpixels/s", "ms_per_launch": round(t, 3),
+                              "frames_per_launch": F, "alg_GBps": round(alg / t / 1e6, 1),
+                              "frac_hbm_alg": round(alg / t / 1e6 / HBM, 4)}), flush=True)
 
 
 def dct_decode(args):

@@ -32,14 +32,20 @@ def test_dwt_encode_decode_vs_reference(case):
     assert np.array_equal(out, d["decoded"])
 
 
-@pytest.mark.parametrize("wavelet", ["db5", "bior4.4", "haar", "sym4", "coif2", "db10"])
-@pytest.mark.parametrize("H,W,L,Q", [(96, 128, 3, 32), (67, 45, 2, 7), (256, 160, 5, 16), (8, 10, 1, 1)])
-def test_dwt_vs_oracle(wavelet, H, W, L, Q):
+@pytest.mark.parametrize("variant", [1, 2], ids=["fused", "separable"])
+@pytest.mark.parametrize("wavelet", ["db5", "bior4.4", "haar", "sym4", "coif2", "db9", "db10"])
+@pytest.mark.parametrize("H,W,L,Q", [(96, 128, 3, 32), (67, 45, 2, 7), (256, 160, 5, 16), (8, 10, 1, 1),
+                                     (141, 301, 4, 3), (17, 200, 3, 32)])
+def test_dwt_vs_oracle(wavelet, H, W, L, Q, variant):
     import vcf_amd.dwt as DW
     shapes = O.dwt_shapes(H, W, L)
     rng = np.random.Generator(np.random.PCG64(H * W + L))
     frames = rng.integers(0, 256, (2, H, W, 3), dtype=np.uint8)
-    got = DW.encode(frames, wavelet, L, Q)
+    if variant == 1 and wavelet == "db10":      # 20 taps: the fused tile exceeds 64 KB of LDS
+        with pytest.raises(NotImplementedError):
+            DW.encode(frames, wavelet, L, Q, variant=1)
+        return
+    got = DW.encode(frames, wavelet, L, Q, variant=variant)
     for f in range(2):
         ref = O.dwt_encode_frame(frames[f], wavelet, L, Q)
         for name, arr in ref.items():
@@ -49,9 +55,37 @@ def test_dwt_vs_oracle(wavelet, H, W, L, Q):
         with pytest.raises(NotImplementedError):
             DW.decode(got[0], H, W, wavelet, L, Q)
         return
-    out = DW.decode(got, H, W, wavelet, L, Q)
+    out = DW.decode(got, H, W, wavelet, L, Q, variant=variant)
     for f in range(2):
         assert np.array_equal(out[f], O.dwt_decode_frame(got[f], H, W, wavelet, L, Q))
+
+
+@pytest.mark.parametrize("wavelet", ["bior4.4", "db5"])
+def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
+    """Config C3 size: the fused and separable kernels agree on whole 4K frames, and frame 0 equals the oracle."""
+    import vcf_amd.dwt as DW
+    H, W, L, Q = 2160, 3840, 5, 32
+    y, x = np.mgrid[0:H, 0:W]
+    base = np.stack([128 + 60 * np.sin(x / 97 + c) + 50 * np.cos(y / 61 - c) for c in range(3)], -1)
+    rng = np.random.Generator(np.random.PCG64(5))
+    frames = np.stack([np.clip(base + rng.normal(0, 4, base.shape), 0, 255).astype(np.uint8) for _ in range(2)])
+    a = DW.encode(frames, wavelet, L, Q, variant=1)
+    b = DW.encode(frames, wavelet, L, Q, variant=2)
+    ref = O.dwt_encode_frame(frames[0], wavelet, L, Q)
+    for name in ref:
+        assert np.array_equal(a[0][name], ref[name]), name
+        assert np.array_equal(a[1][name], b[1][name]), name
+    da = DW.decode(a, H, W, wavelet, L, Q, variant=1)
+    db = DW.decode(a, H, W, wavelet, L, Q, variant=2)
+    assert np.array_equal(da, db)
+    assert np.array_equal(da[0], O.dwt_decode_frame(a[0], H, W, wavelet, L, Q))
+    assert np.abs(da.astype(int) - frames.astype(int)).mean() < 8     # a sane reconstruction
+
+
+def test_dwt_unknown_variant():
+    import vcf_amd.dwt as DW
+    with pytest.raises(ValueError):
+        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=7)
 
 
 def test_dwt_errors():

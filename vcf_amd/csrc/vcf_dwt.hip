@@ -303,6 +303,483 @@ __global__ __launch_bounds__(256) void dwt_to_rgb_kernel(const double *__restric
 }
 
 // ---------------------------------------------------------------------------
+// fused level kernels (variant 1, the default when the tile fits in LDS)
+// ---------------------------------------------------------------------------
+// One launch per level.  A workgroup owns a tile of a level's outputs, stages
+// the input samples it needs (halo included, wrapped at load time) in LDS,
+// runs both separable passes there and writes only the level's products:
+// forward, the three quantized detail subbands (packed bytes) and LL (float64
+// plane for the next level, or u16 at the last); inverse, the next level's
+// float64 plane trimmed to what that level reads, or RGB at level 1.  The
+// column-pass planes of the separable kernels never touch HBM.
+//
+// Every output sums its taps in exactly the order of dwt_tap_sum / idwt_out
+// above: the tile holds samples at *logical* positions (before the periodic
+// wrap), so only the index arithmetic differs.
+constexpr int kFTH = 8;              // forward: output rows per tile
+constexpr int kFIW = 128;            // forward: staged input columns, 2 (tw - 1) + F
+constexpr int kITH = 16, kITW = 64;  // inverse: output tile (level samples)
+constexpr int kG = 4;                // outputs per work item (register window)
+constexpr int kMaxFastF = 18;        // longest filter with a compiled fast path
+
+__host__ __device__ constexpr int fwd_tile_w(int F) { return (kFIW - F) / 2 + 1; }
+
+// forward 'per' wrap of a logical sample position (odd N: extended by x[N-1])
+__device__ __forceinline__ int per_wrap(int p, int N)
+{
+    const int Ne = N + (N & 1);
+    p %= Ne;
+    if (p < 0) p += Ne;
+    return p < N ? p : N - 1;
+}
+
+__device__ __forceinline__ int mod_pos(int p, int N)
+{
+    p %= N;
+    return p < 0 ? p + N : p;
+}
+
+// dwt_tap_sum with the load taking the logical position i - m
+template <typename Load>
+__device__ __forceinline__ double dwt_tap_sum_logical(const double *__restrict__ f, int F, int N, int i, Load &&load)
+{
+    double s = 0.0;
+    if (i >= N) {
+        for (int m = F - 1; m >= 0; --m)
+            if (i - m >= N) s = s + f[m] * load(i - m);
+        for (int m = 0; m < F; ++m)
+            if (i - m < N) s = s + f[m] * load(i - m);
+    } else {
+        for (int m = 0; m < F; ++m) s = s + f[m] * load(i - m);
+    }
+    return s;
+}
+
+// idwt_out with the loads taking the logical input position ii - j
+template <typename LoadA, typename LoadD>
+__device__ __forceinline__ double idwt_out_logical(const double *__restrict__ lo, const double *__restrict__ hi,
+                                                   int F, int N, int n, LoadA &&la, LoadD &&ld)
+{
+    const int F2 = F / 2, T = F2 / 2;
+    const int qq = n + F2 - 1;            // n - shift, >= 0
+    const int q = qq % (2 * N);
+    const int p = q & 1, i = q >> 1, ii = qq >> 1;
+    const int top = i < F2 - 1 ? i : F2 - 1;
+    double s = 0.0;
+    for (int pass = 0; pass < 2; ++pass) {
+        const double *f = pass ? hi : lo;
+        for (int t = 0; t < F2; ++t) {
+            const int j = (i < T) ? (t <= top ? top - t : t) : t;
+            const double c = pass ? ld(ii - j) : la(ii - j);
+            s = s + f[2 * j + p] * c;
+        }
+    }
+    return s;
+}
+
+// filter taps by value: kernel arguments, i.e. scalar registers
+template <int F>
+struct Taps {
+    double lo[F], hi[F];
+};
+
+__device__ __forceinline__ int pad_col(int e) { return e + (e >> 3); }
+
+// Four consecutive outputs of both filters from a register window, pywt's
+// natural tap order per output (0 + f[0] x[i] + f[1] x[i-1] + ...), the tap
+// loop outermost so the eight sums are independent chains.
+template <int F>
+__device__ __forceinline__ void fwd_group(const double (&flo)[F], const double (&fhi)[F],
+                                          const double (&v)[2 * (kG - 1) + F], double (&lo)[kG], double (&hi)[kG])
+{
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+        lo[u] = 0.0;
+        hi[u] = 0.0;
+    }
+#pragma unroll
+    for (int m = 0; m < F; ++m) {
+        const double fl = flo[m], fh = fhi[m];
+#pragma unroll
+        for (int u = 0; u < kG; ++u) {
+            const double x = v[2 * u + F - 1 - m];
+            lo[u] = lo[u] + fl * x;
+            hi[u] = hi[u] + fh * x;
+        }
+    }
+}
+
+// quantize one row-pass result pair into the staged subband bytes / LL
+template <bool LAST>
+__device__ __forceinline__ void fwd_store(int src, double lo, double hi, int e, uint8_t *stage, uint8_t *stage16,
+                                          int SB, int Q, double *stageLL, int ll_index)
+{
+    if (src) {                                   // D rows: da -> LH, dd -> HH
+        stage[0 * SB + e] = quant_u8(lo, Q);
+        stage[2 * SB + e] = quant_u8(hi, Q);
+    } else {                                     // A rows: ad -> HL, aa -> LL
+        stage[1 * SB + e] = quant_u8(hi, Q);
+        if (LAST) {
+            const uint16_t q16 = quant_u16(lo, Q);
+            stage16[2 * e] = (uint8_t)q16;
+            stage16[2 * e + 1] = (uint8_t)(q16 >> 8);
+        } else {
+            stageLL[ll_index] = lo;
+        }
+    }
+}
+
+// Forward level: a tile of kFTH x tw subband samples of all three channels.
+// Per channel: stage the (2 kFTH - 2 + F) x 128 input samples, column pass
+// (work item = one staged column x 4 output rows, its 2*3+F input samples
+// in registers), row pass (work item = one row of A or D x 4 outputs),
+// quantize into a byte image of the three detail subbands; one copy-out of
+// contiguous runs at the end.  Outputs whose taps wrap past the line end
+// (i >= N) take pywt's order through the generic LDS sum.
+template <int F, bool FIRST, bool LAST>
+__global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
+                                                        const double *__restrict__ in, long long plane_stride,
+                                                        double *__restrict__ LLout, uint8_t *__restrict__ packed,
+                                                        long long packed_stride, long long ll_off, long long off_lh,
+                                                        long long off_hl, long long off_hh, int h, int w, int hh,
+                                                        int hw, int Q, Taps<F> tp, Filters flt)
+{
+    constexpr int TW = fwd_tile_w(F), IH = 2 * (kFTH - 1) + F, IW = kFIW;
+    constexpr int NWIN = 2 * (kG - 1) + F;
+    constexpr int NG = (TW + kG - 1) / kG;
+    constexpr int SB = kFTH * TW * 3;
+    static_assert(kFTH == 2 * kG && 2 * (TW - 1) + F == IW, "tile geometry");
+    constexpr int RS = IW + IW / 8;                  // A/D rows padded one double per 8 (bank spread)
+    __shared__ double tin[IH * IW];
+    __shared__ double tA[kFTH * RS + 8], tD[kFTH * RS + 8];   // +8: the last row group's window overhang
+    __shared__ uint8_t stage[3 * SB];
+    __shared__ uint8_t stage16[LAST ? 2 * SB : 1];
+    __shared__ double stageLL[LAST ? 1 : kFTH * TW];
+    const int o0 = blockIdx.y * kFTH, c0 = blockIdx.x * TW;
+    const long long frame = blockIdx.z;
+    const int R0 = F / 2 + 2 * o0 - F + 1, C0 = F / 2 + 2 * c0 - F + 1;
+    const int tid = threadIdx.x;
+    const bool rows_in = R0 >= 0 && R0 + IH <= h, cols_in = C0 >= 0 && C0 + IW <= w;
+    const bool col_tail = F / 2 + 2 * (o0 + kFTH - 1) >= h, row_tail = F / 2 + 2 * (c0 + TW - 1) >= w;
+    // taps into VGPRs through LDS (kernel-argument taps would sit in scalar
+    // registers, which the pass loops exhaust)
+    __shared__ double taps[2 * F];
+    if (tid < F) {
+        taps[tid] = tp.lo[tid];
+        taps[F + tid] = tp.hi[tid];
+    }
+    __syncthreads();
+    double flo[F], fhi[F];
+#pragma unroll
+    for (int m = 0; m < F; ++m) {
+        flo[m] = taps[m];
+        fhi[m] = taps[F + m];
+    }
+    // staged samples of this thread (PER per channel), fetched one channel
+    // ahead into registers: level 1 reads its RGB bytes once for all three
+    // channels, later levels prefetch the next channel's plane during the
+    // current channel's passes
+    constexpr int PER = IH * IW / 256;
+    static_assert(PER * 256 == IH * IW, "staging split");
+    uint32_t pix[FIRST ? PER : 1];
+    double nxt[FIRST ? 1 : PER];
+    auto fetch = [&](int ch) {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int t = tid + 256 * j;
+            const int r = t / IW, c = t % IW;
+            const int y = rows_in ? R0 + r : per_wrap(R0 + r, h);
+            const int x = cols_in ? C0 + c : per_wrap(C0 + c, w);
+            if (FIRST) {
+                const uint8_t *px = rgb + frame * rgb_stride + ((long long)y * w + x) * 3;
+                pix[j] = (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
+            } else {
+                nxt[FIRST ? 0 : j] = in[(frame * 3 + ch) * plane_stride + (long long)y * w + x];
+            }
+        }
+    };
+    fetch(0);
+    for (int ch = 0; ch < 3; ++ch) {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            double v;
+            if (FIRST) {
+                // (int16)(R/4 + G/2 + B/4) etc.: every float term is a multiple of 1/4
+                // below 2^9, so the sums are exact and truncation is integer division
+                const int R = pix[j] & 0xFF, G = (pix[j] >> 8) & 0xFF, B = pix[j] >> 16;
+                int iv;
+                if (ch == 0) iv = (R + 2 * G + B) >> 2;
+                else if (ch == 1) iv = (R - B) / 2;
+                else iv = (2 * G - R - B) / 4;
+                v = (double)iv;
+            } else {
+                v = nxt[FIRST ? 0 : j];
+            }
+            tin[tid + 256 * j] = v;
+        }
+        if (!FIRST && ch < 2) fetch(ch + 1);
+        __syncthreads();
+        {   // column pass (axis 0): 128 columns x 2 groups of 4 output rows
+            const int c = tid % IW, g = tid / IW;
+            double v[NWIN];
+#pragma unroll
+            for (int k = 0; k < NWIN; ++k) v[k] = tin[(2 * kG * g + k) * IW + c];
+            double a[kG], d[kG];
+            fwd_group<F>(flo, fhi, v, a, d);
+#pragma unroll
+            for (int u = 0; u < kG; ++u) {
+                tA[(kG * g + u) * RS + pad_col(c)] = a[u];
+                tD[(kG * g + u) * RS + pad_col(c)] = d[u];
+            }
+        }
+        if (col_tail) {   // tile-uniform: rows whose taps wrap past the end take pywt's order
+            __syncthreads();
+            const int first = max(0, (h - F / 2 + 1) / 2 - o0);   // first tile row with i >= h
+            for (int t = tid; t < (kFTH - first) * IW; t += 256) {
+                const int o = first + t / IW, c = t % IW;
+                const int i = F / 2 + 2 * (o0 + o);
+                auto load = [&](int p) -> double { return tin[(p - R0) * IW + c]; };
+                tA[o * RS + pad_col(c)] = dwt_tap_sum_logical(flt.dec_lo, F, h, i, load);
+                tD[o * RS + pad_col(c)] = dwt_tap_sum_logical(flt.dec_hi, F, h, i, load);
+            }
+        }
+        __syncthreads();
+        // row pass (axis 1): (A or D) x kFTH rows x NG groups of 4 outputs
+        const int first_tail = row_tail ? max(0, (w - F / 2 + 1) / 2 - c0) : TW;   // first column with i >= w
+        for (int t = tid; t < 2 * kFTH * NG; t += 256) {
+            const int src = t / (kFTH * NG), rest = t % (kFTH * NG);
+            const int o = rest / NG, gq = rest % NG, oc0 = kG * gq;
+            const double *row = (src ? tD : tA) + o * RS;
+            double v[NWIN];
+#pragma unroll
+            for (int k = 0; k < NWIN; ++k) v[k] = row[9 * gq + k + (k >> 3)];   // pad_col(8 gq + k)
+            double lo[kG], hi[kG];
+            fwd_group<F>(flo, fhi, v, lo, hi);
+            const bool rv = o0 + o < hh;
+#pragma unroll
+            for (int u = 0; u < kG; ++u) {
+                const int oc = oc0 + u;
+                if (rv && oc < min(TW, hw - c0) && oc < first_tail)
+                    fwd_store<LAST>(src, lo[u], hi[u], (o * TW + oc) * 3 + ch, stage, stage16, SB, Q, stageLL,
+                                    o * TW + oc);
+            }
+        }
+        if (row_tail) {   // tile-uniform: outputs whose taps wrap past the line end
+            const int n = min(TW, hw - c0) - first_tail;
+            for (int t = tid; t < 2 * kFTH * max(n, 0); t += 256) {
+                const int src = t / (kFTH * n), rest = t % (kFTH * n);
+                const int o = rest / n, oc = first_tail + rest % n;
+                if (o0 + o >= hh) continue;
+                const int i = F / 2 + 2 * (c0 + oc);
+                const double *row = (src ? tD : tA) + o * RS;
+                auto load = [&](int p) -> double { return row[pad_col(p - C0)]; };
+                const double lo = dwt_tap_sum_logical(flt.dec_lo, F, w, i, load);
+                const double hi = dwt_tap_sum_logical(flt.dec_hi, F, w, i, load);
+                fwd_store<LAST>(src, lo, hi, (o * TW + oc) * 3 + ch, stage, stage16, SB, Q, stageLL, o * TW + oc);
+            }
+        }
+        __syncthreads();
+        if (!LAST) {   // LL rows leave as contiguous runs of doubles
+            const int rows = min(kFTH, hh - o0), nw = min(TW, hw - c0);
+            double *dst = LLout + (frame * 3 + ch) * plane_stride + (long long)o0 * hw + c0;
+            for (int t = tid; t < rows * TW; t += 256) {
+                const int o = t / TW, oc = t - o * TW;
+                if (oc < nw) dst[(long long)o * hw + oc] = stageLL[t];
+            }
+        }
+    }
+    // copy-out: each subband row of the tile is one contiguous byte run
+    const int rows = min(kFTH, hh - o0), nb = min(TW, hw - c0) * 3;
+    uint8_t *pk = packed + frame * packed_stride;
+    const long long offs[3] = {off_lh, off_hl, off_hh};
+    for (int sb = 0; sb < 3; ++sb)
+        for (int t = tid; t < rows * TW * 3; t += 256) {
+            const int o = t / (TW * 3), b = t - o * (TW * 3);
+            if (b < nb) pk[offs[sb] + ((long long)(o0 + o) * hw + c0) * 3 + b] = stage[sb * SB + t];
+        }
+    if (LAST)
+        for (int t = tid; t < rows * TW * 6; t += 256) {
+            const int o = t / (TW * 6), b = t - o * (TW * 6);
+            if (b < 2 * nb) pk[ll_off + ((long long)(o0 + o) * hw + c0) * 6 + b] = stage16[t];
+        }
+}
+
+// Four consecutive outputs of the inverse from the register windows of the
+// approximation (xa) and detail (xd) inputs: pywt's order for a pair index
+// i >= F/4 (approximation taps j = 0.., then detail taps), tap loop outermost.
+template <int F>
+__device__ __forceinline__ void inv_group(const double (&flo)[F], const double (&fhi)[F],
+                                          const double (&xa)[F / 2 + (((F / 2 - 1) & 1) + kG - 1) / 2],
+                                          const double (&xd)[F / 2 + (((F / 2 - 1) & 1) + kG - 1) / 2],
+                                          double (&s)[kG])
+{
+    constexpr int F2 = F / 2, P0 = (F2 - 1) & 1;
+#pragma unroll
+    for (int u = 0; u < kG; ++u) s[u] = 0.0;
+#pragma unroll
+    for (int j = 0; j < F2; ++j)
+#pragma unroll
+        for (int u = 0; u < kG; ++u) s[u] = s[u] + flo[2 * j + ((P0 + u) & 1)] * xa[F2 - 1 + ((P0 + u) >> 1) - j];
+#pragma unroll
+    for (int j = 0; j < F2; ++j)
+#pragma unroll
+        for (int u = 0; u < kG; ++u) s[u] = s[u] + fhi[2 * j + ((P0 + u) & 1)] * xd[F2 - 1 + ((P0 + u) >> 1) - j];
+}
+
+// the column pass's reordered outputs (rare: first / last rows of a plane)
+__device__ __attribute__((noinline)) double inv_col_generic(Filters flt, int F, int h, int n, const double *ta,
+                                                            const double *td, int K0r, int nc)
+{
+    auto la = [&](int k) -> double { return ta[(k - K0r) * kITW + nc]; };
+    auto ld = [&](int k) -> double { return td[(k - K0r) * kITW + nc]; };
+    return idwt_out_logical(flt.rec_lo, flt.rec_hi, F, h, n, la, ld);
+}
+
+// Inverse level r: subbands h x w (aa from the packed LL or from the previous
+// level's plane with row stride lda) -> outputs [0, oh) x [0, ow) of the
+// 2h x 2w reconstruction (only what the next level reads).  Row pass work
+// item = one staged input row x 4 outputs of 'a' or 'd'; column pass = one
+// column x 4 outputs.  TO_RGB (level 1): all three channels per tile, kept
+// in registers, then to_RGB + clip + u8.  Outputs whose wrapped pair index
+// is below F/4 take pywt's reordered taps through the generic LDS sum.
+template <int F, bool FROM_PACKED_LL, bool TO_RGB>
+__global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
+                                                         long long ll_off, long long off_lh, long long off_hl,
+                                                         long long off_hh, const double *__restrict__ prev,
+                                                         long long plane_stride, int lda, double *__restrict__ out,
+                                                         int h, int w, int oh, int ow, int Q, Taps<F> tp,
+                                                         Filters flt, uint8_t *__restrict__ rgb, long long rgb_stride)
+{
+    constexpr int F2 = F / 2, T = F2 / 2;
+    constexpr int KHm = kITH / 2 + F2, KWm = kITW / 2 + F2;
+    constexpr int P0 = (F2 - 1) & 1;                 // parity of n + F2 - 1 for even n
+    constexpr int NW = F2 + ((P0 + kG - 1) >> 1);    // window of a 4-output group
+    constexpr int NGC = kITW / kG, NGR = kITH / kG;
+    static_assert(NGC * NGR * kG * kG == kITH * kITW && kITW * NGR == 256, "tile geometry");
+    constexpr int S = (KHm * KWm + 1) & ~1;          // even, so the offsets below are odd apart (bank spread)
+    __shared__ double sub[4 * S + 4];
+    __shared__ double ta[KHm * kITW], td[KHm * kITW];
+    double *sAA = sub, *sDA = sub + S + 1, *sAD = sub + 2 * S + 2, *sDD = sub + 3 * S + 3;
+    const int n0r = blockIdx.y * kITH, n0c = blockIdx.x * kITW;
+    const int K0r = ((n0r + F2 - 1) >> 1) - F2 + 1, K0c = ((n0c + F2 - 1) >> 1) - F2 + 1;
+    const int KH = ((n0r + kITH - 1 + F2 - 1) >> 1) - K0r + 1;
+    const int KW = ((n0c + kITW - 1 + F2 - 1) >> 1) - K0c + 1;
+    const bool rows_in = K0r >= 0 && K0r + KH <= h, cols_in = K0c >= 0 && K0c + KW <= w;
+    const bool row_tail = n0c == 0 || n0c + kITW + F2 - 2 >= 2 * w;
+    const bool col_tail = n0r == 0 || n0r + kITH + F2 - 2 >= 2 * h;
+    const int tid = threadIdx.x;
+    const long long frame = TO_RGB ? blockIdx.z : blockIdx.z / 3;
+    const uint8_t *pk = packed + frame * packed_stride;
+    double acc[TO_RGB ? 3 : 1][kG];
+    const int ch_lo = TO_RGB ? 0 : (int)(blockIdx.z % 3), ch_hi = TO_RGB ? 3 : ch_lo + 1;
+    const int nc = tid % kITW, gr = tid / kITW;      // column-pass item
+    __shared__ double taps[2 * F];
+    if (tid < F) {
+        taps[tid] = tp.lo[tid];
+        taps[F + tid] = tp.hi[tid];
+    }
+    __syncthreads();
+    double flo[F], fhi[F];
+#pragma unroll
+    for (int m = 0; m < F; ++m) {
+        flo[m] = taps[m];
+        fhi[m] = taps[F + m];
+    }
+    for (int ch = ch_lo; ch < ch_hi; ++ch) {
+        for (int t = tid; t < KH * KW; t += 256) {
+            const int r = t / KW, c = t - r * KW;
+            const int y = rows_in ? K0r + r : mod_pos(K0r + r, h);
+            const int x = cols_in ? K0c + c : mod_pos(K0c + c, w);
+            const long long e = ((long long)y * w + x) * 3 + ch;
+            double vaa;
+            if (FROM_PACKED_LL) {
+                const uint8_t *q = pk + ll_off + e * 2;
+                vaa = dequant((int16_t)(uint16_t)(q[0] | (q[1] << 8)), Q);
+            } else {
+                vaa = prev[(frame * 3 + ch) * plane_stride + (long long)y * lda + x];
+            }
+            const int l = r * KWm + c;
+            sAA[l] = vaa;
+            sAD[l] = dequant((int16_t)pk[off_hl + e], Q);   // 'ad' = cV = HL
+            sDA[l] = dequant((int16_t)pk[off_lh + e], Q);   // 'da' = cH = LH
+            sDD[l] = dequant((int16_t)pk[off_hh + e], Q);   // 'dd' = cD = HH
+        }
+        __syncthreads();
+        // row pass (axis 1): 'a' = idwt(aa, ad), 'd' = idwt(da, dd)
+        for (int t = tid; t < KH * NGC * 2; t += 256) {
+            const int src = t & 1, r = (t >> 1) / NGC, g = (t >> 1) % NGC;
+            const int n0 = n0c + kG * g;
+            const int base = r * KWm + ((n0 + F2 - 1) >> 1) - F2 + 1 - K0c;
+            const double *X = src ? sDA : sAA, *Y = src ? sDD : sAD;
+            double xa[NW], xd[NW];
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                xa[k] = X[base + k];
+                xd[k] = Y[base + k];
+            }
+            double sum[kG];
+            inv_group<F>(flo, fhi, xa, xd, sum);
+            double *dst = (src ? td : ta) + r * kITW + kG * g;
+#pragma unroll
+            for (int u = 0; u < kG; ++u) dst[u] = sum[u];
+        }
+        if (row_tail) {   // tile-uniform: outputs whose wrapped pair index is below F/4
+            __syncthreads();
+            for (int t = tid; t < KH * kITW * 2; t += 256) {
+                const int src = t & 1, r = (t >> 1) / kITW, nc2 = (t >> 1) % kITW;
+                const int n = n0c + nc2, q = n + F2 - 1;
+                if (n >= ow || ((q % (2 * w)) >> 1) >= T) continue;
+                const double *Xr = (src ? sDA : sAA) + r * KWm - K0c, *Yr = (src ? sDD : sAD) + r * KWm - K0c;
+                auto la = [&](int k) -> double { return Xr[k]; };
+                auto ld = [&](int k) -> double { return Yr[k]; };
+                (src ? td : ta)[r * kITW + nc2] = idwt_out_logical(flt.rec_lo, flt.rec_hi, F, w, n, la, ld);
+            }
+        }
+        __syncthreads();
+        {   // column pass (axis 0): 64 columns x 4 groups of 4 output rows
+            const int n0 = n0r + kG * gr;
+            const int base = ((n0 + F2 - 1) >> 1) - F2 + 1 - K0r;
+            double xa[NW], xd[NW];
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                xa[k] = ta[(base + k) * kITW + nc];
+                xd[k] = td[(base + k) * kITW + nc];
+            }
+            double sum[kG];
+            inv_group<F>(flo, fhi, xa, xd, sum);
+            if (col_tail) {
+#pragma unroll
+                for (int u = 0; u < kG; ++u) {
+                    const int n = n0 + u, q = n + F2 - 1;
+                    if (((q % (2 * h)) >> 1) < T) sum[u] = inv_col_generic(flt, F, h, n, ta, td, K0r, nc);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kG; ++u) acc[TO_RGB ? ch : 0][u] = sum[u];
+        }
+        __syncthreads();
+    }
+    const int m = n0c + nc;
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+        const int n = n0r + kG * gr + u;
+        if (n >= oh || m >= ow) continue;
+        if (TO_RGB) {
+            const double Y = acc[0][u], Co = acc[TO_RGB ? 1 : 0][u], Cg = acc[TO_RGB ? 2 : 0][u];
+            const double v[3] = {Y + Co - Cg, Y + Cg, Y - Co - Cg};
+            uint8_t *o = rgb + frame * rgb_stride + ((long long)n * ow + m) * 3;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const double c = v[k] < 0.0 ? 0.0 : (v[k] > 255.0 ? 255.0 : v[k]);
+                o[k] = (uint8_t)c;
+            }
+        } else {
+            out[(frame * 3 + ch_lo) * plane_stride + (long long)n * ow + m] = acc[0][u];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 // filter banks uploaded once per (device, wavelet)
@@ -362,6 +839,89 @@ int check_dwt(const void *a, const void *b, int64_t n_frames, int32_t H, int32_t
 
 unsigned gx(int n) { return (unsigned)((n + 255) / 256); }
 
+bool fast_filter(int F) { return F >= 2 && F <= kMaxFastF && (F & 1) == 0; }
+
+template <int F>
+Taps<F> taps_of(const double *lo, const double *hi)
+{
+    Taps<F> t;
+    for (int m = 0; m < F; ++m) {
+        t.lo[m] = lo[m];
+        t.hi[m] = hi[m];
+    }
+    return t;
+}
+
+struct LevelArgs {
+    const uint8_t *rgb;
+    long long rgb_stride;
+    const double *in;
+    long long plane_stride;
+    double *LLout;
+    uint8_t *packed;
+    long long packed_stride, ll_off, off_lh, off_hl, off_hh;
+    int h, w, hh, hw, Q, lda;
+    unsigned n_frames;
+    Filters flt;
+    const WaveletDef *wd;
+    hipStream_t s;
+};
+
+template <int F>
+void launch_fwd_level(const LevelArgs &a, bool first, bool last)
+{
+    const Taps<F> tp = taps_of<F>(a.wd->dec_lo, a.wd->dec_hi);
+    constexpr int TW = fwd_tile_w(F);
+    const dim3 grid((a.hw + TW - 1) / TW, (a.hh + kFTH - 1) / kFTH, a.n_frames);
+    auto kern = first ? (last ? dwt_level_kernel<F, true, true> : dwt_level_kernel<F, true, false>)
+                      : (last ? dwt_level_kernel<F, false, true> : dwt_level_kernel<F, false, false>);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed,
+                       a.packed_stride, a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt);
+}
+
+// level r of the inverse: subbands a.h x a.w -> outputs a.hh x a.hw (= oh x ow)
+template <int F>
+void launch_inv_level(const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t *rgb_out)
+{
+    const Taps<F> tp = taps_of<F>(a.wd->rec_lo, a.wd->rec_hi);
+    const dim3 grid((a.hw + kITW - 1) / kITW, (a.hh + kITH - 1) / kITH, to_rgb ? a.n_frames : 3 * a.n_frames);
+    auto kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true> : idwt_level_kernel<F, true, false>)
+                            : (to_rgb ? idwt_level_kernel<F, false, true> : idwt_level_kernel<F, false, false>);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
+                       a.off_hh, a.in, a.plane_stride, a.lda, a.LLout, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, rgb_out,
+                       (long long)a.hh * a.hw * 3);
+}
+
+#define VCF_DWT_FOR_EACH_F(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18)
+
+void fwd_level(int F, const LevelArgs &a, bool first, bool last)
+{
+    switch (F) {
+#define X(n)                                                                                                       \
+    case n:                                                                                                        \
+        launch_fwd_level<n>(a, first, last);                                                                       \
+        break;
+        VCF_DWT_FOR_EACH_F(X)
+#undef X
+    default:
+        break;
+    }
+}
+
+void inv_level(int F, const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t *rgb_out)
+{
+    switch (F) {
+#define X(n)                                                                                                       \
+    case n:                                                                                                        \
+        launch_inv_level<n>(a, from_packed, to_rgb, rgb_out);                                                      \
+        break;
+        VCF_DWT_FOR_EACH_F(X)
+#undef X
+    default:
+        break;
+    }
+}
+
 }  // namespace
 }  // namespace vcf
 
@@ -398,6 +958,15 @@ int vcf_dwt_layout(int32_t H, int32_t W, int32_t levels, int32_t *sub_h, int32_t
 int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                       int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, void *stream)
 {
+    return vcf_dwt_dz_encode_variant(0, rgb_dev, n_frames, H, W, wavelet, levels, Q, packed_dev, workspace_dev,
+                                     stream);
+}
+
+int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
+                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
+                              void *stream)
+{
+    if (variant < 0 || variant > 2) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -416,7 +985,21 @@ int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
     hipStream_t s = (hipStream_t)stream;
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *in = nullptr;
-    for (int l = 1; l <= levels; ++l) {
+    const bool fused = variant == 1 || (variant == 0 && fast_filter(F));
+    if (fused && !fast_filter(F))
+        return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
+                         kMaxFastF);
+    for (int l = 1; fused && l <= levels; ++l) {
+        double *LLout = (l & 1) ? LL0 : LL1;
+        const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
+                          g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
+                          g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s};
+        fwd_level(F, a, l == 1, l == levels);
+        in = LLout;
+        rc = hip_check(hipGetLastError(), "dwt level launch");
+        if (rc != VCF_OK) return rc;
+    }
+    for (int l = 1; !fused && l <= levels; ++l) {
         const int h = g.hs[l - 1], w = g.ws[l - 1], hh = g.hs[l], hw = g.ws[l];
         if (l == 1)
             hipLaunchKernelGGL(dwt_cols_kernel<true>, dim3(gx(w), hh, planes), dim3(256), 0, s, rgb_dev,
@@ -443,6 +1026,15 @@ int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
 int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                       int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, void *stream)
 {
+    return vcf_dwt_dz_decode_variant(0, packed_dev, n_frames, H, W, wavelet, levels, Q, rgb_dev, workspace_dev,
+                                     stream);
+}
+
+int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W,
+                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
+                              void *stream)
+{
+    if (variant < 0 || variant > 2) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -462,6 +1054,26 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *prev = nullptr;
     int lda = 0;
+    const bool fused = variant == 1 || (variant == 0 && fast_filter(F));
+    if (fused && !fast_filter(F))
+        return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
+                         kMaxFastF);
+    if (fused) {
+        for (int r = levels; r >= 1; --r) {
+            const int h = g.hs[r], w = g.ws[r];
+            const int oh = r > 1 ? g.hs[r - 1] : 2 * h, ow = r > 1 ? g.ws[r - 1] : 2 * w;
+            double *out = (r & 1) ? P0 : P1;
+            const LevelArgs a{nullptr, 0, prev, ws_stride, out, const_cast<uint8_t *>(packed_dev), g.packed_bytes,
+                              g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], h, w, oh, ow, Q, lda,
+                              (unsigned)n_frames, flt, &kWavelets[wavelet], s};
+            inv_level(F, a, r == levels, r == 1, rgb_dev);
+            prev = out;
+            lda = ow;
+            rc = hip_check(hipGetLastError(), "idwt level launch");
+            if (rc != VCF_OK) return rc;
+        }
+        return VCF_OK;
+    }
     for (int r = levels; r >= 1; --r) {
         const int h = g.hs[r], w = g.ws[r];
         if (r == levels)

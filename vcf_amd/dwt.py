@@ -62,15 +62,16 @@ def _frames(a, what):
     return np.ascontiguousarray(a)
 
 
-def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32):
-    """HxWx3 u8 (or N of them) -> list of {subband name: indices} per frame."""
+def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32, variant: int = 0):
+    """HxWx3 u8 (or N of them) -> list of {subband name: indices} per frame.
+    variant: 0 automatic, 1 fused level kernels, 2 separable kernels."""
     f = _frames(rgb, "rgb")
     n, H, W, _ = f.shape
     _, pb, wb = layout(H, W, levels)
     din, dout, dws = DeviceBuffer.from_array(f), DeviceBuffer(n * pb), DeviceBuffer(n * wb)
     try:
-        L.call("vcf_dwt_dz_encode", din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q), dout.ptr, dws.ptr,
-               None)
+        L.call("vcf_dwt_dz_encode_variant", int(variant), din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q),
+               dout.ptr, dws.ptr, None)
         packed = dout.download(np.empty((n, pb), np.uint8))
     finally:
         din.free()
@@ -79,7 +80,8 @@ def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32):
     return [unpack(packed[i], H, W, levels) for i in range(n)]
 
 
-def decode(subbands, H: int, W: int, wavelet: str = "db5", levels: int = 5, Q: int = 32) -> np.ndarray:
+def decode(subbands, H: int, W: int, wavelet: str = "db5", levels: int = 5, Q: int = 32,
+           variant: int = 0) -> np.ndarray:
     """{name: indices} (or a list of them) -> u8 RGB (2*ceil(H/2) x 2*ceil(W/2) x 3 each)."""
     single = isinstance(subbands, dict)
     sets = [subbands] if single else list(subbands)
@@ -89,8 +91,8 @@ def decode(subbands, H: int, W: int, wavelet: str = "db5", levels: int = 5, Q: i
     Ho, Wo = 2 * shapes[0][0], 2 * shapes[0][1]
     din, dout, dws = DeviceBuffer.from_array(packed), DeviceBuffer(n * Ho * Wo * 3), DeviceBuffer(n * wb)
     try:
-        L.call("vcf_dwt_dz_decode", din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q), dout.ptr, dws.ptr,
-               None)
+        L.call("vcf_dwt_dz_decode_variant", int(variant), din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q),
+               dout.ptr, dws.ptr, None)
         out = dout.download(np.empty((n, Ho, Wo, 3), np.uint8))
     finally:
         din.free()
