@@ -30,6 +30,7 @@
 #include <cstdint>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 
 #include "vcf_amd.h"
 #include "vcf_internal.h"
@@ -450,7 +451,9 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
     constexpr int SB = kFTH * TW * 3;
     static_assert(kFTH == 2 * kG && 2 * (TW - 1) + F == IW, "tile geometry");
     constexpr int RS = IW + IW / 8;                  // A/D rows padded one double per 8 (bank spread)
-    __shared__ double tin[IH * IW];
+    // level 1 stages int16-valued YCoCg samples, exact in float (half the LDS)
+    using Stage = typename std::conditional<FIRST, float, double>::type;
+    __shared__ Stage tin[IH * IW];
     __shared__ double tA[kFTH * RS + 8], tD[kFTH * RS + 8];   // +8: the last row group's window overhang
     __shared__ uint8_t stage[3 * SB];
     __shared__ uint8_t stage16[LAST ? 2 * SB : 1];
@@ -463,18 +466,8 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
     const bool col_tail = F / 2 + 2 * (o0 + kFTH - 1) >= h, row_tail = F / 2 + 2 * (c0 + TW - 1) >= w;
     // taps into VGPRs through LDS (kernel-argument taps would sit in scalar
     // registers, which the pass loops exhaust)
-    __shared__ double taps[2 * F];
-    if (tid < F) {
-        taps[tid] = tp.lo[tid];
-        taps[F + tid] = tp.hi[tid];
-    }
-    __syncthreads();
-    double flo[F], fhi[F];
-#pragma unroll
-    for (int m = 0; m < F; ++m) {
-        flo[m] = taps[m];
-        fhi[m] = taps[F + m];
-    }
+    const double(&flo)[F] = tp.lo;
+    const double(&fhi)[F] = tp.hi;
     // staged samples of this thread (PER per channel), fetched one channel
     // ahead into registers: level 1 reads its RGB bytes once for all three
     // channels, later levels prefetch the next channel's plane during the
@@ -515,7 +508,7 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
             } else {
                 v = nxt[FIRST ? 0 : j];
             }
-            tin[tid + 256 * j] = v;
+            tin[tid + 256 * j] = (Stage)v;
         }
         if (!FIRST && ch < 2) fetch(ch + 1);
         __syncthreads();
@@ -523,7 +516,7 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
             const int c = tid % IW, g = tid / IW;
             double v[NWIN];
 #pragma unroll
-            for (int k = 0; k < NWIN; ++k) v[k] = tin[(2 * kG * g + k) * IW + c];
+            for (int k = 0; k < NWIN; ++k) v[k] = (double)tin[(2 * kG * g + k) * IW + c];
             double a[kG], d[kG];
             fwd_group<F>(flo, fhi, v, a, d);
 #pragma unroll
@@ -538,7 +531,7 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
             for (int t = tid; t < (kFTH - first) * IW; t += 256) {
                 const int o = first + t / IW, c = t % IW;
                 const int i = F / 2 + 2 * (o0 + o);
-                auto load = [&](int p) -> double { return tin[(p - R0) * IW + c]; };
+                auto load = [&](int p) -> double { return (double)tin[(p - R0) * IW + c]; };
                 tA[o * RS + pad_col(c)] = dwt_tap_sum_logical(flt.dec_lo, F, h, i, load);
                 tD[o * RS + pad_col(c)] = dwt_tap_sum_logical(flt.dec_hi, F, h, i, load);
             }
