@@ -90,7 +90,9 @@ int vcf_dct_padded_shape(int32_t H, int32_t W, int32_t block_size, int32_t *Hp, 
 
 /* n_frames RGB frames (H x W x 3 u8 each) -> n_frames coefficient frames
  * (Hp x Wp x 3 u8 each, k + 128 modulo 256, subband layout unless
- * VCF_DCT_NO_SUBBANDS).  block_size must be 8 (the -B default); Q >= 1 is the
+ * VCF_DCT_NO_SUBBANDS).  block_size is the -B option (2D-DCT.py:29): 8 runs
+ * the fused 8x8 kernels, the other supported sizes (vcf_dct_block_size_supported)
+ * the generic-B kernels; VCF_DCT_PERCEPTUAL needs B = 8.  Q >= 1 is the
  * deadzone quantization step (-q). */
 int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *k_dev,
@@ -114,6 +116,34 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
 int vcf_dct_dz_decode(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev,
                       void *stream);
+
+/* 1 if block_size has a HIP transform: B = 2^a 3^b <= 128 (a <= 7, b <= 1),
+ * the lengths whose pocketfft real FFT factors into 4, 2 and 3 -- including
+ * every size the -L search tries (2, 4, ..., 128; 2D-DCT.py:536).  0 otherwise. */
+int vcf_dct_block_size_supported(int32_t block_size);
+
+/* The generic-B kernels for any supported block size, B = 8 included (tests
+ * and A/B checks against the fused 8x8 kernels); same contract as
+ * vcf_dct_dz_encode / vcf_dct_dz_decode. */
+int vcf_dct_dz_encode_any(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
+                          int32_t Q, uint32_t flags, uint8_t *k_dev, void *stream);
+int vcf_dct_dz_decode_any(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
+                          int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream);
+
+/* The -L rate-distortion search's own analysis/synthesis
+ * (2D-DCT.py optimize_block_size :533-579), which differs from
+ * encode_fn/decode_fn in its integer types and offset.  The search runs from
+ * CoDec.__init__ (:99-103) before the deadzone offset 128 is assigned
+ * (:106-109), so its self.offset is YCoCg's [0, 0, 0] (YCoCg.py:28-29):
+ *   encode_k32: astype(float32) (no -128), from_RGB, analyze, get_subbands,
+ *     quantize (:536-545) -> the int32 k array (Hp x Wp x 3 int32);
+ *   decode_k32: Q*k in int32 (:561), get_blocks, the IDCT stored into int32,
+ *     to_RGB in int32 (no +128), clip, uint8 (:562-568).
+ * No VCF_DCT_PERCEPTUAL (the reference refuses -L with -p, :100-105). */
+int vcf_dct_dz_encode_k32(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
+                          int32_t Q, uint32_t flags, int32_t *k_dev, void *stream);
+int vcf_dct_dz_decode_k32(const int32_t *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
+                          int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream);
 
 /* ---- 2D-DWT + deadzone path (2D-DWT.py, deadzone.py, YCoCg.py) ---------------- */
 

@@ -34,7 +34,8 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(HERE, f) for f in ("vcf_oracle.c", "vcf_dwt_oracle.cpp", "vcf_ipp_oracle.c")]
+        srcs = [os.path.join(HERE, f) for f in ("vcf_oracle.c", "vcf_dwt_oracle.cpp", "vcf_ipp_oracle.c",
+                                                       "vcf_dct_general_oracle.cpp")]
         if not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(f) for f in srcs):
             build()
         L = ctypes.CDLL(LIB_PATH)
@@ -50,6 +51,21 @@ def lib():
         for n in ("vcfo_dct2_8_f64", "vcfo_dct3_8_f64"):
             getattr(L, n).argtypes = [dp]
         L.vcfo_pocketfft_consts.argtypes = [fp, dp, fp, dp, fp, dp]
+        # any block size (vcf_dct_general_oracle.cpp)
+        L.vcfo_dct_supported.argtypes = [ctypes.c_int]
+        for n in ("vcfo_dct2_f32_n", "vcfo_dct3_f32_n"):
+            getattr(L, n).argtypes = [fp, ctypes.c_int, ctypes.c_int]
+        for n in ("vcfo_dct2_f64_n", "vcfo_dct3_f64_n"):
+            getattr(L, n).argtypes = [dp, ctypes.c_int, ctypes.c_int]
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        L.vcfo_dct_dz_encode_b.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_uint, u8p]
+        L.vcfo_dct_dz_decode_b.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_uint, u8p]
+        L.vcfo_dct_dz_encode_k32_b.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_uint, i32p]
+        L.vcfo_dct_dz_decode_k32_b.argtypes = [i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_uint, u8p]
         L.vcfo_perceptual_weights.argtypes = [dp]
         # 2D-DWT path (vcf_dwt_oracle.cpp)
         ip = ctypes.POINTER(ctypes.c_int)
@@ -103,6 +119,58 @@ def decode_frame(k: np.ndarray, H: int, W: int, Q: int = 32, flags: int = 0) -> 
         raise ValueError(f"index array shape {k.shape} != {(Hp, Wp, 3)}")
     out = np.empty((H, W, 3), np.uint8)
     rc = lib().vcfo_dct_dz_decode(_u8(k), H, W, int(Q), flags, _u8(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle decode failed ({rc})")
+    return out
+
+
+def dct_supported(N: int) -> bool:
+    return bool(lib().vcfo_dct_supported(int(N)))
+
+
+def dct_n(x, kind: int = 2, dtype=np.float32):
+    """pocketfft DCT-II (kind 2) / DCT-III (kind 3), ortho, along the last axis, any supported length."""
+    a = np.array(x, dtype=dtype)
+    N = a.shape[-1]
+    b = np.ascontiguousarray(a.reshape(-1, N))
+    ct = ctypes.c_float if dtype == np.float32 else ctypes.c_double
+    sfx = "f32" if dtype == np.float32 else "f64"
+    f = getattr(lib(), f"vcfo_dct{kind}_{sfx}_n")
+    if f(b.ctypes.data_as(ctypes.POINTER(ct)), N, b.shape[0]) != 0:
+        raise ValueError(f"length {N} not covered by the restatement")
+    return b.reshape(a.shape)
+
+
+def encode_frame_b(rgb: np.ndarray, B: int, Q: int = 32, flags: int = 0, k32: bool = False) -> np.ndarray:
+    """Any block size: u8 HxWx3 -> u8 HpxWpx3 (+128, wrapped) or, k32, the int32 k of the -L search."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    H, W = rgb.shape[:2]
+    Hp, Wp = padded_shape(H, W, B)
+    if k32:
+        out = np.empty((Hp, Wp, 3), np.int32)
+        rc = lib().vcfo_dct_dz_encode_k32_b(_u8(rgb), H, W, B, int(Q), flags,
+                                            out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    else:
+        out = np.empty((Hp, Wp, 3), np.uint8)
+        rc = lib().vcfo_dct_dz_encode_b(_u8(rgb), H, W, B, int(Q), flags, _u8(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle encode failed ({rc})")
+    return out
+
+
+def decode_frame_b(k: np.ndarray, H: int, W: int, B: int, Q: int = 32, flags: int = 0) -> np.ndarray:
+    """Any block size: u8 (decode_fn) or int32 (-L synthesis) HpxWpx3 -> u8 HxWx3."""
+    Hp, Wp = padded_shape(H, W, B)
+    if k.shape != (Hp, Wp, 3):
+        raise ValueError(f"index array shape {k.shape} != {(Hp, Wp, 3)}")
+    out = np.empty((H, W, 3), np.uint8)
+    if k.dtype == np.int32:
+        k = np.ascontiguousarray(k)
+        rc = lib().vcfo_dct_dz_decode_k32_b(k.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), H, W, B, int(Q),
+                                            flags, _u8(out))
+    else:
+        k = np.ascontiguousarray(k, dtype=np.uint8)
+        rc = lib().vcfo_dct_dz_decode_b(_u8(k), H, W, B, int(Q), flags, _u8(out))
     if rc != 0:
         raise RuntimeError(f"oracle decode failed ({rc})")
     return out

@@ -19,6 +19,12 @@ import warnings
 
 warnings.filterwarnings("ignore")
 
+if os.environ.get("VCF_GOLDEN_LOG") == "1":
+    # the reference's debug log (main.py:7-10) on stdout, message text only,
+    # e.g. optimize_block_size's "J=... for block_size=..." (2D-DCT.py:576)
+    import logging
+    logging.basicConfig(format="LOG %(message)s", level=logging.DEBUG, stream=sys.stdout)
+
 module, sub, in_fn, out_fn = sys.argv[1:5]
 flags = sys.argv[5:]
 sys.argv = [module + ".py", sub] + flags
@@ -30,3 +36,4 @@ codec = mod.CoDec(args)
 fn = codec.encode_fn if sub == "encode" else codec.decode_fn
 n = fn(in_fn, out_fn)
 print(f"RESULT_BYTES {n}")
+print(f"RESULT_BLOCK_SIZE {getattr(codec, 'block_size', None)}")

@@ -55,7 +55,9 @@ def test_padded_shape_is_host_only():
 
 @pytest.mark.parametrize("args,status", [
     (dict(H=0), L.VCF_ERR_INVALID),              # not an image
-    (dict(block_size=16), L.VCF_ERR_UNSUPPORTED),  # -B 16 not on the HIP path
+    (dict(block_size=5), L.VCF_ERR_UNSUPPORTED),   # -B 5: no radix-5 transform on the HIP path
+    (dict(block_size=256), L.VCF_ERR_UNSUPPORTED),  # beyond the -L range 2..128
+    (dict(block_size=16, flags=2), L.VCF_ERR_UNSUPPORTED),  # -p needs B = 8 (cv2 table resize)
     (dict(Q=0), L.VCF_ERR_INVALID),
     (dict(flags=8), L.VCF_ERR_INVALID),
     (dict(n_frames=-1), L.VCF_ERR_INVALID),
@@ -91,3 +93,10 @@ def test_product_never_imports_the_oracle():
     for p in glob.glob(os.path.join(ROOT, "vcf_amd", "**", "*.py"), recursive=True):
         src = open(p).read()
         assert "oracle" not in re.sub(r"#.*|\"\"\".*?\"\"\"", "", src, flags=re.S), p
+
+
+def test_block_size_coverage():
+    """-B sizes with a HIP transform: B = 2^a 3^b <= 128 (every -L candidate)."""
+    lib = L.lib()
+    have = [b for b in range(0, 300) if lib.vcf_dct_block_size_supported(b)]
+    assert have == [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128]

@@ -1,0 +1,89 @@
+"""The any-block-size CPU oracle against the reference's own outputs (no GPU).
+
+Pins oracle/vcf_dct_general_oracle.cpp -- the checker the generic-B GPU tests
+compare with -- to fixtures tests/golden/make_golden_general.py captured from
+the reference:
+
+  * scipy.fftpack (scipy 1.7.1, the reference's pocketfft) dct/idct with
+    norm='ortho' for every covered length 1..128, bit for bit;
+  * src/2D-DCT.py encode_fn/decode_fn (unmodified glue) at -B 1, 2, 3, 4,
+    12, 16, 32, 64, 96, 128 (padding, -x, several -q): indices and
+    reconstructions bit-exact;
+  * the -L search (optimize_block_size, 2D-DCT.py:533-579): the codec's host
+    logic (vcf_amd/codec/dct2d.py) with the oracle standing in for the GPU
+    transforms reproduces the reference's J for every candidate block size
+    and its choice.  The GPU run of the same search is in test_dct_any_gpu.py.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import oracle as O
+
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest_general.json")))
+
+
+def _qf(flags):
+    Q = int(flags[flags.index("-q") + 1]) if "-q" in flags else 32
+    B = int(flags[flags.index("-B") + 1]) if "-B" in flags else 8
+    return B, Q, (1 if "-x" in flags else 0)
+
+
+@pytest.mark.parametrize("N", MANIFEST["lengths"])
+def test_oracle_dct_lengths_vs_scipy(N):
+    g = np.load(os.path.join(GOLDEN, "blocks_general.npz"))
+    assert O.dct_supported(N)
+    fwd = O.dct_n(g[f"fwd_in_{N}"], 2, np.float32)
+    assert fwd.dtype == g[f"fwd_out_{N}"].dtype == np.float32
+    assert np.array_equal(fwd.view(np.uint32), g[f"fwd_out_{N}"].view(np.uint32))
+    inv = O.dct_n(g[f"inv_in_{N}"].astype(np.float64), 3, np.float64)
+    assert np.array_equal(inv.view(np.uint64), g[f"inv_out_{N}"].view(np.uint64))
+
+
+def test_oracle_dct_uncovered_lengths():
+    for N in (5, 7, 10, 11, 25):
+        assert not O.dct_supported(N)
+
+
+@pytest.mark.parametrize("case", MANIFEST["cases"], ids=lambda c: c["name"])
+def test_oracle_any_block_size_vs_reference(case):
+    d = np.load(os.path.join(GOLDEN, f"dct_{case['name']}.npz"))
+    B, Q, flags = _qf(case["flags"])
+    H, W = d["rgb"].shape[:2]
+    k = O.encode_frame_b(d["rgb"], B, Q, flags)
+    assert k.shape == tuple(case["k_shape"])
+    assert np.array_equal(k, d["k"])
+    assert np.array_equal(O.decode_frame_b(d["k"], H, W, B, Q, flags), d["decoded"])
+
+
+def _args(lam, extra):
+    from vcf_amd.codec import parser as P
+    argv = ["encode", "-L", lam] + extra
+    return P.dct_parser().parse_known_args(argv)[0]
+
+
+@pytest.mark.parametrize("case", MANIFEST["L_cases"], ids=lambda c: c["name"])
+def test_L_search_host_logic_with_oracle_transforms(case, monkeypatch):
+    """optimize_block_size's rate/RMSE/J bookkeeping on the host, with the
+    oracle's int32 analysis/synthesis in place of the GPU kernels."""
+    import vcf_amd.codec.dct2d as C
+    d = np.load(os.path.join(GOLDEN, f"dct_{case['name']}.npz"))
+    rgb = d["rgb"]
+    fl = case["flags"]
+    Q = int(fl[fl.index("-q") + 1]) if "-q" in fl else 32
+    monkeypatch.setattr(C.D, "encode_k32", lambda img, q, f, b: O.encode_frame_b(img, b, q, f, k32=True))
+    monkeypatch.setattr(C.D, "decode_k32", lambda k, H, W, q, f, b: O.decode_frame_b(k, H, W, b, q, f))
+    args = _args(fl[1], fl[2:])
+    args.Lambda = None                       # construct without searching ...
+    codec = C.CoDec(args)
+    codec.Lambda = float(fl[1])
+    assert codec.QSS == Q
+    chosen = codec.optimize_block_size(rgb)  # ... then search this frame
+    assert chosen == int(d["block_size"]) == case["chosen_block_size"]
+    for b, j in zip(d["J_block_sizes"], d["J"]):
+        assert codec.J[int(b)] == float(j), (b, codec.J[int(b)], float(j))
+    # and the frame encode_fn then writes at the chosen size
+    assert np.array_equal(O.encode_frame_b(rgb, chosen, Q, 0), d["k"])

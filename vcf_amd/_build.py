@@ -13,8 +13,10 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libvcf_amd.so")
-SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_quant.hip", "vcf_dwt.hip", "vcf_cbaac.cpp", "vcf_cbahc.cpp", "vcf_ipp.hip"]
-HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h", "vcf_wavelets.h"]
+SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_dct_any.hip", "vcf_quant.hip", "vcf_dwt.hip", "vcf_cbaac.cpp",
+           "vcf_cbahc.cpp", "vcf_ipp.hip"]
+HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h", "vcf_wavelets.h", "vcf_pocketfft.h"]
+OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("VCF_OFFLOAD_ARCH", "gfx950")
 
 
@@ -34,15 +36,39 @@ def needs_rebuild() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _flags():
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17",
+            # bit-exactness: pocketfft's separate multiply and add must not fuse
+            "-ffp-contract=off",
+            "-fPIC", "-Wall",
+            "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile each translation unit to an object (in parallel), then link."""
     if not force and not needs_rebuild():
         return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17",
-           # bit-exactness: pocketfft's separate multiply and add must not fuse
-           "-ffp-contract=off",
-           "-fPIC", "-shared", "-Wall",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC,
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB + ".tmp"]
+    from concurrent.futures import ThreadPoolExecutor
+    os.makedirs(OBJDIR, exist_ok=True)
+    hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
+    hdr_t = max(hdr_t, os.path.getmtime(os.path.join(ROOT, "include", "vcf_amd.h")))
+
+    def compile_one(src):
+        obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+        path = os.path.join(CSRC, src)
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(path)):
+            return obj
+        cmd = [hipcc(), *_flags(), "-c", path, "-o", obj + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "8")), os.cpu_count() or 1))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

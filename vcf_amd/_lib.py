@@ -78,6 +78,11 @@ SIGNATURES = {
     "vcf_dct_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_encode_variant": [ctypes.c_int, _P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_decode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dct_block_size_supported": [_I32],
+    "vcf_dct_dz_encode_any": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dct_dz_decode_any": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dct_dz_encode_k32": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dct_dz_decode_k32": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_wavelet_index": [ctypes.c_char_p, _PI32],
     "vcf_dwt_layout": [_I32, _I32, _I32, _PI32, _PI32, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     "vcf_dwt_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],

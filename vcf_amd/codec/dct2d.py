@@ -9,8 +9,11 @@ span between reading the image and handing the indices to the entropy codec
 libvcf_amd.so (vcf_dct_dz_encode / vcf_dct_dz_decode); there is no CPU
 implementation of it in the product.
 
+-B takes every block size the HIP path has a transform for (B = 2^a 3^b
+<= 128, vcf_dct_block_size_supported), -L runs optimize_block_size
+(2D-DCT.py:533-579) with the GPU doing each candidate's analysis/synthesis.
 Options the HIP path does not implement raise NotImplementedError when the
-codec is constructed (block sizes other than 8 incl. -L, colour transforms
+codec is constructed (other block sizes, -p with B != 8, colour transforms
 other than YCoCg, quantizers other than deadzone, filters other than
 no_filter); entropy codecs come from ENTROPY_CODECS.
 """
@@ -65,12 +68,12 @@ class CoDec(EICCoDec):
         filt = getattr(args, "filter", "no_filter")
         if not self.encoding and filt != "no_filter":
             raise NotImplementedError(f"filter {filt!r}: only no_filter is on the HIP path")
-        if self.block_size != 8:
-            raise NotImplementedError(f"block size {self.block_size}: only B=8 is on the HIP path")
-        if self.encoding and getattr(args, "Lambda", None) is not None \
-                and not getattr(args, "perceptual_quantization", False):
-            # 2D-DCT.py:93-101 -> optimize_block_size over B in {2,...,128}
-            raise NotImplementedError("-L (RD-optimized block size) needs B != 8 transforms")
+        if not D.block_size_supported(self.block_size):
+            raise NotImplementedError(f"block size {self.block_size}: the HIP path covers B = 2^a 3^b <= 128 "
+                                      "(a <= 7, b <= 1)")
+        if self.block_size != 8 and getattr(args, "perceptual_quantization", False):
+            # 2D-DCT.py:85-90 resizes the JPEG tables with cv2 for B != 8 (not on the HIP path)
+            raise NotImplementedError("-p with a block size other than 8")
         ec_name = getattr(args, "entropy_image_codec", "TIFF")
         if ec_name not in ENTROPY_CODECS:
             raise NotImplementedError(f"entropy codec {ec_name!r} (have: {sorted(ENTROPY_CODECS)})")
@@ -81,6 +84,16 @@ class CoDec(EICCoDec):
         self.offset = 128            # 2D-DCT.py:102-105 (quantizer == deadzone)
         self.flags = _flags(args)
         self.original_shape = None
+        self.Lambda = None
+        if self.encoding and getattr(args, "Lambda", None) is not None:
+            # 2D-DCT.py:99-105
+            if not getattr(args, "perceptual_quantization", False):
+                self.Lambda = float(args.Lambda)
+                logging.info("optimizing the block size")
+                self.optimize_block_size()
+                logging.info(f"optimal block_size={self.block_size}")
+            else:
+                logging.warning("sorry, perceptual quantization is only available for block_size=8")
 
     # entropy stage (TIFF.py / CBAAC.py surface)
     def compress(self, img):
@@ -108,6 +121,45 @@ class CoDec(EICCoDec):
         t = (padded_img.shape[0] - H) // 2
         l = (padded_img.shape[1] - W) // 2
         return padded_img[t:t + H, l:l + W, :]
+
+    # ---- -L: RD-optimized block size (2D-DCT.py:533-579) ---------------------
+    def optimize_block_size(self, img: np.ndarray | None = None):
+        """J = rate + Lambda * RMSE for B in 2, 4, ..., 128; the first minimum wins.
+
+        As in the reference: the frame is encode_read()'s default
+        /tmp/original.png (entropy_image_coding.py:67) unless given; the
+        search runs inside __init__ before the deadzone offset of 128 is set
+        (:99-109), so its offset is YCoCg's [0, 0, 0] (YCoCg.py:28-29) -- no
+        -128 on the pixels, no +128 on k; the candidates always use the
+        subband layout (get_subbands/get_blocks are unconditional there);
+        rate = bytes of self.compress(uint8(k)); the reconstruction comes from
+        the int32 k (no uint8 wrap), dequantized, IDCT'd and colour-converted
+        in int32 (vcf_dct_dz_decode_k32); RMSE compares it with the input
+        (:537, :572; A7).
+        A11: for frame sides that are not multiples of B the reference hands
+        the unpadded frame to DCT2D (unpinned); here each candidate pads and
+        crops exactly as encode_fn/decode_fn do."""
+        if img is None:
+            img = self.encode_read()
+        self._check_frame(img)
+        H, W = img.shape[:2]
+        x64 = img.astype(np.float32).astype(np.float64)   # img - [0, 0, 0]
+        J_min = 1000000
+        self.J = {}
+        for block_size in [2 ** i for i in range(1, 8)]:
+            k = D.encode_k32(img, self.QSS, 0, block_size)
+            cs = self.compress(k.astype(np.uint8))
+            cs.seek(0)
+            rate = len(cs.read())
+            y = D.decode_k32(k, H, W, self.QSS, 0, block_size)
+            rmse = float(np.sqrt(np.mean((x64 - y) ** 2)))
+            J = rate + self.Lambda * rmse
+            self.J[block_size] = J
+            logging.debug(f"J={J} for block_size={block_size}")
+            if J < J_min:
+                J_min = J
+                self.block_size = block_size
+        return self.block_size
 
     # ---- the hot path -------------------------------------------------------
     def _check_frame(self, img):

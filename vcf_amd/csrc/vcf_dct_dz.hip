@@ -526,8 +526,7 @@ int check_args(const void *a, const void *b, int64_t n_frames, int32_t H, int32_
     if (H <= 0 || W <= 0)
         return set_error(VCF_ERR_INVALID, "Input image must be a 3D array (height, width, channels).");
     if (block_size != 8)
-        return set_error(VCF_ERR_UNSUPPORTED, "block_size %d: only B=8 is implemented on the HIP path",
-                         block_size);
+        return set_error(VCF_ERR_INVALID, "block_size %d: the 8x8 kernels need B=8", block_size);
     if (Q < 1 || (decode && Q > 32767))
         return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
     // the fp32 divisor Q*2^6 must be exact for a general (non power-of-two) Q
@@ -580,6 +579,8 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t W, int32_t block_size, int32_t Q, uint32_t flags,
                               uint8_t *k_dev, void *stream)
 {
+    if (block_size != 8 && variant == 0)   // -B other than 8: vcf_dct_any.hip
+        return dct_any_encode_u8(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, stream);
     int rc = check_args(rgb_dev, k_dev, n_frames, H, W, block_size, Q, flags, false);
     if (rc != VCF_OK) return rc;
     if (variant < 0 || variant > 4) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
@@ -629,6 +630,8 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
 int vcf_dct_dz_decode(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream)
 {
+    if (block_size != 8)   // -B other than 8: vcf_dct_any.hip
+        return dct_any_decode_u8(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, stream);
     int rc = check_args(k_dev, rgb_dev, n_frames, H, W, block_size, Q, flags, true);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;

@@ -1,9 +1,11 @@
-"""DCT(B=8) + deadzone hot path on the GPU (include/vcf_amd.h vcf_dct_dz_*).
+"""DCT + deadzone hot path on the GPU (include/vcf_amd.h vcf_dct_dz_*).
 
 Replaces, in one fused kernel per direction, the numpy/scipy span of
 src/2D-DCT.py encode_fn :276-361 (to the uint8 indices handed to the entropy
 codec) and decode_fn :399-466 (from the entropy decoder's uint8 array to the
-clipped RGB frame).
+clipped RGB frame).  B = 8 runs the fused 8x8 kernels; the other -B sizes
+(block_size_supported) the generic-B kernels.  encode_k32/decode_k32 are the
+int32 analysis/synthesis of the -L search (optimize_block_size :533-579).
 """
 from __future__ import annotations
 
@@ -16,7 +18,12 @@ from ._lib import VCF_DCT_NO_SUBBANDS, VCF_DCT_PERCEPTUAL, call
 from .device import DeviceBuffer, _h
 
 __all__ = ["padded_shape", "flags_from", "encode_device", "decode_device", "encode", "decode",
-           "VCF_DCT_NO_SUBBANDS", "VCF_DCT_PERCEPTUAL"]
+           "block_size_supported", "encode_k32", "decode_k32", "VCF_DCT_NO_SUBBANDS", "VCF_DCT_PERCEPTUAL"]
+
+
+def block_size_supported(block_size: int) -> bool:
+    """True if the HIP path has a transform of this length (B = 2^a 3^b <= 128)."""
+    return bool(_lib.lib().vcf_dct_block_size_supported(int(block_size)))
 
 
 def padded_shape(H: int, W: int, block_size: int = 8):
@@ -34,7 +41,8 @@ def encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32,
                   variant: int = 0) -> DeviceBuffer:
     """Frames resident in HBM -> coefficient frames in HBM (asynchronous on `stream`).
 
-    variant: 0 automatic, 1 LDS-staged tile kernel, 2 register kernel (see vcf_amd.h)."""
+    variant: 0 automatic, 1 LDS-staged tile kernel, 3 column-per-lane kernel (see vcf_amd.h),
+    -1 the generic-B kernels (any supported B, 8 included)."""
     Hp, Wp = padded_shape(H, W, block_size)
     if rgb.nbytes < n_frames * H * W * 3:
         raise ValueError("input buffer too small")
@@ -42,13 +50,18 @@ def encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32,
         out = DeviceBuffer(n_frames * Hp * Wp * 3)
     elif out.nbytes < n_frames * Hp * Wp * 3:
         raise ValueError("output buffer too small")
-    call("vcf_dct_dz_encode_variant", variant, rgb.ptr, n_frames, H, W, block_size, int(Q), flags,
-         out.ptr, _h(stream))
+    if variant == -1:
+        call("vcf_dct_dz_encode_any", rgb.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
+    else:
+        call("vcf_dct_dz_encode_variant", variant, rgb.ptr, n_frames, H, W, block_size, int(Q), flags,
+             out.ptr, _h(stream))
     return out
 
 
 def decode_device(k: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32, flags: int = 0,
-                  out: DeviceBuffer | None = None, stream=None, block_size: int = 8) -> DeviceBuffer:
+                  out: DeviceBuffer | None = None, stream=None, block_size: int = 8,
+                  variant: int = 0) -> DeviceBuffer:
+    """variant: 0 automatic, -1 the generic-B kernels (any supported B, 8 included)."""
     Hp, Wp = padded_shape(H, W, block_size)
     if k.nbytes < n_frames * Hp * Wp * 3:
         raise ValueError("input buffer too small")
@@ -56,7 +69,8 @@ def decode_device(k: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32, f
         out = DeviceBuffer(n_frames * H * W * 3)
     elif out.nbytes < n_frames * H * W * 3:
         raise ValueError("output buffer too small")
-    call("vcf_dct_dz_decode", k.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
+    name = "vcf_dct_dz_decode_any" if variant == -1 else "vcf_dct_dz_decode"
+    call(name, k.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
     return out
 
 
@@ -86,7 +100,8 @@ def encode(rgb: np.ndarray, Q: int = 32, flags: int = 0, block_size: int = 8,
     return res[0] if single else res
 
 
-def decode(k: np.ndarray, H: int, W: int, Q: int = 32, flags: int = 0, block_size: int = 8) -> np.ndarray:
+def decode(k: np.ndarray, H: int, W: int, Q: int = 32, flags: int = 0, block_size: int = 8,
+           variant: int = 0) -> np.ndarray:
     """Host convenience: HpxWpx3 (or N...) u8 indices -> HxWx3 u8 reconstruction."""
     single = np.asarray(k).ndim == 3
     f = _frames(k, "k")
@@ -95,7 +110,42 @@ def decode(k: np.ndarray, H: int, W: int, Q: int = 32, flags: int = 0, block_siz
     if f.shape[1:3] != (Hp, Wp):
         raise ValueError(f"index frames {f.shape[1:3]} do not match {(Hp, Wp)} for {H}x{W}")
     din = DeviceBuffer.from_array(f)
-    dout = decode_device(din, n, H, W, Q, flags, block_size=block_size)
+    dout = decode_device(din, n, H, W, Q, flags, block_size=block_size, variant=variant)
+    res = dout.download(np.empty((n, H, W, 3), np.uint8))
+    din.free()
+    dout.free()
+    return res[0] if single else res
+
+
+def encode_k32(rgb: np.ndarray, Q: int = 32, flags: int = 0, block_size: int = 8) -> np.ndarray:
+    """-L analysis (2D-DCT.py:538-545): HxWx3 (or N...) u8 -> HpxWpx3 int32 k, before +128/uint8."""
+    single = np.asarray(rgb).ndim == 3
+    f = _frames(rgb, "rgb")
+    n, H, W, _ = f.shape
+    Hp, Wp = padded_shape(H, W, block_size)
+    din = DeviceBuffer.from_array(f)
+    dout = DeviceBuffer(n * Hp * Wp * 3 * 4)
+    call("vcf_dct_dz_encode_k32", din.ptr, n, H, W, block_size, int(Q), flags, dout.ptr, None)
+    res = dout.download(np.empty((n, Hp, Wp, 3), np.int32))
+    din.free()
+    dout.free()
+    return res[0] if single else res
+
+
+def decode_k32(k: np.ndarray, H: int, W: int, Q: int = 32, flags: int = 0, block_size: int = 8) -> np.ndarray:
+    """-L synthesis (2D-DCT.py:560-568): HpxWpx3 (or N...) int32 k -> HxWx3 u8."""
+    k = np.asarray(k)
+    if k.dtype != np.int32:
+        raise TypeError(f"k must be int32, got {k.dtype}")
+    single = k.ndim == 3
+    f = np.ascontiguousarray(k[None] if single else k)
+    n = f.shape[0]
+    Hp, Wp = padded_shape(H, W, block_size)
+    if f.shape[1:] != (Hp, Wp, 3):
+        raise ValueError(f"index frames {f.shape[1:]} do not match {(Hp, Wp, 3)} for {H}x{W}")
+    din = DeviceBuffer.from_array(f)
+    dout = DeviceBuffer(n * H * W * 3)
+    call("vcf_dct_dz_decode_k32", din.ptr, n, H, W, block_size, int(Q), flags, dout.ptr, None)
     res = dout.download(np.empty((n, H, W, 3), np.uint8))
     din.free()
     dout.free()
