@@ -207,6 +207,27 @@ int vcf_ipp_residual(const uint8_t *cur_dev, const uint8_t *comp_dev, int64_t n,
 /* recon = clip(comp + rec - 128, 0, 255) (IPP_DCT.py:559-561, 788-790). */
 int vcf_ipp_reconstruct(const uint8_t *comp_dev, const uint8_t *rec_dev, int64_t n, uint8_t *out_dev, void *stream);
 
+/* -R block-level RDO of IPP.temporal_filter (IPP_DCT.py:441-536): for every
+ * full bs x bs block, IPP.rdo_block_decision (:290-342) on the cv2 RGB2GRAY
+ * luma of cur and of its motion compensation comp -- float64 pocketfft DCT,
+ * round(x / Q) to int16, float32 dequantization and IDCT, numpy-pairwise
+ * mean squared error, get_rate (:265-288) -- and the mode with the smaller
+ * D + lambda R (ties to inter).  modes_dev: (H/bs) x (W/bs) u8, 1 = I
+ * (intra), 0 = P; costs_dev (NULL or 4 doubles per block): D_inter,
+ * R_inter, D_intra, R_intra.  bs in {2, 4, 8, 12, 16, 24, 32}. */
+int vcf_ipp_rdo_modes(const uint8_t *cur_dev, const uint8_t *comp_dev, int32_t H, int32_t W, int32_t bs, int32_t Q,
+                      double lambda, uint8_t *modes_dev, double *costs_dev, void *stream);
+
+/* The frame -R hands to the spatial codec (:489-505): P blocks
+ * clip(cur - comp + 128), I blocks cur, pixels outside full blocks 128. */
+int vcf_ipp_rdo_residual(const uint8_t *cur_dev, const uint8_t *comp_dev, const uint8_t *modes_dev, int32_t H,
+                         int32_t W, int32_t bs, uint8_t *out_dev, void *stream);
+
+/* Mode-aware reconstruction (:512-526, decoder :770-790): P blocks
+ * clip(comp + rec - 128), I blocks rec, pixels outside full blocks 0. */
+int vcf_ipp_rdo_reconstruct(const uint8_t *comp_dev, const uint8_t *rec_dev, const uint8_t *modes_dev, int32_t H,
+                            int32_t W, int32_t bs, uint8_t *out_dev, void *stream);
+
 /* ---- CBAAC entropy codec (CBAAC.py), host code --------------------------------- */
 
 /* Worst-case code-stream bytes for n symbols. */

@@ -64,6 +64,8 @@ def lib():
                                            ctypes.c_uint, u8p]
         L.vcfo_dct_dz_encode_k32_b.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_uint, i32p]
+        L.vcfo_ipp_rdo_modes.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_double, u8p, dp]
         L.vcfo_dct_dz_decode_k32_b.argtypes = [i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_uint, u8p]
         L.vcfo_perceptual_weights.argtypes = [dp]
@@ -347,6 +349,43 @@ def ipp_motion_compensate(frame, mv, bs=16) -> np.ndarray:
     out = np.empty_like(frame)
     H, W = frame.shape[:2]
     lib().vcfo_ipp_mc(_u8(frame), mv.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), H, W, bs, _u8(out))
+    return out
+
+
+def ipp_rdo_modes(cur, comp, bs=16, qss=32, lam=1.0, with_costs=False):
+    """IPP -R block modes (1 = I, 0 = P) of cur against its compensation comp."""
+    cur, comp = np.ascontiguousarray(cur, np.uint8), np.ascontiguousarray(comp, np.uint8)
+    H, W = cur.shape[:2]
+    modes = np.zeros((H // bs, W // bs), np.uint8)
+    costs = np.zeros((H // bs, W // bs, 4), np.float64)
+    rc = lib().vcfo_ipp_rdo_modes(_u8(cur), _u8(comp), H, W, bs, int(qss), float(lam), _u8(modes),
+                                  costs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    if rc != 0:
+        raise RuntimeError(f"oracle rdo failed ({rc})")
+    return (modes, costs) if with_costs else modes
+
+
+def ipp_rdo_residual(cur, comp, modes, bs=16):
+    """:489-505: P blocks clip(cur - comp + 128), I blocks cur, outside full blocks 128."""
+    H, W = cur.shape[:2]
+    out = np.full_like(cur, 128)
+    for by in range(H // bs):
+        for bx in range(W // bs):
+            sl = (slice(by * bs, (by + 1) * bs), slice(bx * bs, (bx + 1) * bs))
+            c = cur[sl].astype(np.int32)
+            out[sl] = c if modes[by, bx] else np.clip(c - comp[sl].astype(np.int32) + 128, 0, 255)
+    return out
+
+
+def ipp_rdo_reconstruct(comp, rec, modes, bs=16):
+    """:512-526: P blocks clip(comp + rec - 128), I blocks rec, outside full blocks 0."""
+    H, W = comp.shape[:2]
+    out = np.zeros_like(comp)
+    for by in range(H // bs):
+        for bx in range(W // bs):
+            sl = (slice(by * bs, (by + 1) * bs), slice(bx * bs, (bx + 1) * bs))
+            r = rec[sl].astype(np.int32)
+            out[sl] = r if modes[by, bx] else np.clip(comp[sl].astype(np.int32) + r - 128, 0, 255)
     return out
 
 

@@ -93,6 +93,9 @@ SIGNATURES = {
     "vcf_ipp_motion_compensate": [_P, _P, _I32, _I32, _I32, _P, _P],
     "vcf_ipp_residual": [_P, _P, _I64, _P, _P],
     "vcf_ipp_reconstruct": [_P, _P, _I64, _P, _P],
+    "vcf_ipp_rdo_modes": [_P, _P, _I32, _I32, _I32, _I32, ctypes.c_double, _P, _P, _P],
+    "vcf_ipp_rdo_residual": [_P, _P, _P, _I32, _I32, _I32, _P, _P],
+    "vcf_ipp_rdo_reconstruct": [_P, _P, _P, _I32, _I32, _I32, _P, _P],
     "vcf_cbaac_bound": [_I64],
     "vcf_cbaac_encode": [_P, _I64, _I32, _P, _I64, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     "vcf_cbaac_decode": [_P, _I64, _I64, _I32, _P],

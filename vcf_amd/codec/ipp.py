@@ -17,8 +17,12 @@ memory (PNG is lossless, so the reconstruction is identical).
 GOPs are independent, so they shard over ranks (one process per GPU); the
 per-frame sizes and motion fields are gathered on rank 0, which writes the
 metadata (at most ceil(N/G) ranks are busy).
---rdo_lambda > 0 (block mode decision, :294-342) is not implemented
-(SURVEY.md §8(f) row 4).
+-R/--rdo_lambda > 0 runs the block-level mode decision on the GPU
+(vcf_amd/csrc/vcf_ipp_rdo.hip: rdo_block_decision :290-342 per block, the
+mixed-mode frame :489-505 and its reconstruction :512-526); the motion file
+then also carries each P frame's mode map, like the reference's
+{"mv", "modes"} entries, and the decoder reconstructs mode by mode
+(:770-790).
 """
 from __future__ import annotations
 
@@ -94,8 +98,6 @@ class CoDec(DCTCoDec):
             self.search_range = 8
         self.use_fast = bool(getattr(args, "fast", False))
         self.rdo_lambda = float(getattr(args, "rdo_lambda", 0.0) or 0.0)
-        if self.encoding and self.rdo_lambda > 0:
-            raise NotImplementedError("-R/--rdo_lambda > 0 (block-level RDO mode decision) is not on the HIP path")
         self.prefix = resolve_prefix(args.output) if getattr(args, "output", None) else None
         self.group = group if group is not None else shard.Group()
 
@@ -117,7 +119,7 @@ class CoDec(DCTCoDec):
         return recon, size
 
     def _gop(self, frames, g0, i_idx, p0):
-        """One GOP: I-frame then P-frames (IPP.temporal_filter :397-575, no RDO)."""
+        """One GOP: I-frame then P-frames (IPP.temporal_filter :397-575)."""
         bs = self.block_size_ME
         recon_I, bits_I = self.encode_decode_proxy(frames[g0], "I", i_idx)
         I = {"bits": bits_I, "idx": g0}
@@ -127,11 +129,22 @@ class CoDec(DCTCoDec):
             cur = frames[g0 + p]
             mv = K.block_matching(ref, cur, bs, self.search_range, self.use_fast)
             comp = K.motion_compensate(ref, mv, bs)
-            res = K.residual(cur, comp)
-            rec_res, bits_P = self.encode_decode_proxy(res, "P", p0 + p - 1)
-            ref = K.reconstruct(comp, rec_res)
+            if self.rdo_lambda > 0:
+                # :441-536: per-block I/P decision, the mixed-mode frame, its reconstruction
+                modes = K.rdo_modes(cur, comp, bs, self.QSS, self.rdo_lambda)
+                res = K.rdo_residual(cur, comp, modes, bs)
+                rec_res, bits_P = self.encode_decode_proxy(res, "P", p0 + p - 1)
+                ref = K.rdo_reconstruct(comp, rec_res, modes, bs)
+                n_i = int(modes.sum())
+                logging.info(f"  RDO (λ={self.rdo_lambda}): {n_i}/{modes.size} I-blocks, "
+                             f"{modes.size - n_i}/{modes.size} P-blocks")
+                mvs.append({"mv": mv, "modes": modes})
+            else:
+                res = K.residual(cur, comp)
+                rec_res, bits_P = self.encode_decode_proxy(res, "P", p0 + p - 1)
+                ref = K.reconstruct(comp, rec_res)
+                mvs.append(mv)
             P.append({"bits": bits_P})
-            mvs.append(mv)
             recon.append(ref)
         return I, P, mvs, recon
 
@@ -153,9 +166,13 @@ class CoDec(DCTCoDec):
             local.append(self._gop(frames, g0, gi, gi * (self.gop_size - 1)))
         # gather per-GOP results on rank 0 (sizes as JSON, motion fields as bytes)
         blob = json.dumps([[I, P] for I, P, _, _ in local]).encode()
-        mvbytes = b"".join(m.astype(np.float32).tobytes() for _, _, mvs, _ in local for m in mvs)
+        rdo = self.rdo_lambda > 0
+        mv_of = (lambda m: m["mv"]) if rdo else (lambda m: m)
+        mvbytes = b"".join(mv_of(m).astype(np.float32).tobytes() for _, _, mvs, _ in local for m in mvs)
         infos = self._gather(blob)
         mvs_all = self._gather(mvbytes)
+        if rdo:
+            modes_all = self._gather(b"".join(m["modes"].tobytes() for _, _, mvs, _ in local for m in mvs))
         if g.rank != 0:
             return None
         I_infos, P_infos = [], []
@@ -166,10 +183,18 @@ class CoDec(DCTCoDec):
         hb, wb = self.height // self.block_size_ME, self.width // self.block_size_ME
         mv = np.frombuffer(b"".join(mvs_all), np.float32).reshape(len(P_infos), hb, wb, 2)
         mv_path = f"{self.prefix}_mv.npz"
-        obj = np.empty(len(P_infos), dtype=object)
-        for i in range(len(P_infos)):
-            obj[i] = mv[i]
-        np.savez_compressed(mv_path, mv=np.array(list(obj), dtype=object), mv_f32=mv)
+        if rdo:
+            # the reference's entries are {"mv": field, "modes": map} (:529)
+            modes = np.frombuffer(b"".join(modes_all), np.uint8).reshape(len(P_infos), hb, wb)
+            obj = np.empty(len(P_infos), dtype=object)
+            for i in range(len(P_infos)):
+                obj[i] = {"mv": mv[i], "modes": modes[i]}
+            np.savez_compressed(mv_path, mv=obj, mv_f32=mv, modes_u8=modes)
+        else:
+            obj = np.empty(len(P_infos), dtype=object)
+            for i in range(len(P_infos)):
+                obj[i] = mv[i]
+            np.savez_compressed(mv_path, mv=np.array(list(obj), dtype=object), mv_f32=mv)
         total_bits = sum(i["bits"] for i in I_infos) + sum(p["bits"] for p in P_infos)
         total_bits += os.path.getsize(mv_path) * 8
         self.total_bits = total_bits
@@ -198,6 +223,7 @@ class CoDec(DCTCoDec):
                 raise NotImplementedError(f"{mv_path}: motion fields stored only as a pickled object array "
                                           "(written by the reference); re-encode or convert to 'mv_f32'")
             mvs = z["mv_f32"]
+            modes = z["modes_u8"] if "modes_u8" in z.files else None
         out_prefix = resolve_prefix(self.args.output)
         _ensure_dir(out_prefix)
         gop, N = meta["gop_size"], meta["n_frames"]
@@ -211,7 +237,10 @@ class CoDec(DCTCoDec):
             for p in range(1, min(gop, N - g0)):
                 rec_res = self._decode_frame(f"{in_prefix}_P_{p_idx}_enc")
                 pred = K.motion_compensate(ref, mvs[p_idx], bs)
-                ref = K.reconstruct(pred, rec_res)
+                if modes is not None:   # RDO was used: mode-aware reconstruction (:770-790)
+                    ref = K.rdo_reconstruct(pred, rec_res, modes[p_idx], bs)
+                else:
+                    ref = K.reconstruct(pred, rec_res)
                 recon.append(ref)
                 p_idx += 1
         for idx, img in enumerate(recon):

@@ -1,0 +1,127 @@
+// vcf_pocketfft_tables.h -- the twiddle tables vcf_pocketfft.h's transforms
+// read: pocketfft's sincos_2pibyn values (computed on the host in double,
+// exactly as pocketfft computes them) for every covered length, uploaded once
+// per device into __constant__ memory.  Each translation unit that includes
+// this gets its own copy of the tables (no relocatable device code).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <mutex>
+
+#include "vcf_amd.h"
+#include "vcf_internal.h"
+#include "vcf_pocketfft.h"
+
+namespace vcf {
+namespace {
+
+constexpr int kSlot = 264;     // >= tw_len + N + 1 for N <= 128
+constexpr int kNumSlots = 14;
+
+// supported lengths and their table slots
+constexpr int kLens[kNumSlots] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128};
+constexpr int slot_of(int n)
+{
+    for (int i = 0; i < kNumSlots; ++i)
+        if (kLens[i] == n) return i;
+    return -1;
+}
+
+__constant__ float c_tw_f32[kNumSlots * kSlot];
+__constant__ double c_tw_f64[kNumSlots * kSlot];
+
+// ---- host: pocketfft sincos_2pibyn<T>(n)[idx].{r,i} (values in double) ----
+void sc_calc(size_t x, size_t n, double ang, double &re, double &im)
+{
+    x <<= 3;
+    if (x < 4 * n) {
+        if (x < 2 * n) {
+            if (x < n) { re = std::cos(double(x) * ang); im = std::sin(double(x) * ang); return; }
+            re = std::sin(double(2 * n - x) * ang); im = std::cos(double(2 * n - x) * ang); return;
+        }
+        x -= 2 * n;
+        if (x < n) { re = -std::sin(double(x) * ang); im = std::cos(double(x) * ang); return; }
+        re = -std::cos(double(2 * n - x) * ang); im = std::sin(double(2 * n - x) * ang); return;
+    }
+    x = 8 * n - x;
+    if (x < 2 * n) {
+        if (x < n) { re = std::cos(double(x) * ang); im = -std::sin(double(x) * ang); return; }
+        re = std::sin(double(2 * n - x) * ang); im = -std::cos(double(2 * n - x) * ang); return;
+    }
+    x -= 4 * n;
+    if (x < n) { re = -std::sin(double(x) * ang); im = -std::cos(double(x) * ang); return; }
+    re = -std::cos(double(2 * n - x) * ang); im = -std::sin(double(2 * n - x) * ang);
+}
+
+// value pocketfft hands out for index idx of a table of length n (cast to T)
+template <typename T> void sincos_2pibyn(size_t n, size_t idx, T &re_out, T &im_out)
+{
+    const long double pi = 3.141592653589793238462643383279502884197L;
+    const double ang = double(0.25L * pi / (long double)n);
+    const size_t nval = (n + 2) / 2;
+    size_t shift = 1;
+    while ((size_t(1) << shift) * (size_t(1) << shift) < nval) ++shift;
+    const size_t mask = (size_t(1) << shift) - 1;
+    bool conj = false;
+    if (2 * idx > n) { idx = n - idx; conj = true; }
+    double r1 = 1.0, i1 = 0.0, r2 = 1.0, i2 = 0.0;
+    if (idx & mask) sc_calc(idx & mask, n, ang, r1, i1);
+    if (idx >> shift) sc_calc((idx >> shift) * (mask + 1), n, ang, r2, i2);
+    re_out = T(r1 * r2 - i1 * i2);
+    T im = T(r1 * i2 + i1 * r2);
+    im_out = conj ? -im : im;
+}
+
+// One slot: rfftp<T>::comp_twiddle values, T_dcst23's twiddle, fct.
+template <typename T> void fill_slot(int n, T *slot)
+{
+    const pfft::Factors F = pfft::factorize(n);
+    size_t l1 = 1;
+    for (int k = 0; k < F.n; ++k) {
+        const int ip = F.f[k], ido = n / ((int)l1 * ip);
+        if (k < F.n - 1)
+            for (int j = 1; j < ip; ++j)
+                for (int i = 1; i <= (ido - 1) / 2; ++i) {
+                    T re, im;
+                    sincos_2pibyn<T>((size_t)n, (size_t)j * l1 * i, re, im);
+                    slot[F.tw_off[k] + (j - 1) * (ido - 1) + 2 * i - 2] = re;
+                    slot[F.tw_off[k] + (j - 1) * (ido - 1) + 2 * i - 1] = im;
+                }
+        l1 *= ip;
+    }
+    for (int i = 0; i < n; ++i) {
+        T re, im;
+        sincos_2pibyn<T>(4 * (size_t)n, (size_t)i + 1, re, im);
+        slot[F.tw_len + i] = re;
+    }
+    slot[F.tw_len + n] = T(1 / std::sqrt((long double)(2 * n)));   // pypocketfft norm_fct
+}
+
+int ensure_tables()
+{
+    static std::mutex mu;
+    static bool done[64] = {};
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc != VCF_OK) return rc;
+    if (dev < 0 || dev >= 64) return set_error(VCF_ERR_INVALID, "device %d", dev);
+    std::lock_guard<std::mutex> lock(mu);
+    if (done[dev]) return VCF_OK;
+    static float tf[kNumSlots * kSlot];
+    static double td[kNumSlots * kSlot];
+    for (int s = 0; s < kNumSlots; ++s) {
+        fill_slot<float>(kLens[s], tf + s * kSlot);
+        fill_slot<double>(kLens[s], td + s * kSlot);
+    }
+    rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_tw_f32), tf, sizeof(tf)), "twiddle upload");
+    if (rc != VCF_OK) return rc;
+    rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_tw_f64), td, sizeof(td)), "twiddle upload");
+    if (rc != VCF_OK) return rc;
+    done[dev] = true;
+    return VCF_OK;
+}
+
+
+}  // namespace
+}  // namespace vcf

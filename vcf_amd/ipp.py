@@ -75,3 +75,55 @@ def residual(cur: np.ndarray, comp: np.ndarray) -> np.ndarray:
 def reconstruct(comp: np.ndarray, rec: np.ndarray) -> np.ndarray:
     """clip(comp + rec - 128, 0, 255) as uint8 (IPP_DCT.py:559-561)."""
     return _binary("vcf_ipp_reconstruct", comp, rec)
+
+
+def rdo_modes(cur: np.ndarray, comp: np.ndarray, bs: int = 16, Q: int = 32, lam: float = 0.0,
+              with_costs: bool = False):
+    """-R block modes (IPP_DCT.py:441-468 + rdo_block_decision :290-342): (H//bs, W//bs) u8, 1 = I, 0 = P."""
+    cur, comp = _rgb(cur), _rgb(comp)
+    if cur.shape != comp.shape:
+        raise ValueError("shape mismatch")
+    H, W = cur.shape[:2]
+    modes = np.zeros((H // bs, W // bs), np.uint8)
+    costs = np.zeros((H // bs, W // bs, 4), np.float64)
+    if modes.size == 0:
+        return (modes, costs) if with_costs else modes
+    dc, dp = DeviceBuffer.from_array(cur), DeviceBuffer.from_array(comp)
+    dm, dk = DeviceBuffer(modes.nbytes), DeviceBuffer(costs.nbytes)
+    try:
+        L.call("vcf_ipp_rdo_modes", dc.ptr, dp.ptr, H, W, int(bs), int(Q), float(lam), dm.ptr, dk.ptr, None)
+        dm.download(modes)
+        dk.download(costs)
+        return (modes, costs) if with_costs else modes
+    finally:
+        for b in (dc, dp, dm, dk):
+            b.free()
+
+
+def _modal(name, a, b, modes, bs):
+    a, b = _rgb(a), _rgb(b)
+    if a.shape != b.shape:
+        raise ValueError("shape mismatch")
+    H, W = a.shape[:2]
+    m = np.ascontiguousarray(modes, np.uint8)
+    if m.shape != (H // bs, W // bs):
+        raise ValueError(f"mode map shape {m.shape} != {(H // bs, W // bs)}")
+    out = np.empty_like(a)
+    da, db, do = DeviceBuffer.from_array(a), DeviceBuffer.from_array(b), DeviceBuffer(a.nbytes)
+    dm = DeviceBuffer.from_array(m if m.size else np.zeros(1, np.uint8))
+    try:
+        L.call(name, da.ptr, db.ptr, dm.ptr, H, W, int(bs), do.ptr, None)
+        return do.download(out)
+    finally:
+        for x in (da, db, do, dm):
+            x.free()
+
+
+def rdo_residual(cur: np.ndarray, comp: np.ndarray, modes: np.ndarray, bs: int = 16) -> np.ndarray:
+    """frame_to_encode_shifted (IPP_DCT.py:489-505)."""
+    return _modal("vcf_ipp_rdo_residual", cur, comp, modes, bs)
+
+
+def rdo_reconstruct(comp: np.ndarray, rec: np.ndarray, modes: np.ndarray, bs: int = 16) -> np.ndarray:
+    """Mode-aware P-frame reconstruction (IPP_DCT.py:512-526, 770-790)."""
+    return _modal("vcf_ipp_rdo_reconstruct", comp, rec, modes, bs)
