@@ -265,6 +265,19 @@ int vcf_cbahc_encode(const uint8_t *symbols, int64_t n, int32_t order, uint8_t *
 /* Inverse (CBAHC.py:226-276): n symbols from the first nbits bits. */
 int vcf_cbahc_decode(const uint8_t *bytes, int64_t nbits, int64_t n, int32_t order, uint8_t *symbols_out);
 
+/* ---- frame ingest: PNG reader (host code) ------------------------------------ */
+
+/* Size of a PNG in memory and whether vcf_png_decode_rgb covers it (bit
+ * depth 8, colour type 0/2/3/4/6, not interlaced). */
+int vcf_png_info(const uint8_t *data, int64_t nbytes, int32_t *H, int32_t *W, int32_t *supported);
+
+/* PNG bytes -> H x W x 3 RGB u8 (host buffer of out_capacity bytes): what
+ * EIC.encode_read_fn reads (entropy_image_coding.py:51-65; A9: PIL's
+ * convert("RGB") -- gray replicated, alpha dropped, palette looked up).
+ * VCF_ERR_UNSUPPORTED for PNGs outside vcf_png_info's set (the caller falls
+ * back to another reader), VCF_ERR_INVALID for corrupt files. */
+int vcf_png_decode_rgb(const uint8_t *data, int64_t nbytes, uint8_t *rgb_out, int64_t out_capacity);
+
 /* ---- deadzone quantizer plug-in (deadzone.py:95-117, assumption A5) ---------- */
 
 /* k[i] = (int32)(x[i] / Q), truncation toward zero; the division is float32

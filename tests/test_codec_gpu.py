@@ -157,3 +157,23 @@ def test_dct_codec_with_context_coders(tmp_path, monkeypatch, ec, ext):
     CoDec(_args("decode", ["-c", ec])).decode_fn(enc, dec)
     k = O.encode_frame(rgb, 32, 0)
     assert np.array_equal(np.asarray(Image.open(dec)), O.decode_frame(k, 40, 48, 32, 0))
+
+
+@pytest.mark.parametrize("n,batch", [(7, 3), (5, 8), (9, 2)])
+def test_staged_pipeline_equals_single_frames(tmp_path, n, batch):
+    """encode_fns through the pinned double-buffered slots (equal-shaped PNGs)
+    writes exactly what encode_fn writes frame by frame."""
+    from vcf_amd.codec.dct2d import CoDec
+    rng = np.random.default_rng(n * 10 + batch)
+    pairs = []
+    for i in range(n):
+        src = _png(tmp_path / f"in_{i}.png", rng.integers(0, 256, (40, 56, 3), dtype=np.uint8))
+        pairs.append((src, str(tmp_path / f"enc_{i}")))
+    c = CoDec(_args("encode"))
+    sizes = c.encode_fns(pairs, batch=batch, io_threads=4)
+    for i, (src, out) in enumerate(pairs):
+        ref = str(tmp_path / f"ref_{i}")
+        m = CoDec(_args("encode")).encode_fn(src, ref)
+        assert sizes[i] == m
+        assert open(out + ".tif", "rb").read() == open(ref + ".tif", "rb").read()
+        assert open(out + "_shape.bin", "rb").read() == open(ref + "_shape.bin", "rb").read()

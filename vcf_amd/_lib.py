@@ -103,6 +103,8 @@ SIGNATURES = {
     "vcf_cbahc_bound": [_I64],
     "vcf_cbahc_encode": [_P, _I64, _I32, _P, _I64, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     "vcf_cbahc_decode": [_P, _I64, _I64, _I32, _P],
+    "vcf_png_info": [_P, _I64, _PI32, _PI32, _PI32],
+    "vcf_png_decode_rgb": [_P, _I64, _P, _I64],
     "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],
     "vcf_deadzone_dequantize": [_P, _I32, _I64, _I32, _P, _P],
 }

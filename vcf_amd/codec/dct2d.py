@@ -95,6 +95,13 @@ class CoDec(EICCoDec):
             else:
                 logging.warning("sorry, perceptual quantization is only available for block_size=8")
 
+    def bye(self):
+        st = getattr(self, "_staged", None)
+        if st is not None:
+            st[1].close()
+            self._staged = None
+        super().bye()
+
     # entropy stage (TIFF.py / CBAAC.py surface)
     def compress(self, img):
         return self.entropy.compress(img)
@@ -203,18 +210,43 @@ class CoDec(EICCoDec):
         return self.decode_fn(in_fn, out_fn)
 
     # ---- batched frames (III runner): one launch per batch of equal shapes --
-    def encode_fns(self, pairs, batch: int = 64, io_threads: int = 8):
+    def encode_fns(self, pairs, batch: int = 64, io_threads: int = 16):
         """encode_fn over (in_fn, out_fn) pairs; returns the bytes written per
-        frame.  Frames of equal shape share one GPU launch; PNG decode and
-        TIFF deflate run on a host thread pool."""
+        frame.  A three-stage pipeline: host threads
+        decode the PNGs of the next two batches while the GPU encodes this
+        one (one launch per group of equal shapes), and TIFF deflate + file
+        writes of the previous batches run behind it on the same pool.  When
+        every input is a PNG of one shape the natively decodable kind, the
+        frames go through pinned double-buffered slots (staging.StagedEncoder):
+        decoded straight into page-locked memory, async copies, no stacking."""
         pairs = list(pairs)
+        if not pairs:
+            return []
+        staged = self._encode_fns_staged(pairs, batch, io_threads)
+        if staged is not None:
+            return staged
         sizes = [0] * len(pairs)
+        batches = [pairs[b0:b0 + batch] for b0 in range(0, len(pairs), batch)]
+
+        def _read(p):
+            img = self.encode_read_fn(p[0])
+            self._check_frame(img)
+            return img
+
+        def _write(out_fn, img_shape, k):
+            with open(f"{out_fn}_shape.bin", "wb") as f:
+                f.write(struct.pack("iii", *img_shape))
+            return self.encode_write_fn(self.compress(k), out_fn)
+
         with ThreadPoolExecutor(max_workers=io_threads) as pool:
-            for b0 in range(0, len(pairs), batch):
-                chunk = pairs[b0:b0 + batch]
-                imgs = list(pool.map(lambda p: self.encode_read_fn(p[0]), chunk))
-                for img in imgs:
-                    self._check_frame(img)
+            reads = {}
+            for b in range(min(2, len(batches))):
+                reads[b] = [pool.submit(_read, p) for p in batches[b]]
+            writes = []
+            for b, chunk in enumerate(batches):
+                imgs = [f.result() for f in reads.pop(b)]
+                if b + 2 < len(batches):
+                    reads[b + 2] = [pool.submit(_read, p) for p in batches[b + 2]]
                 groups = {}
                 for i, img in enumerate(imgs):
                     groups.setdefault(img.shape, []).append(i)
@@ -223,17 +255,72 @@ class CoDec(EICCoDec):
                     out = D.encode(np.stack([imgs[i] for i in idx]), self.QSS, self.flags, self.block_size)
                     for j, i in enumerate(idx):
                         ks[i] = out[j]
+                b0 = b * batch
+                for i in range(len(chunk)):
+                    writes.append((b0 + i, pool.submit(_write, chunk[i][1], imgs[i].shape, ks[i])))
+                self.original_shape = imgs[-1].shape
+            for i, f in writes:
+                sizes[i] = f.result()
+        return sizes
 
-                def _write(i):
-                    out_fn = chunk[i][1]
-                    with open(f"{out_fn}_shape.bin", "wb") as f:
-                        f.write(struct.pack("iii", *imgs[i].shape))
-                    return self.encode_write_fn(self.compress(ks[i]), out_fn)
+    def _encode_fns_staged(self, pairs, batch, io_threads):
+        from .. import staging
+        probes = [staging.png_probe(p[0]) if p[0].lower().endswith(".png") else None for p in pairs]
+        if any(pr is None or not pr[2] for pr in probes) or len({pr[:2] for pr in probes}) != 1:
+            return None
+        H, W = probes[0][:2]
+        batch = max(1, min(batch, len(pairs)))
+        Hp, Wp = D.padded_shape(H, W, self.block_size)
+        qss, flags, bsz = self.QSS, self.flags, self.block_size
 
-                for i, s in enumerate(pool.map(_write, range(len(chunk)))):
-                    sizes[b0 + i] = s
-        if pairs:
-            self.original_shape = imgs[-1].shape
+        def launch(din, n, dout, stream):
+            D.encode_device(din, n, H, W, qss, flags, out=dout, stream=stream, block_size=bsz)
+
+        key = (batch, H, W, Hp, Wp, qss, flags, bsz)
+        cached = getattr(self, "_staged", None)
+        if cached is None or cached[0] != key:
+            if cached is not None:
+                cached[1].close()
+            # pinning is costly (~0.1 s per GB): the slots live as long as the codec
+            self._staged = (key, staging.StagedEncoder(batch, H, W, (Hp, Wp, 3), launch))
+        enc = self._staged[1]
+        sizes = [0] * len(pairs)
+        batches = [pairs[b0:b0 + batch] for b0 in range(0, len(pairs), batch)]
+        in_bytes = [0] * len(pairs)
+
+        def _read(b, i):
+            in_bytes[b * batch + i] = staging.decode_png_into(batches[b][i][0], enc.slot(b)["hin"].array[i])
+
+        def _write(out_fn, k):
+            with open(f"{out_fn}_shape.bin", "wb") as f:
+                f.write(struct.pack("iii", H, W, 3))
+            return self.encode_write_fn(self.compress(k), out_fn)
+
+        try:
+            with ThreadPoolExecutor(max_workers=io_threads) as pool:
+                reads = {0: [pool.submit(_read, 0, i) for i in range(len(batches[0]))]}
+                writes = {}
+                for b, chunk in enumerate(batches):
+                    for f in reads.pop(b):
+                        f.result()
+                    # the other slot's pinned input is free (batch b-1 was copied in
+                    # run(b-1)): decode the next batch's PNGs into it meanwhile
+                    if b + 1 < len(batches):
+                        reads[b + 1] = [pool.submit(_read, b + 1, i) for i in range(len(batches[b + 1]))]
+                    # this slot's pinned output is still read by batch b-2's deflates
+                    for i, f in writes.pop(b - 2, []):
+                        sizes[i] = f.result()
+                    ks = enc.run(b, len(chunk))
+                    writes[b] = [(b * batch + i, pool.submit(_write, chunk[i][1], ks[i])) for i in range(len(chunk))]
+                for lst in writes.values():
+                    for i, f in lst:
+                        sizes[i] = f.result()
+        except BaseException:
+            self._staged = None
+            enc.close()
+            raise
+        self.total_input_size += sum(in_bytes)
+        self.original_shape = (H, W, 3)
         return sizes
 
     def decode_fns(self, pairs, batch: int = 64, io_threads: int = 8):

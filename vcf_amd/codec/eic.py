@@ -17,8 +17,31 @@ import os
 import numpy as np
 
 
+def _read_png_native(fn: str):
+    """The library's PNG reader (vcf_amd/csrc/vcf_png.cpp): 8-bit, non-interlaced
+    PNGs; None when the file is outside what it covers (PIL then reads it)."""
+    import ctypes
+    from .. import _lib
+    with open(fn, "rb") as f:
+        data = f.read()
+    if data[:8] != b"\x89PNG\r\n\x1a\n":
+        return None, len(data)
+    h, w, ok = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    buf = ctypes.c_char_p(data)
+    _lib.call("vcf_png_info", buf, len(data), ctypes.byref(h), ctypes.byref(w), ctypes.byref(ok))
+    if not ok.value:
+        return None, len(data)
+    img = np.empty((h.value, w.value, 3), np.uint8)
+    _lib.call("vcf_png_decode_rgb", buf, len(data), img.ctypes.data_as(ctypes.c_void_p), img.nbytes)
+    return img, len(data)
+
+
 def read_image(fn: str) -> tuple[np.ndarray, int]:
     """(H x W x 3 uint8 RGB array, bytes on disk)."""
+    if fn.lower().endswith(".png"):
+        img, size = _read_png_native(fn)
+        if img is not None:
+            return img, size
     from PIL import Image
     size = os.path.getsize(fn)
     with Image.open(fn) as im:

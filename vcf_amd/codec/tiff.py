@@ -22,6 +22,7 @@ import io
 import json
 import os
 import struct
+import threading
 import zlib
 from concurrent.futures import ThreadPoolExecutor
 
@@ -42,7 +43,9 @@ def _executor():
 
 def _deflate_strips(data: memoryview, strip_bytes: int, nstrips: int, level: int):
     chunks = [data[i * strip_bytes:(i + 1) * strip_bytes] for i in range(nstrips)]
-    if nstrips >= 4 and len(data) >= (1 << 20):
+    # strips in parallel only for a caller on the main thread: frame-level
+    # worker threads (the III pipeline) already keep every core busy
+    if nstrips >= 4 and len(data) >= (1 << 20) and threading.current_thread() is threading.main_thread():
         return list(_executor().map(lambda c: zlib.compress(c, level), chunks))
     return [zlib.compress(c, level) for c in chunks]
 

@@ -1,0 +1,231 @@
+// vcf_png.cpp -- native PNG reader for the frame-ingest path (host code in
+// libvcf_amd.so).
+//
+// Replaces the image read of EIC.encode_read_fn (src/entropy_image_coding.py
+// :51-65: cv2.imread(IMREAD_UNCHANGED) + BGR2RGB, assumption A9: the same RGB
+// array PIL's convert("RGB") gives) for the PNGs the III runner ingests
+// (/tmp/original_%04d.png, III.py:73-89).  SURVEY.md §8(f) row 1: once the
+// kernels run near the HBM roofline, host PNG decoding bounds the end-to-end
+// rate; PIL's decoder spends ~55-70 ms on a 1080p frame, this one ~2-3x less
+// (one inflate of the concatenated IDAT data, row unfiltering in place).
+//
+// Covered: the colour images the reference reads as RGB -- bit depth 8 RGB
+// (type 2) and RGBA (type 6, alpha dropped: cv2 BGR2RGB of a 4-channel image),
+// palette images (type 3, depth 1/2/4/8, looked up: libpng expands them), no
+// interlace -- as PIL's convert("RGB") gives them.  Gray images are not
+// colour frames to the reference (cvtColor(BGR2RGB) of a 2-D array fails,
+// entropy_image_coding.py:55-60): like 16-bit and Adam7 files they return
+// VCF_ERR_UNSUPPORTED and the caller reads them the generic way.  Chunk CRCs
+// are verified; a corrupt file is VCF_ERR_INVALID.
+#include <zlib.h>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "vcf_amd.h"
+#include "vcf_internal.h"
+
+namespace vcf {
+namespace {
+
+uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+struct PngHeader {
+    uint32_t w = 0, h = 0;
+    int depth = 0, ctype = 0, interlace = 0;
+    int channels() const { return ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : 4; }
+    bool covered() const
+    {
+        if (interlace != 0) return false;
+        if (depth == 8) return ctype == 2 || ctype == 3 || ctype == 6;
+        return (depth == 1 || depth == 2 || depth == 4) && ctype == 3;
+    }
+};
+
+const uint8_t kSig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+
+// Walk the chunks: header, palette, IDAT pieces (pointers into data).
+int parse(const uint8_t *data, int64_t n, PngHeader &h, const uint8_t **plte, uint32_t *plte_len,
+          std::vector<std::pair<const uint8_t *, uint32_t>> *idat)
+{
+    if (!data || n < 8 + 25 || std::memcmp(data, kSig, 8) != 0) return set_error(VCF_ERR_INVALID, "not a PNG file");
+    int64_t off = 8;
+    bool have_ihdr = false, have_iend = false;
+    while (off + 12 <= n) {
+        const uint32_t len = be32(data + off);
+        const uint8_t *type = data + off + 4;
+        if (len > (uint32_t)0x7fffffff || off + 12 + (int64_t)len > n)
+            return set_error(VCF_ERR_INVALID, "truncated PNG chunk");
+        const uint8_t *body = data + off + 8;
+        const uint32_t crc = be32(body + len);
+        if ((uint32_t)crc32(crc32(0L, Z_NULL, 0), type, 4 + len) != crc)
+            return set_error(VCF_ERR_INVALID, "broken PNG file (chunk CRC)");
+        if (!std::memcmp(type, "IHDR", 4)) {
+            if (len != 13) return set_error(VCF_ERR_INVALID, "bad IHDR");
+            h.w = be32(body);
+            h.h = be32(body + 4);
+            h.depth = body[8];
+            h.ctype = body[9];
+            h.interlace = body[12];
+            if (body[10] != 0 || body[11] != 0) return set_error(VCF_ERR_INVALID, "bad PNG compression/filter method");
+            have_ihdr = true;
+        } else if (!std::memcmp(type, "PLTE", 4)) {
+            if (plte) { *plte = body; *plte_len = len; }
+        } else if (!std::memcmp(type, "IDAT", 4)) {
+            if (idat) idat->push_back({body, len});
+        } else if (!std::memcmp(type, "IEND", 4)) {
+            have_iend = true;
+            break;
+        }
+        off += 12 + (int64_t)len;
+    }
+    if (!have_ihdr) return set_error(VCF_ERR_INVALID, "PNG without IHDR");
+    if (idat && !have_iend) return set_error(VCF_ERR_INVALID, "truncated PNG (no IEND)");
+    if (h.w == 0 || h.h == 0) return set_error(VCF_ERR_INVALID, "empty PNG");
+    return VCF_OK;
+}
+
+inline uint8_t paeth(int a, int b, int c)
+{
+    const int p = a + b - c;
+    const int pa = p > a ? p - a : a - p, pb = p > b ? p - b : b - p, pc = p > c ? p - c : c - p;
+    if (pa <= pb && pa <= pc) return (uint8_t)a;
+    return pb <= pc ? (uint8_t)b : (uint8_t)c;
+}
+
+// PNG filters 0..4 (ISO 15948 §9) on one scanline, bpp bytes per pixel
+int unfilter(uint8_t *row, const uint8_t *prev, size_t len, int bpp, int ftype)
+{
+    switch (ftype) {
+    case 0: return VCF_OK;
+    case 1:
+        for (size_t i = bpp; i < len; ++i) row[i] = (uint8_t)(row[i] + row[i - bpp]);
+        return VCF_OK;
+    case 2:
+        if (prev) for (size_t i = 0; i < len; ++i) row[i] = (uint8_t)(row[i] + prev[i]);
+        return VCF_OK;
+    case 3:
+        for (size_t i = 0; i < len; ++i) {
+            const int a = i >= (size_t)bpp ? row[i - bpp] : 0, b = prev ? prev[i] : 0;
+            row[i] = (uint8_t)(row[i] + ((a + b) >> 1));
+        }
+        return VCF_OK;
+    case 4:
+        for (size_t i = 0; i < len; ++i) {
+            const int a = i >= (size_t)bpp ? row[i - bpp] : 0, b = prev ? prev[i] : 0;
+            const int c = (prev && i >= (size_t)bpp) ? prev[i - bpp] : 0;
+            row[i] = (uint8_t)(row[i] + paeth(a, b, c));
+        }
+        return VCF_OK;
+    default: return set_error(VCF_ERR_INVALID, "bad PNG filter type %d", ftype);
+    }
+}
+
+}  // namespace
+}  // namespace vcf
+
+using namespace vcf;
+
+extern "C" {
+
+int vcf_png_info(const uint8_t *data, int64_t nbytes, int32_t *H, int32_t *W, int32_t *supported)
+{
+    PngHeader h;
+    int rc = parse(data, nbytes, h, nullptr, nullptr, nullptr);
+    if (rc != VCF_OK) return rc;
+    if (H) *H = (int32_t)h.h;
+    if (W) *W = (int32_t)h.w;
+    if (supported) *supported = h.covered() ? 1 : 0;
+    return VCF_OK;
+}
+
+int vcf_png_decode_rgb(const uint8_t *data, int64_t nbytes, uint8_t *rgb_out, int64_t out_capacity)
+{
+    PngHeader h;
+    const uint8_t *plte = nullptr;
+    uint32_t plte_len = 0;
+    std::vector<std::pair<const uint8_t *, uint32_t>> idat;
+    int rc = parse(data, nbytes, h, &plte, &plte_len, &idat);
+    if (rc != VCF_OK) return rc;
+    if (!h.covered())
+        return set_error(VCF_ERR_UNSUPPORTED, "PNG depth %d colour type %d interlace %d", h.depth, h.ctype,
+                         h.interlace);
+    if (!rgb_out) return set_error(VCF_ERR_INVALID, "null output");
+    const int bpp = h.depth == 8 ? h.channels() : 1;   // filter unit: bytes per pixel, at least 1
+    const size_t stride = h.depth == 8 ? (size_t)h.w * bpp : ((size_t)h.w * h.depth + 7) / 8;
+    const size_t need = (size_t)h.h * h.w * 3;
+    if ((int64_t)need > out_capacity) return set_error(VCF_ERR_INVALID, "output buffer too small");
+    if (h.ctype == 3 && (!plte || plte_len % 3 != 0)) return set_error(VCF_ERR_INVALID, "palette PNG without PLTE");
+
+    // inflate all IDAT data into filtered scanlines (1 filter byte + stride)
+    std::vector<uint8_t> raw((stride + 1) * h.h);
+    z_stream zs;
+    std::memset(&zs, 0, sizeof(zs));
+    if (inflateInit(&zs) != Z_OK) return set_error(VCF_ERR_INVALID, "inflateInit failed");
+    zs.next_out = raw.data();
+    zs.avail_out = (uInt)raw.size();
+    int zr = Z_OK;
+    for (size_t c = 0; c < idat.size() && zr != Z_STREAM_END; ++c) {
+        zs.next_in = const_cast<Bytef *>(idat[c].first);
+        zs.avail_in = idat[c].second;
+        while (zs.avail_in > 0 && zs.avail_out > 0) {
+            zr = inflate(&zs, Z_NO_FLUSH);
+            if (zr == Z_STREAM_END) break;
+            if (zr != Z_OK && zr != Z_BUF_ERROR) {
+                inflateEnd(&zs);
+                return set_error(VCF_ERR_INVALID, "broken PNG data stream (zlib %d)", zr);
+            }
+            if (zr == Z_BUF_ERROR) break;
+        }
+    }
+    const size_t got = raw.size() - zs.avail_out;
+    inflateEnd(&zs);
+    if (got != raw.size()) return set_error(VCF_ERR_INVALID, "image file is truncated (%zu of %zu bytes)", got,
+                                            raw.size());
+
+    // unfilter in place, then expand to RGB
+    const uint8_t *prev = nullptr;
+    for (uint32_t y = 0; y < h.h; ++y) {
+        uint8_t *line = raw.data() + (size_t)y * (stride + 1);
+        rc = unfilter(line + 1, prev, stride, bpp, line[0]);
+        if (rc != VCF_OK) return rc;
+        prev = line + 1;
+        const uint8_t *s = line + 1;
+        uint8_t *d = rgb_out + (size_t)y * h.w * 3;
+        if (h.depth < 8) {   // packed samples, most significant bits first
+            const int per = 8 / h.depth, mask = (1 << h.depth) - 1;
+            for (uint32_t x = 0; x < h.w; ++x) {
+                const int v = (s[x / per] >> ((per - 1 - (int)(x % per)) * h.depth)) & mask;
+                if (3u * v + 2 < plte_len) {
+                    d[3 * x] = plte[3 * v]; d[3 * x + 1] = plte[3 * v + 1]; d[3 * x + 2] = plte[3 * v + 2];
+                } else {
+                    d[3 * x] = d[3 * x + 1] = d[3 * x + 2] = 0;
+                }
+            }
+            continue;
+        }
+        switch (h.ctype) {
+        case 2: std::memcpy(d, s, stride); break;
+        case 6:
+            for (uint32_t x = 0; x < h.w; ++x) { d[3 * x] = s[4 * x]; d[3 * x + 1] = s[4 * x + 1]; d[3 * x + 2] = s[4 * x + 2]; }
+            break;
+        case 0:
+            for (uint32_t x = 0; x < h.w; ++x) d[3 * x] = d[3 * x + 1] = d[3 * x + 2] = s[x];
+            break;
+        case 4:
+            for (uint32_t x = 0; x < h.w; ++x) d[3 * x] = d[3 * x + 1] = d[3 * x + 2] = s[2 * x];
+            break;
+        case 3:
+            for (uint32_t x = 0; x < h.w; ++x) {
+                const uint32_t i = s[x];
+                if (3 * i + 2 < plte_len) { d[3 * x] = plte[3 * i]; d[3 * x + 1] = plte[3 * i + 1]; d[3 * x + 2] = plte[3 * i + 2]; }
+                else { d[3 * x] = d[3 * x + 1] = d[3 * x + 2] = 0; }
+            }
+            break;
+        }
+    }
+    return VCF_OK;
+}
+
+}  // extern "C"
