@@ -145,6 +145,13 @@ int vcf_dct_dz_encode_k32(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, i
 int vcf_dct_dz_decode_k32(const int32_t *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
                           int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream);
 
+/* Same as vcf_dct_dz_decode with an explicit kernel choice (A/B tests and
+ * benchmarks): 0 = automatic (2), 1 = lane-per-block (one block's 64 float64
+ * samples per lane), 2 = column-per-lane (8 lanes per block, LDS transpose).
+ * Outputs identical. */
+int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,
+                              int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream);
+
 /* ---- 2D-DWT + deadzone path (2D-DWT.py, deadzone.py, YCoCg.py) ---------------- */
 
 /* Index of a pywt wavelet name ("db5", "bior4.4", ... -- the -w option,

@@ -74,11 +74,14 @@ def dct_decode(args):
     dk, dout = DeviceBuffer(F * Hp * Wp * 3), DeviceBuffer(F * H * W * 3)
     s = Stream()
     D.encode_device(din, F, H, W, Q, out=dk, stream=s)
-    t = timed(s, lambda: D.decode_device(dk, F, H, W, Q, out=dout, stream=s), args.steps, 3)
     alg = F * (Hp * Wp * 3 + H * W * 3)
-    print(json.dumps({"metric": "Mpixels/s dct_decode 4K Q=32", "value": round(F * H * W / t / 1e3, 1),
-                      "unit": "Mpixels/s", "ms_per_launch": round(t, 4), "frames_per_launch": F,
-                      "alg_GBps": round(alg / t / 1e6, 1), "frac_hbm": round(alg / t / 1e6 / HBM, 4)}), flush=True)
+    for variant, vname in ((2, "column-per-lane"), (1, "lane-per-block")):
+        t = timed(s, lambda: D.decode_device(dk, F, H, W, Q, out=dout, stream=s, variant=variant), args.steps, 3)
+        print(json.dumps({"metric": "Mpixels/s dct_decode 4K Q=32", "variant": vname,
+                          "value": round(F * H * W / t / 1e3, 1),
+                          "unit": "Mpixels/s", "ms_per_launch": round(t, 4), "frames_per_launch": F,
+                          "alg_GBps": round(alg / t / 1e6, 1), "frac_hbm": round(alg / t / 1e6 / HBM, 4)}),
+              flush=True)
 
 
 def dct_encode_pcie(args):

@@ -103,7 +103,7 @@ def test_zero_frames_and_errors():
     with pytest.raises(ValueError):
         D.encode(np.zeros((8, 8), np.uint8))
     with pytest.raises(NotImplementedError):
-        D.encode(np.zeros((16, 16, 3), np.uint8), 32, block_size=16)
+        D.encode(np.zeros((16, 16, 3), np.uint8), 32, block_size=5)
     with pytest.raises(ValueError):
         D.decode(np.zeros((8, 8, 3), np.uint8), 8, 8, 40000)
 
@@ -133,3 +133,24 @@ def test_encode_variant4_generic_colour(Q):
 def test_unknown_variant_rejected():
     with pytest.raises(ValueError):
         D.encode(np.zeros((16, 16, 3), np.uint8), 32, variant=99)
+
+
+@pytest.mark.parametrize("shape", SHAPES + [(2160, 3840), (1080, 1920)])
+@pytest.mark.parametrize("Q,flags", [(32, 0), (7, 1), (1, 0), (5, 3), (64, 2)])
+def test_decode_variants_vs_oracle(shape, Q, flags):
+    """Both decode kernels (1 lane-per-block, 2 column-per-lane) are bit-exact."""
+    H, W = shape
+    rgb = _rand((H, W, 3), seed=H * 31 + W + Q, kind="smooth" if W % 2 else "rand")
+    k = O.encode_frame(rgb, Q, flags) if H * W <= 1 << 20 else D.encode(rgb, Q, flags)
+    want = O.decode_frame(k, H, W, Q, flags)
+    for v in (1, 2):
+        assert np.array_equal(D.decode(k, H, W, Q, flags, variant=v), want), v
+
+
+def test_decode_variants_batched():
+    frames = np.stack([_rand((72, 4104, 3), seed=s, kind="smooth") for s in range(3)])
+    k = D.encode(frames, 32, 0)
+    a = D.decode(k, 72, 4104, 32, 0, variant=1)
+    b = D.decode(k, 72, 4104, 32, 0, variant=2)
+    assert np.array_equal(a, b)
+    assert np.array_equal(a[2], O.decode_frame(k[2], 72, 4104, 32, 0))

@@ -394,6 +394,156 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_encode_cols(const uint8_t *__re
     }
 }
 
+// ---------------------------------------------------------------------------
+// Column-per-lane decode (decode variant 2, the default).  The lane-per-block
+// decode holds a block's 64 float64 samples per lane (212+ VGPRs, 2 waves per
+// SIMD), which leaves the float64 pipe latency-bound.  Here 8 lanes share a
+// block, as in encode variant 3: a workgroup stages the index bytes of TB
+// consecutive blocks of a block row in LDS with 16-byte loads; per channel,
+// lane x dequantizes coefficient column x, runs its DCT-III (dct3_8r, the same
+// float64 op sequence), the block's 8 lanes transpose through a per-block LDS
+// tile (same wave: no workgroup barrier), lane x runs pixel row x and keeps
+// its 8 truncated int16 samples; after the three channels each lane converts
+// its row to RGB and stores its 24 bytes.  ~60 VGPRs: 8 waves per SIMD.
+// ---------------------------------------------------------------------------
+template <int TB>
+struct DecColsSmem {
+    double tr[TB][8][9];   // per-block transpose tile, pitch 9
+    uint8_t stage[64 * TB * 3 + 8 * 32];
+};
+
+template <int TB, bool SUB, bool PERC, bool PAD>
+__global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__restrict__ kin,
+                                                              uint8_t *__restrict__ rgb, Geom g, int Q,
+                                                              int tiles_per_row)
+{
+    __shared__ __attribute__((aligned(16))) DecColsSmem<TB> sm;
+    const int tid = threadIdx.x;
+    const int lb = tid >> 3, x = tid & 7;
+    const int by = blockIdx.x / tiles_per_row;
+    const int bx0 = (blockIdx.x - by * tiles_per_row) * TB;
+    const int nvalid = min(TB, g.nbx - bx0);
+    const int bx = bx0 + lb;
+    const uint8_t *src = kin + blockIdx.y * g.out_stride;
+    uint8_t *dst = rgb + blockIdx.y * g.in_stride;
+
+    // copy the tile's index bytes in: 64 runs of 3*nvalid bytes (or 8 rows of 24*nvalid)
+    constexpr int nseg = SUB ? 64 : 8;
+    auto seg_off = [&](int seg) -> uint32_t {
+        return (uint32_t)(SUB ? seg_offset_sub(g, by, bx0, seg) : seg_offset_nosub(g, by, bx0, seg));
+    };
+    if (g.vec && nvalid == TB && (TB * 3) % 16 == 0) {
+        constexpr int cps = (SUB ? 3 * TB : 24 * TB) / 16, total = nseg * cps;
+#pragma unroll
+        for (int q0 = 0; q0 < total; q0 += TB * 8) {
+            const int q = q0 + tid;
+            if (total % (TB * 8) == 0 || q < total) {
+                const int seg = q / cps, off = (q - seg * cps) << 4;
+                *reinterpret_cast<u32x4 *>(sm.stage + cols_stage_off<TB, SUB>(seg) + off) =
+                    __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + seg_off(seg) + off));
+            }
+        }
+    } else {
+        const int seg_len = SUB ? 3 * nvalid : 24 * nvalid, total = nseg * seg_len;
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+        for (int q = tid; q < total; q += TB * 8) {
+            const int seg = q / seg_len, off = q - seg * seg_len;
+            sm.stage[cols_stage_off<TB, SUB>(seg) + off] = src[seg_off(seg) + off];
+        }
+    }
+    __syncthreads();
+    if (lb >= nvalid) return;
+
+    double (*tr)[9] = sm.tr[lb];
+    int out[3][8];
+#pragma unroll
+    for (int C = 0; C < 3; ++C) {
+        // :399-411 astype(int16) - 128, Q*k in int16 (A5); -p de-weighting (:421-435)
+        double col[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int kb = SUB ? sm.stage[cols_stage_off<TB, SUB>(i * 8 + x) + lb * 3 + C]
+                               : sm.stage[cols_stage_off<TB, SUB>(i) + lb * 24 + x * 3 + C];
+            int16_t yv = (int16_t)(Q * (kb - 128));
+            if (PERC) {
+                const float f = (float)((double)(float)yv / pweight_rt(C, i * 8 + x));
+                yv = (int16_t)(int)f;
+            }
+            col[i] = (double)yv;
+        }
+        // :440 synthesize_image (A2): axis 0 (this lane's column), then axis 1
+        dct3_8r(col);
+#pragma unroll
+        for (int y = 0; y < 8; ++y) tr[y][x] = col[y];
+        wave_lds_fence();
+        double row[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) row[j] = tr[x][j];
+        wave_lds_fence();   // the tile is rewritten by the next channel
+        dct3_8r(row);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) out[C][j] = (int16_t)(int)(row[j] * 0.0625);   // fct 1/4 per pass; int16
+    }
+    // :444 remove_padding, :449 to_RGB (int16), :454 += 128, :466 clip, uint8
+    uint32_t px[24];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int yv = out[0][j], co = out[1][j], cg = out[2][j];
+        px[3 * j + 0] = clip_u8((int16_t)(yv + co - cg));
+        px[3 * j + 1] = clip_u8((int16_t)(yv + cg));
+        px[3 * j + 2] = clip_u8((int16_t)(yv - co - cg));
+    }
+#pragma unroll
+    for (int q = 0; q < 24; ++q) VCF_OPAQUE(px[q]);   // see to_rgb_row: avoids a gfx950 packing miscompile
+    const int y = x;
+    if (!PAD) {
+        uint32_t w[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+            w[q] = px[4 * q] | (px[4 * q + 1] << 8) | (px[4 * q + 2] << 16) | (px[4 * q + 3] << 24);
+        u32x2 *p = reinterpret_cast<u32x2 *>(dst + ((uint32_t)(by * 8 + y) * (uint32_t)g.W + (uint32_t)bx * 8) * 3);
+        __builtin_nontemporal_store(u32x2{w[0], w[1]}, p);
+        __builtin_nontemporal_store(u32x2{w[2], w[3]}, p + 1);
+        __builtin_nontemporal_store(u32x2{w[4], w[5]}, p + 2);
+    } else {
+        const int sy = by * 8 + y - g.top;
+        if (sy < 0 || sy >= g.H) return;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int sx = bx * 8 + j - g.left;
+            if (sx < 0 || sx >= g.W) continue;
+            uint8_t *p = dst + ((uint32_t)sy * (uint32_t)g.W + (uint32_t)sx) * 3;
+            p[0] = (uint8_t)px[3 * j];
+            p[1] = (uint8_t)px[3 * j + 1];
+            p[2] = (uint8_t)px[3 * j + 2];
+        }
+    }
+}
+
+template <int TB>
+int launch_decode_cols(const uint8_t *k_dev, int64_t n_frames, uint8_t *rgb_dev, const Geom &g, int Q, bool sub,
+                       bool perc, bool pad, void *stream)
+{
+    const int tpr = (g.nbx + TB - 1) / TB;
+    for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
+        const dim3 grid(tpr * g.nby, (unsigned)std::min<int64_t>(65535, n_frames - f0));
+        const uint8_t *in = k_dev + f0 * g.out_stride;
+        uint8_t *out = rgb_dev + f0 * g.in_stride;
+#define VCF_DEC2(SB, PC, PD) \
+        if (sub == SB && perc == PC && pad == PD) \
+            hipLaunchKernelGGL((dct_dz_decode_cols<TB, SB, PC, PD>), grid, dim3(TB * 8), 0, \
+                               (hipStream_t)stream, in, out, g, Q, tpr);
+        VCF_DEC2(true, false, false) else VCF_DEC2(true, false, true)
+        else VCF_DEC2(true, true, false) else VCF_DEC2(true, true, true)
+        else VCF_DEC2(false, false, false) else VCF_DEC2(false, false, true)
+        else VCF_DEC2(false, true, false) else VCF_DEC2(false, true, true)
+#undef VCF_DEC2
+        const int rc = hip_check(hipGetLastError(), "dct_dz_decode_cols launch");
+        if (rc != VCF_OK) return rc;
+    }
+    return VCF_OK;
+}
+
 template <int C, bool SUB, bool PERC>
 __device__ __forceinline__ void decode_channel(const uint8_t *stage, int tid, int Q,
                                                uint32_t (&res)[32])
@@ -630,16 +780,24 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
 int vcf_dct_dz_decode(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream)
 {
-    if (block_size != 8)   // -B other than 8: vcf_dct_any.hip
+    return vcf_dct_dz_decode_variant(0, k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, stream);
+}
+
+int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,
+                              int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream)
+{
+    if (block_size != 8 && variant == 0)   // -B other than 8: vcf_dct_any.hip
         return dct_any_decode_u8(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, stream);
     int rc = check_args(k_dev, rgb_dev, n_frames, H, W, block_size, Q, flags, true);
     if (rc != VCF_OK) return rc;
+    if (variant < 0 || variant > 2) return set_error(VCF_ERR_INVALID, "unknown decode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
     const bool sub = !(flags & VCF_DCT_NO_SUBBANDS);
     const bool perc = (flags & VCF_DCT_PERCEPTUAL) != 0;
     const bool pad = (g.Hp != H) || (g.Wp != W);
+    if (variant != 1) return launch_decode_cols<32>(k_dev, n_frames, rgb_dev, g, (int)Q, sub, perc, pad, stream);
     for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
         const dim3 grid(g.tiles_per_frame, (unsigned)std::min<int64_t>(65535, n_frames - f0));
         VCF_DEC_CASE(true, false, false) else VCF_DEC_CASE(true, false, true)

@@ -61,7 +61,8 @@ def encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32,
 def decode_device(k: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32, flags: int = 0,
                   out: DeviceBuffer | None = None, stream=None, block_size: int = 8,
                   variant: int = 0) -> DeviceBuffer:
-    """variant: 0 automatic, -1 the generic-B kernels (any supported B, 8 included)."""
+    """variant: 0 automatic, 1 lane-per-block, 2 column-per-lane (see vcf_amd.h), -1 the generic-B
+    kernels (any supported B, 8 included)."""
     Hp, Wp = padded_shape(H, W, block_size)
     if k.nbytes < n_frames * Hp * Wp * 3:
         raise ValueError("input buffer too small")
@@ -69,8 +70,11 @@ def decode_device(k: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32, f
         out = DeviceBuffer(n_frames * H * W * 3)
     elif out.nbytes < n_frames * H * W * 3:
         raise ValueError("output buffer too small")
-    name = "vcf_dct_dz_decode_any" if variant == -1 else "vcf_dct_dz_decode"
-    call(name, k.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
+    if variant == -1:
+        call("vcf_dct_dz_decode_any", k.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
+    else:
+        call("vcf_dct_dz_decode_variant", variant, k.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr,
+             _h(stream))
     return out
 
 
