@@ -169,3 +169,43 @@ def test_ipp_cli(tmp_path):
         r = subprocess.run([sys.executable, cli] + argv, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
     assert all(os.path.exists(f"{dec}_{i:04d}.png") for i in range(4))
+
+
+def test_ipp_over_2d_dwt_matches_oracle_loop(tmp_path):
+    """--st 2D-DWT (IPP_DCT.py:45-87 subclasses the module --st names): I frames
+    and residuals coded by the 2D-DWT codec (3l+1 subband TIFFs per frame); the
+    decoded sequence equals the reference's GOP loop over the oracle's DWT
+    round trip, and the CLI takes the DWT options."""
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec.ipp import codec_class
+    frames = _moving(64, 96, 5, 23)
+    pat = _write_seq(str(tmp_path), frames)
+    enc, dec = str(tmp_path / "enc" / "v"), str(tmp_path / "dec" / "v")
+    p = P.ipp_parser(space_transform="2D-DWT")
+    flags = ["--st", "2D-DWT", "-N", "5", "-G", "3", "-M", "16", "-S", "6", "-l", "3", "-w", "bior4.4", "-q", "16"]
+    cls = codec_class("2D-DWT")
+    cls(P.parse(p, ["encode", "-i", pat, "-O", enc] + flags)).encode()
+    assert os.path.exists(f"{enc}_P_0_enc_LL_3.tif") and os.path.exists(f"{enc}_I_1_enc_HH_1.tif")
+    d = cls(P.parse(p, ["decode", "-i", enc, "-O", dec, "-M", "16", "--st", "2D-DWT", "-l", "3", "-w", "bior4.4",
+                        "-q", "16"]))
+    assert d.decode() == 5
+
+    def rt(img):
+        H, W = img.shape[:2]
+        return O.dwt_decode_frame(O.dwt_encode_frame(img, "bior4.4", 3, 16), H, W, "bior4.4", 3, 16)
+    want = []
+    for g0 in range(0, 5, 3):
+        ref = rt(frames[g0])
+        want.append(ref)
+        for p_ in range(1, min(3, 5 - g0)):
+            mv = O.ipp_block_matching(ref, frames[g0 + p_], 16, 6, False)
+            comp = O.ipp_motion_compensate(ref, mv, 16)
+            ref = O.ipp_reconstruct(comp, rt(O.ipp_residual(frames[g0 + p_], comp)))
+            want.append(ref)
+    for i in range(5):
+        got = np.asarray(Image.open(f"{dec}_{i:04d}.png").convert("RGB"))
+        assert np.array_equal(got, want[i]), f"frame {i}"
+    cli = os.path.join(ROOT, "vcf_amd", "cli", "IPP_DCT.py")
+    r = subprocess.run([sys.executable, cli, "encode", "-i", pat, "-O", str(tmp_path / "c" / "v")] + flags,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]

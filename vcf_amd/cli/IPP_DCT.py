@@ -1,16 +1,22 @@
 #!/usr/bin/env python3
 """Drop-in for `python IPP_DCT.py [-g] {encode,decode} -i ... -O ... -N -G -M -S
 [--fast] ...` (src/IPP_DCT.py): block motion search, compensation and
-residual coding with the 2D-DCT codec, on the GPU.  Multi-GPU: launch one
+residual coding with the 2D-DCT (or --st 2D-DWT) codec, on the GPU.  Multi-GPU: launch one
 process per GPU with torch.distributed.run; GOPs are sharded."""
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
+import argparse  # noqa: E402
+
 from vcf_amd.codec import parser as P  # noqa: E402
-from vcf_amd.codec.ipp import CoDec  # noqa: E402
+from vcf_amd.codec.ipp import codec_class  # noqa: E402
 from vcf_amd.codec.main import main  # noqa: E402
 
 if __name__ == "__main__":
-    main(P.ipp_parser(), CoDec)
+    # IPP_DCT.py:45-87: --st is read first and picks the spatial codec (and its options)
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--st", dest="space_transform", type=str, default="2D-DCT")
+    st = pre.parse_known_args()[0].space_transform
+    main(P.ipp_parser(space_transform=st), codec_class(st))

@@ -1,6 +1,8 @@
 """IPP hybrid video coding: the drop-in for src/IPP_DCT.py (IPP + CoDec).
 
-Each GOP is an I-frame coded by the spatial codec (--st, default 2D-DCT)
+Each GOP is an I-frame coded by the spatial codec (--st: 2D-DCT, the
+default, or 2D-DWT -- the reference subclasses whichever module --st names,
+IPP_DCT.py:45-87; here codec_class(st) picks CoDec or CoDecDWT)
 followed by P-frames: block matching against the previous reconstruction,
 motion compensation, the residual shifted by 128 and clipped, coded by the
 same spatial codec, and the reconstruction clip(pred + rec - 128)
@@ -38,6 +40,7 @@ import numpy as np
 from .. import ipp as K
 from . import shard
 from .dct2d import CoDec as DCTCoDec
+from .dwt2d import CoDec as DWTCoDec
 from .eic import read_image, write_image
 
 _TMP_DIR = "/tmp"   # os.path.join(_SCRIPT_DIR, "/tmp") == "/tmp" (IPP_DCT.py:20)
@@ -83,13 +86,10 @@ def read_frames(src: str, n: int):
     return [read_image(f)[0] for f in files]
 
 
-class CoDec(DCTCoDec):
-    """IPP_DCT.CoDec (:578-720) over the 2D-DCT spatial codec."""
+class _IPP:
+    """IPP_DCT.CoDec (:578-720) over a spatial codec base class (the MRO's next)."""
 
     def __init__(self, args, group=None):
-        st = getattr(args, "space_transform", "2D-DCT")
-        if st != "2D-DCT":
-            raise NotImplementedError(f"--st {st}: the IPP driver runs over 2D-DCT")
         super().__init__(args)
         self.gop_size = getattr(args, "gop_size", 10) or 10
         self.block_size_ME = getattr(args, "block_size_ME", 16) or 16
@@ -106,17 +106,9 @@ class CoDec(DCTCoDec):
             bpp = self.total_bits / (self.N_frames * self.width * self.height)
             logging.info(f"Output bit-rate = {bpp:.4f} bits/pixel")
 
-    # IPP_DCT.py:595-626, in memory
+    # IPP_DCT.py:595-626: encode_fn to the frame's files, decode_fn back (in memory)
     def encode_decode_proxy(self, img, frame_type, seq_idx):
-        base = f"{self.prefix}_{frame_type}_{seq_idx}_enc"
-        k = self.encode_indices(img)
-        with open(f"{base}_shape.bin", "wb") as f:
-            f.write(struct.pack("iii", *img.shape))
-        cs = self.compress(k)
-        data = cs.getvalue()
-        size = self.encode_write_fn(io.BytesIO(data), base)
-        recon = self.decode_indices(self.decompress(data), img.shape)
-        return recon, size
+        return self._code_frame(img, f"{self.prefix}_{frame_type}_{seq_idx}_enc")
 
     def _gop(self, frames, g0, i_idx, p0):
         """One GOP: I-frame then P-frames (IPP.temporal_filter :397-575)."""
@@ -249,8 +241,54 @@ class CoDec(DCTCoDec):
         self.recon = recon
         return len(recon)
 
+
+
+class CoDec(_IPP, DCTCoDec):
+    """IPP over 2D-DCT (the default --st)."""
+
+    def _code_frame(self, img, base):
+        k = self.encode_indices(img)
+        with open(f"{base}_shape.bin", "wb") as f:
+            f.write(struct.pack("iii", *img.shape))
+        cs = self.compress(k)
+        data = cs.getvalue()
+        size = self.encode_write_fn(io.BytesIO(data), base)
+        recon = self.decode_indices(self.decompress(data), img.shape)
+        return recon, size
+
     def _decode_frame(self, base):
         data = self.decode_read_fn(base)
         with open(f"{base}_shape.bin", "rb") as f:
             shape = struct.unpack("iii", f.read(12))
         return self.decode_indices(self.decompress(data), shape)
+
+
+class CoDecDWT(_IPP, DWTCoDec):
+    """IPP over 2D-DWT (--st 2D-DWT): each frame's 3l+1 subband TIFFs
+    ({base}_LL_l.tif, {base}_{LH,HL,HH}_r.tif, 2D-DWT.py:162-200).  The
+    reconstruction is waverec2's 2*ceil(H/2) x 2*ceil(W/2), as in the
+    reference (whose IPP loop therefore needs even frame sides)."""
+
+    def _code_frame(self, img, base):
+        from .. import dwt as DW
+        if img.ndim != 3 or img.shape[2] != 3 or img.dtype != np.uint8:
+            raise ValueError("Input image must be a 3D array (height, width, channels).")
+        sb = DW.encode(img, self.wavelet, self.levels, self.QSS)[0]
+        size = self.write_decom_fn(sb, base)
+        H, W = self._geometry(sb)
+        return DW.decode(sb, H, W, self.wavelet, self.levels, self.QSS), size
+
+    def _decode_frame(self, base):
+        from .. import dwt as DW
+        sb = self.read_decom_fn(base)
+        H, W = self._geometry(sb)
+        return DW.decode(sb, H, W, self.wavelet, self.levels, self.QSS)
+
+
+def codec_class(space_transform: str = "2D-DCT"):
+    """The IPP codec class over the spatial codec --st names (IPP_DCT.py:45-87)."""
+    if space_transform == "2D-DCT":
+        return CoDec
+    if space_transform == "2D-DWT":
+        return CoDecDWT
+    raise NotImplementedError(f"--st {space_transform}: 2D-DCT and 2D-DWT are on the HIP path")

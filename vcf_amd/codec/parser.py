@@ -226,10 +226,14 @@ IPP_BLOCK_ME = 16
 IPP_SEARCH = 8
 
 
-def ipp_parser(description: str = "IPP hybrid video coding using motion compensation and DCT."):
-    """`python IPP_DCT.py ...` over the default 2D-DCT chain."""
+def ipp_parser(description: str = "IPP hybrid video coding using motion compensation and DCT.",
+               space_transform: str = "2D-DCT"):
+    """`python IPP_DCT.py ...` over the 2D-DCT chain (or, --st 2D-DWT, the 2D-DWT one)."""
     p, enc, dec = base_parser(description)
-    add_dct(enc, dec)
+    if space_transform == "2D-DWT":
+        add_dwt(enc, dec)
+    else:
+        add_dct(enc, dec)
     add_ycocg(enc, dec)
     add_deadzone(enc, dec)
     add_filter(enc, dec)
