@@ -88,13 +88,17 @@ class Group:
         out = [None] * n_frames
         for i in range(lo, hi):
             out[i] = bytes(local_payloads[i - lo])
+        # post every peer's receive at once: each xGMI peer has its own link to
+        # rank 0, so the P-1 transfers run concurrently (link-bound, not serial)
+        pending = []
         for r in range(1, self.world):
             rlo, rhi = frame_range(n_frames, r, self.world)
             if rhi <= rlo:
                 continue
-            total = int(sizes[rlo:rhi].sum())
-            t = torch.empty(total, dtype=torch.uint8, device=self.device)
-            self.dist.recv(t, src=r)
+            t = torch.empty(int(sizes[rlo:rhi].sum()), dtype=torch.uint8, device=self.device)
+            pending.append((r, rlo, rhi, t, self.dist.irecv(t, src=r)))
+        for r, rlo, rhi, t, req in pending:
+            req.wait()
             blob = t.cpu().numpy().tobytes()
             off = 0
             for i in range(rlo, rhi):
