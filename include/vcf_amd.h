@@ -285,6 +285,18 @@ int vcf_png_info(const uint8_t *data, int64_t nbytes, int32_t *H, int32_t *W, in
  * back to another reader), VCF_ERR_INVALID for corrupt files. */
 int vcf_png_decode_rgb(const uint8_t *data, int64_t nbytes, uint8_t *rgb_out, int64_t out_capacity);
 
+/* RGB u8 (H x W x 3, host) -> PNG file bytes: 8-bit truecolour, Up-filtered
+ * scanlines, one zlib stream at `level` deflated in 1 MiB pieces on up to
+ * `threads` threads (pigz's construction: each piece primed with the previous
+ * 32 KiB, sync-flushed, adler32 combined).  The writer of the decode side's
+ * PNGs (EIC.decode_write_fn, entropy_image_coding.py:101-112) and of IPP's
+ * frame dumps: pixel-exact, not byte-identical to other PNG writers.
+ * out_capacity >= vcf_png_encode_bound(H, W) always suffices; *out_bytes
+ * receives the file size. */
+int vcf_png_encode_rgb(const uint8_t *rgb, int32_t H, int32_t W, int32_t level, int32_t threads, uint8_t *out,
+                       int64_t out_capacity, int64_t *out_bytes);
+int64_t vcf_png_encode_bound(int32_t H, int32_t W);
+
 /* ---- deadzone quantizer plug-in (deadzone.py:95-117, assumption A5) ---------- */
 
 /* k[i] = (int32)(x[i] / Q), truncation toward zero; the division is float32

@@ -5,6 +5,7 @@
   dct_decode               4K DCT+deadzone decode (64 frames resident)
   dct_encode_pcie          4K encode incl. host->device and device->host copies (pinned buffers)
   cbaac / cbahc            host entropy coders on a 1080p k-array (config C2), symbols/s
+  configs                  whole-codec runs of configs C2 (CBAAC) and C5 (IPP) with files
 
 Usage: python scripts/bench_paths.py [--only name,name]
 """
@@ -158,10 +159,63 @@ def entropy(args):
                               "sample": "1080p S-smooth frame, DCT+deadzone indices (config C2)"}), flush=True)
 
 
+def configs(args):
+    """Whole-codec runs of BASELINE.json configs C2 and C5 on one GPU, files included.
+
+    C2: 1080p frame -> 2D-DCT CoDec with -c CBAAC (encode_fn: PNG read, GPU
+        transform + quantizer, host CBAAC order 0, file write), frames/s over
+        16 frames coded by a 16-thread pool (frames are independent);
+    C5: IPP_DCT CoDec over 4K frames from an .npy (I + P frames, GOP 10, full
+        search bs 16 S 8: GPU ME/MC/residual/transform, host TIFF deflate, the
+        reference's original-frame PNG dumps), frames/s."""
+    import shutil
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    from PIL import Image
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec.dct2d import CoDec
+    from vcf_amd.codec.ipp import CoDec as IPPCoDec
+    tmp = tempfile.mkdtemp(prefix="vcf_cfg_")
+    try:
+        # C2
+        n = 16
+        srcs = []
+        for i in range(n):
+            srcs.append(os.path.join(tmp, f"c2_{i}.png"))
+            Image.fromarray(bench.synth_frame(1080, 1920, i)).save(srcs[-1], compress_level=1)
+        codec = CoDec(P.parse(P.dct_parser(), ["encode", "-c", "CBAAC"]))
+        codec.encode_fn(srcs[0], os.path.join(tmp, "warm"))
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(16) as ex:
+            sizes = list(ex.map(lambda i: codec.encode_fn(srcs[i], os.path.join(tmp, f"c2_enc_{i}")), range(n)))
+        t = time.perf_counter() - t0
+        print(json.dumps({"metric": "config C2: 1080p 2D-DCT + deadzone + CBAAC encode_fn, files included",
+                          "value": round(n * 1080 * 1920 / t / 1e6, 1), "unit": "Mpixels/s",
+                          "frames_per_s": round(n / t, 2), "threads": 16, "frames": n,
+                          "bits_per_pixel": round(8 * sum(sizes) / (n * 1080 * 1920), 4)}), flush=True)
+        # C5
+        nf = int(os.environ.get("C5_FRAMES", "20"))
+        f0 = bench.synth_frame(2160, 3840, 0)
+        frames = np.stack([np.roll(f0, (3 * t, t), axis=(0, 1)) for t in range(nf)])
+        np.save(os.path.join(tmp, "c5.npy"), frames)
+        argv = ["encode", "-i", os.path.join(tmp, "c5.npy"), "-O", os.path.join(tmp, "c5", "v"), "-N", str(nf),
+                "-G", "10", "-M", "16", "-S", "8"]
+        t0 = time.perf_counter()
+        IPPCoDec(P.parse(P.ipp_parser(), argv)).encode()
+        t = time.perf_counter() - t0
+        print(json.dumps({"metric": "config C5: IPP_DCT encode of 4K frames (GOP 10, ME bs 16 S 8), files included",
+                          "value": round(nf * 2160 * 3840 / t / 1e6, 1), "unit": "Mpixels/s",
+                          "frames_per_s": round(nf / t, 2), "frames": nf,
+                          "note": "serial within a GOP; includes the reference's PNG dumps of the originals"}),
+              flush=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--only", default="dwt,dct_decode,dct_encode_pcie,ipp,entropy")
+    ap.add_argument("--only", default="dwt,dct_decode,dct_encode_pcie,ipp,entropy,configs")
     args = ap.parse_args()
     set_device(0)
     for name in args.only.split(","):

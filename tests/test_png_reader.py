@@ -140,3 +140,24 @@ def test_read_image_uses_native_reader(tmp_path):
     Image.fromarray(arr).save(p)
     got, n = eic.read_image(str(p))
     assert np.array_equal(got, arr) and n == p.stat().st_size
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (3, 5), (17, 1000), (600, 700), (1100, 1000)])
+def test_png_writer_round_trip(shape, tmp_path):
+    """eic.write_image's native writer (vcf_png_encode_rgb): PIL and the native
+    reader read back the same pixels; the bytes do not depend on the thread
+    count (fixed 1 MiB deflate pieces)."""
+    rng = np.random.default_rng(shape[0] * 7 + shape[1])
+    a = rng.integers(0, 256, shape + (3,), dtype=np.uint8)
+    a[: shape[0] // 2] //= 16                 # some compressible rows
+    outs = []
+    for th in (1, 8):
+        eic.PNG_THREADS = th
+        p = tmp_path / f"w{th}.png"
+        n = eic.write_image(str(p), a)
+        assert n == p.stat().st_size
+        assert np.array_equal(np.asarray(Image.open(p).convert("RGB")), a)
+        assert np.array_equal(eic.read_image(str(p))[0], a)
+        outs.append(p.read_bytes())
+    eic.PNG_THREADS = 16
+    assert outs[0] == outs[1]

@@ -106,6 +106,8 @@ SIGNATURES = {
     "vcf_cbahc_decode": [_P, _I64, _I64, _I32, _P],
     "vcf_png_info": [_P, _I64, _PI32, _PI32, _PI32],
     "vcf_png_decode_rgb": [_P, _I64, _P, _I64],
+    "vcf_png_encode_rgb": [_P, _I32, _I32, _I32, _I32, _P, _I64, ctypes.POINTER(_I64)],
+    "vcf_png_encode_bound": [_I32, _I32],
     "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],
     "vcf_deadzone_dequantize": [_P, _I32, _I64, _I32, _P, _P],
 }
@@ -139,6 +141,7 @@ def lib():
             L.vcf_last_error.restype = ctypes.c_char_p
             L.vcf_cbaac_bound.restype = ctypes.c_int64
             L.vcf_cbahc_bound.restype = ctypes.c_int64
+            L.vcf_png_encode_bound.restype = ctypes.c_int64
             _lib = L
     return _lib
 

@@ -54,9 +54,28 @@ def read_image(fn: str) -> tuple[np.ndarray, int]:
     return np.ascontiguousarray(img), size
 
 
+PNG_LEVEL = 6        # zlib level of the PNGs written (PIL's / imageio's default)
+PNG_THREADS = 16     # deflate pieces of one PNG in parallel (the box's CPU share)
+
+
 def write_image(fn: str, img: np.ndarray) -> int:
+    """Write img; H x W x 3 uint8 to .png goes through the library's parallel
+    PNG writer (vcf_png_encode_rgb: pixel-exact), anything else through PIL."""
+    a = np.ascontiguousarray(img)
+    if fn.lower().endswith(".png") and a.ndim == 3 and a.shape[2] == 3 and a.dtype == np.uint8 and a.size:
+        import ctypes
+        from .. import _lib
+        H, W = a.shape[:2]
+        cap = int(_lib.lib().vcf_png_encode_bound(H, W))
+        buf = np.empty(cap, np.uint8)
+        n = ctypes.c_int64()
+        _lib.call("vcf_png_encode_rgb", a.ctypes.data_as(ctypes.c_void_p), H, W, PNG_LEVEL, PNG_THREADS,
+                  buf.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(n))
+        with open(fn, "wb") as f:
+            f.write(memoryview(buf)[:n.value])
+        return n.value
     from PIL import Image
-    Image.fromarray(np.ascontiguousarray(img)).save(fn)
+    Image.fromarray(a).save(fn)
     return os.path.getsize(fn)
 
 
