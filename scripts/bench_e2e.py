@@ -64,6 +64,17 @@ def main():
         with ThreadPoolExecutor(a.threads) as ex:
             list(ex.map(lambda i: codec.encode_write_fn(codec.compress(ks[i]), pairs[i][1] + "_w"), range(a.frames)))
         t_write = time.perf_counter() - t0
+        # decode side: .tif + _shape.bin -> decoded PNG files
+        dpairs = [(p[1], os.path.join(tmp, f"decoded_{i:04d}.png")) for i, p in enumerate(pairs)]
+        dcodec = CoDec(P.parse(P.dct_parser(), ["decode"]))
+        dcodec.decode_fns(dpairs[:a.batch], batch=a.batch, io_threads=a.threads)
+        t0 = time.perf_counter()
+        dcodec.decode_fns(dpairs, batch=a.batch, io_threads=a.threads)
+        t_dec = time.perf_counter() - t0
+        print(json.dumps({
+            "metric": "Mpixels/s III decode end to end (.tif files -> PNG files), 1 GPU",
+            "value": round(px / t_dec / 1e6, 1), "unit": "Mpixels/s", "frames": a.frames,
+            "frame": [a.H, a.W, 3], "threads": a.threads, "batch": a.batch}), flush=True)
         print(json.dumps({
             "metric": "Mpixels/s III encode end to end (PNG files -> .tif files), 1 GPU",
             "value": round(px / t_e2e / 1e6, 1), "unit": "Mpixels/s", "frames": a.frames,

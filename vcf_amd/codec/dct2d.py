@@ -323,21 +323,29 @@ class CoDec(EICCoDec):
         self.original_shape = (H, W, 3)
         return sizes
 
-    def decode_fns(self, pairs, batch: int = 64, io_threads: int = 8):
-        """decode_fn over (in_fn, out_fn) pairs, batched like encode_fns."""
+    def decode_fns(self, pairs, batch: int = 64, io_threads: int = 16):
+        """decode_fn over (in_fn, out_fn) pairs, pipelined like encode_fns: the
+        next two batches' TIFFs are inflated on host threads while the GPU
+        decodes this one, and the PNG writes of earlier batches run behind."""
         pairs = list(pairs)
+        if not pairs:
+            return []
         sizes = [0] * len(pairs)
+        batches = [pairs[b0:b0 + batch] for b0 in range(0, len(pairs), batch)]
+
+        def _read(p):
+            cs = self.decode_read_fn(p[0])
+            with open(f"{p[0]}_shape.bin", "rb") as f:
+                shp = struct.unpack("iii", f.read(12))
+            return self.decompress(cs), shp
+
         with ThreadPoolExecutor(max_workers=io_threads) as pool:
-            for b0 in range(0, len(pairs), batch):
-                chunk = pairs[b0:b0 + batch]
-
-                def _read(p):
-                    cs = self.decode_read_fn(p[0])
-                    with open(f"{p[0]}_shape.bin", "rb") as f:
-                        shp = struct.unpack("iii", f.read(12))
-                    return self.decompress(cs), shp
-
-                got = list(pool.map(_read, chunk))
+            reads = {b: [pool.submit(_read, p) for p in batches[b]] for b in range(min(2, len(batches)))}
+            writes = []
+            for b, chunk in enumerate(batches):
+                got = [f.result() for f in reads.pop(b)]
+                if b + 2 < len(batches):
+                    reads[b + 2] = [pool.submit(_read, p) for p in batches[b + 2]]
                 groups = {}
                 for i, (k, shp) in enumerate(got):
                     groups.setdefault(tuple(shp), []).append(i)
@@ -347,9 +355,12 @@ class CoDec(EICCoDec):
                                    self.flags, self.block_size)
                     for j, i in enumerate(idx):
                         ys[i] = out[j]
-                for i, s in enumerate(pool.map(lambda i: self.decode_write_fn(ys[i], chunk[i][1]),
-                                               range(len(chunk)))):
-                    sizes[b0 + i] = s
+                self.original_shape = got[-1][1]
+                b0 = b * batch
+                for i in range(len(chunk)):
+                    writes.append((b0 + i, pool.submit(self.decode_write_fn, ys[i], chunk[i][1])))
+            for i, f in writes:
+                sizes[i] = f.result()
         return sizes
 
     # ---- quantizer surface (deadzone.py:95-124) -----------------------------

@@ -69,7 +69,10 @@ def write_image(fn: str, img: np.ndarray) -> int:
         cap = int(_lib.lib().vcf_png_encode_bound(H, W))
         buf = np.empty(cap, np.uint8)
         n = ctypes.c_int64()
-        _lib.call("vcf_png_encode_rgb", a.ctypes.data_as(ctypes.c_void_p), H, W, PNG_LEVEL, PNG_THREADS,
+        import threading
+        # frame-level worker threads already run in parallel: fewer deflate threads each
+        th = PNG_THREADS if threading.current_thread() is threading.main_thread() else 2
+        _lib.call("vcf_png_encode_rgb", a.ctypes.data_as(ctypes.c_void_p), H, W, PNG_LEVEL, th,
                   buf.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(n))
         with open(fn, "wb") as f:
             f.write(memoryview(buf)[:n.value])
