@@ -117,9 +117,10 @@ int vcf_dct_dz_decode(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev,
                       void *stream);
 
-/* 1 if block_size has a HIP transform: B = 2^a 3^b <= 128 (a <= 7, b <= 1),
- * the lengths whose pocketfft real FFT factors into 4, 2 and 3 -- including
- * every size the -L search tries (2, 4, ..., 128; 2D-DCT.py:536).  0 otherwise. */
+/* 1 if block_size has a HIP transform: the 5-smooth B <= 128 (pocketfft's
+ * radix 2/3/4/5 passes; 38 sizes, every -L candidate 2, 4, ..., 128 among
+ * them, 2D-DCT.py:536).  0 otherwise (a prime factor > 5 needs pocketfft's
+ * generic radfg/radbg, not restated). */
 int vcf_dct_block_size_supported(int32_t block_size);
 
 /* The generic-B kernels for any supported block size, B = 8 included (tests

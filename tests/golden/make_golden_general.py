@@ -33,7 +33,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import make_golden as G  # noqa: E402
 
-LENGTHS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128]
+LENGTHS = [1, 2, 3, 4, 5, 6, 8, 9, 10, 12, 15, 16, 18, 20, 24, 25, 27, 30, 32, 36, 40, 45, 48, 50, 54, 60, 64,
+           72, 75, 80, 81, 90, 96, 100, 108, 120, 125, 128]   # the 5-smooth N <= 128
 
 B_CASES = [
     # name, kind, H, W, seed, flags
@@ -47,6 +48,16 @@ B_CASES = [
     ("b3_rand_30x20", "rand", 30, 20, 27, ["-B", "3"]),
     ("b1_rand_5x7", "rand", 5, 7, 28, ["-B", "1", "-q", "3"]),
     ("b96_smooth_96x96_x", "smooth", 96, 96, 29, ["-B", "96", "-x"]),
+    ("b5_rand_37x41", "rand", 37, 41, 30, ["-B", "5"]),
+    ("b10_smooth_64x70_q7", "smooth", 64, 70, 31, ["-B", "10", "-q", "7"]),
+    ("b15_rand_45x46_x", "rand", 45, 46, 32, ["-B", "15", "-x"]),
+    ("b20_smooth_83x61", "smooth", 83, 61, 33, ["-B", "20"]),
+    ("b25_flat_75x50_q1", "flat", 75, 50, 34, ["-B", "25", "-q", "1"]),
+    ("b45_smooth_90x101", "smooth", 90, 101, 35, ["-B", "45"]),
+    ("b100_rand_100x120_q5", "rand", 100, 120, 36, ["-B", "100", "-q", "5"]),
+    ("b125_smooth_130x125", "smooth", 130, 125, 37, ["-B", "125"]),
+    ("b27_rand_54x60", "rand", 54, 60, 38, ["-B", "27"]),
+    ("b81_smooth_81x90_x", "smooth", 81, 90, 39, ["-B", "81", "-x"]),
 ]
 L_CASES = [
     # name, kind, H, W, seed, lambda, extra flags

@@ -55,7 +55,7 @@ def test_padded_shape_is_host_only():
 
 @pytest.mark.parametrize("args,status", [
     (dict(H=0), L.VCF_ERR_INVALID),              # not an image
-    (dict(block_size=5), L.VCF_ERR_UNSUPPORTED),   # -B 5: no radix-5 transform on the HIP path
+    (dict(block_size=7), L.VCF_ERR_UNSUPPORTED),   # -B 7: no radix-7 (radfg) transform on the HIP path
     (dict(block_size=256), L.VCF_ERR_UNSUPPORTED),  # beyond the -L range 2..128
     (dict(block_size=16, flags=2), L.VCF_ERR_UNSUPPORTED),  # -p needs B = 8 (cv2 table resize)
     (dict(Q=0), L.VCF_ERR_INVALID),
@@ -96,7 +96,15 @@ def test_product_never_imports_the_oracle():
 
 
 def test_block_size_coverage():
-    """-B sizes with a HIP transform: B = 2^a 3^b <= 128 (every -L candidate)."""
+    """-B sizes with a HIP transform: the 5-smooth B <= 128 (every -L candidate among them)."""
     lib = L.lib()
     have = [b for b in range(0, 300) if lib.vcf_dct_block_size_supported(b)]
-    assert have == [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128]
+    assert have == [b for b in range(1, 129) if _five_smooth(b)]
+    assert len(have) == 38 and all(2 ** i in have for i in range(1, 8))
+
+
+def _five_smooth(n):
+    for p in (2, 3, 5):
+        while n % p == 0:
+            n //= p
+    return n == 1

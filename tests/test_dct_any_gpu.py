@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 D = pytest.importorskip("vcf_amd.dct")
 MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest_general.json")))
-LENGTHS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128]
+LENGTHS = [1, 2, 3, 4, 5, 6, 8, 9, 10, 12, 15, 16, 18, 20, 24, 25, 27, 30, 32, 36, 40, 45, 48, 50, 54, 60, 64, 72, 75, 80, 81, 90, 96, 100, 108, 120, 125, 128]
 
 
 def _qf(flags):
@@ -129,7 +129,7 @@ def test_codec_block_size_files_match_reference(case, tmp_path):
 def test_unsupported_block_sizes_raise():
     from vcf_amd._lib import VCFUnsupported
     rgb = _smooth(20, 20, 0)
-    for B in (5, 7, 10, 256):
+    for B in (7, 11, 14, 49, 256):
         assert not D.block_size_supported(B)
         with pytest.raises(VCFUnsupported):
             D.encode(rgb, 32, 0, block_size=B)

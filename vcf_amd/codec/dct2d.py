@@ -9,8 +9,8 @@ span between reading the image and handing the indices to the entropy codec
 libvcf_amd.so (vcf_dct_dz_encode / vcf_dct_dz_decode); there is no CPU
 implementation of it in the product.
 
--B takes every block size the HIP path has a transform for (B = 2^a 3^b
-<= 128, vcf_dct_block_size_supported), -L runs optimize_block_size
+-B takes every block size the HIP path has a transform for (the 5-smooth
+B <= 128, vcf_dct_block_size_supported), -L runs optimize_block_size
 (2D-DCT.py:533-579) with the GPU doing each candidate's analysis/synthesis.
 Options the HIP path does not implement raise NotImplementedError when the
 codec is constructed (other block sizes, -p with B != 8, colour transforms
@@ -69,8 +69,8 @@ class CoDec(EICCoDec):
         if not self.encoding and filt != "no_filter":
             raise NotImplementedError(f"filter {filt!r}: only no_filter is on the HIP path")
         if not D.block_size_supported(self.block_size):
-            raise NotImplementedError(f"block size {self.block_size}: the HIP path covers B = 2^a 3^b <= 128 "
-                                      "(a <= 7, b <= 1)")
+            raise NotImplementedError(f"block size {self.block_size}: the HIP path covers the 5-smooth "
+                                      "B <= 128")
         if self.block_size != 8 and getattr(args, "perceptual_quantization", False):
             # 2D-DCT.py:85-90 resizes the JPEG tables with cv2 for B != 8 (not on the HIP path)
             raise NotImplementedError("-p with a block size other than 8")

@@ -5,8 +5,9 @@
 // What is computed is the same frame pipeline as vcf_dct_dz.hip
 // (src/2D-DCT.py:276-361 encode, :399-466 decode; assumptions A1-A5), with the
 // length-B pocketfft transforms of vcf_pocketfft.h.  Supported B: the
-// lengths pocketfft factors into 4, 2 and 3 (1, 2, 3, 4, 6, 8, 12, 16, 24,
-// 32, 48, 64, 96, 128); larger or other B return VCF_ERR_UNSUPPORTED.
+// lengths pocketfft factors into 4, 2, 3 and 5 up to 128 (1, 2, 3, 4, 5, 6,
+// 8, 9, 10, 12, 15, 16, ..., 120, 125, 128: 38 sizes); larger B or a prime
+// factor above 5 (pocketfft's generic radfg/radbg) return VCF_ERR_UNSUPPORTED.
 //
 // Mapping.  A "unit" is one channel of one BxB block.  A workgroup holds
 // U = 256/B units (encode, fp32) or 128/B units (decode, fp64), B lanes per
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(256) void dct_any_encode_kernel(const uint8_t *__re
     constexpr int U = enc_units<B>();
     constexpr int LD = B + 1;   // padded row: row-pass reads stride LD words (no bank conflicts)
     __shared__ float tile[U * B * LD];
-    const float *tw = c_tw_f32 + slot_of(B) * kSlot;
+    const float *tw = c_tw_f32 + slot_off(B);
 
     const int t = threadIdx.x;
     const int lu = t / B, x = t % B;
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(128) void dct_any_decode_kernel(const void *__restr
     constexpr int U = dec_units<B>();
     constexpr int LD = B + 1;
     __shared__ double tile[U * B * LD];
-    const double *tw = c_tw_f64 + slot_of(B) * kSlot;
+    const double *tw = c_tw_f64 + slot_off(B);
 
     const int t = threadIdx.x;
     const int lu = t / B, x = t % B;
@@ -309,14 +310,22 @@ int launch_decode(const void *kin, void *ws, bool k32, const GeomB &g, int Q, hi
     return hip_check(hipGetLastError(), "dct_any_decode_kernel launch");
 }
 
-#define VCF_ANY_SWITCH(B, CALL)                                                            \
-    switch (B) {                                                                           \
-    case 1: return CALL(1); case 2: return CALL(2); case 3: return CALL(3);                \
-    case 4: return CALL(4); case 6: return CALL(6); case 8: return CALL(8);                \
-    case 12: return CALL(12); case 16: return CALL(16); case 24: return CALL(24);          \
-    case 32: return CALL(32); case 48: return CALL(48); case 64: return CALL(64);          \
-    case 96: return CALL(96); case 128: return CALL(128);                                  \
-    default: return set_error(VCF_ERR_UNSUPPORTED, "block size %d is not supported", B);   \
+// the 5-smooth block sizes <= 128 (kLens)
+#define VCF_ANY_SWITCH(B, CALL)                                                                  \
+    switch (B) {                                                                                 \
+    case 1: return CALL(1); case 2: return CALL(2); case 3: return CALL(3); case 4: return CALL(4); \
+    case 5: return CALL(5); case 6: return CALL(6); case 8: return CALL(8); case 9: return CALL(9); \
+    case 10: return CALL(10); case 12: return CALL(12); case 15: return CALL(15);                \
+    case 16: return CALL(16); case 18: return CALL(18); case 20: return CALL(20);                \
+    case 24: return CALL(24); case 25: return CALL(25); case 27: return CALL(27);                \
+    case 30: return CALL(30); case 32: return CALL(32); case 36: return CALL(36);                \
+    case 40: return CALL(40); case 45: return CALL(45); case 48: return CALL(48);                \
+    case 50: return CALL(50); case 54: return CALL(54); case 60: return CALL(60);                \
+    case 64: return CALL(64); case 72: return CALL(72); case 75: return CALL(75);                \
+    case 80: return CALL(80); case 81: return CALL(81); case 90: return CALL(90);                \
+    case 96: return CALL(96); case 100: return CALL(100); case 108: return CALL(108);            \
+    case 120: return CALL(120); case 125: return CALL(125); case 128: return CALL(128);          \
+    default: return set_error(VCF_ERR_UNSUPPORTED, "block size %d is not supported", B);         \
     }
 
 int check_any(const void *a, const void *b, int64_t n_frames, int H, int W, int B, int Q, uint32_t flags,
@@ -329,7 +338,7 @@ int check_any(const void *a, const void *b, int64_t n_frames, int H, int W, int 
     if (B < 1) return set_error(VCF_ERR_INVALID, "block size %d", B);
     if (slot_of(B) < 0)
         return set_error(VCF_ERR_UNSUPPORTED,
-                         "block size %d: the HIP path covers B = 2^a 3^b <= 128 with a <= 7, b <= 1", B);
+                         "block size %d: the HIP path covers the 5-smooth B <= 128 (pocketfft radix 2/3/4/5)", B);
     if (Q < 1 || (decode && !k32 && Q > 32767))
         return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
     if (flags & VCF_DCT_PERCEPTUAL)

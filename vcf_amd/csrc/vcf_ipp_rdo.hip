@@ -156,8 +156,8 @@ __global__ __launch_bounds__(64) void ipp_rdo_modes_kernel(const uint8_t *__rest
     __shared__ RdoShared<BS> sh;
     const int lane = threadIdx.x;
     const int bx = blockIdx.x, by = blockIdx.y, nbx = gridDim.x;
-    const double *tw64 = c_tw_f64 + slot_of(BS) * kSlot;
-    const float *tw32 = c_tw_f32 + slot_of(BS) * kSlot;
+    const double *tw64 = c_tw_f64 + slot_off(BS);
+    const float *tw32 = c_tw_f32 + slot_off(BS);
     for (int e = lane; e < BS * BS; e += 64) {
         const int y = e / BS, x = e % BS;
         const long long o = ((long long)(by * BS + y) * W + bx * BS + x) * 3;

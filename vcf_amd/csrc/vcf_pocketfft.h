@@ -7,9 +7,10 @@
 // (assumptions A1/A2, idiom at src/IPP_DCT.py:257-259), i.e. pocketfft's
 // T_dcst23<T>::exec over rfftp<T>.  Bit-exactness needs the same float
 // operations in the same order, so this restates that code path:
-//   - rfftp factorisation: 4s first, then a 2 swapped to the front, then 3s;
-//   - backward (DCT-II) runs radb2/radb3/radb4 in factor order, forward
-//     (DCT-III) runs radf4/radf2/radf3 in reverse factor order, each pass
+//   - rfftp factorisation: 4s first, then a 2 swapped to the front, then 3s
+//     and 5s;
+//   - backward (DCT-II) runs radb2/3/4/5 in factor order, forward (DCT-III)
+//     runs radf4/2/3/5 in reverse factor order, each pass
 //     reading one register array and writing the other;
 //   - the final multiplication by fct = 1/sqrt(2N) (copy_and_norm);
 //   - T_dcst23's pre/post twiddle loops and the ortho sqrt2 scalings.
@@ -48,7 +49,7 @@ constexpr Factors factorize(int len)
     if (l > 1) r.f[r.n++] = l;
     int l1 = 1, off = 0;
     for (int k = 0; k < r.n; ++k) {
-        if (r.f[k] != 2 && r.f[k] != 3 && r.f[k] != 4) r.ok = false;
+        if (r.f[k] != 2 && r.f[k] != 3 && r.f[k] != 4 && r.f[k] != 5) r.ok = false;
         int ip = r.f[k], ido = len / (l1 * ip);
         r.tw_off[k] = off;
         if (k < r.n - 1) off += (ip - 1) * (ido - 1);
@@ -185,6 +186,65 @@ __device__ __forceinline__ void radf4(const T *cc, T *ch, const T *wa)
 #undef WA
 }
 
+template <typename T>
+__device__ __forceinline__ void rearrange(T &rx, T &ix, T &ry, T &iy)   // POCKETFFT_REARRANGE
+{
+    const T t1 = rx + ry, t2 = ry - rx, t3 = ix + iy, t4 = ix - iy;
+    rx = t1; ix = t3; ry = t4; iy = t2;
+}
+
+template <typename T, int IDO, int L1>
+__device__ __forceinline__ void radf5(const T *cc, T *ch, const T *wa)
+{
+    const T tr11 = T(0.3090169943749474241022934171828191L), ti11 = T(0.9510565162951535721164393333793821L),
+            tr12 = T(-0.8090169943749474241022934171828191L), ti12 = T(0.5877852522924731291687059546390728L);
+#define CC(a, b, c) cc[(a) + IDO * ((b) + L1 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + 5 * (c))]
+#define WA(x, i) wa[(i) + (x) * (IDO - 1)]
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        T cr2, cr3, ci4, ci5;
+        PM(cr2, ci5, CC(0, k, 4), CC(0, k, 1));
+        PM(cr3, ci4, CC(0, k, 3), CC(0, k, 2));
+        CH(0, 0, k) = CC(0, k, 0) + cr2 + cr3;
+        CH(IDO - 1, 1, k) = CC(0, k, 0) + tr11 * cr2 + tr12 * cr3;
+        CH(0, 2, k) = ti11 * ci5 + ti12 * ci4;
+        CH(IDO - 1, 3, k) = CC(0, k, 0) + tr12 * cr2 + tr11 * cr3;
+        CH(0, 4, k) = ti12 * ci5 - ti11 * ci4;
+    }
+    if constexpr (IDO > 1) {
+#pragma unroll
+        for (int k = 0; k < L1; ++k)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                const int ic = IDO - i;
+                T di2, di3, di4, di5, dr2, dr3, dr4, dr5;
+                MULPM(dr2, di2, WA(0, i - 2), WA(0, i - 1), CC(i - 1, k, 1), CC(i, k, 1));
+                MULPM(dr3, di3, WA(1, i - 2), WA(1, i - 1), CC(i - 1, k, 2), CC(i, k, 2));
+                MULPM(dr4, di4, WA(2, i - 2), WA(2, i - 1), CC(i - 1, k, 3), CC(i, k, 3));
+                MULPM(dr5, di5, WA(3, i - 2), WA(3, i - 1), CC(i - 1, k, 4), CC(i, k, 4));
+                rearrange(dr2, di2, dr5, di5);
+                rearrange(dr3, di3, dr4, di4);
+                CH(i - 1, 0, k) = CC(i - 1, k, 0) + dr2 + dr3;
+                CH(i, 0, k) = CC(i, k, 0) + di2 + di3;
+                T tr2 = CC(i - 1, k, 0) + tr11 * dr2 + tr12 * dr3;
+                T ti2 = CC(i, k, 0) + tr11 * di2 + tr12 * di3;
+                T tr3 = CC(i - 1, k, 0) + tr12 * dr2 + tr11 * dr3;
+                T ti3 = CC(i, k, 0) + tr12 * di2 + tr11 * di3;
+                T tr5, tr4, ti5, ti4;
+                MULPM(tr5, tr4, dr5, dr4, ti11, ti12);
+                MULPM(ti5, ti4, di5, di4, ti11, ti12);
+                PM(CH(i - 1, 2, k), CH(ic - 1, 1, k), tr2, tr5);
+                PM(CH(i, 2, k), CH(ic, 1, k), ti5, ti2);
+                PM(CH(i - 1, 4, k), CH(ic - 1, 3, k), tr3, tr4);
+                PM(CH(i, 4, k), CH(ic, 3, k), ti4, ti3);
+            }
+    }
+#undef CC
+#undef CH
+#undef WA
+}
+
 // ---- backward passes (halfcomplex -> real) -------------------------------
 template <typename T, int IDO, int L1>
 __device__ __forceinline__ void radb2(const T *cc, T *ch, const T *wa)
@@ -312,6 +372,64 @@ __device__ __forceinline__ void radb4(const T *cc, T *ch, const T *wa)
 #undef WA
 }
 
+template <typename T, int IDO, int L1>
+__device__ __forceinline__ void radb5(const T *cc, T *ch, const T *wa)
+{
+    const T tr11 = T(0.3090169943749474241022934171828191L), ti11 = T(0.9510565162951535721164393333793821L),
+            tr12 = T(-0.8090169943749474241022934171828191L), ti12 = T(0.5877852522924731291687059546390728L);
+#define CC(a, b, c) cc[(a) + IDO * ((b) + 5 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + L1 * (c))]
+#define WA(x, i) wa[(i) + (x) * (IDO - 1)]
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        T ti5 = CC(0, 2, k) + CC(0, 2, k);
+        T ti4 = CC(0, 4, k) + CC(0, 4, k);
+        T tr2 = CC(IDO - 1, 1, k) + CC(IDO - 1, 1, k);
+        T tr3 = CC(IDO - 1, 3, k) + CC(IDO - 1, 3, k);
+        CH(0, k, 0) = CC(0, 0, k) + tr2 + tr3;
+        T cr2 = CC(0, 0, k) + tr11 * tr2 + tr12 * tr3;
+        T cr3 = CC(0, 0, k) + tr12 * tr2 + tr11 * tr3;
+        T ci4, ci5;
+        MULPM(ci5, ci4, ti5, ti4, ti11, ti12);
+        PM(CH(0, k, 4), CH(0, k, 1), cr2, ci5);
+        PM(CH(0, k, 3), CH(0, k, 2), cr3, ci4);
+    }
+    if constexpr (IDO > 1) {
+#pragma unroll
+        for (int k = 0; k < L1; ++k)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                const int ic = IDO - i;
+                T tr2, tr3, tr4, tr5, ti2, ti3, ti4, ti5;
+                PM(tr2, tr5, CC(i - 1, 2, k), CC(ic - 1, 1, k));
+                PM(ti5, ti2, CC(i, 2, k), CC(ic, 1, k));
+                PM(tr3, tr4, CC(i - 1, 4, k), CC(ic - 1, 3, k));
+                PM(ti4, ti3, CC(i, 4, k), CC(ic, 3, k));
+                CH(i - 1, k, 0) = CC(i - 1, 0, k) + tr2 + tr3;
+                CH(i, k, 0) = CC(i, 0, k) + ti2 + ti3;
+                T cr2 = CC(i - 1, 0, k) + tr11 * tr2 + tr12 * tr3;
+                T ci2 = CC(i, 0, k) + tr11 * ti2 + tr12 * ti3;
+                T cr3 = CC(i - 1, 0, k) + tr12 * tr2 + tr11 * tr3;
+                T ci3 = CC(i, 0, k) + tr12 * ti2 + tr11 * ti3;
+                T ci4, ci5, cr5, cr4;
+                MULPM(cr5, cr4, tr5, tr4, ti11, ti12);
+                MULPM(ci5, ci4, ti5, ti4, ti11, ti12);
+                T dr2, dr3, dr4, dr5, di2, di3, di4, di5;
+                PM(dr4, dr3, cr3, ci4);
+                PM(di3, di4, ci3, cr4);
+                PM(dr5, dr2, cr2, ci5);
+                PM(di2, di5, ci2, cr5);
+                MULPM(CH(i, k, 1), CH(i - 1, k, 1), WA(0, i - 2), WA(0, i - 1), di2, dr2);
+                MULPM(CH(i, k, 2), CH(i - 1, k, 2), WA(1, i - 2), WA(1, i - 1), di3, dr3);
+                MULPM(CH(i, k, 3), CH(i - 1, k, 3), WA(2, i - 2), WA(2, i - 1), di4, dr4);
+                MULPM(CH(i, k, 4), CH(i - 1, k, 4), WA(3, i - 2), WA(3, i - 1), di5, dr5);
+            }
+    }
+#undef CC
+#undef CH
+#undef WA
+}
+
 // ---- rfftp backward()/forward() over the whole factor list ----------------
 // p1 holds the data; each pass writes the other array.  Returns (statically)
 // which array holds the result: true = p1.
@@ -323,7 +441,8 @@ __device__ __forceinline__ void backward_passes(T *p1, T *p2, const T *tw)
         constexpr int ip = F.f[K], ido = N / (ip * L1);
         if constexpr (ip == 4) radb4<T, ido, L1>(p1, p2, tw + F.tw_off[K]);
         else if constexpr (ip == 2) radb2<T, ido, L1>(p1, p2, tw + F.tw_off[K]);
-        else radb3<T, ido, L1>(p1, p2, tw + F.tw_off[K]);
+        else if constexpr (ip == 3) radb3<T, ido, L1>(p1, p2, tw + F.tw_off[K]);
+        else radb5<T, ido, L1>(p1, p2, tw + F.tw_off[K]);
         backward_passes<T, N, K + 1, L1 * ip>(p2, p1, tw);
     }
 }
@@ -336,7 +455,8 @@ __device__ __forceinline__ void forward_passes(T *p1, T *p2, const T *tw)
         constexpr int k = F.n - K1 - 1, ip = F.f[k], ido = N / L1, l1 = L1 / ip;
         if constexpr (ip == 4) radf4<T, ido, l1>(p1, p2, tw + F.tw_off[k]);
         else if constexpr (ip == 2) radf2<T, ido, l1>(p1, p2, tw + F.tw_off[k]);
-        else radf3<T, ido, l1>(p1, p2, tw + F.tw_off[k]);
+        else if constexpr (ip == 3) radf3<T, ido, l1>(p1, p2, tw + F.tw_off[k]);
+        else radf5<T, ido, l1>(p1, p2, tw + F.tw_off[k]);
         forward_passes<T, N, K1 + 1, l1>(p2, p1, tw);
     }
 }

@@ -16,20 +16,28 @@
 namespace vcf {
 namespace {
 
-constexpr int kSlot = 264;     // >= tw_len + N + 1 for N <= 128
-constexpr int kNumSlots = 14;
-
-// supported lengths and their table slots
-constexpr int kLens[kNumSlots] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128};
+// supported lengths: the 5-smooth B <= 128 (pocketfft's radix-2/3/4/5 passes)
+constexpr int kNumSlots = 38;
+constexpr int kLens[kNumSlots] = {1,  2,  3,  4,  5,  6,  8,  9,  10, 12,  15,  16,  18,  20,  24,  25,  27,  30,  32,
+                                  36, 40, 45, 48, 50, 54, 60, 64, 72, 75, 80, 81, 90, 96, 100, 108, 120, 125, 128};
 constexpr int slot_of(int n)
 {
     for (int i = 0; i < kNumSlots; ++i)
         if (kLens[i] == n) return i;
     return -1;
 }
+// a length's table: its rfftp twiddles, then N DCT twiddles, then fct (<= 2N + 1 values)
+constexpr int slot_size(int n) { return 2 * n + 1; }
+constexpr int slot_off(int n)
+{
+    int off = 0;
+    for (int i = 0; i < kNumSlots && kLens[i] != n; ++i) off += slot_size(kLens[i]);
+    return off;
+}
+constexpr int kTableSize = slot_off(1 << 30);   // all slots
 
-__constant__ float c_tw_f32[kNumSlots * kSlot];
-__constant__ double c_tw_f64[kNumSlots * kSlot];
+__constant__ float c_tw_f32[kTableSize];
+__constant__ double c_tw_f64[kTableSize];
 
 // ---- host: pocketfft sincos_2pibyn<T>(n)[idx].{r,i} (values in double) ----
 void sc_calc(size_t x, size_t n, double ang, double &re, double &im)
@@ -108,11 +116,11 @@ int ensure_tables()
     if (dev < 0 || dev >= 64) return set_error(VCF_ERR_INVALID, "device %d", dev);
     std::lock_guard<std::mutex> lock(mu);
     if (done[dev]) return VCF_OK;
-    static float tf[kNumSlots * kSlot];
-    static double td[kNumSlots * kSlot];
+    static float tf[kTableSize];
+    static double td[kTableSize];
     for (int s = 0; s < kNumSlots; ++s) {
-        fill_slot<float>(kLens[s], tf + s * kSlot);
-        fill_slot<double>(kLens[s], td + s * kSlot);
+        fill_slot<float>(kLens[s], tf + slot_off(kLens[s]));
+        fill_slot<double>(kLens[s], td + slot_off(kLens[s]));
     }
     rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_tw_f32), tf, sizeof(tf)), "twiddle upload");
     if (rc != VCF_OK) return rc;

@@ -22,7 +22,7 @@ __all__ = ["padded_shape", "flags_from", "encode_device", "decode_device", "enco
 
 
 def block_size_supported(block_size: int) -> bool:
-    """True if the HIP path has a transform of this length (B = 2^a 3^b <= 128)."""
+    """True if the HIP path has a transform of this length (5-smooth B <= 128)."""
     return bool(_lib.lib().vcf_dct_block_size_supported(int(block_size)))
 
 
