@@ -99,14 +99,20 @@ int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
                       void *stream);
 
 /* Same as vcf_dct_dz_encode with an explicit kernel choice (benchmarking and
- * tests): 0 = automatic, 1 = lane-per-block tile kernel (the default),
+ * tests): 0 = automatic (5 for a power-of-two Q without -p, else 1),
+ * 1 = lane-per-block tile kernel, scalar fp32 transforms,
  * 2 = diagnostic: variant 1's arithmetic with no memory traffic (writes one
  * word per block, not the coefficients; power-of-two Q only),
  * 3 = column-per-lane tile kernel (8 lanes per block, LDS transpose),
  * 4 = variant 1 with compiler-generated byte code for the colour conversion
  * instead of SDWA operands (A/B reference; power-of-two Q, default flags,
- * frames that need no padding).
- * Variants 1, 3 and 4 produce identical bytes. */
+ * frames that need no padding),
+ * 5 = variant 1 with packed-fp32 transforms (two 1-D transforms per
+ * v_pk_add_f32 / v_pk_mul_f32; power-of-two Q, no -p; else as 1),
+ * 6 = diagnostic 2 with variant 5's arithmetic,
+ * 8 = diagnostic: variant 1's loads, LDS image and copy-out without the
+ * transforms (output bytes are not the coefficients; aligned frames, subbands).
+ * Variants 1, 3, 4 and 5 produce identical bytes. */
 int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H,
                               int32_t W, int32_t block_size, int32_t Q, uint32_t flags,
                               uint8_t *k_dev, void *stream);

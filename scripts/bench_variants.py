@@ -25,7 +25,7 @@ for v in variants:
 s.synchronize()
 ref = outs[variants[0]].download(np.empty((F, Hp, Wp, 3), np.uint8))
 for v in variants[1:]:
-    if v == 2:
+    if v in (2, 6, 8):
         continue   # diagnostic variants do not produce the output
     o = outs[v].download(np.empty((F, Hp, Wp, 3), np.uint8))
     print(f"variant {v} == variant {variants[0]}: {np.array_equal(o, ref)}", flush=True)

@@ -108,7 +108,7 @@ def test_zero_frames_and_errors():
         D.decode(np.zeros((8, 8, 3), np.uint8), 8, 8, 40000)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3])
+@pytest.mark.parametrize("variant", [0, 1, 3, 5])
 @pytest.mark.parametrize("Q,flags", [(32, 0), (7, 0), (1, 0), (32, 1), (5, 3), (64, 2)])
 def test_encode_variants_vs_oracle(variant, Q, flags):
     """Both encode kernels on shapes both support (no padding, W % 32 == 0)."""
@@ -154,3 +154,21 @@ def test_decode_variants_batched():
     b = D.decode(k, 72, 4104, 32, 0, variant=2)
     assert np.array_equal(a, b)
     assert np.array_equal(a[2], O.decode_frame(k[2], 72, 4104, 32, 0))
+
+
+@pytest.mark.parametrize("variant", [0, 1, 5])
+@pytest.mark.parametrize("shape,n,flags", [((1080, 1920), 8, 0), ((100, 300), 400, 0), ((100, 300), 400, 1),
+                                           ((72, 4104), 12, 0), ((13, 29), 900, 1)])
+def test_packed_encode_batches(variant, shape, n, flags):
+    """The tile kernels (scalar and packed-fp32 transforms, full-tile and
+    generic copy-out) on large batches with partial last tiles, padding and
+    both output layouts: equal to each other and spot-checked against the oracle."""
+    H, W = shape
+    rng = np.random.default_rng(H + W + n)
+    frames = rng.integers(0, 256, (n, H, W, 3), dtype=np.uint8)
+    frames[: n // 2] = _rand((H, W, 3), 5, "smooth")
+    want = D.encode(frames, 32, flags, variant=3)   # the column-per-lane kernel, independent code
+    got = D.encode(frames, 32, flags, variant=variant)
+    assert np.array_equal(got, want)
+    for i in (0, n // 2, n - 1):
+        assert np.array_equal(got[i], O.encode_frame(frames[i], 32, flags)), i

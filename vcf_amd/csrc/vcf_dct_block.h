@@ -473,22 +473,27 @@ VCF_HD constexpr FinalK final_k(float pair_scale, float single_scale)
                   VCF_TWF2 * pair_scale, VCF_TWF4 * pair_scale, VCF_TWF3 * single_scale, VCF_HF * single_scale};
 }
 
-// dct2_8r with caller-chosen final multipliers (see above)
-VCF_HD void dct2_8f(float (&c)[8], const FinalK &k)
+// dct2_8r with caller-chosen final multipliers (see above).  T = float, or
+// (device) a 2-vector of floats: two independent transforms in lock step,
+// which clang issues as packed v_pk_add_f32 / v_pk_mul_f32 -- each element
+// sees the same IEEE operations in the same order, so the results are the
+// scalar ones bit for bit.
+template <typename T>
+VCF_HD void dct2_8f(T (&c)[8], const FinalK &k)
 {
-    const float x1 = c[1] + c[2], x2 = c[2] - c[1];
-    const float x3 = c[3] + c[4], x7 = c[3] - c[4];
-    const float x5 = c[5] + c[6], x6 = c[6] - c[5];
-    const float a0 = c[0] + c[7], a4 = c[0] - c[7];
-    const float a1 = x1 + x5, tr2 = x1 - x5;
-    const float ti2 = x2 + x6, a2 = x2 - x6;
-    const float a6 = VCF_HF * ti2 + VCF_HF * tr2;
-    const float a5 = VCF_HF * tr2 - VCF_HF * ti2;
-    const float T2 = a0 + x3, T1 = a0 - x3;
-    const float r0 = T2 + a1, r4 = T2 - a1, r6 = T1 + a2, r2 = T1 - a2;
-    const float U2 = a4 + x7, U1 = a4 - x7;
-    const float r1 = U2 + a5, r5 = U2 - a5, r7 = U1 + a6, r3 = U1 - a6;
-    float t1, t2;
+    const T x1 = c[1] + c[2], x2 = c[2] - c[1];
+    const T x3 = c[3] + c[4], x7 = c[3] - c[4];
+    const T x5 = c[5] + c[6], x6 = c[6] - c[5];
+    const T a0 = c[0] + c[7], a4 = c[0] - c[7];
+    const T a1 = x1 + x5, tr2 = x1 - x5;
+    const T ti2 = x2 + x6, a2 = x2 - x6;
+    const T a6 = VCF_HF * ti2 + VCF_HF * tr2;
+    const T a5 = VCF_HF * tr2 - VCF_HF * ti2;
+    const T T2 = a0 + x3, T1 = a0 - x3;
+    const T r0 = T2 + a1, r4 = T2 - a1, r6 = T1 + a2, r2 = T1 - a2;
+    const T U2 = a4 + x7, U1 = a4 - x7;
+    const T r1 = U2 + a5, r5 = U2 - a5, r7 = U1 + a6, r3 = U1 - a6;
+    T t1, t2;
     t1 = k.p0a * r7 + k.p0b * r1; t2 = k.p0a * r1 - k.p0b * r7;
     c[1] = t1 + t2; c[7] = t1 - t2;
     t1 = k.p1a * r6 + k.p1b * r2; t2 = k.p1a * r2 - k.p1b * r6;
@@ -655,6 +660,82 @@ VCF_HD void encode_block_channel_fold(const uint32_t (&raw)[8][6], const FinalK 
         }
     }
 }
+
+#if defined(__HIPCC__)
+// ---- packed-fp32 channel encoder (POW2 Q, no -p) --------------------------
+// The same arithmetic as encode_block_channel_fold<C, true, false, true>, two
+// 1-D transforms per instruction: the column pass runs pixel columns (x, x+1)
+// as one float2 transform, a 2x2 transpose per (row pair, column pair)
+// regroups the results as rows (i, i+1), and the row pass runs those row
+// pairs.  Element for element the IEEE operations and their order are those
+// of the scalar path (tests/test_dct_gpu.py checks every variant against the
+// oracle), at about half the VALU instructions for the transforms.
+typedef float vcf_f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t vcf_u2 __attribute__((ext_vector_type(2)));
+
+// bits of (channel C of pixel X) + magic, before the float subtraction
+template <int C, int X>
+VCF_HD uint32_t ycocg_bits_sdwa(const uint32_t (&row)[6], uint32_t magic)
+{
+    constexpr int nr = 3 * X, ng = 3 * X + 1, nb = 3 * X + 2;
+    const uint32_t wr = row[nr >> 2], wg = row[ng >> 2], wb = row[nb >> 2];
+    if (C == 0) return add_sdwa<nr & 3, nb & 3>(wr, wb) + twice_byte<ng & 3>(wg) + magic;
+    if (C == 1) return sub_sdwa<-1, nb & 3>(add_sdwa<-1, nr & 3>(magic, wr), wb);
+    const uint32_t rb = add_sdwa<nr & 3, nb & 3>(wr, wb);
+    return add_sdwa<-1, ng & 3>(add_sdwa<-1, ng & 3>(magic - rb, wg), wg);
+}
+
+template <int C, int XP>
+VCF_HD void fold_columns_pk(const uint32_t (&raw)[8][6], uint32_t magic, const FinalK &colk,
+                            vcf_f2 (&v)[8][4], vcf_f2 &dep)
+{
+    if constexpr (XP < 4) {
+        constexpr float centre = C == 1 ? 8388608.0f + 256.0f : 8388608.0f + 512.0f;
+        vcf_f2 col[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) {
+            const vcf_u2 b = {ycocg_bits_sdwa<C, 2 * XP>(raw[y], magic),
+                              ycocg_bits_sdwa<C, 2 * XP + 1>(raw[y], magic)};
+            col[y] = __builtin_bit_cast(vcf_f2, b) - centre;
+        }
+        chain8(col, dep);
+        dct2_8f(col, colk);
+#pragma unroll
+        for (int y = 0; y < 8; ++y) v[y][XP] = col[y];
+        dep = col[0];
+        fold_columns_pk<C, XP + 1>(raw, magic, colk, v, dep);
+    }
+}
+
+template <int C, typename Sink>
+VCF_HD void encode_block_channel_pk(const uint32_t (&raw)[8][6], const FinalK &rowk, float dep0, Sink &&sink)
+{
+    constexpr float cs = C == 1 ? 0.5f : 0.25f;
+    constexpr FinalK colk = final_k(cs * 0.25f, cs * 0.5f);
+    vcf_f2 v[8][4];
+    vcf_f2 dep = {dep0, dep0};
+    uint32_t magic = ycocg_magic_word<C>();
+    VCF_OPAQUE(magic);
+    fold_columns_pk<C, 0>(raw, magic, colk, v, dep);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        vcf_f2 r[8];
+#pragma unroll
+        for (int xp = 0; xp < 4; ++xp) {
+            r[2 * xp] = __builtin_shufflevector(v[2 * p][xp], v[2 * p + 1][xp], 0, 2);
+            r[2 * xp + 1] = __builtin_shufflevector(v[2 * p][xp], v[2 * p + 1][xp], 1, 3);
+        }
+        chain8(r, dep);
+        dct2_8f(r, rowk);
+        dep = r[0];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            sink(2 * p, j, (uint32_t)cvt_trunc_i32(r[j].x));
+            sink(2 * p + 1, j, (uint32_t)cvt_trunc_i32(r[j].y));
+        }
+    }
+}
+#endif
 
 VCF_HD uint32_t byte_at(const uint32_t (&K)[16], int n)
 {

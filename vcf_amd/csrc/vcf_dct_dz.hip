@@ -125,6 +125,37 @@ __device__ __forceinline__ void move_runs_tab(const Geom &g, uint8_t *stage, con
     }
 }
 
+// Copy-out of a full tile (nvalid == kTile, g.vec): compile-time chunk
+// geometry (12 16-byte chunks per lane), every LDS read issued before the
+// stores -- the generic loop above waits on each read in turn (4-5 % of the
+// encode).
+template <bool SUB>
+__device__ __forceinline__ void move_runs_full(const Geom &g, const uint8_t *stage, const uint32_t *rowbase,
+                                               uint8_t *frame)
+{
+    constexpr int nseg = SUB ? 64 : 8;
+    constexpr int bpb = SUB ? 3 : 24;
+    constexpr int lds_stride = SUB ? kSegBytes : kTile * 24;
+    constexpr int cps = (kTile * bpb) >> 4;
+    constexpr int per_lane = nseg * cps / kTile;
+    static_assert(nseg * cps % kTile == 0, "whole stores per lane");
+    const int tid = threadIdx.x;
+    u32x4 v[per_lane];
+    uint32_t go[per_lane];
+#pragma unroll
+    for (int r = 0; r < per_lane; ++r) {
+        const int q = tid + r * kTile;
+        const int seg = q / cps;
+        const int off = (q - seg * cps) << 4;
+        const int blk = off / bpb;
+        go[r] = rowbase[blk] + seg_base<SUB>(g, seg) + (uint32_t)(off - blk * bpb);
+        v[r] = *reinterpret_cast<const u32x4 *>(stage + seg * lds_stride + off);
+    }
+#pragma unroll
+    for (int r = 0; r < per_lane; ++r)
+        __builtin_nontemporal_store(v[r] ^ 0x80808080u, reinterpret_cast<u32x4 *>(frame + go[r]));
+}
+
 // Make raw[] look redefined *after* `dep` exists, so a channel's byte
 // extractions can neither be CSE'd with the previous channel's nor hoisted
 // above it (either keeps 2-3 channels' inputs live at once and spills).
@@ -171,7 +202,7 @@ __device__ __forceinline__ void load_block(const Geom &g, const uint8_t *src, in
     }
 }
 
-template <bool POW2, bool SUB, bool PERC, bool SDWA>
+template <bool POW2, bool SUB, bool PERC, bool SDWA, bool PK = false, bool MEMONLY = false>
 __device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncConsts &K, const FinalK &rowk,
                                              uint8_t *stage, int tid)
 {
@@ -189,17 +220,35 @@ __device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncCon
         if (SUB) stage[(i * 8 + j) * kSegBytes + tid * 3 + 2] = (uint8_t)w;
         else stage[i * (kTile * 24) + tid * 24 + j * 3 + 2] = (uint8_t)w;
     };
-    encode_block_channel_fold<0, POW2, PERC, SDWA>(raw, rowk, K.qd, s0);
-    opaque(raw, (uint32_t)tid);
-    encode_block_channel_fold<1, POW2, PERC, SDWA>(raw, rowk, K.qd, s1);
-    opaque(raw, (uint32_t)tid);
-    encode_block_channel_fold<2, POW2, PERC, SDWA>(raw, rowk, K.qd, s2);
+    if constexpr (MEMONLY) {   // diagnostic: the same LDS and HBM traffic, no transform
+#pragma unroll
+        for (int n = 0; n < 64; ++n) {
+            const uint32_t w = raw[n >> 3][(n * 3 / 4) % 6] >> (8 * (n & 3));
+            s0(n >> 3, n & 7, w);
+            s1(n >> 3, n & 7, w >> 1);
+            s2(n >> 3, n & 7, w >> 2);
+        }
+    } else if constexpr (PK && POW2 && !PERC) {
+        encode_block_channel_pk<0>(raw, rowk, K.qd[0], s0);
+        opaque(raw, (uint32_t)tid);
+        encode_block_channel_pk<1>(raw, rowk, K.qd[0], s1);
+        opaque(raw, (uint32_t)tid);
+        encode_block_channel_pk<2>(raw, rowk, K.qd[0], s2);
+    } else {
+        encode_block_channel_fold<0, POW2, PERC, SDWA>(raw, rowk, K.qd, s0);
+        opaque(raw, (uint32_t)tid);
+        encode_block_channel_fold<1, POW2, PERC, SDWA>(raw, rowk, K.qd, s1);
+        opaque(raw, (uint32_t)tid);
+        encode_block_channel_fold<2, POW2, PERC, SDWA>(raw, rowk, K.qd, s2);
+    }
 }
 
-template <bool POW2, bool SUB, bool PERC, bool PAD, bool SDWA = true>
-__global__ __launch_bounds__(kTile, 2) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
-                                                                 uint8_t *__restrict__ kout, Geom g,
-                                                                 EncConsts K, FinalK rowk)
+// PK: packed-fp32 transforms (power-of-two Q, no -p); MEMONLY: diagnostic
+// with the same loads, LDS image and copy-out but no transforms.
+template <bool POW2, bool SUB, bool PERC, bool PAD, bool SDWA = true, bool PK = false, bool MEMONLY = false>
+__global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
+                                                              uint8_t *__restrict__ kout, Geom g,
+                                                              EncConsts K, FinalK rowk)
 {
     __shared__ __attribute__((aligned(16))) uint8_t stage[kStageBytes];
     __shared__ uint32_t rowbase[kTile];
@@ -213,15 +262,17 @@ __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_kernel(const uint8_t *
         rowbase[tid] = block_rowbase<SUB>(g, by, bx);
         uint32_t raw[8][6];
         load_block<PAD>(g, rgb + frame * g.in_stride, by, bx, raw);
-        encode_block<POW2, SUB, PERC, SDWA>(raw, K, rowk, stage, tid);
+        encode_block<POW2, SUB, PERC, SDWA, PK, MEMONLY>(raw, K, rowk, stage, tid);
     }
     __syncthreads();
-    move_runs_tab<SUB, true>(g, stage, rowbase, kout + frame * g.out_stride, nvalid);
+    if (nvalid == kTile && g.vec) move_runs_full<SUB>(g, stage, rowbase, kout + frame * g.out_stride);
+    else move_runs_tab<SUB, true>(g, stage, rowbase, kout + frame * g.out_stride, nvalid);
 }
 
 // Diagnostic (encode variant 2): the same body with no memory traffic at all
 // -- raw synthesised from the lane id, one word stored per lane -- to split
 // kernel time into arithmetic and memory (scripts/bench_variants.py).
+template <bool PK>
 __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_diag(uint8_t *__restrict__ kout, Geom g,
                                                                EncConsts K, FinalK rowk, long long nblocks)
 {
@@ -234,11 +285,19 @@ __global__ __launch_bounds__(kTile, 2) void dct_dz_encode_diag(uint8_t *__restri
         for (int w = 0; w < 6; ++w) raw[y][w] = (uint32_t)(gid * 2654435761u) ^ (y * 0x01010101u * (w + 1));
     uint32_t acc = 0;
     auto sink = [&](int i, int j, uint32_t w) { acc += w << ((i + j) & 7); };
-    encode_block_channel_fold<0, true, false, true>(raw, rowk, K.qd, sink);
-    opaque(raw, acc);
-    encode_block_channel_fold<1, true, false, true>(raw, rowk, K.qd, sink);
-    opaque(raw, acc);
-    encode_block_channel_fold<2, true, false, true>(raw, rowk, K.qd, sink);
+    if constexpr (PK) {
+        encode_block_channel_pk<0>(raw, rowk, K.qd[0], sink);
+        opaque(raw, acc);
+        encode_block_channel_pk<1>(raw, rowk, K.qd[0], sink);
+        opaque(raw, acc);
+        encode_block_channel_pk<2>(raw, rowk, K.qd[0], sink);
+    } else {
+        encode_block_channel_fold<0, true, false, true>(raw, rowk, K.qd, sink);
+        opaque(raw, acc);
+        encode_block_channel_fold<1, true, false, true>(raw, rowk, K.qd, sink);
+        opaque(raw, acc);
+        encode_block_channel_fold<2, true, false, true>(raw, rowk, K.qd, sink);
+    }
     reinterpret_cast<uint32_t *>(kout)[gid] = acc;
 }
 
@@ -733,7 +792,7 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         return dct_any_encode_u8(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, stream);
     int rc = check_args(rgb_dev, k_dev, n_frames, H, W, block_size, Q, flags, false);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 4) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
+    if (variant < 0 || variant > 8 || variant == 7) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -744,11 +803,15 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
     EncConsts K;
     make_enc_consts(K, Q);
     const FinalK rowk = pow2 ? row_final_k(Q) : final_k(1.0f, 1.0f);
-    if (variant == 2) {
+    if (variant == 2 || variant == 6) {   // 6: the diagnostic body with packed transforms
         if (!pow2) return set_error(VCF_ERR_INVALID, "diagnostic variant needs a power-of-two Q");
         const long long nblocks = (long long)n_frames * g.nbx * g.nby;
-        hipLaunchKernelGGL(dct_dz_encode_diag, dim3((unsigned)((nblocks + kTile - 1) / kTile)), dim3(kTile),
-                           0, (hipStream_t)stream, k_dev, g, K, rowk, nblocks);
+        if (variant == 6)
+            hipLaunchKernelGGL(dct_dz_encode_diag<true>, dim3((unsigned)((nblocks + kTile - 1) / kTile)),
+                               dim3(kTile), 0, (hipStream_t)stream, k_dev, g, K, rowk, nblocks);
+        else
+            hipLaunchKernelGGL(dct_dz_encode_diag<false>, dim3((unsigned)((nblocks + kTile - 1) / kTile)),
+                               dim3(kTile), 0, (hipStream_t)stream, k_dev, g, K, rowk, nblocks);
         return hip_check(hipGetLastError(), "dct_dz_encode_diag launch");
     }
     if (variant == 4) {   // A/B reference: variant 1 with generic byte code for the colour conversion
@@ -759,6 +822,30 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                                (hipStream_t)stream, rgb_dev + f0 * g.in_stride, k_dev + f0 * g.out_stride, g, K, rowk);
         }
         return hip_check(hipGetLastError(), "variant 4 launch");
+    }
+    if (variant == 8) {   // diagnostic: variant 1's memory traffic without the transforms (output wrong)
+        if (!(sub && !pad)) return set_error(VCF_ERR_INVALID, "variant 8: aligned frames, subband layout");
+        for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
+            const dim3 grid(g.tiles_per_frame, (unsigned)std::min<int64_t>(65535, n_frames - f0));
+            hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, false, true>), grid,
+                               dim3(kTile), 0, (hipStream_t)stream, rgb_dev + f0 * g.in_stride,
+                               k_dev + f0 * g.out_stride, g, K, rowk);
+        }
+        return hip_check(hipGetLastError(), "variant 8 launch");
+    }
+    if ((variant == 5 || (variant == 0 && pow2 && !perc)) && pow2 && !perc) {   // packed-fp32 transforms
+        for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
+            const dim3 grid(g.tiles_per_frame, (unsigned)std::min<int64_t>(65535, n_frames - f0));
+#define VCF_ENC_PK(SB, PD)                                                                                  \
+    if (sub == SB && pad == PD)                                                                             \
+        hipLaunchKernelGGL((dct_dz_encode_kernel<true, SB, false, PD, true, true>), grid, dim3(kTile), 0,   \
+                           (hipStream_t)stream, rgb_dev + f0 * g.in_stride, k_dev + f0 * g.out_stride, g, K, rowk);
+            VCF_ENC_PK(true, false) else VCF_ENC_PK(true, true) else VCF_ENC_PK(false, false) else VCF_ENC_PK(false, true)
+#undef VCF_ENC_PK
+            rc = hip_check(hipGetLastError(), "dct_dz_encode_kernel (packed) launch");
+            if (rc != VCF_OK) return rc;
+        }
+        return VCF_OK;
     }
     if (variant == 3) return launch_cols<128>(rgb_dev, n_frames, k_dev, g, K, pow2, sub, perc, pad, stream);
     for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {

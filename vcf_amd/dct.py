@@ -41,8 +41,8 @@ def encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32,
                   variant: int = 0) -> DeviceBuffer:
     """Frames resident in HBM -> coefficient frames in HBM (asynchronous on `stream`).
 
-    variant: 0 automatic, 1 LDS-staged tile kernel, 3 column-per-lane kernel (see vcf_amd.h),
-    -1 the generic-B kernels (any supported B, 8 included)."""
+    variant: 0 automatic, 1 LDS-staged tile kernel, 3 column-per-lane kernel, 5 packed-fp32
+    tile kernel (see vcf_amd.h for all), -1 the generic-B kernels (any supported B, 8 included)."""
     Hp, Wp = padded_shape(H, W, block_size)
     if rgb.nbytes < n_frames * H * W * 3:
         raise ValueError("input buffer too small")
