@@ -1,7 +1,7 @@
-"""A/B the encode kernel variants in one process (interleaved rounds, §5.4 rule 24)."""
+"""A/B the encode (or, with DECODE=1, the decode) kernel variants in one process
+(interleaved ABBA rounds, §5.4 rule 24)."""
 import os
 import sys
-import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -12,22 +12,34 @@ from vcf_amd.device import DeviceBuffer, Event, Stream, set_device
 
 set_device(0)
 H, W, F, Q = 2160, 3840, 64, 32
+DECODE = os.environ.get("DECODE", "0") == "1"
 variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["1", "2"])]
 Hp, Wp = D.padded_shape(H, W)
 frames = [bench.synth_frame(H, W, s) for s in range(4)]
 din = DeviceBuffer(F * H * W * 3)
 for f in range(F):
     din.upload(frames[f % 4], offset=f * H * W * 3)
-outs = {v: DeviceBuffer(F * Hp * Wp * 3) for v in variants}
 s = Stream()
+if DECODE:
+    dk = DeviceBuffer(F * Hp * Wp * 3)
+    D.encode_device(din, F, H, W, Q, out=dk, stream=s)
+    outs = {v: DeviceBuffer(F * H * W * 3) for v in variants}
+    run = lambda v: D.decode_device(dk, F, H, W, Q, out=outs[v], stream=s, variant=v)
+    oshape = (F, H, W, 3)
+    diag = ()
+else:
+    outs = {v: DeviceBuffer(F * Hp * Wp * 3) for v in variants}
+    run = lambda v: D.encode_device(din, F, H, W, Q, out=outs[v], stream=s, variant=v)
+    oshape = (F, Hp, Wp, 3)
+    diag = (2, 6, 8)   # diagnostic variants do not produce the output
 for v in variants:
-    D.encode_device(din, F, H, W, Q, out=outs[v], stream=s, variant=v)
+    run(v)
 s.synchronize()
-ref = outs[variants[0]].download(np.empty((F, Hp, Wp, 3), np.uint8))
+ref = outs[variants[0]].download(np.empty(oshape, np.uint8))
 for v in variants[1:]:
-    if v in (2, 6, 8):
-        continue   # diagnostic variants do not produce the output
-    o = outs[v].download(np.empty((F, Hp, Wp, 3), np.uint8))
+    if v in diag:
+        continue
+    o = outs[v].download(np.empty(oshape, np.uint8))
     print(f"variant {v} == variant {variants[0]}: {np.array_equal(o, ref)}", flush=True)
 res = {v: [] for v in variants}
 e0, e1 = Event(), Event()
@@ -37,7 +49,7 @@ for rnd in range(ROUNDS):
     for v in order:
         e0.record(s)
         for _ in range(10):
-            D.encode_device(din, F, H, W, Q, out=outs[v], stream=s, variant=v)
+            run(v)
         e1.record(s)
         s.synchronize()
         res[v].append(e0.elapsed_ms(e1) / 10)
@@ -46,6 +58,6 @@ base = np.array(res[variants[0]])
 for v in variants:
     t = np.median(res[v])
     ratio = np.median(np.array(res[v]) / base)
-    print(f"variant {v}: median {t:.4f} ms/launch (min {min(res[v]):.4f}) -> "
+    print(f"{'decode' if DECODE else 'encode'} variant {v}: median {t:.4f} ms/launch (min {min(res[v]):.4f}) -> "
           f"{alg / t / 1e6:.0f} GB/s ({alg / t / 1e6 / 8000:.1%} of 8 TB/s), "
           f"{F * H * W / t / 1e3:.0f} Mpix/s; per-round ratio to {variants[0]}: {ratio:.4f}", flush=True)
