@@ -58,7 +58,8 @@ def _moving(H, W, n, seed, noise=4):
 
 
 @pytest.mark.parametrize("H,W,bs,sr", [(64, 64, 16, 8), (96, 130, 16, 12), (77, 91, 8, 5), (128, 128, 32, 16),
-                                       (40, 64, 4, 3), (16, 16, 16, 8), (64, 48, 64, 32), (33, 35, 7, 0)])
+                                       (40, 64, 4, 3), (16, 16, 16, 8), (64, 48, 64, 32), (33, 35, 7, 0),
+                                       (61, 99, 12, 7), (80, 83, 20, 9), (50, 50, 16, 0), (90, 131, 4, 32)])
 @pytest.mark.parametrize("fast", [False, True], ids=["full", "tss"])
 def test_block_matching_vs_oracle(K, H, W, bs, sr, fast):
     fr = _moving(H, W, 3, H * W + bs)
@@ -66,6 +67,23 @@ def test_block_matching_vs_oracle(K, H, W, bs, sr, fast):
         mv = K.block_matching(fr[t - 1], fr[t], bs, sr, fast)
         assert np.array_equal(mv, O.ipp_block_matching(fr[t - 1], fr[t], bs, sr, fast))
         assert np.array_equal(K.motion_compensate(fr[t - 1], mv, bs), O.ipp_motion_compensate(fr[t - 1], mv, bs))
+
+
+@pytest.mark.parametrize("bs,sr", [(16, 8), (8, 5), (12, 3), (32, 16), (4, 32)])
+def test_full_search_word_and_byte_kernels_agree(K, bs, sr):
+    """The word kernel (default for bs % 4 == 0) and the byte kernel give the
+    same vectors, ties included (flat areas, textured areas, frame edges)."""
+    rng = np.random.Generator(np.random.PCG64(bs * 100 + sr))
+    fr = _moving(120, 200, 2, bs + sr)
+    noisy = rng.integers(0, 256, (120, 200, 3), dtype=np.uint8)
+    flat = np.full((120, 200, 3), 40, np.uint8)
+    for a, b in ((fr[0], fr[1]), (noisy, fr[1]), (flat, flat), (fr[1], noisy)):
+        try:
+            K.set_full_search_variant(1)
+            want = K.block_matching(a, b, bs, sr, False)
+        finally:
+            K.set_full_search_variant(0)
+        assert np.array_equal(K.block_matching(a, b, bs, sr, False), want)
 
 
 def test_flat_frames_tie_break_first_minimum(K):

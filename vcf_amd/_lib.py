@@ -91,6 +91,7 @@ SIGNATURES = {
     "vcf_dwt_dz_encode_variant": [_I32, _P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
     "vcf_dwt_dz_decode_variant": [_I32, _P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
     "vcf_ipp_block_match": [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
+    "vcf_ipp_set_full_search_variant": [_I32],
     "vcf_ipp_motion_compensate": [_P, _P, _I32, _I32, _I32, _P, _P],
     "vcf_ipp_residual": [_P, _P, _I64, _P, _P],
     "vcf_ipp_reconstruct": [_P, _P, _I64, _P, _P],

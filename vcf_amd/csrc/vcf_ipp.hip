@@ -104,6 +104,100 @@ __global__ __launch_bounds__(256) void ipp_full_search_kernel(const uint8_t *__r
     }
 }
 
+// Full search on words (bs % 4 == 0, the default path): the block's rows and
+// the search window sit in LDS as 32-bit words of 4 luma bytes; a thread owns
+// one candidate (the workgroup has a lane per candidate, up to 1024) and
+// forms each window word at its byte offset with one v_alignbyte, then
+// v_sad_u8 adds 4 |differences| at a time -- 2 LDS reads, 1 align and 1 SAD
+// per 4 pixels where the byte kernel above needs 8 byte reads and the
+// packing.  The SAD is the same integer sum, the argmin the same (SAD, scan
+// index) key, so the vectors are identical.
+template <int WQ>   // words per block row (bs / 4); 0 = run-time
+__global__ __launch_bounds__(1024) void ipp_full_search_words(const uint8_t *__restrict__ ref,
+                                                              const uint8_t *__restrict__ cur, int H, int W,
+                                                              int bs, int sr, float *__restrict__ mv)
+{
+    constexpr int kWinW = (kMaxBs + 2 * kMaxSr + 3) / 4 + 1;   // words per window row, max
+    __shared__ uint32_t cbw[kMaxBs * kMaxBs / 4];
+    __shared__ uint32_t winw[(kMaxBs + 2 * kMaxSr) * kWinW];
+    __shared__ unsigned long long best[16];
+    const int bx = blockIdx.x, by = blockIdx.y;
+    const int i = by * bs, j = bx * bs;
+    const int ws = bs + 2 * sr;
+    const int wq = WQ ? WQ : bs >> 2;
+    const int wp = (ws + 3) / 4 + 1;   // one spare word: a row's last aligned read
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    for (int t = tid; t < bs * wq; t += nthr) {
+        const int y = t / wq, q = t - y * wq;
+        const uint8_t *p = cur + (long long)(i + y) * W + j + 4 * q;
+        cbw[t] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+    }
+    for (int t = tid; t < ws * wp; t += nthr) {
+        const int r = t / wp, q = t - r * wp;
+        const int y = i - sr + r;
+        uint32_t v = 0;
+        if (y >= 0 && y < H) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int x = j - sr + 4 * q + b;
+                if (x >= 0 && x < W) v |= (uint32_t)ref[(long long)y * W + x] << (8 * b);
+            }
+        }
+        winw[t] = v;
+    }
+    __syncthreads();
+    const int side = 2 * sr + 1, ncand = side * side;
+    unsigned long long key = ~0ULL;
+    for (int c = tid; c < ncand; c += nthr) {
+        const int dyi = c / side, dxi = c - dyi * side;   // window offsets dy + sr, dx + sr
+        const int ry = i + dyi - sr, rx = j + dxi - sr;
+        if (ry < 0 || ry + bs > H || rx < 0 || rx + bs > W) continue;
+        const int w0 = dxi >> 2;
+        const uint32_t sh = (uint32_t)(dxi & 3);
+        uint32_t sad = 0;
+        for (int y = 0; y < bs; ++y) {
+            const uint32_t *a = cbw + y * wq;
+            const uint32_t *b = winw + (dyi + y) * wp + w0;
+            uint32_t lo = b[0];
+            if (WQ) {
+#pragma unroll
+                for (int q = 0; q < WQ; ++q) {
+                    const uint32_t hi = b[q + 1];
+                    sad = __builtin_amdgcn_sad_u8(a[q], __builtin_amdgcn_alignbyte(hi, lo, sh), sad);
+                    lo = hi;
+                }
+            } else {
+                for (int q = 0; q < wq; ++q) {
+                    const uint32_t hi = b[q + 1];
+                    sad = __builtin_amdgcn_sad_u8(a[q], __builtin_amdgcn_alignbyte(hi, lo, sh), sad);
+                    lo = hi;
+                }
+            }
+        }
+        const unsigned long long k = ((unsigned long long)sad << 20) | (unsigned long long)c;
+        key = k < key ? k : key;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(key, off, 64);
+        key = o < key ? o : key;
+    }
+    if ((tid & 63) == 0) best[tid >> 6] = key;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long k = best[0];
+        for (int w = 1; w < (nthr >> 6); ++w) k = best[w] < k ? best[w] : k;
+        float dxv = 0.f, dyv = 0.f;
+        if (k != ~0ULL) {
+            const int c = (int)(k & 0xFFFFF);
+            dyv = (float)(c / side - sr);
+            dxv = (float)(c % side - sr);
+        }
+        float *m = mv + ((long long)by * gridDim.x + bx) * 2;
+        m[0] = dxv;
+        m[1] = dyv;
+    }
+}
+
 // SAD of the block at (i, j) against the reference at (ry, rx), one wave
 __device__ uint32_t wave_sad(const uint8_t *cb, const uint8_t *ref, int W, int bs, int ry, int rx)
 {
@@ -203,6 +297,9 @@ __global__ __launch_bounds__(256) void ipp_recon_kernel(const uint8_t *__restric
 
 unsigned blocks_for(long long n) { return (unsigned)((n + 255) / 256); }
 
+int g_full_search_variant = 0;   // 0: word kernel when bs % 4 == 0; 1: byte kernel (A/B)
+int ipp_full_search_variant() { return g_full_search_variant; }
+
 }  // namespace
 }  // namespace vcf
 
@@ -224,11 +321,30 @@ int vcf_ipp_block_match(const uint8_t *ref_rgb_dev, const uint8_t *cur_rgb_dev, 
     uint8_t *rg = gray_workspace_dev, *cg = gray_workspace_dev + npx;
     hipLaunchKernelGGL(ipp_gray_kernel, dim3(blocks_for(npx)), dim3(256), 0, s, ref_rgb_dev, rg, npx);
     hipLaunchKernelGGL(ipp_gray_kernel, dim3(blocks_for(npx)), dim3(256), 0, s, cur_rgb_dev, cg, npx);
-    if (fast)
+    if (fast) {
         hipLaunchKernelGGL(ipp_tss_kernel, dim3(nbx, nby), dim3(64), 0, s, rg, cg, H, W, bs, sr, mv_dev);
-    else
+    } else if (bs % 4 != 0 || ipp_full_search_variant() == 1) {
         hipLaunchKernelGGL(ipp_full_search_kernel, dim3(nbx, nby), dim3(256), 0, s, rg, cg, H, W, bs, sr, mv_dev);
+    } else {
+        const int ncand = (2 * sr + 1) * (2 * sr + 1);
+        const int nthr = std::min(1024, (ncand + 63) / 64 * 64);
+        const dim3 grid(nbx, nby);
+        switch (bs) {
+        case 4: hipLaunchKernelGGL(ipp_full_search_words<1>, grid, dim3(nthr), 0, s, rg, cg, H, W, bs, sr, mv_dev); break;
+        case 8: hipLaunchKernelGGL(ipp_full_search_words<2>, grid, dim3(nthr), 0, s, rg, cg, H, W, bs, sr, mv_dev); break;
+        case 16: hipLaunchKernelGGL(ipp_full_search_words<4>, grid, dim3(nthr), 0, s, rg, cg, H, W, bs, sr, mv_dev); break;
+        case 32: hipLaunchKernelGGL(ipp_full_search_words<8>, grid, dim3(nthr), 0, s, rg, cg, H, W, bs, sr, mv_dev); break;
+        default: hipLaunchKernelGGL(ipp_full_search_words<0>, grid, dim3(nthr), 0, s, rg, cg, H, W, bs, sr, mv_dev); break;
+        }
+    }
     return hip_check(hipGetLastError(), "ipp block match launch");
+}
+
+int vcf_ipp_set_full_search_variant(int32_t variant)
+{
+    if (variant < 0 || variant > 1) return set_error(VCF_ERR_INVALID, "unknown full-search variant %d", variant);
+    g_full_search_variant = variant;
+    return VCF_OK;
 }
 
 int vcf_ipp_motion_compensate(const uint8_t *ref_rgb_dev, const float *mv_dev, int32_t H, int32_t W, int32_t bs,

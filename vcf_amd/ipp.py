@@ -34,6 +34,11 @@ def block_matching(ref: np.ndarray, cur: np.ndarray, bs: int = 16, sr: int = 8, 
             b.free()
 
 
+def set_full_search_variant(variant: int) -> None:
+    """0: word kernel when bs % 4 == 0 (default), 1: byte kernel (A/B; same vectors)."""
+    L.call("vcf_ipp_set_full_search_variant", int(variant))
+
+
 def motion_compensate(frame: np.ndarray, mv: np.ndarray, bs: int = 16) -> np.ndarray:
     frame = _rgb(frame)
     H, W = frame.shape[:2]
