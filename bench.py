@@ -211,7 +211,12 @@ def main():
                          "traffic": traffic,
                          "kernel_ms_per_launch": round(kernel_ms, 4),
                          "alg_bytes_per_launch": alg_bytes,
-                         "traffic_source": tsrc},
+                         "traffic_source": tsrc,
+                         # the north star's "HBM-read" view: input bytes only; with one
+                         # byte written per byte read, reads can use at most half the peak
+                         "read_bytes_per_launch": F * H * W * 3,
+                         "read_GBps": round(F * H * W * 3 / (kernel_ms * 1e-3) / 1e9, 1),
+                         "read_frac_of_peak": round(F * H * W * 3 / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "cpu_baseline": cpu,
             "parity": parity,
         }
