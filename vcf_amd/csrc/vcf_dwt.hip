@@ -389,7 +389,13 @@ __device__ __forceinline__ int pad_col(int e) { return e + (e >> 3); }
 // Four consecutive outputs of both filters from a register window, pywt's
 // natural tap order per output (0 + f[0] x[i] + f[1] x[i-1] + ...), the tap
 // loop outermost so the eight sums are independent chains.
-template <int F>
+// ZLO / ZHI: compile-time masks of zero taps (bit m = tap m is 0.0), which
+// are skipped.  With finite samples a zero tap adds a signed zero, which can
+// change only the sign of a zero sum, and pywt's sums (started at +0.0) are
+// never -0, so the outputs are bit-identical (tests/test_dwt_gpu.py).  A
+// run-time branch per tap measured 15-20 % slower; the masks are template
+// arguments for the filters that have zeros and matter (bior4.4 = CDF 9/7).
+template <int F, unsigned ZLO = 0, unsigned ZHI = 0>
 __device__ __forceinline__ void fwd_group(const double (&flo)[F], const double (&fhi)[F],
                                           const double (&v)[2 * (kG - 1) + F], double (&lo)[kG], double (&hi)[kG])
 {
@@ -404,8 +410,8 @@ __device__ __forceinline__ void fwd_group(const double (&flo)[F], const double (
 #pragma unroll
         for (int u = 0; u < kG; ++u) {
             const double x = v[2 * u + F - 1 - m];
-            lo[u] = lo[u] + fl * x;
-            hi[u] = hi[u] + fh * x;
+            if (!((ZLO >> m) & 1u)) lo[u] = lo[u] + fl * x;
+            if (!((ZHI >> m) & 1u)) hi[u] = hi[u] + fh * x;
         }
     }
 }
@@ -437,7 +443,7 @@ __device__ __forceinline__ void fwd_store(int src, double lo, double hi, int e, 
 // quantize into a byte image of the three detail subbands; one copy-out of
 // contiguous runs at the end.  Outputs whose taps wrap past the line end
 // (i >= N) take pywt's order through the generic LDS sum.
-template <int F, bool FIRST, bool LAST>
+template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0>
 __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
@@ -518,7 +524,7 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
 #pragma unroll
             for (int k = 0; k < NWIN; ++k) v[k] = (double)tin[(2 * kG * g + k) * IW + c];
             double a[kG], d[kG];
-            fwd_group<F>(flo, fhi, v, a, d);
+            fwd_group<F, ZLO, ZHI>(flo, fhi, v, a, d);
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
                 tA[(kG * g + u) * RS + pad_col(c)] = a[u];
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
 #pragma unroll
             for (int k = 0; k < NWIN; ++k) v[k] = row[9 * gq + k + (k >> 3)];   // pad_col(8 gq + k)
             double lo[kG], hi[kG];
-            fwd_group<F>(flo, fhi, v, lo, hi);
+            fwd_group<F, ZLO, ZHI>(flo, fhi, v, lo, hi);
             const bool rv = o0 + o < hh;
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
@@ -600,7 +606,7 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
 // Four consecutive outputs of the inverse from the register windows of the
 // approximation (xa) and detail (xd) inputs: pywt's order for a pair index
 // i >= F/4 (approximation taps j = 0.., then detail taps), tap loop outermost.
-template <int F>
+template <int F, unsigned ZLO = 0, unsigned ZHI = 0>   // zero-tap masks as in fwd_group
 __device__ __forceinline__ void inv_group(const double (&flo)[F], const double (&fhi)[F],
                                           const double (&xa)[F / 2 + (((F / 2 - 1) & 1) + kG - 1) / 2],
                                           const double (&xd)[F / 2 + (((F / 2 - 1) & 1) + kG - 1) / 2],
@@ -612,11 +618,15 @@ __device__ __forceinline__ void inv_group(const double (&flo)[F], const double (
 #pragma unroll
     for (int j = 0; j < F2; ++j)
 #pragma unroll
-        for (int u = 0; u < kG; ++u) s[u] = s[u] + flo[2 * j + ((P0 + u) & 1)] * xa[F2 - 1 + ((P0 + u) >> 1) - j];
+        for (int u = 0; u < kG; ++u)
+            if (!((ZLO >> (2 * j + ((P0 + u) & 1))) & 1u))
+                s[u] = s[u] + flo[2 * j + ((P0 + u) & 1)] * xa[F2 - 1 + ((P0 + u) >> 1) - j];
 #pragma unroll
     for (int j = 0; j < F2; ++j)
 #pragma unroll
-        for (int u = 0; u < kG; ++u) s[u] = s[u] + fhi[2 * j + ((P0 + u) & 1)] * xd[F2 - 1 + ((P0 + u) >> 1) - j];
+        for (int u = 0; u < kG; ++u)
+            if (!((ZHI >> (2 * j + ((P0 + u) & 1))) & 1u))
+                s[u] = s[u] + fhi[2 * j + ((P0 + u) & 1)] * xd[F2 - 1 + ((P0 + u) >> 1) - j];
 }
 
 // the column pass's reordered outputs (rare: first / last rows of a plane)
@@ -635,7 +645,7 @@ __device__ __attribute__((noinline)) double inv_col_generic(Filters flt, int F, 
 // column x 4 outputs.  TO_RGB (level 1): all three channels per tile, kept
 // in registers, then to_RGB + clip + u8.  Outputs whose wrapped pair index
 // is below F/4 take pywt's reordered taps through the generic LDS sum.
-template <int F, bool FROM_PACKED_LL, bool TO_RGB>
+template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0>
 __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
                                                          long long ll_off, long long off_lh, long long off_hl,
                                                          long long off_hh, const double *__restrict__ prev,
@@ -711,7 +721,7 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
                 xd[k] = Y[base + k];
             }
             double sum[kG];
-            inv_group<F>(flo, fhi, xa, xd, sum);
+            inv_group<F, ZLO, ZHI>(flo, fhi, xa, xd, sum);
             double *dst = (src ? td : ta) + r * kITW + kG * g;
 #pragma unroll
             for (int u = 0; u < kG; ++u) dst[u] = sum[u];
@@ -739,7 +749,7 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
                 xd[k] = td[(base + k) * kITW + nc];
             }
             double sum[kG];
-            inv_group<F>(flo, fhi, xa, xd, sum);
+            inv_group<F, ZLO, ZHI>(flo, fhi, xa, xd, sum);
             if (col_tail) {
 #pragma unroll
                 for (int u = 0; u < kG; ++u) {
@@ -860,29 +870,63 @@ struct LevelArgs {
     hipStream_t s;
 };
 
+// bit m set = tap m is exactly 0.0
+unsigned zero_mask(const double *t, int F)
+{
+    unsigned m = 0;
+    for (int k = 0; k < F && k < 32; ++k)
+        if (t[k] == 0.0) m |= 1u << k;
+    return m;
+}
+
+// the zero-tap masks of bior4.4 (CDF 9/7, config C3): decomposition lo / hi,
+// reconstruction lo / hi
+constexpr unsigned kB44DecLo = 0x001u, kB44DecHi = 0x301u, kB44RecLo = 0x301u, kB44RecHi = 0x001u;
+
+template <int F, unsigned ZLO, unsigned ZHI>
+void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, bool first, bool last)
+{
+    auto kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI> : dwt_level_kernel<F, true, false, ZLO, ZHI>)
+                      : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI> : dwt_level_kernel<F, false, false, ZLO, ZHI>);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed,
+                       a.packed_stride, a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt);
+}
+
 template <int F>
 void launch_fwd_level(const LevelArgs &a, bool first, bool last)
 {
     const Taps<F> tp = taps_of<F>(a.wd->dec_lo, a.wd->dec_hi);
     constexpr int TW = fwd_tile_w(F);
     const dim3 grid((a.hw + TW - 1) / TW, (a.hh + kFTH - 1) / kFTH, a.n_frames);
-    auto kern = first ? (last ? dwt_level_kernel<F, true, true> : dwt_level_kernel<F, true, false>)
-                      : (last ? dwt_level_kernel<F, false, true> : dwt_level_kernel<F, false, false>);
-    hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed,
-                       a.packed_stride, a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt);
+    if (F == 10 && zero_mask(a.wd->dec_lo, F) == kB44DecLo && zero_mask(a.wd->dec_hi, F) == kB44DecHi)
+        launch_fwd_kernel<F, (F == 10 ? kB44DecLo : 0u), (F == 10 ? kB44DecHi : 0u)>(a, tp, grid, first, last);
+    else
+        launch_fwd_kernel<F, 0u, 0u>(a, tp, grid, first, last);
 }
 
 // level r of the inverse: subbands a.h x a.w -> outputs a.hh x a.hw (= oh x ow)
+template <int F, unsigned ZLO, unsigned ZHI>
+void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, bool from_packed, bool to_rgb,
+                       uint8_t *rgb_out)
+{
+    auto kern = from_packed
+                    ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI> : idwt_level_kernel<F, true, false, ZLO, ZHI>)
+                    : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI> : idwt_level_kernel<F, false, false, ZLO, ZHI>);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
+                       a.off_hh, a.in, a.plane_stride, a.lda, a.LLout, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, rgb_out,
+                       (long long)a.hh * a.hw * 3);
+}
+
 template <int F>
 void launch_inv_level(const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t *rgb_out)
 {
     const Taps<F> tp = taps_of<F>(a.wd->rec_lo, a.wd->rec_hi);
     const dim3 grid((a.hw + kITW - 1) / kITW, (a.hh + kITH - 1) / kITH, to_rgb ? a.n_frames : 3 * a.n_frames);
-    auto kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true> : idwt_level_kernel<F, true, false>)
-                            : (to_rgb ? idwt_level_kernel<F, false, true> : idwt_level_kernel<F, false, false>);
-    hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
-                       a.off_hh, a.in, a.plane_stride, a.lda, a.LLout, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, rgb_out,
-                       (long long)a.hh * a.hw * 3);
+    if (F == 10 && zero_mask(a.wd->rec_lo, F) == kB44RecLo && zero_mask(a.wd->rec_hi, F) == kB44RecHi)
+        launch_inv_kernel<F, (F == 10 ? kB44RecLo : 0u), (F == 10 ? kB44RecHi : 0u)>(a, tp, grid, from_packed,
+                                                                                        to_rgb, rgb_out);
+    else
+        launch_inv_kernel<F, 0u, 0u>(a, tp, grid, from_packed, to_rgb, rgb_out);
 }
 
 #define VCF_DWT_FOR_EACH_F(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18)
