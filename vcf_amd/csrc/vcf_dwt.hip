@@ -132,15 +132,24 @@ __device__ __forceinline__ double idwt_out(const double *__restrict__ lo, const 
     return s;
 }
 
+// x / Q, correctly rounded as numpy divides.  For a power-of-two Q the
+// quotient is an exact power-of-two scaling, which v_ldexp_f64 also rounds
+// correctly: the same double without the ~12-instruction float64 division
+// sequence (a sixth of the level-1 forward kernel's VALU instructions).
+__device__ __forceinline__ double div_q(double x, int Q)
+{
+    return (Q & (Q - 1)) == 0 ? __builtin_ldexp(x, -__builtin_ctz((unsigned)Q)) : x / (double)Q;
+}
+
 __device__ __forceinline__ uint8_t quant_u8(double x, int Q)
 {
-    const int32_t k = (int32_t)(x / (double)Q);     // astype(int32): truncation toward zero
+    const int32_t k = (int32_t)div_q(x, Q);         // astype(int32): truncation toward zero
     return (uint8_t)(uint32_t)(k + 128);            // += 128, astype(uint8): wraps
 }
 
 __device__ __forceinline__ uint16_t quant_u16(double x, int Q)
 {
-    const int32_t k = (int32_t)(x / (double)Q);
+    const int32_t k = (int32_t)div_q(x, Q);
     return (uint16_t)(uint32_t)(k + 128);
 }
 
