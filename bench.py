@@ -136,9 +136,13 @@ def main():
 
     world, rank, local, pg = dist_setup(args.gpus)
     import vcf_amd.dct as D
-    from vcf_amd.device import DeviceBuffer, Event, Stream, set_device, synchronize
+    from vcf_amd.device import DeviceBuffer, Event, Stream, device_count, set_device, synchronize
 
-    set_device(local)
+    ndev = device_count()
+    if 0 < ndev < world and rank == 0:
+        print(f"warning: {world} ranks on {ndev} GPU(s): ranks share devices (a rehearsal of the N-rank path, "
+              "not a scaling measurement)", file=sys.stderr, flush=True)
+    set_device(local % ndev if ndev > 0 else local)
     H, W, F, Q = args.height, args.width, args.frames, args.QSS
     Hp, Wp = D.padded_shape(H, W)
     frame_bytes = H * W * 3
