@@ -211,10 +211,12 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
 int vcf_ipp_block_match(const uint8_t *ref_rgb_dev, const uint8_t *cur_rgb_dev, int32_t H, int32_t W, int32_t bs,
                         int32_t sr, int32_t fast, float *mv_dev, uint8_t *gray_workspace_dev, void *stream);
 
-/* Full-search kernel choice (benchmarking and tests; process-wide): 0 = the
- * word kernel (v_alignbyte + v_sad_u8 on 4-pixel words, one lane per
- * candidate) when bs % 4 == 0, else the byte kernel; 1 = always the byte
- * kernel.  Both give identical motion fields. */
+/* Block-matching kernel choice (benchmarking and tests; process-wide):
+ * 0 = the word kernels -- full search on 4-pixel words (v_alignbyte +
+ * v_sad_u8, one lane per candidate) when bs % 4 == 0, and for bs = 16 the
+ * three-step search in parallel rounds of its 8 neighbours; 1 = the byte
+ * kernels (full search) and the serial three-step kernel.  Both give
+ * identical motion fields. */
 int vcf_ipp_set_full_search_variant(int32_t variant);
 
 /* IPP.motion_compensate (IPP_DCT.py:378-395). */

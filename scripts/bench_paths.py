@@ -122,7 +122,7 @@ def ipp(args):
     dmv, dg = DeviceBuffer((H // bs) * (W // bs) * 8), DeviceBuffer(2 * H * W)
     dcomp, dres = DeviceBuffer(H * W * 3), DeviceBuffer(H * W * 3)
     s = Stream()
-    for fast, kv in ((0, 0), (0, 1), (1, 0)):
+    for fast, kv in ((0, 0), (0, 1), (1, 0), (1, 1)):
         L.call("vcf_ipp_set_full_search_variant", kv)
 
         def me():
@@ -137,7 +137,8 @@ def ipp(args):
         sads = (H // bs) * (W // bs) * (2 * sr + 1) ** 2 * bs * bs
         L.call("vcf_ipp_set_full_search_variant", 0)
         print(json.dumps({"metric": f"ipp {'tss' if fast else 'full-search'} motion estimation 4K bs=16 S=8",
-                          "variant": "three-step" if fast else ("byte kernel" if kv else "word kernel"),
+                          "variant": ("three-step, " + ("serial kernel" if kv else "parallel rounds")) if fast
+                          else ("byte kernel" if kv else "word kernel"),
                           "value": round(H * W / t_me / 1e3, 1), "unit": "Mpixels/s", "ms_per_frame": round(t_me, 4),
                           "p_frame_tools_ms": round(t_p, 4),
                           "note": ("289 candidates x 256 |diff| per block = %.2f G abs-diffs/frame" % (sads / 1e9))

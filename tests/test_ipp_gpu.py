@@ -86,6 +86,26 @@ def test_full_search_word_and_byte_kernels_agree(K, bs, sr):
         assert np.array_equal(K.block_matching(a, b, bs, sr, False), want)
 
 
+@pytest.mark.parametrize("sr", [8, 4, 16, 32, 1, 0])
+def test_tss16_parallel_rounds_agree_with_serial_kernel(K, sr):
+    """bs 16 --fast: the parallel-round kernel (default) and the serial one give
+    the same vectors -- smooth motion, noise (centres that wander and leave
+    the staged window), flat frames, frame edges."""
+    rng = np.random.Generator(np.random.PCG64(sr + 7))
+    fr = _moving(144, 208, 2, 5 + sr)
+    noisy = rng.integers(0, 256, (144, 208, 3), dtype=np.uint8)
+    flat = np.full((144, 208, 3), 90, np.uint8)
+    for a, b in ((fr[0], fr[1]), (noisy, fr[1]), (fr[1], noisy), (flat, flat), (noisy, noisy[::-1].copy())):
+        try:
+            K.set_full_search_variant(1)
+            want = K.block_matching(a, b, 16, sr, True)
+        finally:
+            K.set_full_search_variant(0)
+        got = K.block_matching(a, b, 16, sr, True)
+        assert np.array_equal(got, want)
+        assert np.array_equal(got, O.ipp_block_matching(a, b, 16, sr, True))
+
+
 def test_flat_frames_tie_break_first_minimum(K):
     """All SADs equal: the first in-bounds candidate (top-left of the window) wins (full), (0,0) for TSS."""
     f = np.full((64, 64, 3), 77, np.uint8)

@@ -249,6 +249,137 @@ __global__ __launch_bounds__(64) void ipp_tss_kernel(const uint8_t *__restrict__
     }
 }
 
+// Three-step search for bs = 16 (the default block size), same decisions as
+// ipp_tss_kernel: the 8 neighbours of the current centre are evaluated in one
+// parallel round (8 lanes per candidate, 2 block rows of 4 words per lane,
+// v_alignbyte + v_sad_u8), then scanned in the reference's order; at the
+// first improvement the centre moves and the candidates after it are
+// evaluated again around the new centre, exactly as the serial loop would.
+// Candidates read a (16 + 2R)^2 window of the reference staged in LDS as
+// words; one outside it (a centre that wandered > R - step) takes the
+// byte path from global memory.
+constexpr int kTssR = 16;                          // window margin
+constexpr int kTssWS = 16 + 2 * kTssR;             // window side (bytes)
+constexpr int kTssWP = kTssWS / 4 + 1;             // words per window row (+1 spare)
+
+__global__ __launch_bounds__(64) void ipp_tss16_kernel(const uint8_t *__restrict__ ref,
+                                                       const uint8_t *__restrict__ cur, int H, int W, int sr,
+                                                       float *__restrict__ mv)
+{
+    __shared__ uint32_t win[kTssWS * kTssWP];
+    __shared__ uint32_t sads[9];
+    const int bx = blockIdx.x, by = blockIdx.y, lane = threadIdx.x;
+    const int i = by * 16, j = bx * 16;
+    const int wy0 = i - kTssR, wx0 = j - kTssR;      // frame position of window (0, 0)
+    // whole words straight from the frame when the window lies inside it and
+    // rows are word aligned (W % 4 == 0; wx0 is a multiple of 16); else bytes
+    const bool words = (W & 3) == 0 && wx0 >= 0 && wx0 + 4 * kTssWP <= W && wy0 >= 0 && wy0 + kTssWS <= H;
+    for (int t = lane; t < kTssWS * kTssWP; t += 64) {
+        const int r = t / kTssWP, q = t - r * kTssWP;
+        const int y = wy0 + r;
+        uint32_t v = 0;
+        if (words) {
+            v = *reinterpret_cast<const uint32_t *>(ref + (long long)y * W + wx0 + 4 * q);
+        } else if (y >= 0 && y < H) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int x = wx0 + 4 * q + b;
+                if (x >= 0 && x < W) v |= (uint32_t)ref[(long long)y * W + x] << (8 * b);
+            }
+        }
+        win[t] = v;
+    }
+    // this lane's block words: rows 2g, 2g+1 (g = lane & 7), 4 words each
+    const int g = lane & 7, cand = lane >> 3;
+    uint32_t cw[8];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint8_t *p = cur + (long long)(i + 2 * g + r) * W + j + 4 * q;
+            cw[r * 4 + q] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+        }
+    __syncthreads();
+    // SAD of this lane's 8 words against the reference block at frame (ry, rx)
+    auto part_sad = [&](int ry, int rx) -> uint32_t {
+        const int wy = ry - wy0, wx = rx - wx0;
+        uint32_t s = 0;
+        if (wy >= 0 && wy + 16 <= kTssWS && wx >= 0 && wx + 16 <= kTssWS) {
+            const uint32_t sh = (uint32_t)(wx & 3);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t *b = win + (wy + 2 * g + r) * kTssWP + (wx >> 2);
+                uint32_t lo = b[0];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t hi = b[q + 1];
+                    s = __builtin_amdgcn_sad_u8(cw[r * 4 + q], __builtin_amdgcn_alignbyte(hi, lo, sh), s);
+                    lo = hi;
+                }
+            }
+        } else {   // outside the staged window (rare): bytes from global memory
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) {
+                    const int a = (int)((cw[r * 4 + (x >> 2)] >> (8 * (x & 3))) & 0xFFu);
+                    const int b = ref[(long long)(ry + 2 * g + r) * W + rx + x];
+                    s += (uint32_t)abs(a - b);
+                }
+        }
+        return s;
+    };
+    auto group_sum = [&](uint32_t s) -> uint32_t {   // sum over the 8 lanes of a candidate group
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        return s;
+    };
+    auto inb = [&](int ry, int rx) { return ry >= 0 && ry + 16 <= H && rx >= 0 && rx + 16 <= W; };
+    // the centre's SAD (the block itself, always in bounds): every group computes it, group 0 publishes
+    uint32_t best = group_sum(part_sad(i, j));
+    int cy = i, cx = j, bxv = 0, byv = 0;
+    int step = sr / 2;
+    while (step >= 1) {
+        bool improved = false;
+        int k = 0;                   // next neighbour (scan order dy outer, dx inner, centre skipped)
+        while (k < 8) {
+            // neighbour m: (a, b) = offsets of the m-th of the 8 in scan order
+            const int m = cand, mm = m + (m >= 4);   // skip the centre (index 4 of 3x3)
+            const int ry = cy + (mm / 3 - 1) * step, rx = cx + (mm % 3 - 1) * step;
+            uint32_t sv = 0xFFFFFFFFu;
+            if (m >= k && inb(ry, rx)) sv = group_sum(part_sad(ry, rx));
+            else group_sum(0u);      // keep the shuffles uniform
+            if (g == 0) sads[m] = sv;
+            __syncthreads();
+            int moved = -1;
+            for (int t = k; t < 8; ++t) {
+                const uint32_t st = sads[t];
+                if (st != 0xFFFFFFFFu && st < best) {
+                    const int tt = t + (t >= 4);
+                    best = st;
+                    cy += (tt / 3 - 1) * step;
+                    cx += (tt % 3 - 1) * step;
+                    byv = cy - i;
+                    bxv = cx - j;
+                    improved = true;
+                    moved = t;
+                    break;
+                }
+            }
+            __syncthreads();         // sads[] is rewritten by the next round
+            if (moved < 0) break;
+            k = moved + 1;
+        }
+        step = improved ? (step / 2 > 1 ? step / 2 : 1) : step / 2;
+    }
+    if (lane == 0) {
+        float *o = mv + ((long long)by * gridDim.x + bx) * 2;
+        o[0] = (float)bxv;
+        o[1] = (float)byv;
+    }
+}
+
 __global__ __launch_bounds__(256) void ipp_mc_kernel(const uint8_t *__restrict__ ref, const float *__restrict__ mv,
                                                      int H, int W, int bs, uint8_t *__restrict__ out)
 {
@@ -322,7 +453,10 @@ int vcf_ipp_block_match(const uint8_t *ref_rgb_dev, const uint8_t *cur_rgb_dev, 
     hipLaunchKernelGGL(ipp_gray_kernel, dim3(blocks_for(npx)), dim3(256), 0, s, ref_rgb_dev, rg, npx);
     hipLaunchKernelGGL(ipp_gray_kernel, dim3(blocks_for(npx)), dim3(256), 0, s, cur_rgb_dev, cg, npx);
     if (fast) {
-        hipLaunchKernelGGL(ipp_tss_kernel, dim3(nbx, nby), dim3(64), 0, s, rg, cg, H, W, bs, sr, mv_dev);
+        if (bs == 16 && ipp_full_search_variant() == 0)
+            hipLaunchKernelGGL(ipp_tss16_kernel, dim3(nbx, nby), dim3(64), 0, s, rg, cg, H, W, sr, mv_dev);
+        else
+            hipLaunchKernelGGL(ipp_tss_kernel, dim3(nbx, nby), dim3(64), 0, s, rg, cg, H, W, bs, sr, mv_dev);
     } else if (bs % 4 != 0 || ipp_full_search_variant() == 1) {
         hipLaunchKernelGGL(ipp_full_search_kernel, dim3(nbx, nby), dim3(256), 0, s, rg, cg, H, W, bs, sr, mv_dev);
     } else {

@@ -35,7 +35,8 @@ def block_matching(ref: np.ndarray, cur: np.ndarray, bs: int = 16, sr: int = 8, 
 
 
 def set_full_search_variant(variant: int) -> None:
-    """0: word kernel when bs % 4 == 0 (default), 1: byte kernel (A/B; same vectors)."""
+    """0: word kernels (full search for bs % 4 == 0, parallel-round TSS for bs 16; default),
+    1: byte / serial kernels (A/B; same vectors)."""
     L.call("vcf_ipp_set_full_search_variant", int(variant))
 
 
