@@ -110,9 +110,14 @@ int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
  * 5 = variant 1 with packed-fp32 transforms (two 1-D transforms per
  * v_pk_add_f32 / v_pk_mul_f32; power-of-two Q, no -p; else as 1),
  * 6 = diagnostic 2 with variant 5's arithmetic,
+ * 7 = variant 5 with its earlier store policy (non-temporal stores, tiles in
+ *     dispatch order; A/B reference, aligned frames with subbands),
  * 8 = diagnostic: variant 1's loads, LDS image and copy-out without the
- * transforms (output bytes are not the coefficients; aligned frames, subbands).
- * Variants 1, 3, 4 and 5 produce identical bytes. */
+ * transforms (output bytes are not the coefficients; aligned frames, subbands),
+ * 9, 10 = diagnostics: 8 with the image written as 64 aligned streams that
+ * continue from tile to tile (9), or the same streams 32 bytes off line
+ * boundaries (10) -- the cost of partial lines (output bytes wrong).
+ * Variants 1, 3, 4, 5 and 7 produce identical bytes. */
 int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H,
                               int32_t W, int32_t block_size, int32_t Q, uint32_t flags,
                               uint8_t *k_dev, void *stream);

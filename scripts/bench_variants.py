@@ -31,7 +31,7 @@ else:
     outs = {v: DeviceBuffer(F * Hp * Wp * 3) for v in variants}
     run = lambda v: D.encode_device(din, F, H, W, Q, out=outs[v], stream=s, variant=v)
     oshape = (F, Hp, Wp, 3)
-    diag = (2, 6, 8)   # diagnostic variants do not produce the output
+    diag = (2, 6, 8, 9, 10)   # diagnostic variants do not produce the output
 for v in variants:
     run(v)
 s.synchronize()

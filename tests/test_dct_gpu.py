@@ -172,3 +172,13 @@ def test_packed_encode_batches(variant, shape, n, flags):
     assert np.array_equal(got, want)
     for i in (0, n // 2, n - 1):
         assert np.array_equal(got[i], O.encode_frame(frames[i], 32, flags)), i
+
+
+def test_store_policy_ab_variant_equal():
+    """Variant 7 (the earlier non-temporal store policy) writes the same bytes
+    as the default; it only exists for A/B timing."""
+    frames = np.stack([_rand((1080, 1920, 3), s, "smooth") for s in range(3)])
+    want = D.encode(frames, 32, 0, variant=1)
+    for v in (0, 5, 7):
+        assert np.array_equal(D.encode(frames, 32, 0, variant=v), want), v
+    assert np.array_equal(want[1], O.encode_frame(frames[1], 32, 0))

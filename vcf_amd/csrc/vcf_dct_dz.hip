@@ -128,8 +128,12 @@ __device__ __forceinline__ void move_runs_tab(const Geom &g, uint8_t *stage, con
 // Copy-out of a full tile (nvalid == kTile, g.vec): compile-time chunk
 // geometry (12 16-byte chunks per lane), every LDS read issued before the
 // stores -- the generic loop above waits on each read in turn (4-5 % of the
-// encode).
-template <bool SUB>
+// encode).  Store policy (NT = 0, the default): plain stores,
+// so the 128-byte lines a tile shares with its neighbours at run joins stay
+// in the XCD's L2 until the neighbour's half arrives (the tile order keeps
+// neighbours on one XCD, see dct_dz_encode_kernel); non-temporal stores
+// wrote those lines twice, half at a time (2 % slower).
+template <bool SUB, int NT = 1>   // NT: 1 non-temporal stores, 0 plain, 2 plain within 128 B of a run's ends
 __device__ __forceinline__ void move_runs_full(const Geom &g, const uint8_t *stage, const uint32_t *rowbase,
                                                uint8_t *frame)
 {
@@ -142,6 +146,7 @@ __device__ __forceinline__ void move_runs_full(const Geom &g, const uint8_t *sta
     const int tid = threadIdx.x;
     u32x4 v[per_lane];
     uint32_t go[per_lane];
+    bool edge[per_lane];
 #pragma unroll
     for (int r = 0; r < per_lane; ++r) {
         const int q = tid + r * kTile;
@@ -150,10 +155,15 @@ __device__ __forceinline__ void move_runs_full(const Geom &g, const uint8_t *sta
         const int blk = off / bpb;
         go[r] = rowbase[blk] + seg_base<SUB>(g, seg) + (uint32_t)(off - blk * bpb);
         v[r] = *reinterpret_cast<const u32x4 *>(stage + seg * lds_stride + off);
+        edge[r] = off < 128 || off + 16 > cps * 16 - 128;
     }
 #pragma unroll
-    for (int r = 0; r < per_lane; ++r)
-        __builtin_nontemporal_store(v[r] ^ 0x80808080u, reinterpret_cast<u32x4 *>(frame + go[r]));
+    for (int r = 0; r < per_lane; ++r) {
+        if (NT == 1 || (NT == 2 && !edge[r]))
+            __builtin_nontemporal_store(v[r] ^ 0x80808080u, reinterpret_cast<u32x4 *>(frame + go[r]));
+        else
+            *reinterpret_cast<u32x4 *>(frame + go[r]) = v[r] ^ 0x80808080u;
+    }
 }
 
 // Make raw[] look redefined *after* `dep` exists, so a channel's byte
@@ -245,7 +255,8 @@ __device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncCon
 
 // PK: packed-fp32 transforms (power-of-two Q, no -p); MEMONLY: diagnostic
 // with the same loads, LDS image and copy-out but no transforms.
-template <bool POW2, bool SUB, bool PERC, bool PAD, bool SDWA = true, bool PK = false, bool MEMONLY = false>
+template <bool POW2, bool SUB, bool PERC, bool PAD, bool SDWA = true, bool PK = false, bool MEMONLY = false,
+          int STREAMS = 0, int NT = 0, bool XCD = true>
 __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
                                                               uint8_t *__restrict__ kout, Geom g,
                                                               EncConsts K, FinalK rowk)
@@ -253,8 +264,17 @@ __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__r
     __shared__ __attribute__((aligned(16))) uint8_t stage[kStageBytes];
     __shared__ uint32_t rowbase[kTile];
     const int tid = threadIdx.x;
-    const long long frame = blockIdx.y;
-    const int n0 = blockIdx.x * kTile;
+    long long frame = blockIdx.y;
+    int tile = blockIdx.x;
+    if (XCD) {   // each XCD takes a contiguous range of tiles (workgroups are dealt round robin), so
+                 // neighbouring tiles -- which share partial lines at run joins -- meet in one L2
+        const unsigned n = gridDim.x * gridDim.y, gid = blockIdx.y * gridDim.x + blockIdx.x;
+        const unsigned q = n >> 3, r = n & 7, x = gid & 7;
+        const unsigned t = x * q + min(x, r) + (gid >> 3);
+        frame = t / gridDim.x;
+        tile = (int)(t - (unsigned)frame * gridDim.x);
+    }
+    const int n0 = tile * kTile;
     const int nvalid = min(kTile, g.nblocks - n0);
     if (tid < nvalid) {
         int by, bx;
@@ -265,7 +285,21 @@ __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__r
         encode_block<POW2, SUB, PERC, SDWA, PK, MEMONLY>(raw, K, rowk, stage, tid);
     }
     __syncthreads();
-    if (nvalid == kTile && g.vec) move_runs_full<SUB>(g, stage, rowbase, kout + frame * g.out_stride);
+    if (STREAMS) {   // diagnostic: the image as 64 streams (run seg of tile t at seg*S + t*768 [+32]); wrong layout
+        const long long S = (long long)g.out_stride * gridDim.y / 64 / 4096 * 4096;
+        const long long t = (long long)blockIdx.y * gridDim.x + blockIdx.x;
+        const int shift = STREAMS == 2 ? 32 : 0;
+        if (nvalid == kTile)
+#pragma unroll
+            for (int r = 0; r < 12; ++r) {
+                const int q = tid + r * kTile, seg = q / 48, off = (q - seg * 48) * 16;
+                if (t * 768 + shift + off + 16 <= S)
+                    __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(stage + q * 16),
+                                                reinterpret_cast<u32x4 *>(kout + seg * S + t * 768 + shift + off));
+            }
+        return;
+    }
+    if (nvalid == kTile && g.vec) move_runs_full<SUB, NT>(g, stage, rowbase, kout + frame * g.out_stride);
     else move_runs_tab<SUB, true>(g, stage, rowbase, kout + frame * g.out_stride, nvalid);
 }
 
@@ -792,7 +826,7 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         return dct_any_encode_u8(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, stream);
     int rc = check_args(rgb_dev, k_dev, n_frames, H, W, block_size, Q, flags, false);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 8 || variant == 7) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
+    if (variant < 0 || variant > 10) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -823,15 +857,30 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         }
         return hip_check(hipGetLastError(), "variant 4 launch");
     }
-    if (variant == 8) {   // diagnostic: variant 1's memory traffic without the transforms (output wrong)
+    if (variant == 8 || variant == 9 || variant == 10) {   // diagnostics: memory traffic without the transforms
         if (!(sub && !pad)) return set_error(VCF_ERR_INVALID, "variant 8: aligned frames, subband layout");
+        if (variant != 8 && n_frames > 65535) return set_error(VCF_ERR_INVALID, "variants 9/10: <= 65535 frames");
         for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
             const dim3 grid(g.tiles_per_frame, (unsigned)std::min<int64_t>(65535, n_frames - f0));
-            hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, false, true>), grid,
-                               dim3(kTile), 0, (hipStream_t)stream, rgb_dev + f0 * g.in_stride,
-                               k_dev + f0 * g.out_stride, g, K, rowk);
+            if (variant == 8)
+                hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, false, true>), grid,
+                                   dim3(kTile), 0, (hipStream_t)stream, rgb_dev + f0 * g.in_stride,
+                                   k_dev + f0 * g.out_stride, g, K, rowk);
+            else if (variant == 9)   // 64 aligned streams continuing from tile to tile
+                hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, false, true, 1>), grid,
+                                   dim3(kTile), 0, (hipStream_t)stream, rgb_dev, k_dev, g, K, rowk);
+            else   // the same streams shifted by 32 bytes: partial lines at every tile join
+                hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, false, true, 2>), grid,
+                                   dim3(kTile), 0, (hipStream_t)stream, rgb_dev, k_dev, g, K, rowk);
         }
         return hip_check(hipGetLastError(), "variant 8 launch");
+    }
+    if (variant == 7 && pow2 && !perc && sub && !pad) {   // A/B: variant 5 with the earlier store policy
+        if (n_frames > 65535) return set_error(VCF_ERR_INVALID, "variant 7: <= 65535 frames");
+        const dim3 grid(g.tiles_per_frame, (unsigned)n_frames);
+        hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, true, false, 0, 1, false>), grid,
+                           dim3(kTile), 0, (hipStream_t)stream, rgb_dev, k_dev, g, K, rowk);
+        return hip_check(hipGetLastError(), "variant 7 launch");
     }
     if ((variant == 5 || (variant == 0 && pow2 && !perc)) && pow2 && !perc) {   // packed-fp32 transforms
         for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
