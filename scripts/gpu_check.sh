@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 fatal() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 
-timeout -k 10 900 python -m pytest tests -m gpu -q -x > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest_gpu rc=$rc"; tail -3 "$OUT/pytest_gpu.log"
 if fatal $rc; then echo "fatal pytest rc=$rc"; exit $rc; fi
 
