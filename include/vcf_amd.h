@@ -118,8 +118,12 @@ int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
  * continue from tile to tile (9), or the same streams 32 bytes off line
  * boundaries (10) -- the cost of partial lines (output bytes wrong),
  * 11 = variant 5 with non-temporal input loads (the earlier load policy;
- *      A/B reference, aligned frames with subbands).
- * Variants 1, 3, 4, 5, 7 and 11 produce identical bytes. */
+ *      A/B reference, aligned frames with subbands),
+ * 12-16 = variant 5 with wave priority 3 for the load issue and copy-out
+ *      (12, the default's setting), 1 for both (13), the copy-out only (14),
+ *      the loads only (15), none (16) (A/B references, aligned frames with
+ *      subbands).
+ * Variants 1, 3, 4, 5, 7 and 11-16 produce identical bytes. */
 int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H,
                               int32_t W, int32_t block_size, int32_t Q, uint32_t flags,
                               uint8_t *k_dev, void *stream);
@@ -162,8 +166,9 @@ int vcf_dct_dz_decode_k32(const int32_t *k_dev, int64_t n_frames, int32_t H, int
 /* Same as vcf_dct_dz_decode with an explicit kernel choice (A/B tests and
  * benchmarks): 0 = automatic (2), 1 = lane-per-block (one block's 64 float64
  * samples per lane), 2 = column-per-lane (8 lanes per block, LDS transpose),
- * 3, 4 = variant 2 with non-temporal index loads (3, the earlier policy) or
- * plain pixel stores (4) (A/B references; aligned frames, subbands, no -p).
+ * 3, 4, 5 = variant 2 with non-temporal index loads (3, the earlier policy),
+ * plain pixel stores (4) or no raised wave priority for the load phase (5)
+ * (A/B references; aligned frames, subbands, no -p).
  * Outputs identical. */
 int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,
                               int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream);

@@ -152,7 +152,7 @@ def test_decode_variants_batched():
     k = D.encode(frames, 32, 0)
     a = D.decode(k, 72, 4104, 32, 0, variant=1)
     b = D.decode(k, 72, 4104, 32, 0, variant=2)
-    for v in (3, 4):   # load/store-hint A/B variants of 2
+    for v in (3, 4, 5):   # load/store-hint and priority A/B variants of 2
         assert np.array_equal(D.decode(k, 72, 4104, 32, 0, variant=v), b), v
     assert np.array_equal(a, b)
     assert np.array_equal(a[2], O.decode_frame(k[2], 72, 4104, 32, 0))
@@ -181,6 +181,6 @@ def test_store_policy_ab_variant_equal():
     as the default; it only exists for A/B timing."""
     frames = np.stack([_rand((1080, 1920, 3), s, "smooth") for s in range(3)])
     want = D.encode(frames, 32, 0, variant=1)
-    for v in (0, 5, 7, 11):
+    for v in (0, 5, 7, 11, 12, 13, 14, 15, 16):
         assert np.array_equal(D.encode(frames, 32, 0, variant=v), want), v
     assert np.array_equal(want[1], O.encode_frame(frames[1], 32, 0))

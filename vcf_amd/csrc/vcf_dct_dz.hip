@@ -258,8 +258,13 @@ __device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncCon
 
 // PK: packed-fp32 transforms (power-of-two Q, no -p); MEMONLY: diagnostic
 // with the same loads, LDS image and copy-out but no transforms.
+// PRIO: wave priority (s_setprio) while the input loads issue (low 2 bits)
+// and during the copy-out (bits 2-3), 0 during the transforms: a workgroup
+// entering or leaving its memory phase is not held behind the resident
+// workgroups' VALU streams (15, the default, measured 1-2.5 % faster than 0
+// over three boxes, ABBA; variants 12-15 and 16 = PRIO 0 are the A/B records).
 template <bool POW2, bool SUB, bool PERC, bool PAD, bool SDWA = true, bool PK = false, bool MEMONLY = false,
-          int STREAMS = 0, int NT = 0, bool XCD = true, int LD = 1, int PRIO = 0>
+          int STREAMS = 0, int NT = 0, bool XCD = true, int LD = 1, int PRIO = 15>
 __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
                                                               uint8_t *__restrict__ kout, Geom g,
                                                               EncConsts K, FinalK rowk)
@@ -284,13 +289,13 @@ __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__r
         tile_block(g, n0 + tid, by, bx);
         rowbase[tid] = block_rowbase<SUB>(g, by, bx);
         uint32_t raw[8][6];
-        if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+        if (PRIO & 3) __builtin_amdgcn_s_setprio(PRIO & 3);
         load_block<PAD, LD>(g, rgb + frame * g.in_stride, by, bx, raw);
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
+        if (PRIO & 3) __builtin_amdgcn_s_setprio(0);
         encode_block<POW2, SUB, PERC, SDWA, PK, MEMONLY>(raw, K, rowk, stage, tid);
     }
     __syncthreads();
-    if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+    if (PRIO >> 2) __builtin_amdgcn_s_setprio(PRIO >> 2);
     if (STREAMS) {   // diagnostic: the image as 64 streams (run seg of tile t at seg*S + t*768 [+32]); wrong layout
         const long long S = (long long)g.out_stride * gridDim.y / 64 / 4096 * 4096;
         const long long t = (long long)blockIdx.y * gridDim.x + blockIdx.x;
@@ -513,8 +518,9 @@ struct DecColsSmem {
 
 // NTL / NTS: non-temporal index loads / pixel stores.  Plain loads measured
 // 1.7 % faster than non-temporal ones; the store hint does not matter
-// (decode variants 3 and 4 are the A/B records).
-template <int TB, bool SUB, bool PERC, bool PAD, bool NTL = false, bool NTS = true>
+// (decode variants 3 and 4 are the A/B records).  PRIO: wave
+// priority while the index loads issue (3: 1 % faster than 0, variant 5).
+template <int TB, bool SUB, bool PERC, bool PAD, bool NTL = false, bool NTS = true, int PRIO = 3>
 __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__restrict__ kin,
                                                               uint8_t *__restrict__ rgb, Geom g, int Q,
                                                               int tiles_per_row)
@@ -534,6 +540,7 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
     auto seg_off = [&](int seg) -> uint32_t {
         return (uint32_t)(SUB ? seg_offset_sub(g, by, bx0, seg) : seg_offset_nosub(g, by, bx0, seg));
     };
+    if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
     if (g.vec && nvalid == TB && (TB * 3) % 16 == 0) {
         constexpr int cps = (SUB ? 3 * TB : 24 * TB) / 16, total = nseg * cps;
 #pragma unroll
@@ -554,6 +561,7 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
             sm.stage[cols_stage_off<TB, SUB>(seg) + off] = src[seg_off(seg) + off];
         }
     }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     if (lb >= nvalid) return;
 
@@ -842,7 +850,7 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         return dct_any_encode_u8(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, stream);
     int rc = check_args(rgb_dev, k_dev, n_frames, H, W, block_size, Q, flags, false);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 13) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
+    if (variant < 0 || variant > 16) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -891,17 +899,17 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         }
         return hip_check(hipGetLastError(), "variant 8 launch");
     }
-    if (variant == 12 || variant == 13) {   // experiment: wave priority raised for the load issue and copy-out
-        if (!(pow2 && !perc && sub && !pad)) return set_error(VCF_ERR_INVALID, "variant 12: pow2 Q, aligned, default flags");
-        if (n_frames > 65535) return set_error(VCF_ERR_INVALID, "variant 12: <= 65535 frames");
+    if (variant >= 12 && variant <= 16) {   // A/B: wave priority for the load issue / copy-out (PRIO)
+        if (!(pow2 && !perc && sub && !pad)) return set_error(VCF_ERR_INVALID, "variants 12-16: pow2 Q, aligned, default flags");
+        if (n_frames > 65535) return set_error(VCF_ERR_INVALID, "variants 12-16: <= 65535 frames");
         const dim3 grid(g.tiles_per_frame, (unsigned)n_frames);
-        if (variant == 12)
-            hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, true, false, 0, 0, true, 1, 3>), grid,
+#define VCF_ENC_PRIO(V, P) \
+        if (variant == V) \
+            hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, true, false, 0, 0, true, 1, P>), grid, \
                                dim3(kTile), 0, (hipStream_t)stream, rgb_dev, k_dev, g, K, rowk);
-        else
-            hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, true, false, 0, 0, true, 1, 1>), grid,
-                               dim3(kTile), 0, (hipStream_t)stream, rgb_dev, k_dev, g, K, rowk);
-        return hip_check(hipGetLastError(), "variant 12 launch");
+        VCF_ENC_PRIO(12, 15) VCF_ENC_PRIO(13, 5) VCF_ENC_PRIO(14, 12) VCF_ENC_PRIO(15, 3) VCF_ENC_PRIO(16, 0)
+#undef VCF_ENC_PRIO
+        return hip_check(hipGetLastError(), "variant 12-16 launch");
     }
     if (variant == 11) {   // A/B: variant 5 with the earlier non-temporal input loads
         if (!(pow2 && !perc && sub && !pad)) return set_error(VCF_ERR_INVALID, "variant 11: pow2 Q, aligned, default flags");
@@ -962,7 +970,7 @@ int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frame
         return dct_any_decode_u8(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, stream);
     int rc = check_args(k_dev, rgb_dev, n_frames, H, W, block_size, Q, flags, true);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 4) return set_error(VCF_ERR_INVALID, "unknown decode variant %d", variant);
+    if (variant < 0 || variant > 5) return set_error(VCF_ERR_INVALID, "unknown decode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -977,8 +985,11 @@ int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frame
         if (variant == 3)   // the earlier non-temporal index loads
             hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, true, true>), grid, dim3(256), 0,
                                (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
-        else   // plain pixel stores
+        else if (variant == 4)   // plain pixel stores
             hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, false>), grid, dim3(256), 0,
+                               (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
+        else   // no wave priority for the load phase
+            hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 0>), grid, dim3(256), 0,
                                (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
         return hip_check(hipGetLastError(), "decode variant 3/4 launch");
     }
