@@ -26,9 +26,17 @@ from vcf_amd.device import DeviceBuffer, Event, Stream, set_device
 HBM = 8000.0
 
 
-def timed(stream, fn, steps, warmup):
-    for _ in range(warmup):
+def timed(stream, fn, steps, warmup, settle_s=0.5):
+    """ms per call over `steps` calls, after `warmup` calls and at least
+    settle_s seconds of back-to-back launches (the clocks ramp over the first
+    ~30 launches)."""
+    t0 = time.perf_counter()
+    n = 0
+    while n < warmup or time.perf_counter() - t0 < settle_s:
         fn()
+        n += 1
+        if n % 8 == 0:
+            stream.synchronize()
     stream.synchronize()
     e0, e1 = Event(), Event()
     e0.record(stream)
@@ -37,6 +45,21 @@ def timed(stream, fn, steps, warmup):
     e1.record(stream)
     stream.synchronize()
     return e0.elapsed_ms(e1) / steps
+
+
+def cpu_port(fn, px, what, budget=3.0):
+    """The oracle (test infrastructure: the checker) timed on this host, 1 thread,
+    for ~budget seconds, as the cpu_baseline beside a GPU line; returns it and
+    the last output (compared with the GPU's by the caller)."""
+    n, t0 = 0, time.perf_counter()
+    while True:
+        out = fn()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget:
+            break
+    return dict(value=round(n * px / el / 1e6, 3), unit="Mpixels/s", cores=1, kind="port",
+                sample=f"{n} x {what}, {el:.1f} s"), out
 
 
 def dwt(args):
@@ -50,6 +73,11 @@ def dwt(args):
     dout = DeviceBuffer(F * Ho * Wo * 3)
     s = Stream()
     px = F * H * W
+    from oracle import oracle as O
+    cpu_e, sb = cpu_port(lambda: O.dwt_encode_frame(frames[0], "bior4.4", L_, Q), H * W,
+                         "one 4K S-smooth frame, oracle/vcf_dwt_oracle.cpp (pywt 1.1.1 'per' restated)")
+    cpu_d, _ = cpu_port(lambda: O.dwt_decode_frame(sb, H, W, "bior4.4", L_, Q), H * W,
+                        "one 4K frame's subbands, oracle/vcf_dwt_oracle.cpp")
     for variant, vname in ((1, "fused level kernels"), (2, "separable kernels")):
         enc = lambda: L.call("vcf_dwt_dz_encode_variant", variant, din.ptr, F, H, W, w, L_, Q, dpk.ptr, dws.ptr,
                              s.handle)
@@ -61,7 +89,8 @@ def dwt(args):
             print(json.dumps({"metric": f"Mpixels/s {name} 4K l=5 bior4.4 Q=32", "variant": vname,
                               "value": round(px / t / 1e3, 1), "unit": "Mpixels/s", "ms_per_launch": round(t, 3),
                               "frames_per_launch": F, "alg_GBps": round(alg / t / 1e6, 1),
-                              "frac_hbm_alg": round(alg / t / 1e6 / HBM, 4)}), flush=True)
+                              "frac_hbm_alg": round(alg / t / 1e6 / HBM, 4),
+                              "cpu_baseline": cpu_e if name == "dwt_encode" else cpu_d}), flush=True)
 
 
 def dct_decode(args):
@@ -76,12 +105,16 @@ def dct_decode(args):
     s = Stream()
     D.encode_device(din, F, H, W, Q, out=dk, stream=s)
     alg = F * (Hp * Wp * 3 + H * W * 3)
+    from oracle import oracle as O
+    k0 = O.encode_frame(frames[0], Q)
+    cpu, _ = cpu_port(lambda: O.decode_frame(k0, H, W, Q), H * W, "one 4K frame, oracle/vcf_oracle.c")
     for variant, vname in ((2, "column-per-lane"), (1, "lane-per-block")):
         t = timed(s, lambda: D.decode_device(dk, F, H, W, Q, out=dout, stream=s, variant=variant), args.steps, 3)
         print(json.dumps({"metric": "Mpixels/s dct_decode 4K Q=32", "variant": vname,
                           "value": round(F * H * W / t / 1e3, 1),
                           "unit": "Mpixels/s", "ms_per_launch": round(t, 4), "frames_per_launch": F,
-                          "alg_GBps": round(alg / t / 1e6, 1), "frac_hbm": round(alg / t / 1e6 / HBM, 4)}),
+                          "alg_GBps": round(alg / t / 1e6, 1), "frac_hbm": round(alg / t / 1e6 / HBM, 4),
+                          "cpu_baseline": cpu}),
               flush=True)
 
 
@@ -122,6 +155,9 @@ def ipp(args):
     dmv, dg = DeviceBuffer((H // bs) * (W // bs) * 8), DeviceBuffer(2 * H * W)
     dcomp, dres = DeviceBuffer(H * W * 3), DeviceBuffer(H * W * 3)
     s = Stream()
+    from oracle import oracle as O
+    cpu = {fast: cpu_port(lambda: O.ipp_block_matching(f0, f1, bs, sr, bool(fast)), H * W,
+                          "one 4K frame pair, oracle/vcf_ipp_oracle.c")[0] for fast in (0, 1)}
     for fast, kv in ((0, 0), (0, 1), (1, 0), (1, 1)):
         L.call("vcf_ipp_set_full_search_variant", kv)
 
@@ -142,7 +178,8 @@ def ipp(args):
                           "value": round(H * W / t_me / 1e3, 1), "unit": "Mpixels/s", "ms_per_frame": round(t_me, 4),
                           "p_frame_tools_ms": round(t_p, 4),
                           "note": ("289 candidates x 256 |diff| per block = %.2f G abs-diffs/frame" % (sads / 1e9))
-                          if not fast else "serial three-step search, one wave per block"}), flush=True)
+                          if not fast else "serial three-step search, one wave per block",
+                          "cpu_baseline": cpu[fast]}), flush=True)
 
 
 def entropy(args):
@@ -219,7 +256,7 @@ def configs(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--only", default="dwt,dct_decode,dct_encode_pcie,ipp,entropy,configs")
     args = ap.parse_args()
     set_device(0)
