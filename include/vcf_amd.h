@@ -206,7 +206,9 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
 /* Same, with an explicit kernel choice (for A/B tests and benchmarks):
  * 0 = automatic (1 when its LDS tile fits, else 2), 1 = fused LDS-tiled level
  * kernels (one launch per level; filters up to 18 taps), 2 = separable
- * column/row kernels through float64 workspace planes.  Outputs identical. */
+ * column/row kernels through float64 workspace planes, 3 = 1 with the
+ * earlier three-barrier schedule for bior4.4 (A/B reference; other filters
+ * as 1).  Outputs identical. */
 int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream);

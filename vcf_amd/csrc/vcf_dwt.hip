@@ -428,7 +428,7 @@ __device__ __forceinline__ void fwd_group(const double (&flo)[F], const double (
 // quantize one row-pass result pair into the staged subband bytes / LL
 template <bool LAST>
 __device__ __forceinline__ void fwd_store(int src, double lo, double hi, int e, uint8_t *stage, uint8_t *stage16,
-                                          int SB, int Q, double *stageLL, int ll_index)
+                                          int SB, int Q, double *ll_dst)
 {
     if (src) {                                   // D rows: da -> LH, dd -> HH
         stage[0 * SB + e] = quant_u8(lo, Q);
@@ -440,7 +440,7 @@ __device__ __forceinline__ void fwd_store(int src, double lo, double hi, int e, 
             stage16[2 * e] = (uint8_t)q16;
             stage16[2 * e + 1] = (uint8_t)(q16 >> 8);
         } else {
-            stageLL[ll_index] = lo;
+            *ll_dst = lo;
         }
     }
 }
@@ -452,7 +452,13 @@ __device__ __forceinline__ void fwd_store(int src, double lo, double hi, int e, 
 // quantize into a byte image of the three detail subbands; one copy-out of
 // contiguous runs at the end.  Outputs whose taps wrap past the line end
 // (i >= N) take pywt's order through the generic LDS sum.
-template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0>
+// PIPE (default): two barriers per channel instead of three -- channel c+1's
+// samples are staged during channel c's row pass (the staging tile is free
+// once the column pass has read it) -- and the LL outputs of a non-final
+// level go straight from the row pass to HBM (4 consecutive doubles per work
+// item, contiguous across a wave) instead of through an LDS tile and a third
+// barrier.  PIPE = false is the earlier schedule (dwt encode variant 3).
+template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true>
 __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
@@ -472,7 +478,7 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
     __shared__ double tA[kFTH * RS + 8], tD[kFTH * RS + 8];   // +8: the last row group's window overhang
     __shared__ uint8_t stage[3 * SB];
     __shared__ uint8_t stage16[LAST ? 2 * SB : 1];
-    __shared__ double stageLL[LAST ? 1 : kFTH * TW];
+    __shared__ double stageLL[LAST || PIPE ? 1 : kFTH * TW];
     const int o0 = blockIdx.y * kFTH, c0 = blockIdx.x * TW;
     const long long frame = blockIdx.z;
     const int R0 = F / 2 + 2 * o0 - F + 1, C0 = F / 2 + 2 * c0 - F + 1;
@@ -506,8 +512,8 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
             }
         }
     };
-    fetch(0);
-    for (int ch = 0; ch < 3; ++ch) {
+    // stage channel ch's samples into tin (level 1: YCoCg from the RGB bytes)
+    auto stage_in = [&](int ch) {
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             double v;
@@ -525,7 +531,17 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
             }
             tin[tid + 256 * j] = (Stage)v;
         }
-        if (!FIRST && ch < 2) fetch(ch + 1);
+    };
+    fetch(0);
+    if (PIPE) {
+        stage_in(0);
+        if (!FIRST) fetch(1);
+    }
+    for (int ch = 0; ch < 3; ++ch) {
+        if (!PIPE) {
+            stage_in(ch);
+            if (!FIRST && ch < 2) fetch(ch + 1);
+        }
         __syncthreads();
         {   // column pass (axis 0): 128 columns x 2 groups of 4 output rows
             const int c = tid % IW, g = tid / IW;
@@ -552,6 +568,15 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
             }
         }
         __syncthreads();
+        if (PIPE && ch < 2) {   // tin is free: stage the next channel while this one's rows run
+            stage_in(ch + 1);
+            if (!FIRST && ch == 0) fetch(2);
+        }
+        // LL of a non-final level: straight to HBM (PIPE) or through stageLL
+        double *const llp = LLout + (frame * 3 + ch) * plane_stride + (long long)o0 * hw + c0;
+        auto ll_dst = [&](int o, int oc) -> double * {
+            return PIPE ? llp + (long long)o * hw + oc : stageLL + (o * TW + oc);
+        };
         // row pass (axis 1): (A or D) x kFTH rows x NG groups of 4 outputs
         const int first_tail = row_tail ? max(0, (w - F / 2 + 1) / 2 - c0) : TW;   // first column with i >= w
         for (int t = tid; t < 2 * kFTH * NG; t += 256) {
@@ -568,8 +593,8 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
             for (int u = 0; u < kG; ++u) {
                 const int oc = oc0 + u;
                 if (rv && oc < min(TW, hw - c0) && oc < first_tail)
-                    fwd_store<LAST>(src, lo[u], hi[u], (o * TW + oc) * 3 + ch, stage, stage16, SB, Q, stageLL,
-                                    o * TW + oc);
+                    fwd_store<LAST>(src, lo[u], hi[u], (o * TW + oc) * 3 + ch, stage, stage16, SB, Q,
+                                    ll_dst(o, oc));
             }
         }
         if (row_tail) {   // tile-uniform: outputs whose taps wrap past the line end
@@ -583,19 +608,21 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
                 auto load = [&](int p) -> double { return row[pad_col(p - C0)]; };
                 const double lo = dwt_tap_sum_logical(flt.dec_lo, F, w, i, load);
                 const double hi = dwt_tap_sum_logical(flt.dec_hi, F, w, i, load);
-                fwd_store<LAST>(src, lo, hi, (o * TW + oc) * 3 + ch, stage, stage16, SB, Q, stageLL, o * TW + oc);
+                fwd_store<LAST>(src, lo, hi, (o * TW + oc) * 3 + ch, stage, stage16, SB, Q, ll_dst(o, oc));
             }
         }
-        __syncthreads();
-        if (!LAST) {   // LL rows leave as contiguous runs of doubles
-            const int rows = min(kFTH, hh - o0), nw = min(TW, hw - c0);
-            double *dst = LLout + (frame * 3 + ch) * plane_stride + (long long)o0 * hw + c0;
-            for (int t = tid; t < rows * TW; t += 256) {
-                const int o = t / TW, oc = t - o * TW;
-                if (oc < nw) dst[(long long)o * hw + oc] = stageLL[t];
+        if (!PIPE) {
+            __syncthreads();
+            if (!LAST) {   // LL rows leave as contiguous runs of doubles
+                const int rows = min(kFTH, hh - o0), nw = min(TW, hw - c0);
+                for (int t = tid; t < rows * TW; t += 256) {
+                    const int o = t / TW, oc = t - o * TW;
+                    if (oc < nw) llp[(long long)o * hw + oc] = stageLL[t];
+                }
             }
         }
     }
+    if (PIPE) __syncthreads();   // the byte image is complete
     // copy-out: each subband row of the tile is one contiguous byte run
     const int rows = min(kFTH, hh - o0), nb = min(TW, hw - c0) * 3;
     uint8_t *pk = packed + frame * packed_stride;
@@ -877,6 +904,7 @@ struct LevelArgs {
     Filters flt;
     const WaveletDef *wd;
     hipStream_t s;
+    int pipe = 1;   // forward fused levels: 0 = the three-barrier schedule (bior4.4 only, variant 3)
 };
 
 // bit m set = tap m is exactly 0.0
@@ -897,6 +925,13 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
 {
     auto kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI> : dwt_level_kernel<F, true, false, ZLO, ZHI>)
                       : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI> : dwt_level_kernel<F, false, false, ZLO, ZHI>);
+    if constexpr (F == 10 && ZLO != 0) {   // bior4.4: the earlier three-barrier schedule for A/B (variant 3)
+        if (a.pipe == 0)
+            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, false>
+                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, false>)
+                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, false>
+                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, false>);
+    }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed,
                        a.packed_stride, a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt);
 }
@@ -1012,7 +1047,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 2) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant > 3) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1031,7 +1066,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
     hipStream_t s = (hipStream_t)stream;
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *in = nullptr;
-    const bool fused = variant == 1 || (variant == 0 && fast_filter(F));
+    const bool fused = variant == 1 || variant == 3 || (variant == 0 && fast_filter(F));
     if (fused && !fast_filter(F))
         return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
                          kMaxFastF);
@@ -1039,7 +1074,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         double *LLout = (l & 1) ? LL0 : LL1;
         const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
                           g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
-                          g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s};
+                          g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s, variant == 3 ? 0 : 1};
         fwd_level(F, a, l == 1, l == levels);
         in = LLout;
         rc = hip_check(hipGetLastError(), "dwt level launch");
