@@ -458,7 +458,22 @@ __device__ __forceinline__ void fwd_store(int src, double lo, double hi, int e, 
 // level go straight from the row pass to HBM (4 consecutive doubles per work
 // item, contiguous across a wave) instead of through an LDS tile and a third
 // barrier.  PIPE = false is the earlier schedule (dwt encode variant 3).
-template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true>
+// bior4.4's decomposition taps (CDF 9/7, config C3) as compile-time
+// constants, bit for bit the table's (vcf_wavelets.h; the launcher checks).
+__host__ __device__ constexpr double b44_dec(bool hi, int m)
+{
+    constexpr double lo_[10] = {0x0.0p+0, 0x1.35e4056861677p-5, -0x1.86bfe8124f578p-6, -0x1.c51e1871dddccp-4,
+                                0x1.8275e4e918b25p-2, 0x1.b494ebd75f071p-1, 0x1.8275e4e918b25p-2,
+                                -0x1.c51e1871dddccp-4, -0x1.86bfe8124f578p-6, 0x1.35e4056861677p-5};
+    constexpr double hi_[10] = {-0x0.0p+0, -0x1.0859ec635ec44p-4, 0x1.4d53e4bd96b38p-5, 0x1.ac206180c9dfcp-2,
+                                -0x1.93b462ffa8216p-1, 0x1.ac206180c9dfcp-2, 0x1.4d53e4bd96b38p-5,
+                                -0x1.0859ec635ec44p-4, -0x0.0p+0, 0x0.0p+0};
+    return hi ? hi_[m] : lo_[m];
+}
+
+// CT: the taps are bior4.4's as compile-time constants (rematerialised
+// instead of held in -- and spilled from -- scalar registers).
+template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true, bool CT = false>
 __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
@@ -487,8 +502,12 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
     const bool col_tail = F / 2 + 2 * (o0 + kFTH - 1) >= h, row_tail = F / 2 + 2 * (c0 + TW - 1) >= w;
     // taps into VGPRs through LDS (kernel-argument taps would sit in scalar
     // registers, which the pass loops exhaust)
-    const double(&flo)[F] = tp.lo;
-    const double(&fhi)[F] = tp.hi;
+    double flo[F], fhi[F];
+#pragma unroll
+    for (int m = 0; m < F; ++m) {
+        flo[m] = CT ? b44_dec(false, m) : tp.lo[m];
+        fhi[m] = CT ? b44_dec(true, m) : tp.hi[m];
+    }
     // staged samples of this thread (PER per channel), fetched one channel
     // ahead into registers: level 1 reads its RGB bytes once for all three
     // channels, later levels prefetch the next channel's plane during the
@@ -904,7 +923,7 @@ struct LevelArgs {
     Filters flt;
     const WaveletDef *wd;
     hipStream_t s;
-    int pipe = 1;   // forward fused levels: 0 = the three-barrier schedule (bior4.4 only, variant 3)
+    int pipe = 1;   // forward fused levels, bior4.4: 0 = the three-barrier schedule (variant 3), 2 = run-time taps (4)
 };
 
 // bit m set = tap m is exactly 0.0
@@ -925,7 +944,17 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
 {
     auto kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI> : dwt_level_kernel<F, true, false, ZLO, ZHI>)
                       : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI> : dwt_level_kernel<F, false, false, ZLO, ZHI>);
-    if constexpr (F == 10 && ZLO != 0) {   // bior4.4: the earlier three-barrier schedule for A/B (variant 3)
+    if constexpr (F == 10 && ZLO != 0) {   // bior4.4: constant taps; the earlier schedule for A/B (variant 3)
+        bool ct = a.pipe == 1;   // pipe 2: run-time taps (dwt variant 4, A/B)
+        for (int m = 0; m < F; ++m) {
+            const double l = b44_dec(false, m), h = b44_dec(true, m);
+            ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
+        }
+        if (ct)
+            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, true>
+                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, true>)
+                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, true>
+                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, true, true>);
         if (a.pipe == 0)
             kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, false>
                                  : dwt_level_kernel<F, true, false, ZLO, ZHI, false>)
@@ -1047,7 +1076,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 3) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant > 4) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1066,7 +1095,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
     hipStream_t s = (hipStream_t)stream;
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *in = nullptr;
-    const bool fused = variant == 1 || variant == 3 || (variant == 0 && fast_filter(F));
+    const bool fused = variant == 1 || variant >= 3 || (variant == 0 && fast_filter(F));
     if (fused && !fast_filter(F))
         return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
                          kMaxFastF);
@@ -1074,7 +1103,8 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         double *LLout = (l & 1) ? LL0 : LL1;
         const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
                           g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
-                          g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s, variant == 3 ? 0 : 1};
+                          g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s,
+                          variant == 3 ? 0 : variant == 4 ? 2 : 1};
         fwd_level(F, a, l == 1, l == levels);
         in = LLout;
         rc = hip_check(hipGetLastError(), "dwt level launch");
