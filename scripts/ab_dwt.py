@@ -20,14 +20,26 @@ frames = np.stack([bench.synth_frame(H, W, s) for s in range(F)])
 din, dws = DeviceBuffer.from_array(frames), DeviceBuffer(F * wb)
 outs = {v: DeviceBuffer(F * pb) for v in variants}
 s = Stream()
-run = lambda v: L.call("vcf_dwt_dz_encode_variant", v, din.ptr, F, H, W, w, LV, Q, outs[v].ptr, dws.ptr, s.handle)
+DECODE = os.environ.get("DECODE", "0") == "1"
+if DECODE:   # decode the default encode's subbands; outputs are RGB frames
+    dpk = DeviceBuffer(F * pb)
+    L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, LV, Q, dpk.ptr, dws.ptr, s.handle)
+    Ho, Wo = 2 * shapes[0][0], 2 * shapes[0][1]
+    nout = F * Ho * Wo * 3
+    outs = {v: DeviceBuffer(nout) for v in variants}
+    run = lambda v: L.call("vcf_dwt_dz_decode_variant", v, dpk.ptr, F, H, W, w, LV, Q, outs[v].ptr, dws.ptr,
+                           s.handle)
+else:
+    nout = F * pb
+    run = lambda v: L.call("vcf_dwt_dz_encode_variant", v, din.ptr, F, H, W, w, LV, Q, outs[v].ptr, dws.ptr,
+                           s.handle)
 for v in variants:
     run(v)
 s.synchronize()
-ref = outs[variants[0]].download(np.empty(F * pb, np.uint8))
+ref = outs[variants[0]].download(np.empty(nout, np.uint8))
 for v in variants[1:]:
     print(f"variant {v} == variant {variants[0]}: "
-          f"{np.array_equal(outs[v].download(np.empty(F * pb, np.uint8)), ref)}", flush=True)
+          f"{np.array_equal(outs[v].download(np.empty(nout, np.uint8)), ref)}", flush=True)
 for _ in range(300):   # past the clock ramp
     run(variants[0])
 res = {v: [] for v in variants}
@@ -42,5 +54,5 @@ for rnd in range(16):
         res[v].append(e0.elapsed_ms(e1) / 10)
 base = np.array(res[variants[0]])
 for v in variants:
-    print(f"dwt encode variant {v}: median {np.median(res[v]):.4f} ms per {F} 4K frames; "
+    print(f"dwt {'decode' if DECODE else 'encode'} variant {v}: median {np.median(res[v]):.4f} ms per {F} 4K frames; "
           f"per-round ratio to {variants[0]}: {np.median(np.array(res[v]) / base):.4f}", flush=True)

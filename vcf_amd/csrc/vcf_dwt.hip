@@ -700,7 +700,20 @@ __device__ __attribute__((noinline)) double inv_col_generic(Filters flt, int F, 
 // column x 4 outputs.  TO_RGB (level 1): all three channels per tile, kept
 // in registers, then to_RGB + clip + u8.  Outputs whose wrapped pair index
 // is below F/4 take pywt's reordered taps through the generic LDS sum.
-template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0>
+__host__ __device__ constexpr double b44_rec(bool hi, int m)
+{
+    constexpr double lo_[10] = {0x0.0p+0, -0x1.0859ec635ec44p-4, -0x1.4d53e4bd96b38p-5, 0x1.ac206180c9dfcp-2,
+                                0x1.93b462ffa8216p-1, 0x1.ac206180c9dfcp-2, -0x1.4d53e4bd96b38p-5,
+                                -0x1.0859ec635ec44p-4, 0x0.0p+0, 0x0.0p+0};
+    constexpr double hi_[10] = {0x0.0p+0, -0x1.35e4056861677p-5, -0x1.86bfe8124f578p-6, 0x1.c51e1871dddccp-4,
+                                0x1.8275e4e918b25p-2, -0x1.b494ebd75f071p-1, 0x1.8275e4e918b25p-2,
+                                0x1.c51e1871dddccp-4, -0x1.86bfe8124f578p-6, -0x1.35e4056861677p-5};
+    return hi ? hi_[m] : lo_[m];
+}
+
+// CT: bior4.4's reconstruction taps as compile-time constants (no tap
+// registers: 40 fewer VGPRs than taps staged through LDS)
+template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0, bool CT = false>
 __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
                                                          long long ll_off, long long off_lh, long long off_hl,
                                                          long long off_hh, const double *__restrict__ prev,
@@ -731,17 +744,19 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
     double acc[TO_RGB ? 3 : 1][kG];
     const int ch_lo = TO_RGB ? 0 : (int)(blockIdx.z % 3), ch_hi = TO_RGB ? 3 : ch_lo + 1;
     const int nc = tid % kITW, gr = tid / kITW;      // column-pass item
-    __shared__ double taps[2 * F];
-    if (tid < F) {
-        taps[tid] = tp.lo[tid];
-        taps[F + tid] = tp.hi[tid];
+    __shared__ double taps[CT ? 1 : 2 * F];
+    if (!CT) {
+        if (tid < F) {
+            taps[tid] = tp.lo[tid];
+            taps[F + tid] = tp.hi[tid];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     double flo[F], fhi[F];
 #pragma unroll
     for (int m = 0; m < F; ++m) {
-        flo[m] = taps[m];
-        fhi[m] = taps[F + m];
+        flo[m] = CT ? b44_rec(false, m) : taps[m];
+        fhi[m] = CT ? b44_rec(true, m) : taps[F + m];
     }
     for (int ch = ch_lo; ch < ch_hi; ++ch) {
         for (int t = tid; t < KH * KW; t += 256) {
@@ -985,6 +1000,18 @@ void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
     auto kern = from_packed
                     ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI> : idwt_level_kernel<F, true, false, ZLO, ZHI>)
                     : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI> : idwt_level_kernel<F, false, false, ZLO, ZHI>);
+    if constexpr (F == 10 && ZLO != 0) {   // bior4.4: constant taps (run-time taps for A/B: dwt decode variant 4)
+        bool ct = a.pipe == 1;
+        for (int m = 0; m < F; ++m) {
+            const double l = b44_rec(false, m), h = b44_rec(true, m);
+            ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
+        }
+        if (ct)
+            kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI, true>
+                                         : idwt_level_kernel<F, true, false, ZLO, ZHI, true>)
+                               : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, true>
+                                         : idwt_level_kernel<F, false, false, ZLO, ZHI, true>);
+    }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
                        a.off_hh, a.in, a.plane_stride, a.lda, a.LLout, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, rgb_out,
                        (long long)a.hh * a.hw * 3);
@@ -1145,7 +1172,7 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 2) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || (variant > 2 && variant != 4)) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1165,7 +1192,7 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *prev = nullptr;
     int lda = 0;
-    const bool fused = variant == 1 || (variant == 0 && fast_filter(F));
+    const bool fused = variant == 1 || variant == 4 || (variant == 0 && fast_filter(F));
     if (fused && !fast_filter(F))
         return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
                          kMaxFastF);
@@ -1176,7 +1203,7 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
             double *out = (r & 1) ? P0 : P1;
             const LevelArgs a{nullptr, 0, prev, ws_stride, out, const_cast<uint8_t *>(packed_dev), g.packed_bytes,
                               g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], h, w, oh, ow, Q, lda,
-                              (unsigned)n_frames, flt, &kWavelets[wavelet], s};
+                              (unsigned)n_frames, flt, &kWavelets[wavelet], s, variant == 4 ? 2 : 1};
             inv_level(F, a, r == levels, r == 1, rgb_dev);
             prev = out;
             lda = ow;
