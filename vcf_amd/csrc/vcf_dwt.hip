@@ -458,22 +458,32 @@ __device__ __forceinline__ void fwd_store(int src, double lo, double hi, int e, 
 // level go straight from the row pass to HBM (4 consecutive doubles per work
 // item, contiguous across a wave) instead of through an LDS tile and a third
 // barrier.  PIPE = false is the earlier schedule (dwt encode variant 3).
-// bior4.4's decomposition taps (CDF 9/7, config C3) as compile-time
-// constants, bit for bit the table's (vcf_wavelets.h; the launcher checks).
-__host__ __device__ constexpr double b44_dec(bool hi, int m)
+// Decomposition taps as compile-time constants, bit for bit the table's
+// (vcf_wavelets.h; the launcher checks): id 1 = bior4.4 (CDF 9/7, config
+// C3), id 2 = db5 (the reference's default -w).
+__host__ __device__ constexpr double ct_dec(int id, bool hi, int m)
 {
-    constexpr double lo_[10] = {0x0.0p+0, 0x1.35e4056861677p-5, -0x1.86bfe8124f578p-6, -0x1.c51e1871dddccp-4,
-                                0x1.8275e4e918b25p-2, 0x1.b494ebd75f071p-1, 0x1.8275e4e918b25p-2,
-                                -0x1.c51e1871dddccp-4, -0x1.86bfe8124f578p-6, 0x1.35e4056861677p-5};
-    constexpr double hi_[10] = {-0x0.0p+0, -0x1.0859ec635ec44p-4, 0x1.4d53e4bd96b38p-5, 0x1.ac206180c9dfcp-2,
-                                -0x1.93b462ffa8216p-1, 0x1.ac206180c9dfcp-2, 0x1.4d53e4bd96b38p-5,
-                                -0x1.0859ec635ec44p-4, -0x0.0p+0, 0x0.0p+0};
-    return hi ? hi_[m] : lo_[m];
+    constexpr double b44lo[10] = {0x0.0p+0, 0x1.35e4056861677p-5, -0x1.86bfe8124f578p-6, -0x1.c51e1871dddccp-4,
+                                  0x1.8275e4e918b25p-2, 0x1.b494ebd75f071p-1, 0x1.8275e4e918b25p-2,
+                                  -0x1.c51e1871dddccp-4, -0x1.86bfe8124f578p-6, 0x1.35e4056861677p-5};
+    constexpr double b44hi[10] = {-0x0.0p+0, -0x1.0859ec635ec44p-4, 0x1.4d53e4bd96b38p-5, 0x1.ac206180c9dfcp-2,
+                                  -0x1.93b462ffa8216p-1, 0x1.ac206180c9dfcp-2, 0x1.4d53e4bd96b38p-5,
+                                  -0x1.0859ec635ec44p-4, -0x0.0p+0, 0x0.0p+0};
+    constexpr double db5lo[10] = {0x1.b5385e04e3c09p-9, -0x1.9c3eff3294128p-7, -0x1.990ad4579f2e8p-8,
+                                  0x1.3dbb9b52515aap-4, -0x1.0826648a8dc74p-5, -0x1.f0384d3f81474p-3,
+                                  0x1.1b80373befcc6p-3, 0x1.72d89143b54f5p-1, 0x1.35291c2c4b00cp-1,
+                                  0x1.47e3c41a7b911p-3};
+    constexpr double db5hi[10] = {-0x1.47e3c41a7b911p-3, 0x1.35291c2c4b00cp-1, -0x1.72d89143b54f5p-1,
+                                  0x1.1b80373befcc6p-3, 0x1.f0384d3f81474p-3, -0x1.0826648a8dc74p-5,
+                                  -0x1.3dbb9b52515aap-4, -0x1.990ad4579f2e8p-8, 0x1.9c3eff3294128p-7,
+                                  0x1.b5385e04e3c09p-9};
+    return id == 1 ? (hi ? b44hi[m] : b44lo[m]) : (hi ? db5hi[m] : db5lo[m]);
 }
 
-// CT: the taps are bior4.4's as compile-time constants (rematerialised
-// instead of held in -- and spilled from -- scalar registers).
-template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true, bool CT = false>
+// CT: the taps are wavelet CT's (ct_dec) as compile-time constants,
+// rematerialised instead of held in -- and spilled from -- scalar registers;
+// 0 = taps from the kernel arguments.
+template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true, int CT = 0>
 __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
@@ -505,8 +515,8 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
     double flo[F], fhi[F];
 #pragma unroll
     for (int m = 0; m < F; ++m) {
-        flo[m] = CT ? b44_dec(false, m) : tp.lo[m];
-        fhi[m] = CT ? b44_dec(true, m) : tp.hi[m];
+        flo[m] = CT ? ct_dec(CT, false, m) : tp.lo[m];
+        fhi[m] = CT ? ct_dec(CT, true, m) : tp.hi[m];
     }
     // staged samples of this thread (PER per channel), fetched one channel
     // ahead into registers: level 1 reads its RGB bytes once for all three
@@ -700,20 +710,29 @@ __device__ __attribute__((noinline)) double inv_col_generic(Filters flt, int F, 
 // column x 4 outputs.  TO_RGB (level 1): all three channels per tile, kept
 // in registers, then to_RGB + clip + u8.  Outputs whose wrapped pair index
 // is below F/4 take pywt's reordered taps through the generic LDS sum.
-__host__ __device__ constexpr double b44_rec(bool hi, int m)
+// reconstruction taps as compile-time constants (ids as ct_dec)
+__host__ __device__ constexpr double ct_rec(int id, bool hi, int m)
 {
-    constexpr double lo_[10] = {0x0.0p+0, -0x1.0859ec635ec44p-4, -0x1.4d53e4bd96b38p-5, 0x1.ac206180c9dfcp-2,
-                                0x1.93b462ffa8216p-1, 0x1.ac206180c9dfcp-2, -0x1.4d53e4bd96b38p-5,
-                                -0x1.0859ec635ec44p-4, 0x0.0p+0, 0x0.0p+0};
-    constexpr double hi_[10] = {0x0.0p+0, -0x1.35e4056861677p-5, -0x1.86bfe8124f578p-6, 0x1.c51e1871dddccp-4,
-                                0x1.8275e4e918b25p-2, -0x1.b494ebd75f071p-1, 0x1.8275e4e918b25p-2,
-                                0x1.c51e1871dddccp-4, -0x1.86bfe8124f578p-6, -0x1.35e4056861677p-5};
-    return hi ? hi_[m] : lo_[m];
+    constexpr double b44lo[10] = {0x0.0p+0, -0x1.0859ec635ec44p-4, -0x1.4d53e4bd96b38p-5, 0x1.ac206180c9dfcp-2,
+                                  0x1.93b462ffa8216p-1, 0x1.ac206180c9dfcp-2, -0x1.4d53e4bd96b38p-5,
+                                  -0x1.0859ec635ec44p-4, 0x0.0p+0, 0x0.0p+0};
+    constexpr double b44hi[10] = {0x0.0p+0, -0x1.35e4056861677p-5, -0x1.86bfe8124f578p-6, 0x1.c51e1871dddccp-4,
+                                  0x1.8275e4e918b25p-2, -0x1.b494ebd75f071p-1, 0x1.8275e4e918b25p-2,
+                                  0x1.c51e1871dddccp-4, -0x1.86bfe8124f578p-6, -0x1.35e4056861677p-5};
+    constexpr double db5lo[10] = {0x1.47e3c41a7b911p-3, 0x1.35291c2c4b00cp-1, 0x1.72d89143b54f5p-1,
+                                  0x1.1b80373befcc6p-3, -0x1.f0384d3f81474p-3, -0x1.0826648a8dc74p-5,
+                                  0x1.3dbb9b52515aap-4, -0x1.990ad4579f2e8p-8, -0x1.9c3eff3294128p-7,
+                                  0x1.b5385e04e3c09p-9};
+    constexpr double db5hi[10] = {0x1.b5385e04e3c09p-9, 0x1.9c3eff3294128p-7, -0x1.990ad4579f2e8p-8,
+                                  -0x1.3dbb9b52515aap-4, -0x1.0826648a8dc74p-5, 0x1.f0384d3f81474p-3,
+                                  0x1.1b80373befcc6p-3, -0x1.72d89143b54f5p-1, 0x1.35291c2c4b00cp-1,
+                                  -0x1.47e3c41a7b911p-3};
+    return id == 1 ? (hi ? b44hi[m] : b44lo[m]) : (hi ? db5hi[m] : db5lo[m]);
 }
 
-// CT: bior4.4's reconstruction taps as compile-time constants (no tap
-// registers: 40 fewer VGPRs than taps staged through LDS)
-template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0, bool CT = false>
+// CT: reconstruction taps of wavelet CT (ct_rec) as compile-time constants
+// (no tap registers: 40 fewer VGPRs than taps staged through LDS)
+template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0>
 __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
                                                          long long ll_off, long long off_lh, long long off_hl,
                                                          long long off_hh, const double *__restrict__ prev,
@@ -755,8 +774,8 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
     double flo[F], fhi[F];
 #pragma unroll
     for (int m = 0; m < F; ++m) {
-        flo[m] = CT ? b44_rec(false, m) : taps[m];
-        fhi[m] = CT ? b44_rec(true, m) : taps[F + m];
+        flo[m] = CT ? ct_rec(CT, false, m) : taps[m];
+        fhi[m] = CT ? ct_rec(CT, true, m) : taps[F + m];
     }
     for (int ch = ch_lo; ch < ch_hi; ++ch) {
         for (int t = tid; t < KH * KW; t += 256) {
@@ -959,22 +978,25 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
 {
     auto kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI> : dwt_level_kernel<F, true, false, ZLO, ZHI>)
                       : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI> : dwt_level_kernel<F, false, false, ZLO, ZHI>);
-    if constexpr (F == 10 && ZLO != 0) {   // bior4.4: constant taps; the earlier schedule for A/B (variant 3)
-        bool ct = a.pipe == 1;   // pipe 2: run-time taps (dwt variant 4, A/B)
+    if constexpr (F == 10) {   // bior4.4 / db5: constant taps (pipe 2: run-time taps, dwt variant 4)
+        constexpr int id = ZLO != 0 ? 1 : 2;
+        bool ct = a.pipe == 1;
         for (int m = 0; m < F; ++m) {
-            const double l = b44_dec(false, m), h = b44_dec(true, m);
+            const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
             ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
         }
         if (ct)
-            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, true>
-                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, true>)
-                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, true>
-                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, true, true>);
-        if (a.pipe == 0)
-            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, false>
-                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, false>)
-                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, false>
-                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, false>);
+            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id>
+                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id>)
+                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, id>
+                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, true, id>);
+        if constexpr (ZLO != 0) {   // bior4.4: the earlier three-barrier schedule for A/B (variant 3)
+            if (a.pipe == 0)
+                kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, false>
+                                     : dwt_level_kernel<F, true, false, ZLO, ZHI, false>)
+                             : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, false>
+                                     : dwt_level_kernel<F, false, false, ZLO, ZHI, false>);
+        }
     }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed,
                        a.packed_stride, a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt);
@@ -1000,17 +1022,18 @@ void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
     auto kern = from_packed
                     ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI> : idwt_level_kernel<F, true, false, ZLO, ZHI>)
                     : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI> : idwt_level_kernel<F, false, false, ZLO, ZHI>);
-    if constexpr (F == 10 && ZLO != 0) {   // bior4.4: constant taps (run-time taps for A/B: dwt decode variant 4)
+    if constexpr (F == 10) {   // bior4.4 / db5: constant taps (run-time taps for A/B: dwt decode variant 4)
+        constexpr int id = ZLO != 0 ? 1 : 2;
         bool ct = a.pipe == 1;
         for (int m = 0; m < F; ++m) {
-            const double l = b44_rec(false, m), h = b44_rec(true, m);
+            const double l = ct_rec(id, false, m), h = ct_rec(id, true, m);
             ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
         }
         if (ct)
-            kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI, true>
-                                         : idwt_level_kernel<F, true, false, ZLO, ZHI, true>)
-                               : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, true>
-                                         : idwt_level_kernel<F, false, false, ZLO, ZHI, true>);
+            kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI, id>
+                                         : idwt_level_kernel<F, true, false, ZLO, ZHI, id>)
+                               : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id>
+                                         : idwt_level_kernel<F, false, false, ZLO, ZHI, id>);
     }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
                        a.off_hh, a.in, a.plane_stride, a.lda, a.LLout, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, rgb_out,
