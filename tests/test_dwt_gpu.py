@@ -73,12 +73,14 @@ def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
     b = DW.encode(frames, wavelet, L, Q, variant=2)
     c = DW.encode(frames, wavelet, L, Q, variant=3)   # the earlier three-barrier schedule of the fused kernels
     e = DW.encode(frames, wavelet, L, Q, variant=4)   # run-time taps
+    f = DW.encode(frames, wavelet, L, Q, variant=5)   # level 1 staged as float
     ref = O.dwt_encode_frame(frames[0], wavelet, L, Q)
     for name in ref:
         assert np.array_equal(a[0][name], ref[name]), name
         assert np.array_equal(a[1][name], b[1][name]), name
         assert np.array_equal(c[1][name], a[1][name]), name
         assert np.array_equal(e[1][name], a[1][name]), name
+        assert np.array_equal(f[1][name], a[1][name]), name
     da = DW.decode(a, H, W, wavelet, L, Q, variant=1)
     db = DW.decode(a, H, W, wavelet, L, Q, variant=2)
     assert np.array_equal(da, db)

@@ -483,8 +483,15 @@ __host__ __device__ constexpr double ct_dec(int id, bool hi, int m)
 // CT: the taps are wavelet CT's (ct_dec) as compile-time constants,
 // rematerialised instead of held in -- and spilled from -- scalar registers;
 // 0 = taps from the kernel arguments.
-template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true, int CT = 0>
-__global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
+// STG (level 1): 1 = the YCoCg samples staged as int16 (exact; 29 KB of LDS
+// instead of 35 KB) with the registers held to 5 waves, so five workgroups
+// fit a CU; 0 = staged as float, 4 waves.  Used for db5 (−7.5 %, ABBA); for
+// bior4.4 the register cap spills (+2 %), so it keeps 0 (dwt variant 5
+// flips db5 back to 0 for A/B).
+template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true, int CT = 0,
+          int STG = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIRST && STG ? 5 : 1)))
+void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
                                                         long long packed_stride, long long ll_off, long long off_lh,
@@ -497,8 +504,9 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
     constexpr int SB = kFTH * TW * 3;
     static_assert(kFTH == 2 * kG && 2 * (TW - 1) + F == IW, "tile geometry");
     constexpr int RS = IW + IW / 8;                  // A/D rows padded one double per 8 (bank spread)
-    // level 1 stages int16-valued YCoCg samples, exact in float (half the LDS)
-    using Stage = typename std::conditional<FIRST, float, double>::type;
+    // level 1 stages int16-valued YCoCg samples (as int16, or exact in float)
+    using Stage = typename std::conditional<FIRST, typename std::conditional<STG == 1, int16_t, float>::type,
+                                            double>::type;
     __shared__ Stage tin[IH * IW];
     __shared__ double tA[kFTH * RS + 8], tD[kFTH * RS + 8];   // +8: the last row group's window overhang
     __shared__ uint8_t stage[3 * SB];
@@ -554,11 +562,11 @@ __global__ __launch_bounds__(256) void dwt_level_kernel(const uint8_t *__restric
                 if (ch == 0) iv = (R + 2 * G + B) >> 2;
                 else if (ch == 1) iv = (R - B) / 2;
                 else iv = (2 * G - R - B) / 4;
-                v = (double)iv;
+                tin[tid + 256 * j] = (Stage)iv;
             } else {
                 v = nxt[FIRST ? 0 : j];
+                tin[tid + 256 * j] = (Stage)v;
             }
-            tin[tid + 256 * j] = (Stage)v;
         }
     };
     fetch(0);
@@ -957,7 +965,8 @@ struct LevelArgs {
     Filters flt;
     const WaveletDef *wd;
     hipStream_t s;
-    int pipe = 1;   // forward fused levels, bior4.4: 0 = the three-barrier schedule (variant 3), 2 = run-time taps (4)
+    int pipe = 1;   // fused levels, bior4.4/db5: 0 = the three-barrier schedule (variant 3), 2 = run-time taps (4),
+                    // 3 = level 1 staged as float (5)
 };
 
 // bit m set = tap m is exactly 0.0
@@ -980,16 +989,20 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
                       : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI> : dwt_level_kernel<F, false, false, ZLO, ZHI>);
     if constexpr (F == 10) {   // bior4.4 / db5: constant taps (pipe 2: run-time taps, dwt variant 4)
         constexpr int id = ZLO != 0 ? 1 : 2;
-        bool ct = a.pipe == 1;
+        bool ct = a.pipe == 1 || a.pipe == 3;
         for (int m = 0; m < F; ++m) {
             const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
             ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
         }
+        constexpr int stg = id == 2 ? 1 : 0;
         if (ct)
-            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id>
-                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id>)
+            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, stg>
+                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, stg>)
                          : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, id>
                                  : dwt_level_kernel<F, false, false, ZLO, ZHI, true, id>);
+        if (ct && a.pipe == 3 && first)   // level 1 staged as float (dwt variant 5, A/B)
+            kern = last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, 0>
+                        : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, 0>;
         if constexpr (ZLO != 0) {   // bior4.4: the earlier three-barrier schedule for A/B (variant 3)
             if (a.pipe == 0)
                 kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, false>
@@ -1126,7 +1139,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 4) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant > 5) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1154,7 +1167,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
                           g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
                           g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s,
-                          variant == 3 ? 0 : variant == 4 ? 2 : 1};
+                          variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : 1};
         fwd_level(F, a, l == 1, l == levels);
         in = LLout;
         rc = hip_check(hipGetLastError(), "dwt level launch");
