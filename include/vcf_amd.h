@@ -210,7 +210,8 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
  * earlier three-barrier schedule for bior4.4 (A/B reference; other filters
  * as 1), 4 = 1 with bior4.4's taps as kernel arguments instead of
  * compile-time constants (A/B reference), 5 = 1 with level 1 staging its
- * samples as float at 4 waves/SIMD (A/B reference for db5; bior4.4 as 1).  vcf_dwt_dz_decode_variant takes
+ * samples as float at 4 waves/SIMD and no raised wave priority for its
+ * loads and copy-out (A/B reference).  vcf_dwt_dz_decode_variant takes
  * 0, 1, 2 and 4 (bior4.4's reconstruction taps at run time).  Outputs
  * identical. */
 int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,

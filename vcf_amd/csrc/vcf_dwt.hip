@@ -489,7 +489,7 @@ __host__ __device__ constexpr double ct_dec(int id, bool hi, int m)
 // bior4.4 the register cap spills (+2 %), so it keeps 0 (dwt variant 5
 // flips db5 back to 0 for A/B).
 template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true, int CT = 0,
-          int STG = 0>
+          int STG = 0, int PRI = 3>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIRST && STG ? 5 : 1)))
 void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
@@ -569,7 +569,11 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
             }
         }
     };
+    // PRI: wave priority while a workgroup issues its loads and its copy-out
+    // (as the DCT encode); 0 = none (dwt variant 5, A/B)
+    if (PRI) __builtin_amdgcn_s_setprio(PRI);
     fetch(0);
+    if (PRI) __builtin_amdgcn_s_setprio(0);
     if (PIPE) {
         stage_in(0);
         if (!FIRST) fetch(1);
@@ -660,6 +664,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
         }
     }
     if (PIPE) __syncthreads();   // the byte image is complete
+    if (PRI) __builtin_amdgcn_s_setprio(PRI);
     // copy-out: each subband row of the tile is one contiguous byte run
     const int rows = min(kFTH, hh - o0), nb = min(TW, hw - c0) * 3;
     uint8_t *pk = packed + frame * packed_stride;
@@ -1000,9 +1005,9 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
                                  : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, stg>)
                          : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, id>
                                  : dwt_level_kernel<F, false, false, ZLO, ZHI, true, id>);
-        if (ct && a.pipe == 3 && first)   // level 1 staged as float (dwt variant 5, A/B)
-            kern = last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, 0>
-                        : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, 0>;
+        if (ct && a.pipe == 3 && first)   // level 1 staged as float, no wave priority (dwt variant 5, A/B)
+            kern = last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, 0, 0>
+                        : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, 0, 0>;
         if constexpr (ZLO != 0) {   // bior4.4: the earlier three-barrier schedule for A/B (variant 3)
             if (a.pipe == 0)
                 kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, false>
