@@ -212,7 +212,8 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
  * compile-time constants (A/B reference), 5 = 1 with level 1 staging its
  * samples as float at 4 waves/SIMD and no raised wave priority for its
  * loads and copy-out (A/B reference).  vcf_dwt_dz_decode_variant takes
- * 0, 1, 2 and 4 (bior4.4's reconstruction taps at run time).  Outputs
+ * 0, 1, 2, 4 (bior4.4's reconstruction taps at run time) and 5 (no raised
+ * wave priority while the subbands are staged).  Outputs
  * identical. */
 int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,

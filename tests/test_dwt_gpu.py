@@ -85,6 +85,7 @@ def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
     db = DW.decode(a, H, W, wavelet, L, Q, variant=2)
     assert np.array_equal(da, db)
     assert np.array_equal(DW.decode(a, H, W, wavelet, L, Q, variant=4), da)   # run-time taps
+    assert np.array_equal(DW.decode(a, H, W, wavelet, L, Q, variant=5), da)   # no staging priority
     assert np.array_equal(da[0], O.dwt_decode_frame(a[0], H, W, wavelet, L, Q))
     assert np.abs(da.astype(int) - frames.astype(int)).mean() < 8     # a sane reconstruction
 

@@ -745,7 +745,7 @@ __host__ __device__ constexpr double ct_rec(int id, bool hi, int m)
 
 // CT: reconstruction taps of wavelet CT (ct_rec) as compile-time constants
 // (no tap registers: 40 fewer VGPRs than taps staged through LDS)
-template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0>
+template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0, int PRI = 3>
 __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
                                                          long long ll_off, long long off_lh, long long off_hl,
                                                          long long off_hh, const double *__restrict__ prev,
@@ -791,6 +791,8 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
         fhi[m] = CT ? ct_rec(CT, true, m) : taps[F + m];
     }
     for (int ch = ch_lo; ch < ch_hi; ++ch) {
+        // PRI: wave priority while the subbands are staged (0: decode variant 5, A/B)
+        if (PRI) __builtin_amdgcn_s_setprio(PRI);
         for (int t = tid; t < KH * KW; t += 256) {
             const int r = t / KW, c = t - r * KW;
             const int y = rows_in ? K0r + r : mod_pos(K0r + r, h);
@@ -809,6 +811,7 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
             sDA[l] = dequant((int16_t)pk[off_lh + e], Q);   // 'da' = cH = LH
             sDD[l] = dequant((int16_t)pk[off_hh + e], Q);   // 'dd' = cD = HH
         }
+        if (PRI) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         // row pass (axis 1): 'a' = idwt(aa, ad), 'd' = idwt(da, dd)
         for (int t = tid; t < KH * NGC * 2; t += 256) {
@@ -1042,7 +1045,7 @@ void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
                     : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI> : idwt_level_kernel<F, false, false, ZLO, ZHI>);
     if constexpr (F == 10) {   // bior4.4 / db5: constant taps (run-time taps for A/B: dwt decode variant 4)
         constexpr int id = ZLO != 0 ? 1 : 2;
-        bool ct = a.pipe == 1;
+        bool ct = a.pipe == 1 || a.pipe == 3;
         for (int m = 0; m < F; ++m) {
             const double l = ct_rec(id, false, m), h = ct_rec(id, true, m);
             ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
@@ -1052,6 +1055,11 @@ void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
                                          : idwt_level_kernel<F, true, false, ZLO, ZHI, id>)
                                : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id>
                                          : idwt_level_kernel<F, false, false, ZLO, ZHI, id>);
+        if (ct && a.pipe == 3)   // no wave priority for the staging (dwt decode variant 5, A/B)
+            kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI, id, 0>
+                                         : idwt_level_kernel<F, true, false, ZLO, ZHI, id, 0>)
+                               : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id, 0>
+                                         : idwt_level_kernel<F, false, false, ZLO, ZHI, id, 0>);
     }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
                        a.off_hh, a.in, a.plane_stride, a.lda, a.LLout, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, rgb_out,
@@ -1213,7 +1221,7 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || (variant > 2 && variant != 4)) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || (variant > 2 && variant != 4 && variant != 5)) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1233,7 +1241,7 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *prev = nullptr;
     int lda = 0;
-    const bool fused = variant == 1 || variant == 4 || (variant == 0 && fast_filter(F));
+    const bool fused = variant == 1 || variant >= 4 || (variant == 0 && fast_filter(F));
     if (fused && !fast_filter(F))
         return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
                          kMaxFastF);
@@ -1244,7 +1252,8 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
             double *out = (r & 1) ? P0 : P1;
             const LevelArgs a{nullptr, 0, prev, ws_stride, out, const_cast<uint8_t *>(packed_dev), g.packed_bytes,
                               g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], h, w, oh, ow, Q, lda,
-                              (unsigned)n_frames, flt, &kWavelets[wavelet], s, variant == 4 ? 2 : 1};
+                              (unsigned)n_frames, flt, &kWavelets[wavelet], s,
+                              variant == 4 ? 2 : variant == 5 ? 3 : 1};
             inv_level(F, a, r == levels, r == 1, rgb_dev);
             prev = out;
             lda = ow;
