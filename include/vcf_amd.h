@@ -347,6 +347,43 @@ int vcf_deadzone_quantize(const void *x_dev, int32_t x_dtype, int64_t n, int32_t
 int vcf_deadzone_dequantize(const void *k_dev, int32_t k_dtype, int64_t n, int32_t Q, void *y_dev,
                             void *stream);
 
+/* ---- cross-rank exchange on RCCL over xGMI -------------------
+ * Frames shard across one process per GPU with no collective on the data
+ * path; the one exchange step of the III / IPP drivers is after coding: an
+ * all-gather of the per-frame code-stream sizes and a gather of the
+ * variable-length payloads to rank 0.  It replaces the point where the
+ * reference's sequential frame loop has every coded frame in one process
+ * (src/III.py:77-115 encode, :132-144 decode).  librccl is opened on first
+ * use (dlopen); without it these return VCF_ERR_UNSUPPORTED.  Buffers are
+ * device pointers, work is enqueued on `stream`. */
+#define VCF_COMM_ID_BYTES 128
+#define VCF_COMM_SUM 0
+#define VCF_COMM_MAX 1
+#define VCF_COMM_MIN 2
+typedef struct vcf_comm *vcf_comm_t;
+
+/* One rank creates the id (ncclGetUniqueId) and hands it to the others
+ * out of band (vcf_amd/comm.py: a TCP host group). */
+int vcf_comm_unique_id(uint8_t *id, size_t capacity);
+/* Collective over `world` processes, each with its device already set
+ * (vcf_set_device). */
+int vcf_comm_init(vcf_comm_t *comm, const uint8_t *id, int rank, int world);
+int vcf_comm_destroy(vcf_comm_t comm);
+int vcf_comm_rank(vcf_comm_t comm, int *rank, int *world);
+/* recv_dev[r * count + i] = rank r's send_dev[i] (ncclAllGather, int64). */
+int vcf_comm_allgather_i64(vcf_comm_t comm, const int64_t *send_dev, int64_t count, int64_t *recv_dev,
+                           void *stream);
+/* Element-wise VCF_COMM_SUM / MAX / MIN over ranks (ncclAllReduce, float64). */
+int vcf_comm_allreduce_f64(vcf_comm_t comm, const double *send_dev, double *recv_dev, int64_t count, int op,
+                           void *stream);
+/* Gather with per-rank byte counts: rank r sends counts[r] bytes (= send_bytes)
+ * and the root receives them packed in rank order in recv_dev.  counts (host,
+ * `world` entries, the same on every rank -- e.g. from the size all-gather).
+ * One grouped ncclSend per peer, P-1 concurrent ncclRecv on the root: each
+ * xGMI peer uses its own link to the root (RCCL has no gatherv). */
+int vcf_comm_gatherv(vcf_comm_t comm, const void *send_dev, int64_t send_bytes, void *recv_dev,
+                     const int64_t *counts, int root, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,135 @@
+"""The multi-rank drivers with the real GPU codec.
+
+- RCCL through libvcf_amd.so's vcf_comm_* ABI, single rank (a 1-GPU box
+  cannot hold two RCCL ranks: RCCL refuses two ranks on one device, so the
+  P-rank exchange over xGMI runs only on the driver's 8-GPU node);
+- III and IPP at world size 2, both ranks on this box's GPU running the real
+  HIP codec, the exchange on the host group: decoded frames equal the
+  oracle's, rank 0's gathered code-streams equal every frame's file;
+- `bench.py --gpus 2` without a launcher (the parent spawns the ranks).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rccl_single_rank_collectives():
+    from vcf_amd.comm import HostGroup
+    from vcf_amd.device import set_device
+    from vcf_amd.rccl import MAX, SUM, Communicator
+    set_device(0)
+    c = Communicator(HostGroup(0, 1))
+    v = np.arange(-3, 1000, 7, dtype=np.int64)
+    assert np.array_equal(c.all_gather_i64(v), v[None])
+    x = np.array([1.5, -2.0, 3e300])
+    assert np.array_equal(c.allreduce_f64(x, MAX), x)
+    assert np.array_equal(c.allreduce_f64(x, SUM), x)
+    blob = np.random.default_rng(3).integers(0, 256, 1 << 20, dtype=np.uint8)
+    got = c.gatherv(blob, [blob.size])
+    assert np.array_equal(got, blob)
+    assert c.gatherv(b"", [0]).size == 0
+    with pytest.raises(ValueError):
+        c.gatherv(b"abc", [2])
+    c.close()
+
+
+def _frames(n, H, W, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return [rng.integers(0, 256, (H, W, 3), dtype=np.uint8) for _ in range(n)]
+
+
+def _iii_worker(rank, world, tmp, n):
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec import shard
+    from vcf_amd.codec.iii import CoDec
+    from vcf_amd.device import set_device
+    set_device(0)                           # both ranks share this box's one GPU
+    g = shard.Group("host")
+    args = P.parse(P.iii_parser(), ["encode", "-N", str(n), "-o", os.path.join(tmp, "original_%04d.png")])
+    c = CoDec(args, group=g, encode_prefix=os.path.join(tmp, "enc"), decode_prefix=os.path.join(tmp, "dec"),
+              batch=3)
+    total = c.encode()
+    payloads = c.gather_codestreams()
+    g.barrier()
+    d = CoDec(P.parse(P.iii_parser(), ["decode", "-N", str(n)]), group=g, encode_prefix=os.path.join(tmp, "enc"),
+              decode_prefix=os.path.join(tmp, "dec"), batch=3)
+    dtotal = d.decode()
+    g.close()
+    return total, list(map(int, c.sizes)), payloads, dtotal
+
+
+def test_iii_two_ranks_real_codec(tmp_path):
+    from _dist import run_ranks
+    from oracle import oracle as O
+    from vcf_amd.codec.tiff import imwrite_bytes
+    n, H, W = 9, 40, 56
+    frames = _frames(n, H, W, 21)
+    for i, f in enumerate(frames):
+        Image.fromarray(f).save(str(tmp_path / f"original_{i:04d}.png"))
+    res = run_ranks(_iii_worker, 2, str(tmp_path), n)
+    total, sizes, payloads, _ = res[0]
+    assert res[1][2] is None and res[1][1] == sizes and res[1][0] == total
+    for i, f in enumerate(frames):
+        k = O.encode_frame(f, 32, 0)
+        tif = open(str(tmp_path / f"enc_{i:04d}.tif"), "rb").read()
+        assert tif == imwrite_bytes(k)
+        assert payloads[i] == tif and sizes[i] == len(tif)
+        got = np.asarray(Image.open(str(tmp_path / f"dec_{i:04d}.png")))
+        assert np.array_equal(got, O.decode_frame(k, H, W, 32, 0)), f"frame {i}"
+
+
+def _ipp_worker(rank, world, pat, prefix):
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec import shard
+    from vcf_amd.codec.ipp import CoDec
+    from vcf_amd.device import set_device
+    set_device(0)
+    g = shard.Group("host")
+    c = CoDec(P.parse(P.ipp_parser(), ["encode", "-i", pat, "-O", prefix, "-N", "8", "-G", "3", "-M", "16",
+                                       "-S", "8"]), group=g)
+    total = c.encode()
+    g.close()
+    return total
+
+
+def test_ipp_two_ranks_real_codec(tmp_path):
+    from _dist import run_ranks
+    from test_ipp_gpu import _ipp_loop, _moving, _write_seq
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec.ipp import CoDec
+    frames = _moving(64, 96, 8, 5)
+    pat = _write_seq(str(tmp_path), frames)
+    res = run_ranks(_ipp_worker, 2, pat, str(tmp_path / "enc" / "v"))
+    assert res[1] is None and res[0] > 0
+    meta = json.load(open(str(tmp_path / "enc" / "v_meta.json")))
+    assert len(meta["I_info"]) == 3 and len(meta["P_info"]) == 5
+    dec = str(tmp_path / "dec" / "v")
+    assert CoDec(P.parse(P.ipp_parser(), ["decode", "-i", str(tmp_path / "enc" / "v"), "-O", dec,
+                                          "-M", "16"])).decode() == 8
+    want, want_mv = _ipp_loop(frames, 3, 16, 8, False, 32)
+    with np.load(str(tmp_path / "enc" / "v_mv.npz"), allow_pickle=False) as z:
+        assert np.array_equal(z["mv_f32"], np.stack(want_mv))
+    for i in range(8):
+        got = np.asarray(Image.open(f"{dec}_{i:04d}.png").convert("RGB"))
+        assert np.array_equal(got, want[i]), f"frame {i}"
+
+
+def test_bench_two_ranks_without_launcher():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--frames", "4",
+                        "--steps", "3", "--warmup", "1", "--settle-max-s", "0", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 8 and line["value"] > 0

@@ -1,10 +1,9 @@
 """III frame sharding on the CPU: partition properties, and a world_size-2
-gloo job that codes its chunks, all-gathers the per-frame sizes and gathers
+job (host group, no GPU) that codes its chunks, all-gathers the per-frame sizes and gathers
 the code-streams on rank 0.  The per-frame codec here is a
 stand-in that writes deterministic files -- the GPU codec itself is covered
 by tests/test_codec_gpu.py; this checks the driver around it."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -47,56 +46,58 @@ class FakeCodec:
         return sizes
 
 
-def _worker(rank, world, port, tmp, n, q):
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker(rank, world, tmp, n):
     from vcf_amd.codec import parser as P
     from vcf_amd.codec.iii import CoDec
-    try:
-        g = shard.Group("gloo")
-        args = P.parse(P.iii_parser(), ["encode", "-N", str(n), "-o", os.path.join(tmp, "orig_%04d.png")])
-        c = CoDec(args, codec=FakeCodec(), group=g, encode_prefix=os.path.join(tmp, "enc"),
-                  decode_prefix=os.path.join(tmp, "dec"))
-        total = c.encode()
-        payloads = c.gather_codestreams()
-        dargs = P.parse(P.iii_parser(), ["decode", "-N", str(n)])
-        d = CoDec(dargs, codec=FakeCodec(), group=g, encode_prefix=os.path.join(tmp, "enc"),
-                  decode_prefix=os.path.join(tmp, "dec"))
-        g.barrier()
-        dtotal = d.decode()
-        q.put((rank, total, list(c.sizes), None if payloads is None else [len(p) for p in payloads],
-               None if payloads is None else [p[:1] for p in payloads], dtotal))
-        g.close()
-    except Exception as e:  # surfaced by the parent
-        q.put((rank, "error", repr(e)))
+    g = shard.Group("host")
+    args = P.parse(P.iii_parser(), ["encode", "-N", str(n), "-o", os.path.join(tmp, "orig_%04d.png")])
+    c = CoDec(args, codec=FakeCodec(), group=g, encode_prefix=os.path.join(tmp, "enc"),
+              decode_prefix=os.path.join(tmp, "dec"))
+    total = c.encode()
+    payloads = c.gather_codestreams()
+    dargs = P.parse(P.iii_parser(), ["decode", "-N", str(n)])
+    d = CoDec(dargs, codec=FakeCodec(), group=g, encode_prefix=os.path.join(tmp, "enc"),
+              decode_prefix=os.path.join(tmp, "dec"))
+    g.barrier()
+    dtotal = d.decode()
+    g.close()
+    return (total, list(c.sizes), None if payloads is None else [len(p) for p in payloads],
+            None if payloads is None else [p[:1] for p in payloads], dtotal)
 
 
-def test_iii_two_ranks_gloo(tmp_path):
-    import torch.multiprocessing as mp
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+def test_iii_two_ranks_host_group(tmp_path):
+    from _dist import run_ranks
     n, world = 11, 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), n, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-    res = {r[0]: r for r in res}
-    for r in res.values():
-        assert r[1] != "error", r
+    res = run_ranks(_worker, world, str(tmp_path), n)
     expect = [100 + 7 * i for i in range(n)]
     for rank in range(world):
-        _, total, sizes, plens, heads, dtotal = res[rank]
+        total, sizes, plens, heads, dtotal = res[rank]
         assert sizes == expect and total == sum(expect)
         assert dtotal == sum(e // 2 for e in expect)
-    assert res[0][3] == expect and res[0][4] == [bytes([i % 251]) for i in range(n)]
-    assert res[1][3] is None
+    assert res[0][2] == expect and res[0][3] == [bytes([i % 251]) for i in range(n)]
+    assert res[1][2] is None
     # every frame was written exactly once, by its owner
     for i in range(n):
         assert os.path.getsize(os.path.join(tmp_path, "enc_%04d.tif" % i)) == expect[i]
         assert os.path.exists(os.path.join(tmp_path, "dec_%04d.png" % i))
+
+
+def _host_group_worker(rank, world):
+    from vcf_amd.comm import HostGroup
+    g = HostGroup()
+    got = g.all_gather_bytes(bytes([rank]) * (rank + 1))
+    mx = g.allreduce_max(rank * 1.5)
+    sm = g.allreduce_sum(rank + 1)
+    b = g.broadcast_bytes(b"root" if rank == 0 else None)
+    g.barrier()
+    g.close()
+    return got, mx, sm, b
+
+
+def test_host_group_collectives():
+    from _dist import run_ranks
+    res = run_ranks(_host_group_worker, 3)
+    for r in range(3):
+        got, mx, sm, b = res[r]
+        assert got == [b"\x00", b"\x01\x01", b"\x02\x02\x02"]
+        assert mx == 3.0 and sm == 6.0 and b == b"root"

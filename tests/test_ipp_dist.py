@@ -1,11 +1,10 @@
-"""IPP GOP sharding on the CPU: a world_size-2 gloo job encodes its GOPs and
+"""IPP GOP sharding on the CPU: a world_size-2 job (host group) encodes its GOPs and
 rank 0 gathers per-frame sizes and motion fields into the metadata; the
 result must equal the single-rank run's.  The GPU tools
 and the spatial codec are replaced by the oracle here -- they are covered by
 tests/test_ipp_gpu.py; this checks the driver around them."""
 import json
 import os
-import socket
 import types
 
 import numpy as np
@@ -35,38 +34,21 @@ def _codec(prefix, src, n, gop, group=None):
     return StandIn(args, group=group)
 
 
-def _worker(rank, world, port, tmp, n, gop, q):
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker(rank, world, tmp, n, gop):
     from vcf_amd.codec import shard
-    try:
-        g = shard.Group("gloo")
-        total = _codec(os.path.join(tmp, "dist", "v"), os.path.join(tmp, "frames.npy"), n, gop, g).encode()
-        q.put((rank, total))
-        g.close()
-    except Exception as e:
-        q.put((rank, "error", repr(e)))
+    g = shard.Group("host")
+    total = _codec(os.path.join(tmp, "dist", "v"), os.path.join(tmp, "frames.npy"), n, gop, g).encode()
+    g.close()
+    return total
 
 
-def test_ipp_two_ranks_gloo_equals_one_rank(tmp_path):
-    import torch.multiprocessing as mp
+def test_ipp_two_ranks_equals_one_rank(tmp_path):
+    from _dist import run_ranks
     n, gop, world = 9, 3, 2
     np.save(tmp_path / "frames.npy", _frames(n))
     single = _codec(str(tmp_path / "one" / "v"), str(tmp_path / "frames.npy"), n, gop).encode()
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), n, gop, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = dict((r[0], r) for r in (q.get(timeout=180) for _ in range(world)))
-    for p in procs:
-        p.join(timeout=60)
-    assert all(r[1] != "error" for r in res.values()), res
-    assert res[1][1] is None
+    res = run_ranks(_worker, world, str(tmp_path), n, gop)
+    assert res[1] is None
     m1 = json.load(open(tmp_path / "one" / "v_meta.json"))
     m2 = json.load(open(tmp_path / "dist" / "v_meta.json"))
     for k in ("n_frames", "gop_size", "I_info", "P_info", "width", "height"):
@@ -76,6 +58,6 @@ def test_ipp_two_ranks_gloo_equals_one_rank(tmp_path):
         assert np.array_equal(a["mv_f32"], b["mv_f32"]) and a["mv_f32"].shape == (6, 3, 4, 2)
     # single run's total includes its own mv.npz size; the P/I sums agree
     assert single - os.path.getsize(tmp_path / "one" / "v_mv.npz") * 8 == \
-        res[0][1] - os.path.getsize(tmp_path / "dist" / "v_mv.npz") * 8
+        res[0] - os.path.getsize(tmp_path / "dist" / "v_mv.npz") * 8
     for i in range(n):
         assert os.path.exists(tmp_path / "dist" / f"v_O_{i:04d}.png")

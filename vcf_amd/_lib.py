@@ -111,6 +111,13 @@ SIGNATURES = {
     "vcf_png_encode_bound": [_I32, _I32],
     "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],
     "vcf_deadzone_dequantize": [_P, _I32, _I64, _I32, _P, _P],
+    "vcf_comm_unique_id": [_P, _SZ],
+    "vcf_comm_init": [ctypes.POINTER(_P), _P, ctypes.c_int, ctypes.c_int],
+    "vcf_comm_destroy": [_P],
+    "vcf_comm_rank": [_P, _PI, _PI],
+    "vcf_comm_allgather_i64": [_P, _P, _I64, _P, _P],
+    "vcf_comm_allreduce_f64": [_P, _P, _P, _I64, ctypes.c_int, _P],
+    "vcf_comm_gatherv": [_P, _P, _I64, _P, _P, ctypes.c_int, _P],
 }
 
 _lib = None

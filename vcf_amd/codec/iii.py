@@ -80,11 +80,8 @@ class CoDec:
                  encode_prefix: str = ENCODE_OUTPUT_PREFIX, decode_prefix: str = DECODE_OUTPUT_PREFIX):
         self.args = args
         self.encoding = args.subparser_name == "encode"
+        # a multi-rank Group selects this rank's GPU (local rank) before any codec work
         self.group = group if group is not None else shard.Group()
-        if codec is None and self.group.world > 1:
-            from ..device import device_count, set_device
-            if device_count() > 0:
-                set_device(self.group.local)
         self.transform_codec = codec if codec is not None else transform_codec(args)
         self.batch = batch
         self.encode_prefix = encode_prefix

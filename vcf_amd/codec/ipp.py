@@ -204,11 +204,7 @@ class _IPP:
 
     def _gather(self, blob: bytes):
         """Rank 0: every rank's blob in rank order (item r belongs to rank r)."""
-        g = self.group
-        if g.dist is None:
-            return [blob]
-        sizes = g.all_gather_sizes(g.world, [len(blob)])
-        return g.gather_payloads(g.world, [blob], sizes)
+        return self.group.gather_blobs(blob)
 
     def decode(self):
         in_prefix = resolve_prefix(self.args.input)

@@ -1,28 +1,31 @@
-"""Frame sharding for the III driver.
+"""Frame sharding for the III / IPP drivers.
 
 Frames of a sequence are independent units (intra-only coding; every model
 and state resets per frame in encode_fn/decode_fn), so N frames split into P
 contiguous chunks, frame i on rank floor(i * P / N), with no collective on
 the data path.  The one exchange step is after coding: an all-gather of the
 per-frame code-stream sizes (int64) and, when the code-streams must end up
-on rank 0 (no shared filesystem), point-to-point sends of the variable-length
-payloads to rank 0 -- RCCL has no gatherv, and on xGMI each peer has its own
-link to rank 0, so P-1 concurrent sends are link-bound, not ring-bound.
+on rank 0 (no shared filesystem), a gather of the variable-length payloads
+to rank 0 -- RCCL has no gatherv, so libvcf_amd.so's `vcf_comm_gatherv`
+posts one send per peer and P-1 concurrent receives on the root: on xGMI
+each peer has its own link to rank 0, the step is link-bound, not
+ring-bound.  This replaces the point where the reference's sequential frame
+loop holds every coded frame in one process (src/III.py:77-115, :132-144).
 
-One process per GPU: RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR come from
-torch.distributed.run; backend "nccl" (= RCCL) when the ranks own GPUs,
-"gloo" otherwise (the CPU tests).
+One process per GPU: RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR /
+MASTER_PORT come from the launcher (torch.distributed.run's names; any
+launcher that sets them works).  Backends:
+- "rccl" (default when the ranks see a GPU): sizes and payloads over RCCL
+  through vcf_amd.rccl.Communicator;
+- "host": the TCP host group carries them (CPU tests only -- no GPU there).
+The host group (vcf_amd/comm.py) bootstraps RCCL and carries the barrier
+either way.  No PyTorch.
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 
-
-def env_world():
-    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
-            int(os.environ.get("LOCAL_RANK", "0")))
+from ..comm import HostGroup, env_world
 
 
 def frame_range(n_frames: int, rank: int, world: int):
@@ -36,80 +39,106 @@ def owner(i: int, n_frames: int, world: int) -> int:
     return i * world // n_frames
 
 
+def _gpu_count() -> int:
+    from ..device import device_count
+    try:
+        return device_count()
+    except Exception:      # no ROCm device in this process (CPU tests)
+        return 0
+
+
 class Group:
-    """A torch.distributed process group (or the trivial single-rank one)."""
+    """The ranks of a frame-sharded job (or the trivial single-rank one)."""
 
     def __init__(self, backend: str | None = None):
         self.rank, self.world, self.local = env_world()
-        self.dist = None
-        self.device = None
-        if self.world > 1:
-            import torch
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
-            if not dist.is_initialized():
-                dist.init_process_group(backend, rank=self.rank, world_size=self.world)
-            self.dist = dist
-            self.backend = backend
-            self.device = torch.device("cuda", self.local) if backend == "nccl" else torch.device("cpu")
-        else:
-            self.backend = None
+        self.host = None
+        self.comm = None
+        self.backend = None
+        if self.world <= 1:
+            return
+        ndev = _gpu_count() if backend in (None, "rccl") else 0
+        if backend is None:
+            backend = "rccl" if ndev > 0 else "host"
+        if backend not in ("rccl", "host"):
+            raise ValueError(f"backend {backend!r}: 'rccl' or 'host'")
+        self.host = HostGroup(self.rank, self.world)
+        self.backend = backend
+        if backend == "rccl":
+            if ndev <= 0:
+                raise RuntimeError("backend 'rccl' needs a GPU in every rank")
+            from ..device import set_device
+            from ..rccl import Communicator
+            set_device(self.local % ndev)
+            self.comm = Communicator(self.host)
 
-    def _t(self, a):
-        import torch
-        return torch.as_tensor(a).to(self.device)
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
 
     def all_gather_sizes(self, n_frames: int, local_sizes) -> np.ndarray:
         """Per-frame sizes (int64, length n_frames) on every rank."""
-        if self.dist is None:
-            return np.asarray(local_sizes, np.int64)
-        import torch
-        full = np.zeros(n_frames, np.int64)
+        mine = np.asarray(local_sizes, np.int64)
+        if not self.distributed:
+            return mine.copy()
         lo, hi = frame_range(n_frames, self.rank, self.world)
-        full[lo:hi] = np.asarray(local_sizes, np.int64)
-        t = self._t(full)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)   # disjoint chunks: sum == gather
-        return t.cpu().numpy().astype(np.int64)
+        if mine.size != hi - lo:
+            raise ValueError(f"rank {self.rank} owns frames {lo}..{hi} but reports {mine.size} sizes")
+        full = np.zeros(n_frames, np.int64)
+        full[lo:hi] = mine
+        if self.comm is not None:
+            rows = self.comm.all_gather_i64(full)
+        else:
+            rows = np.stack([np.frombuffer(b, np.int64) for b in self.host.all_gather_bytes(full.tobytes())])
+        out = np.zeros(n_frames, np.int64)
+        for r in range(self.world):                  # each rank fills only its own chunk
+            rlo, rhi = frame_range(n_frames, r, self.world)
+            out[rlo:rhi] = rows[r, rlo:rhi]
+        return out
 
     def gather_payloads(self, n_frames: int, local_payloads, sizes: np.ndarray):
         """Rank 0 receives every frame's code-stream bytes (list of bytes,
         frame order); other ranks return None.  `sizes` from all_gather_sizes."""
-        if self.dist is None:
-            return list(local_payloads)
-        import torch
+        if not self.distributed:
+            return [bytes(p) for p in local_payloads]
+        sizes = np.asarray(sizes, np.int64)
         lo, hi = frame_range(n_frames, self.rank, self.world)
-        if self.rank != 0:
-            if hi > lo:
-                buf = np.frombuffer(b"".join(local_payloads), np.uint8).copy()
-                self.dist.send(self._t(buf), dst=0)
-            return None
-        out = [None] * n_frames
-        for i in range(lo, hi):
-            out[i] = bytes(local_payloads[i - lo])
-        # post every peer's receive at once: each xGMI peer has its own link to
-        # rank 0, so the P-1 transfers run concurrently (link-bound, not serial)
-        pending = []
-        for r in range(1, self.world):
-            rlo, rhi = frame_range(n_frames, r, self.world)
-            if rhi <= rlo:
-                continue
-            t = torch.empty(int(sizes[rlo:rhi].sum()), dtype=torch.uint8, device=self.device)
-            pending.append((r, rlo, rhi, t, self.dist.irecv(t, src=r)))
-        for r, rlo, rhi, t, req in pending:
-            req.wait()
-            blob = t.cpu().numpy().tobytes()
-            off = 0
-            for i in range(rlo, rhi):
-                out[i] = blob[off:off + int(sizes[i])]
-                off += int(sizes[i])
+        blob = b"".join(bytes(p) for p in local_payloads)
+        if len(blob) != int(sizes[lo:hi].sum()):
+            raise ValueError("local payload bytes disagree with the gathered sizes")
+        if self.comm is not None:
+            counts = np.array([sizes[slice(*frame_range(n_frames, r, self.world))].sum()
+                               for r in range(self.world)], np.int64)
+            packed = self.comm.gatherv(blob, counts, root=0)
+            if self.rank != 0:
+                return None
+            packed = packed.tobytes()
+        else:
+            blobs = self.host.all_gather_bytes(blob if self.rank != 0 else b"")
+            if self.rank != 0:
+                return None
+            packed = blob + b"".join(blobs[1:])
+        out, off = [], 0
+        for i in range(n_frames):
+            out.append(packed[off:off + int(sizes[i])])
+            off += int(sizes[i])
         return out
 
+    def gather_blobs(self, blob: bytes):
+        """Rank 0: every rank's blob in rank order (item r belongs to rank r)."""
+        if not self.distributed:
+            return [bytes(blob)]
+        sizes = self.all_gather_sizes(self.world, [len(blob)])
+        return self.gather_payloads(self.world, [blob], sizes)
+
     def barrier(self):
-        if self.dist is not None:
-            self.dist.barrier()
+        if self.host is not None:
+            self.host.barrier()
 
     def close(self):
-        if self.dist is not None and self.dist.is_initialized():
-            self.dist.destroy_process_group()
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
+        if self.host is not None:
+            self.host.close()
+            self.host = None
