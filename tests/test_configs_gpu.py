@@ -6,7 +6,7 @@
   the indices, the .tif bytes and the decoded PNG's pixels equal the
   reference's.
 - C4's per-rank batch (256 1080p frames over 8 ranks = 32 per launch) and the
-  bench's 64 x 4K launch (1.59 GB in, offsets past 2^31 bytes): one launch
+  bench's 64 x 4K launch (1.59 GB in), and 96 x 4K (2.39 GB: frame offsets past 2^31 bytes): one launch
   each, frames first / middle / last against the oracle.
 - C5 (IPP_DCT 4K; IPP_DCT.py:344-395): one 4K frame pair of full search and
   three-step search (bs 16, S 8), compensation, residual and reconstruction
@@ -64,7 +64,8 @@ def _smooth(H, W, seed):
     return synth_frame(H, W, seed)
 
 
-@pytest.mark.parametrize("H,W,n", [(1080, 1920, 32), (2160, 3840, 64)], ids=["c4_32x1080p", "bench_64x4k"])
+@pytest.mark.parametrize("H,W,n", [(1080, 1920, 32), (2160, 3840, 64), (2160, 3840, 96)],
+                         ids=["c4_32x1080p", "bench_64x4k", "96x4k_past_2GiB"])
 def test_full_size_single_launch_vs_oracle(H, W, n):
     import vcf_amd.dct as D
     from vcf_amd.device import DeviceBuffer, Stream
@@ -82,7 +83,7 @@ def test_full_size_single_launch_vs_oracle(H, W, n):
     dst = DeviceBuffer(n * fb)
     D.encode_device(src, n, H, W, 32, 0, out=dst, stream=s)
     s.synchronize()
-    assert n * fb > (1 << 31) or H == 1080
+    assert n < 96 or n * fb > (1 << 31)      # 96 x 4K: frame offsets past 2^31 bytes
     for f, rgb in chosen.items():
         got = dst.download(np.empty((H, W, 3), np.uint8), offset=f * fb)
         assert np.array_equal(got, O.encode_frame(rgb, 32, 0)), f"frame {f}"
