@@ -37,6 +37,9 @@
  * construction, so results are bitwise equal to scipy (checked in
  * tests/test_oracle.py against tests/golden fixtures made by the reference's
  * own glue; see tests/golden/make_golden.py).
+  *
+ * Restates pocketfft (BSD-3-Clause, Copyright (C) 2010-2019 Max-Planck-Society);
+ * license text in THIRD_PARTY_NOTICES.md.
  */
 #include <math.h>
 #include <stdint.h>

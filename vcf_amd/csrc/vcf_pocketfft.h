@@ -18,6 +18,8 @@
 // live in VGPRs.  The twiddles (pocketfft's sincos_2pibyn values, computed in
 // double on the host, vcf_dct_any.hip) are read from a __constant__ table at
 // compile-time offsets, i.e. with scalar loads.  Build with -ffp-contract=off.
+// Restates pocketfft (BSD-3-Clause, Copyright (C) 2010-2019 Max-Planck-Society);
+// license text in THIRD_PARTY_NOTICES.md.
 #pragma once
 #include <hip/hip_runtime.h>
 

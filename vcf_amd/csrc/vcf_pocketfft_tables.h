@@ -3,6 +3,8 @@
 // exactly as pocketfft computes them) for every covered length, uploaded once
 // per device into __constant__ memory.  Each translation unit that includes
 // this gets its own copy of the tables (no relocatable device code).
+// Restates pocketfft (BSD-3-Clause, Copyright (C) 2010-2019 Max-Planck-Society);
+// license text in THIRD_PARTY_NOTICES.md.
 #pragma once
 #include <hip/hip_runtime.h>
 
