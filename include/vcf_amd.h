@@ -293,6 +293,32 @@ int vcf_cbaac_decode(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t or
  * symbol (3*n int32), for parity checks against the reference's model. */
 int vcf_cbaac_model_trace(const uint8_t *symbols, int64_t n, int32_t order, int32_t *triples);
 
+/* ---- tiled CBAAC on the GPU ------------------------------
+ * The flattened symbols split into consecutive segments of seg_len symbols
+ * (a multiple of 256); each segment is coded exactly as vcf_cbaac_encode
+ * codes it alone: CBAAC.CoDec._encode (CBAAC.py:114-131) with a fresh
+ * ContextManager (:49-69) and history per segment, one wave per segment.
+ * Orders 0 and 1 (VCF_ERR_UNSUPPORTED above).  Device pointers; the
+ * container (segment sizes + payload) is vcf_amd/tcbaac.py's. */
+int64_t vcf_cbaac_tiled_segments(int64_t n, int64_t seg_len);
+/* scratch bytes (ws_dev) for vcf_cbaac_tiled_encode / _trace */
+int64_t vcf_cbaac_tiled_workspace(int64_t n, int64_t seg_len);
+/* an out_capacity that always suffices */
+int64_t vcf_cbaac_tiled_bound(int64_t n, int64_t seg_len);
+/* Segments packed back to back into out_dev; seg_bytes_dev (segments + 1
+ * int64) receives each segment's byte count and, last, the total (> capacity
+ * means the output was cut: retry with vcf_cbaac_tiled_bound bytes). */
+int vcf_cbaac_tiled_encode(const uint8_t *sym_dev, int64_t n, int32_t order, int64_t seg_len, uint8_t *out_dev,
+                           int64_t out_capacity, int64_t *seg_bytes_dev, void *ws_dev, void *stream);
+/* The model alone: the (low, high, total) triple handed to the coder for
+ * every symbol (3*n int32), segment by segment (parity checks). */
+int vcf_cbaac_tiled_trace(const uint8_t *sym_dev, int64_t n, int32_t order, int64_t seg_len, int32_t *triples_dev,
+                          int64_t *seg_bytes_dev, void *ws_dev, void *stream);
+/* Inverse: segment s's bytes are in_dev[offs[s] .. offs[s+1]) (segments + 1
+ * int64 byte offsets, device); n symbols out. */
+int vcf_cbaac_tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
+                           int64_t seg_len, uint8_t *sym_dev, void *stream);
+
 /* ---- CBAHC entropy codec (CBAHC.py), host code --------------------------------- */
 
 /* Worst-case code-stream bytes for n symbols. */

@@ -75,5 +75,40 @@ def main():
     print(cases)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(__import__("sys").argv) == 1:
     main()
+
+
+# ---- tiled CBAAC (the GPU entropy stage) ----------------------------
+# The tiled variant splits the flattened symbol stream into consecutive
+# segments of seg_len symbols and runs CBAAC.CoDec._encode's model loop
+# (:114-131) on each segment from scratch: a fresh ContextManager, history
+# reset to `order` zeros.  These traces are the reference's own classes run
+# exactly that way, segment by segment.
+#
+#     python tests/golden/make_golden_cbaac.py tiled
+
+TILED_SEG = 24576   # a multiple of 256 (the GPU kernel's chunk); long enough for order-0 rescales
+
+
+def main_tiled():
+    _, ContextManager = load_classes()
+    arrays, cases = {}, []
+    s = streams()
+    for name in ("laplace", "skewed"):
+        sym = s[name]
+        arrays[f"sym_{name}"] = sym
+        for order in (0, 1):
+            parts = [trace(sym[i:i + TILED_SEG], order, ContextManager) for i in range(0, len(sym), TILED_SEG)]
+            arrays[f"trace_{name}_o{order}"] = np.concatenate(parts).astype(np.int32)
+            cases.append(dict(stream=name, order=order, n=int(len(sym)), seg_len=TILED_SEG, segments=len(parts)))
+    np.savez_compressed(os.path.join(HERE, "cbaac_tiled.npz"), **arrays)
+    json.dump(dict(generator="tests/golden/make_golden_cbaac.py tiled",
+                   reference="Sistemas-Multimedia/VCF src/CBAAC.py AdaptiveModel/ContextManager (AST-extracted, "
+                             "executed unmodified), one fresh ContextManager per segment",
+                   cases=cases), open(os.path.join(HERE, "manifest_cbaac_tiled.json"), "w"), indent=1)
+    print(cases)
+
+
+if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "tiled":
+    main_tiled()

@@ -1,0 +1,108 @@
+"""Tiled CBAAC on the GPU (vcf_amd/csrc/vcf_cbaac_gpu.hip through the C ABI).
+
+- The model, segment by segment, equals the reference's own AdaptiveModel /
+  ContextManager run on each segment from scratch (traces made by executing
+  the reference's classes: tests/golden/make_golden_cbaac.py tiled).
+- Every segment's bytes equal the host serial coder's (vcf_cbaac_encode) on
+  that segment alone; the GPU decoder inverts both exactly.
+- Edge cases: empty, 1 symbol, partial last chunk / segment, runs, uniform
+  noise (no compression), orders 0 and 1, long segments with rescales.
+- The DCT CoDec with `-c TCBAAC`: the indices never leave HBM; the decoded
+  frame equals the oracle's.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from vcf_amd import tcbaac as T
+
+pytestmark = pytest.mark.gpu
+
+_MAN = json.load(open(os.path.join(GOLDEN, "manifest_cbaac_tiled.json")))
+
+
+@pytest.mark.parametrize("case", _MAN["cases"], ids=lambda c: f"{c['stream']}_o{c['order']}")
+def test_segment_traces_equal_reference_classes(case):
+    d = np.load(os.path.join(GOLDEN, "cbaac_tiled.npz"))
+    sym = d[f"sym_{case['stream']}"]
+    ref = d[f"trace_{case['stream']}_o{case['order']}"]
+    got = T.TiledCoder(case["order"], case["seg_len"]).trace(sym)
+    bad = np.nonzero(np.any(got != ref, axis=1))[0]
+    assert bad.size == 0, (bad[:5], got[bad[:3]], ref[bad[:3]])
+
+
+def _streams():
+    rng = np.random.Generator(np.random.PCG64(5))
+    lap = np.clip(np.rint(rng.laplace(128, 2.5, 300_001)), 0, 255).astype(np.uint8)
+    skew = np.where(rng.random(70_000) < 0.985, 128, rng.integers(0, 256, 70_000)).astype(np.uint8)
+    return {
+        "laplace": lap,
+        "skewed": skew,
+        "uniform": rng.integers(0, 256, 40_000, dtype=np.uint8),
+        "runs": np.repeat(rng.integers(0, 256, 300, dtype=np.uint8), 97),
+        "const255": np.full(5000, 255, np.uint8),
+        "one": np.array([17], np.uint8),
+        "tiny": rng.integers(0, 256, 255, dtype=np.uint8),
+        "empty": np.zeros(0, np.uint8),
+    }
+
+
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("seg_len", [256, 4096, 1 << 17])
+def test_segments_equal_host_coder_and_round_trip(order, seg_len):
+    coder = T.TiledCoder(order, seg_len)
+    for name, sym in _streams().items():
+        if seg_len == 256 and sym.size > 50_000:
+            sym = sym[:50_000 + 77]
+        sizes, payload = coder.encode(sym)
+        host = T.host_segments(sym, order, seg_len)
+        assert list(sizes) == [len(h) for h in host], name
+        assert payload == b"".join(host), name
+        assert np.array_equal(coder.decode(payload, sizes, sym.size), sym), name
+
+
+def test_decode_with_one_fresh_coder_per_call():
+    sym = _streams()["laplace"]
+    sizes, payload = T.TiledCoder(0, 8192).encode(sym)
+    assert np.array_equal(T.TiledCoder(0, 8192).decode(payload, sizes, sym.size), sym)
+
+
+def test_codec_container_and_errors():
+    rng = np.random.Generator(np.random.PCG64(2))
+    img = np.clip(np.rint(rng.laplace(128, 3, (96, 130, 3))), 0, 255).astype(np.uint8)
+    c = T.TiledCBAACCodec(order=1, seg_len=4096)
+    b = c.compress(img)
+    assert c.file_extension == ".tadpt_arith"
+    assert np.array_equal(c.decompress(b.getvalue()), img)
+    assert np.array_equal(T.TiledCBAACCodec().decompress(b.getvalue()), img)   # order/seg_len from the header
+    with pytest.raises(NotImplementedError):
+        T.TiledCoder(2, 4096).encode(img.ravel())
+    with pytest.raises(ValueError):
+        T.TiledCoder(0, 1000).encode(img.ravel())                              # not a multiple of 256
+
+
+def test_dct_codec_with_tcbaac_frame(tmp_path):
+    from PIL import Image
+
+    from bench import synth_frame
+    from oracle import oracle as O
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec.dct2d import CoDec
+    rgb = synth_frame(1080, 1920, 3)
+    src = str(tmp_path / "f.png")
+    Image.fromarray(rgb).save(src)
+    enc = CoDec(P.parse(P.dct_parser(), ["encode", "-c", "TCBAAC"]))
+    nbytes = enc.encode_fn(src, str(tmp_path / "enc"))
+    data = open(str(tmp_path / "enc.tadpt_arith"), "rb").read()
+    assert nbytes == len(data)
+    k = O.encode_frame(rgb, 32, 0)
+    shape, order, seg_len, sizes, payload = T.unpack(data)
+    assert shape == k.shape and order == 0 and seg_len == T.DEFAULT_SEG
+    assert payload == b"".join(T.host_segments(k, 0, seg_len))
+    dec = CoDec(P.parse(P.dct_parser(), ["decode", "-c", "TCBAAC"]))
+    dec.decode_fn(str(tmp_path / "enc"), str(tmp_path / "out.png"))
+    out = np.asarray(Image.open(str(tmp_path / "out.png")))
+    assert np.array_equal(out, O.decode_frame(k, 1080, 1920, 32, 0))

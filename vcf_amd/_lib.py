@@ -111,6 +111,12 @@ SIGNATURES = {
     "vcf_png_encode_bound": [_I32, _I32],
     "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],
     "vcf_deadzone_dequantize": [_P, _I32, _I64, _I32, _P, _P],
+    "vcf_cbaac_tiled_segments": [_I64, _I64],
+    "vcf_cbaac_tiled_workspace": [_I64, _I64],
+    "vcf_cbaac_tiled_bound": [_I64, _I64],
+    "vcf_cbaac_tiled_encode": [_P, _I64, _I32, _I64, _P, _I64, _P, _P, _P],
+    "vcf_cbaac_tiled_trace": [_P, _I64, _I32, _I64, _P, _P, _P, _P],
+    "vcf_cbaac_tiled_decode": [_P, _P, _I64, _I32, _I64, _P, _P],
     "vcf_comm_unique_id": [_P, _SZ],
     "vcf_comm_init": [ctypes.POINTER(_P), _P, ctypes.c_int, ctypes.c_int],
     "vcf_comm_destroy": [_P],
@@ -150,6 +156,8 @@ def lib():
             L.vcf_cbaac_bound.restype = ctypes.c_int64
             L.vcf_cbahc_bound.restype = ctypes.c_int64
             L.vcf_png_encode_bound.restype = ctypes.c_int64
+            for name in ("vcf_cbaac_tiled_segments", "vcf_cbaac_tiled_workspace", "vcf_cbaac_tiled_bound"):
+                getattr(L, name).restype = ctypes.c_int64
             _lib = L
     return _lib
 

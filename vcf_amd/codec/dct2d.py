@@ -40,7 +40,14 @@ def _cbahc(args=None):
     return CBAHCCodec(getattr(args, "order", 0) if args is not None else 0)
 
 
-ENTROPY_CODECS = {"TIFF": TIFFCodec, "CBAAC": _cbaac, "CBAHC": _cbahc}
+def _tcbaac(args=None):
+    from ..tcbaac import DEFAULT_SEG, TiledCBAACCodec
+    return TiledCBAACCodec(getattr(args, "order", 0) if args is not None else 0,
+                           getattr(args, "segment_symbols", DEFAULT_SEG) if args is not None else DEFAULT_SEG)
+
+
+# TCBAAC: CBAAC in independent segments on the GPU (vcf_amd/tcbaac.py, a new container)
+ENTROPY_CODECS = {"TIFF": TIFFCodec, "CBAAC": _cbaac, "CBAHC": _cbahc, "TCBAAC": _tcbaac}
 
 
 def register_entropy_codec(name, cls):
@@ -78,7 +85,7 @@ class CoDec(EICCoDec):
         if ec_name not in ENTROPY_CODECS:
             raise NotImplementedError(f"entropy codec {ec_name!r} (have: {sorted(ENTROPY_CODECS)})")
         maker = ENTROPY_CODECS[ec_name]
-        self.entropy = maker(args) if maker in (_cbaac, _cbahc) else maker()
+        self.entropy = maker(args) if maker in (_cbaac, _cbahc, _tcbaac) else maker()
         self.file_extension = self.entropy.file_extension
         self.QSS = int(getattr(args, "QSS", 32))
         self.offset = 128            # 2D-DCT.py:102-105 (quantizer == deadzone)
@@ -189,10 +196,28 @@ class CoDec(EICCoDec):
 
     def encode_fn(self, in_fn, out_fn):
         img = self.encode_read_fn(in_fn)
-        k = self.encode_indices(img)
+        if hasattr(self.entropy, "compress_device"):
+            cs = self._encode_compress_device(img)
+        else:
+            cs = self.compress(self.encode_indices(img))
         with open(f"{out_fn}_shape.bin", "wb") as f:
             f.write(struct.pack("iii", *self.original_shape))
-        return self.encode_write_fn(self.compress(k), out_fn)
+        return self.encode_write_fn(cs, out_fn)
+
+    def _encode_compress_device(self, img):
+        """GPU-resident entropy stage: the indices stay in HBM between the
+        encode kernel and the coder (TCBAAC); only the code-stream comes back."""
+        from ..device import DeviceBuffer
+        self._check_frame(img)
+        self.original_shape = img.shape
+        H, W = img.shape[:2]
+        Hp, Wp = D.padded_shape(H, W, self.block_size)
+        coder = self.entropy.coder
+        src = DeviceBuffer.from_array(img, coder.stream)
+        k = DeviceBuffer(Hp * Wp * 3)
+        D.encode_device(src, 1, H, W, self.QSS, self.flags, out=k, stream=coder.stream,
+                        block_size=self.block_size)
+        return self.entropy.compress_device(k, (Hp, Wp, 3))
 
     def encode(self, in_fn="/tmp/original.png", out_fn="/tmp/encoded"):
         # 2D-DCT.py:374-375: the reference's encode() ignores -o/-e
