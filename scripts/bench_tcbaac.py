@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Tiled CBAAC (§8(f) row 2) measurements on one GPU; one JSON line per case.
+
+- rate: bits of the tiled stream vs the serial stream (vcf_cbaac_encode over
+  the whole frame, the reference's CBAAC.py layout) for several segment
+  lengths, on the indices of S-smooth 1080p / 4K frames (DCT B=8, Q=32);
+- GPU time per frame (HIP events around the encode / decode launches, data
+  resident in HBM) and the host serial coder's time for the same frame;
+- C2 end to end: encode_fn of a 1080p PNG with -c TCBAAC (PNG read, DCT +
+  tiled CBAAC on the GPU, file write) vs -c CBAAC (host coder), wall clock.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def frame_indices(H, W, seed=0, Q=32):
+    from bench import synth_frame
+    import vcf_amd.dct as D
+    return D.encode(synth_frame(H, W, seed), Q)
+
+
+def time_gpu(fn, stream, reps):
+    from vcf_amd.device import Event
+    fn()
+    stream.synchronize()
+    e0, e1 = Event(), Event()
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    stream.synchronize()
+    return e0.elapsed_ms(e1) / reps
+
+
+def case(H, W, order, seg_len, reps=5):
+    from vcf_amd import _lib as L
+    from vcf_amd import cbaac, tcbaac
+    from vcf_amd.device import DeviceBuffer
+    k = frame_indices(H, W)
+    n = k.size
+    coder = tcbaac.TiledCoder(order, seg_len)
+    sizes, payload = coder.encode(k)
+    # kernel timing: encode (code + scan + pack) with the symbols in HBM
+    lib = L.lib()
+    sym = DeviceBuffer.from_array(k.ravel(), coder.stream)
+    ws = DeviceBuffer(int(lib.vcf_cbaac_tiled_workspace(n, seg_len)))
+    cap = int(lib.vcf_cbaac_tiled_bound(n, seg_len))
+    out = DeviceBuffer(cap)
+    sb = DeviceBuffer(8 * (len(sizes) + 1))
+    enc_ms = time_gpu(lambda: L.call("vcf_cbaac_tiled_encode", sym.ptr, n, order, seg_len, out.ptr, cap, sb.ptr,
+                                     ws.ptr, coder.stream.handle), coder.stream, reps)
+    dec_out = DeviceBuffer(n)
+    coder.decode_to_device(payload, sizes, n, dec_out)
+    offs = DeviceBuffer.from_array(np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64), coder.stream)
+    src = DeviceBuffer.from_array(np.frombuffer(payload, np.uint8), coder.stream)
+    dec_ms = time_gpu(lambda: L.call("vcf_cbaac_tiled_decode", src.ptr, offs.ptr, n, order, seg_len, dec_out.ptr,
+                                     coder.stream.handle), coder.stream, reps)
+    back = np.empty(n, np.uint8)
+    dec_out.download(back)
+    t0 = time.perf_counter()
+    serial = cbaac.encode_symbols(k, order)
+    host_ms = (time.perf_counter() - t0) * 1e3
+    return dict(case="tcbaac", frame=[H, W, 3], order=order, seg_len=seg_len, segments=len(sizes), symbols=n,
+                serial_bytes=len(serial), tiled_bytes=len(payload),
+                rate_overhead=round(len(payload) / len(serial) - 1, 4),
+                bits_per_symbol=round(8 * len(payload) / n, 4),
+                gpu_encode_ms=round(enc_ms, 3), gpu_decode_ms=round(dec_ms, 3),
+                gpu_encode_Msym_s=round(n / enc_ms / 1e3, 1), gpu_decode_Msym_s=round(n / dec_ms / 1e3, 1),
+                host_serial_ms=round(host_ms, 2), round_trip=bool(np.array_equal(back, k.ravel())))
+
+
+def c2_end_to_end(reps=5):
+    from PIL import Image
+
+    from bench import synth_frame
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec.dct2d import CoDec
+    rows = []
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "f.png")
+        Image.fromarray(synth_frame(1080, 1920, 0)).save(src)
+        for ec in ("TCBAAC", "CBAAC"):
+            c = CoDec(P.parse(P.dct_parser(), ["encode", "-c", ec]))
+            c.encode_fn(src, os.path.join(d, "e"))        # warm (allocations, first launch)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                nbytes = c.encode_fn(src, os.path.join(d, "e"))
+            ms = (time.perf_counter() - t0) / reps * 1e3
+            rows.append(dict(case="c2_encode_fn", entropy=ec, frame=[1080, 1920, 3], ms_per_frame=round(ms, 2),
+                             Mpix_s=round(1080 * 1920 / ms / 1e3, 1), bytes=nbytes))
+    return rows
+
+
+def main():
+    from vcf_amd.device import set_device
+    set_device(0)
+    for H, W in ((1080, 1920), (2160, 3840)):
+        for order in (0, 1):
+            for seg in (1 << 15, 1 << 16, 1 << 17, 1 << 18):
+                print(json.dumps(case(H, W, order, seg)), flush=True)
+    for r in c2_end_to_end():
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

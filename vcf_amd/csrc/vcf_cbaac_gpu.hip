@@ -20,15 +20,15 @@
 //     C[t] for t > s in every lane (4 compares, no cross-lane work); the
 //     rescale (every ~16 k symbols: stale total >= 16384, f = (f >> 1) + 1)
 //     rebuilds C with one wave prefix scan.  The decoder's
-//     get_symbol_from_scaled_value (:43-47) is one ballot of C[4l] <= v plus
-//     four readlanes.
+//     get_symbol_from_scaled_value (:43-47) becomes one ballot over the
+//     lanes' interval ends (see the decode kernel).
 //   - Order 1: the 256 context models (one per previous symbol) as 16-bit
 //     cumulative tables in LDS (128 KiB + totals), the current context's row
 //     read into the same four VGPRs per lane and written back after the
 //     update.
 //   - The coder state (low, high, pending bits, the bit writer) is
-//     wave-uniform; floor(range * c / total) is one float64 division plus an
-//     exact correction (operands < 2^47).  Bits are packed MSB-first into
+//     wave-uniform; floor(range * c / total) is a float64 multiply by an
+//     estimated 1/total plus an exact correction (operands < 2^47).  Bits are packed MSB-first into
 //     words that lane 0 stores (vector stores); symbols stream in 256 at a
 //     time (one dword per lane, the next chunk prefetched).
 // A second pass packs the segments back to back (a scan of their sizes and a
@@ -42,7 +42,7 @@ namespace vcf {
 namespace {
 
 constexpr uint32_t kMaxFreq = 16384;   // AdaptiveModel(max_freq=16384), CBAAC.py:18
-constexpr uint32_t kHalf = 0x80000000u, kQ1 = 0x40000000u, kQ3 = 0xC0000000u;
+constexpr uint32_t kQ1 = 0x40000000u;
 constexpr int kChunk = 256;            // symbols (or bytes) per wave load: one dword per lane
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
@@ -50,38 +50,44 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
 
-// floor(a / b) for a < 2^53, 0 < b < 2^33: the correctly rounded float64
-// quotient is floor(a/b) or floor(a/b) + 1 (a and b are exact doubles and
-// RN is monotonic), one multiply-compare picks the right one.
-__device__ __forceinline__ uint64_t udiv(uint64_t a, uint64_t b)
-{
-    uint64_t q = (uint64_t)((double)a / (double)b);
-    if (q * b > a) --q;
-    return q;
-}
-
-// lane l holds C[4l + j], j = 0..3; total = C[256] (uniform)
+// ---- the model --------------------------------------------------------------------
+// Lane l holds C[4l..4l+3] (C[s] = sum of freqs[0..s)) as packed u16 pairs:
+// p0 = C[4l] | C[4l+1] << 16, p1 = C[4l+2] | C[4l+3] << 16 (every count
+// <= 16385).  total = C[256] is wave-uniform.
 struct Model {
-    uint32_t c[4];
+    uint32_t p0, p1;
     uint32_t total;
 };
 
-__device__ __forceinline__ uint32_t pick(const Model &m, uint32_t j)
-{
-    return j == 0 ? m.c[0] : j == 1 ? m.c[1] : j == 2 ? m.c[2] : m.c[3];
-}
-
 __device__ __forceinline__ void model_reset(Model &m, uint32_t lane)
 {
-    for (int j = 0; j < 4; ++j) m.c[j] = 4 * lane + j;   // all frequencies 1
+    m.p0 = (4 * lane) | ((4 * lane + 1) << 16);   // all frequencies 1
+    m.p1 = (4 * lane + 2) | ((4 * lane + 3) << 16);
     m.total = 256;
+}
+
+// C[4L..4L+4] of lane L as one 64-bit word + C[4L+4]
+struct Quad {
+    uint64_t w;
+    uint32_t next;
+};
+
+__device__ __forceinline__ Quad model_quad(const Model &m, uint32_t L)
+{
+    Quad q;
+    q.w = (uint64_t)rl(m.p0, L) | ((uint64_t)rl(m.p1, L) << 32);
+    const uint32_t nx = rl(m.p0, (L + 1) & 63) & 0xFFFFu;
+    q.next = L == 63 ? m.total : nx;
+    return q;
 }
 
 // (cum[s], cum[s+1]) of get_range (CBAAC.py:40-41)
 __device__ __forceinline__ void model_range(const Model &m, uint32_t s, uint32_t &lo, uint32_t &hi)
 {
-    lo = rl(pick(m, s & 3), s >> 2);
-    hi = s == 255 ? m.total : rl(pick(m, (s + 1) & 3), (s + 1) >> 2);
+    const Quad q = model_quad(m, s >> 2);
+    const uint32_t j = s & 3;
+    lo = (uint32_t)(q.w >> (16 * j)) & 0xFFFFu;
+    hi = j == 3 ? q.next : (uint32_t)(q.w >> (16 * j + 16)) & 0xFFFFu;
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane)
@@ -94,51 +100,37 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane)
     return incl - v;
 }
 
-// update(s) (CBAAC.py:32-36): freqs[s] += 1; if the total *before* the
-// increment is >= max_freq, every frequency becomes (f >> 1) + 1.
+// update(s) (CBAAC.py:32-36): freqs[s] += 1, i.e. C[t] += 1 for t > s; if the
+// total *before* the increment is >= max_freq, every frequency becomes
+// (f >> 1) + 1 and C is rebuilt.
 __device__ __forceinline__ void model_update(Model &m, uint32_t s, uint32_t lane)
 {
+    const uint32_t L = s >> 2, j = s & 3;
+    // increments of lane L's two words: entries 4L+j+1 .. 4L+3
+    const uint32_t i0 = j == 0 ? 0x10000u : 0u;
+    const uint32_t i1 = j <= 1 ? 0x10001u : (j == 2 ? 0x10000u : 0u);
+    m.p0 += lane > L ? 0x10001u : (lane == L ? i0 : 0u);
+    m.p1 += lane > L ? 0x10001u : (lane == L ? i1 : 0u);
     const uint32_t stale = m.total;
-    for (int j = 0; j < 4; ++j) m.c[j] += (4 * lane + j > s) ? 1u : 0u;
     m.total = stale + 1;
     if (stale >= kMaxFreq) {
-        const uint32_t nxt0 = __shfl_down(m.c[0], 1, 64);
+        const uint32_t c0 = m.p0 & 0xFFFFu, c1 = m.p0 >> 16, c2 = m.p1 & 0xFFFFu, c3 = m.p1 >> 16;
+        const uint32_t nxt0 = __shfl_down(c0, 1, 64);
         const uint32_t end = lane == 63 ? m.total : nxt0;
-        uint32_t f[4] = {m.c[1] - m.c[0], m.c[2] - m.c[1], m.c[3] - m.c[2], end - m.c[3]};
-        uint32_t sum = 0;
-        for (int j = 0; j < 4; ++j) {
-            f[j] = (f[j] >> 1) + 1;
-            sum += f[j];
-        }
+        const uint32_t f0 = ((c1 - c0) >> 1) + 1, f1 = ((c2 - c1) >> 1) + 1, f2 = ((c3 - c2) >> 1) + 1,
+                       f3 = ((end - c3) >> 1) + 1;
+        const uint32_t sum = f0 + f1 + f2 + f3;
         const uint32_t ex = wave_excl_scan(sum, lane);
-        m.c[0] = ex;
-        m.c[1] = ex + f[0];
-        m.c[2] = m.c[1] + f[1];
-        m.c[3] = m.c[2] + f[2];
+        m.p0 = ex | ((ex + f0) << 16);
+        m.p1 = (ex + f0 + f1) | ((ex + f0 + f1 + f2) << 16);
         m.total = rl(ex + sum, 63);
     }
 }
 
-// get_symbol_from_scaled_value (CBAAC.py:43-47): the s with C[s] <= v < C[s+1]
-__device__ __forceinline__ uint32_t model_find(const Model &m, uint32_t v, uint32_t &lo, uint32_t &hi)
-{
-    const uint64_t mask = __ballot(m.c[0] <= v);   // a prefix of the lanes (C is increasing)
-    const uint32_t L = (uint32_t)__popcll(mask) - 1;
-    const uint32_t a0 = rl(m.c[0], L), a1 = rl(m.c[1], L), a2 = rl(m.c[2], L), a3 = rl(m.c[3], L);
-    const uint32_t a4 = L == 63 ? m.total : rl(m.c[0], L + 1);
-    if (v < a1) { lo = a0; hi = a1; return 4 * L; }
-    if (v < a2) { lo = a1; hi = a2; return 4 * L + 1; }
-    if (v < a3) { lo = a2; hi = a3; return 4 * L + 2; }
-    lo = a3;
-    hi = a4;
-    return 4 * L + 3;
-}
-
-// order-1 context tables: 256 models x 256 cumulative counts (u16: every
-// count <= 16385) + 256 totals, in LDS
+// order-1 context tables: 256 models x 256 cumulative counts (u16) + totals, in LDS
 struct Tables {
-    uint16_t c[256 * 256];
-    uint16_t total[256];
+    uint2 c[256 * 64];     // row ctx: lane l's (p0, p1)
+    uint32_t total[256];
 };
 
 // the order-1 kernels' LDS (a function-scope __shared__ variable is
@@ -158,69 +150,126 @@ struct Lds<1> {
 
 __device__ __forceinline__ void tables_reset(Tables &t, uint32_t lane)
 {
-    for (uint32_t r = 0; r < 256; ++r) {
-        uint2 v;
-        v.x = (4 * lane) | ((4 * lane + 1) << 16);
-        v.y = (4 * lane + 2) | ((4 * lane + 3) << 16);
-        *reinterpret_cast<uint2 *>(&t.c[r * 256 + 4 * lane]) = v;
-    }
+    Model m;
+    model_reset(m, lane);
+    for (uint32_t r = 0; r < 256; ++r) t.c[r * 64 + lane] = make_uint2(m.p0, m.p1);
     for (uint32_t r = lane; r < 256; r += 64) t.total[r] = 256;
     __syncthreads();
 }
 
 __device__ __forceinline__ void tables_read(const Tables &t, uint32_t ctx, uint32_t lane, Model &m)
 {
-    const uint2 v = *reinterpret_cast<const uint2 *>(&t.c[ctx * 256 + 4 * lane]);
-    m.c[0] = v.x & 0xFFFFu;
-    m.c[1] = v.x >> 16;
-    m.c[2] = v.y & 0xFFFFu;
-    m.c[3] = v.y >> 16;
+    const uint2 v = t.c[ctx * 64 + lane];
+    m.p0 = v.x;
+    m.p1 = v.y;
     m.total = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.total[ctx]);
 }
 
 __device__ __forceinline__ void tables_write(Tables &t, uint32_t ctx, uint32_t lane, const Model &m)
 {
-    uint2 v;
-    v.x = m.c[0] | (m.c[1] << 16);
-    v.y = m.c[2] | (m.c[3] << 16);
-    *reinterpret_cast<uint2 *>(&t.c[ctx * 256 + 4 * lane]) = v;
-    if (lane == 0) t.total[ctx] = (uint16_t)m.total;
+    t.c[ctx * 64 + lane] = make_uint2(m.p0, m.p1);
+    if (lane == 0) t.total[ctx] = m.total;
 }
 
-// MSB-first bit writer (bitarray endian='big'); lane 0 stores whole words
+// ---- the A8 coder's arithmetic ---------------------------------------------------------
+// floor(a / t) for integers a < 2^47, 0 < t <= 2^19 held exactly in doubles,
+// given inv ~= 1/t (relative error < 2^-50): q = trunc(a * inv) is within 1
+// of the floor, r = a - q t is exact (an fma of integers < 2^47) and lies in
+// (-t, 2t), and floor(r * inv + 2^-20) is the step (-1, 0 or +1) that fixes
+// q: r / t = m + j/t with j in 0..t-1, and 2^-20 is below 1/t
+// (t <= 2^19) and above the error of r * inv.
+__device__ __forceinline__ double floordiv(double a, double t, double inv)
+{
+    const double q = __builtin_trunc(a * inv);
+    const double r = __builtin_fma(-q, t, a);
+    return q + __builtin_floor(__builtin_fma(r, inv, 0x1p-20));
+}
+
+// 1/t for 1 <= t < 2^33: the hardware estimate and two Newton steps
+// (relative error far below the 2^-50 floordiv needs).
+__device__ __forceinline__ double rcp_nr(double t)
+{
+    double x = __builtin_amdgcn_rcp(t);
+    x = __builtin_fma(x, __builtin_fma(-t, x, 1.0), x);
+    x = __builtin_fma(x, __builtin_fma(-t, x, 1.0), x);
+    return x;
+}
+
+// MSB-first bit writer (bitarray endian='big'); lane 0 stores whole words.
+// acc holds nb < 32 pending bits at its top.
 struct BitWriter {
     uint32_t *out;
-    uint32_t acc = 0, nb = 0;
+    uint64_t acc = 0;
+    uint32_t nb = 0;
     uint64_t words = 0;
 
-    __device__ __forceinline__ void flush_word(uint32_t lane)
+    // append the top k bits of v (1 <= k <= 32)
+    __device__ __forceinline__ void bits(uint32_t v, uint32_t k, uint32_t lane)
     {
-        if (lane == 0) out[words] = __builtin_bswap32(acc);
-        ++words;
-        acc = 0;
-        nb = 0;
-    }
-    __device__ __forceinline__ void put(uint32_t bit, uint32_t lane)
-    {
-        acc |= bit << (31 - nb);
-        if (++nb == 32) flush_word(lane);
+        if (k < 32) v &= ~(0xFFFFFFFFu >> k);
+        acc |= (uint64_t)v << (32 - nb);
+        nb += k;
+        if (nb >= 32) {
+            if (lane == 0) out[words] = __builtin_bswap32((uint32_t)(acc >> 32));
+            ++words;
+            acc <<= 32;
+            nb -= 32;
+        }
     }
     __device__ __forceinline__ void run(uint32_t bit, uint64_t count, uint32_t lane)
     {
-        while (count) {
-            const uint32_t room = 32 - nb;
-            const uint32_t take = count < room ? (uint32_t)count : room;
-            if (bit) acc |= (take == 32 ? 0xFFFFFFFFu : ((1u << take) - 1u)) << (room - take);
-            nb += take;
-            count -= take;
-            if (nb == 32) flush_word(lane);
-        }
+        const uint32_t v = bit ? 0xFFFFFFFFu : 0u;
+        for (; count >= 32; count -= 32) bits(v, 32, lane);
+        if (count) bits(v, (uint32_t)count, lane);
     }
     __device__ __forceinline__ uint64_t finish(uint32_t lane)
     {
-        const uint64_t bits = words * 32 + nb;
-        if (nb && lane == 0) out[words] = __builtin_bswap32(acc);
-        return bits;
+        if (nb && lane == 0) out[words] = __builtin_bswap32((uint32_t)(acc >> 32));
+        return words * 32 + nb;
+    }
+};
+
+// Encoder state: the interval and the pending (underflow) bits.
+struct Encoder {
+    uint32_t low = 0, high = 0xFFFFFFFFu;
+    uint64_t pending = 0;
+
+    // interval update + renormalisation of the A8 coder (vcf_cbaac.cpp's loop,
+    // done in one step: the loop emits the common leading bits of low and
+    // high, each followed by the pending bits after the first, then counts
+    // the underflow steps while low = 01.. and high = 10..)
+    __device__ __forceinline__ void code(uint32_t lo, uint32_t hi, double tot, double inv, BitWriter &w,
+                                         uint32_t lane)
+    {
+        const double rng = (double)(high - low) + 1.0;
+        const double qh = floordiv(rng * (double)hi, tot, inv);
+        const double ql = floordiv(rng * (double)lo, tot, inv);
+        high = low + (uint32_t)(qh - 1.0);
+        low = low + (uint32_t)ql;
+        const uint32_t d = __builtin_clz(low ^ high);   // high > low: d <= 31
+        if (d) {
+            const uint32_t b = low >> 31;
+            w.bits(low, 1, lane);
+            w.run(b ^ 1u, pending, lane);
+            pending = 0;
+            if (d > 1) w.bits(low << 1, d - 1, lane);
+            low <<= d;
+            high = (high << d) | ((1u << d) - 1u);
+        }
+        const uint32_t x = (low << 1) & ~(high << 1);
+        const uint32_t p = __builtin_clz(~x);
+        if (p) {
+            pending += p;
+            low = (low << p) & 0x7FFFFFFFu;
+            high = (high << p) | ((1u << p) - 1u) | 0x80000000u;
+        }
+    }
+    // flush (CBAAC.py:130 -> A8): one more pending bit and a disambiguating bit
+    __device__ __forceinline__ void flush(BitWriter &w, uint32_t lane)
+    {
+        const uint32_t b = low < kQ1 ? 0u : 1u;
+        w.bits(b << 31, 1, lane);
+        w.run(b ^ 1u, pending + 1, lane);
     }
 };
 
@@ -233,6 +282,8 @@ __device__ __forceinline__ uint32_t load_sym4(const uint8_t *p, int64_t off, int
         if (i + j < len) v |= (uint32_t)p[i + j] << (8 * j);
     return v;
 }
+
+__device__ __forceinline__ double rcp_exact(uint32_t t) { return rcp_nr((double)t); }
 
 template <int ORDER, bool TRACE>
 __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *__restrict__ sym, int64_t n,
@@ -254,8 +305,7 @@ __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *_
 
     BitWriter w;
     w.out = slots + seg * slot_words;
-    uint32_t low = 0, high = 0xFFFFFFFFu;
-    uint64_t pending = 0;
+    Encoder e;
 
     uint32_t cur = load_sym4(src, 0, len, lane);
     for (int64_t off = 0; off < len; off += kChunk) {
@@ -264,9 +314,10 @@ __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *_
         for (int k = 0; k < cnt; ++k) {
             const uint32_t s = (rl(cur, k >> 2) >> (8 * (k & 3))) & 255u;
             if constexpr (ORDER == 1) tables_read(tabs[0], ctx, lane, m);
+            const uint32_t tot = m.total;
+            const double inv = rcp_exact(tot);
             uint32_t lo, hi;
             model_range(m, s, lo, hi);
-            const uint32_t tot = m.total;
             if constexpr (TRACE) {
                 if (lane == 0) {
                     int32_t *t = trace + 3 * (start + off + k);
@@ -275,31 +326,7 @@ __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *_
                     t[2] = (int32_t)tot;
                 }
             }
-            // A8 interval update (vcf_cbaac.cpp, encode)
-            const uint64_t range = (uint64_t)(high - low) + 1;
-            high = low + (uint32_t)(udiv(range * hi, tot) - 1);
-            low = low + (uint32_t)udiv(range * lo, tot);
-            for (;;) {
-                if (high < kHalf) {
-                    w.put(0, lane);
-                    w.run(1, pending, lane);
-                    pending = 0;
-                } else if (low >= kHalf) {
-                    w.put(1, lane);
-                    w.run(0, pending, lane);
-                    pending = 0;
-                    low -= kHalf;
-                    high -= kHalf;
-                } else if (low >= kQ1 && high < kQ3) {
-                    ++pending;
-                    low -= kQ1;
-                    high -= kQ1;
-                } else {
-                    break;
-                }
-                low <<= 1;
-                high = (high << 1) | 1u;
-            }
+            e.code(lo, hi, (double)tot, inv, w, lane);
             model_update(m, s, lane);
             if constexpr (ORDER == 1) {
                 tables_write(tabs[0], ctx, lane, m);
@@ -308,22 +335,22 @@ __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *_
         }
         cur = nxt;
     }
-    // flush (CBAAC.py:130 -> A8): one more pending bit and a disambiguating bit
-    ++pending;
-    const uint32_t b = low < kQ1 ? 0u : 1u;
-    w.put(b, lane);
-    w.run(b ^ 1u, pending, lane);
+    e.flush(w, lane);
     const uint64_t bits = w.finish(lane);
     if (lane == 0) seg_bits[seg] = (int64_t)bits;
 }
 
-// MSB-first bit reader over a segment's bytes, zeros past its end (A8)
+// MSB-first bit reader over a segment's bytes, zeros past its end (A8).
+// buf holds `avail` unread bits at its top; words come from 256-byte chunks
+// held one big-endian dword per lane (the next chunk prefetched).
 struct BitReader {
     const uint8_t *src;
     int64_t nbytes;
     int64_t chunk = 0;         // byte offset of `cur`
-    uint32_t cur = 0, nxt = 0; // 256 bytes each, one big-endian dword per lane
-    uint32_t wi = 0, word = 0, used = 0;
+    uint32_t cur = 0, nxt = 0;
+    uint32_t wi = 0;           // next word of `cur`
+    uint64_t buf = 0;
+    uint32_t avail = 0;
 
     __device__ __forceinline__ uint32_t load(int64_t off, uint32_t lane) const
     {
@@ -334,27 +361,31 @@ struct BitReader {
         }
         return v;
     }
+    __device__ __forceinline__ void refill(uint32_t lane)
+    {
+        if (wi == 64) {
+            wi = 0;
+            chunk += kChunk;
+            cur = nxt;
+            nxt = load(chunk + kChunk, lane);
+        }
+        buf |= (uint64_t)rl(cur, wi++) << (32 - avail);
+        avail += 32;
+    }
     __device__ __forceinline__ void start(uint32_t lane)
     {
         cur = load(0, lane);
         nxt = load(kChunk, lane);
-        wi = 0;
-        word = rl(cur, 0);
-        used = 32;   // the first 32 bits go straight into `value`
+        refill(lane);
     }
-    __device__ __forceinline__ uint32_t get(uint32_t lane)
+    // the next k bits (1 <= k <= 32), right-aligned
+    __device__ __forceinline__ uint32_t get(uint32_t k, uint32_t lane)
     {
-        if (used == 32) {
-            if (++wi == 64) {
-                wi = 0;
-                chunk += kChunk;
-                cur = nxt;
-                nxt = load(chunk + kChunk, lane);
-            }
-            word = rl(cur, wi);
-            used = 0;
-        }
-        return (word >> (31 - used++)) & 1u;
+        if (avail < k) refill(lane);
+        const uint32_t v = (uint32_t)(buf >> (64 - k));
+        buf <<= k;
+        avail -= k;
+        return v;
     }
 };
 
@@ -379,34 +410,46 @@ __global__ __launch_bounds__(64) void cbaac_tiled_decode_kernel(const uint8_t *_
     br.src = in + offs[seg];
     br.nbytes = offs[seg + 1] - offs[seg];
     br.start(lane);
-    uint32_t low = 0, high = 0xFFFFFFFFu, value = br.word;
+    uint32_t low = 0, high = 0xFFFFFFFFu, value = br.get(32, lane);
 
     uint32_t obuf = 0, acc = 0;
     for (int64_t i = 0; i < len; ++i) {
         if constexpr (ORDER == 1) tables_read(tabs[0], ctx, lane, m);
-        const uint64_t range = (uint64_t)(high - low) + 1;
-        const uint32_t tot = m.total;
-        const uint32_t v = (uint32_t)udiv(((uint64_t)(value - low) + 1) * tot - 1, range);
-        uint32_t lo, hi;
-        const uint32_t s = model_find(m, v, lo, hi);
-        high = low + (uint32_t)(udiv(range * hi, tot) - 1);
-        low = low + (uint32_t)udiv(range * lo, tot);
-        for (;;) {
-            if (high < kHalf) {
-            } else if (low >= kHalf) {
-                low -= kHalf;
-                high -= kHalf;
-                value -= kHalf;
-            } else if (low >= kQ1 && high < kQ3) {
-                low -= kQ1;
-                high -= kQ1;
-                value -= kQ1;
-            } else {
-                break;
-            }
-            low <<= 1;
-            high = (high << 1) | 1u;
-            value = (value << 1) | br.get(lane);
+        const double tot = (double)m.total;
+        const double inv = rcp_nr(tot);
+        const uint32_t span = high - low;                 // range - 1
+        const double rng = (double)span + 1.0;
+        // The A8 decoder picks s with C[s] <= floor(((T + 1) total - 1) / range)
+        // < C[s+1], T = value - low; for integers that is
+        // floor(range C[s] / total) <= T < floor(range C[s+1] / total), and
+        // those floors are the new interval's ends: every lane computes them
+        // for its four counts, a ballot finds the lane, no division by range.
+        const uint32_t T = value - low;
+        const uint32_t f0 = (uint32_t)floordiv(rng * (double)(m.p0 & 0xFFFFu), tot, inv);
+        const uint32_t f1 = (uint32_t)floordiv(rng * (double)(m.p0 >> 16), tot, inv);
+        const uint32_t f2 = (uint32_t)floordiv(rng * (double)(m.p1 & 0xFFFFu), tot, inv);
+        const uint32_t f3 = (uint32_t)floordiv(rng * (double)(m.p1 >> 16), tot, inv);
+        const uint32_t L = (uint32_t)__popcll(__ballot(f0 <= T)) - 1;   // f0 increases with the lane
+        const uint32_t g0 = rl(f0, L), g1 = rl(f1, L), g2 = rl(f2, L), g3 = rl(f3, L);
+        const uint32_t g4m1 = L == 63 ? span : rl(f0, (L + 1) & 63) - 1;   // floor(range C[4L+4] / total) - 1
+        const uint32_t j = (T >= g1 ? 1u : 0u) + (T >= g2 ? 1u : 0u) + (T >= g3 ? 1u : 0u);
+        const uint32_t s = 4 * L + j;
+        const uint32_t ql = j == 0 ? g0 : j == 1 ? g1 : j == 2 ? g2 : g3;
+        const uint32_t qhm1 = j == 0 ? g1 - 1 : j == 1 ? g2 - 1 : j == 2 ? g3 - 1 : g4m1;
+        high = low + qhm1;
+        low = low + ql;
+        const uint32_t d = __builtin_clz(low ^ high);
+        if (d) {
+            low <<= d;
+            high = (high << d) | ((1u << d) - 1u);
+            value = (value << d) | br.get(d, lane);
+        }
+        const uint32_t x = (low << 1) & ~(high << 1);
+        const uint32_t p = __builtin_clz(~x);
+        if (p) {
+            low = (low << p) & 0x7FFFFFFFu;
+            high = (high << p) | ((1u << p) - 1u) | 0x80000000u;
+            value = ((value << p) ^ 0x80000000u) | br.get(p, lane);
         }
         model_update(m, s, lane);
         if constexpr (ORDER == 1) {
