@@ -32,7 +32,7 @@ def test_dwt_encode_decode_vs_reference(case):
     assert np.array_equal(out, d["decoded"])
 
 
-@pytest.mark.parametrize("variant", [1, 2], ids=["fused", "separable"])
+@pytest.mark.parametrize("variant", [1, 2, 6], ids=["fused", "separable", "strip"])
 @pytest.mark.parametrize("wavelet", ["db5", "bior4.4", "haar", "sym4", "coif2", "db9", "db10"])
 @pytest.mark.parametrize("H,W,L,Q", [(96, 128, 3, 32), (67, 45, 2, 7), (256, 160, 5, 16), (8, 10, 1, 1),
                                      (141, 301, 4, 3), (17, 200, 3, 32)])
@@ -41,7 +41,7 @@ def test_dwt_vs_oracle(wavelet, H, W, L, Q, variant):
     shapes = O.dwt_shapes(H, W, L)
     rng = np.random.Generator(np.random.PCG64(H * W + L))
     frames = rng.integers(0, 256, (2, H, W, 3), dtype=np.uint8)
-    if variant == 1 and wavelet == "db10":      # 20 taps: the fused tile exceeds 64 KB of LDS
+    if variant in (1, 6) and wavelet == "db10":      # 20 taps: the fused tile exceeds 64 KB of LDS
         with pytest.raises(NotImplementedError):
             DW.encode(frames, wavelet, L, Q, variant=1)
         return
@@ -55,7 +55,7 @@ def test_dwt_vs_oracle(wavelet, H, W, L, Q, variant):
         with pytest.raises(NotImplementedError):
             DW.decode(got[0], H, W, wavelet, L, Q)
         return
-    out = DW.decode(got, H, W, wavelet, L, Q, variant=variant)
+    out = DW.decode(got, H, W, wavelet, L, Q, variant={6: 1}.get(variant, variant))
     for f in range(2):
         assert np.array_equal(out[f], O.dwt_decode_frame(got[f], H, W, wavelet, L, Q))
 
@@ -74,6 +74,8 @@ def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
     c = DW.encode(frames, wavelet, L, Q, variant=3)   # the earlier three-barrier schedule of the fused kernels
     e = DW.encode(frames, wavelet, L, Q, variant=4)   # run-time taps
     f = DW.encode(frames, wavelet, L, Q, variant=5)   # level 1 staged as float
+    g = DW.encode(frames, wavelet, L, Q, variant=6)   # strip kernels (sums started by their first product)
+    h = DW.encode(frames, wavelet, L, Q, variant=7)   # strip kernels, sums started at 0.0
     ref = O.dwt_encode_frame(frames[0], wavelet, L, Q)
     for name in ref:
         assert np.array_equal(a[0][name], ref[name]), name
@@ -81,6 +83,9 @@ def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
         assert np.array_equal(c[1][name], a[1][name]), name
         assert np.array_equal(e[1][name], a[1][name]), name
         assert np.array_equal(f[1][name], a[1][name]), name
+        assert np.array_equal(g[0][name], ref[name]), name
+        assert np.array_equal(g[1][name], a[1][name]), name
+        assert np.array_equal(h[1][name], a[1][name]), name
     da = DW.decode(a, H, W, wavelet, L, Q, variant=1)
     db = DW.decode(a, H, W, wavelet, L, Q, variant=2)
     assert np.array_equal(da, db)
@@ -93,7 +98,7 @@ def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
 def test_dwt_unknown_variant():
     import vcf_amd.dwt as DW
     with pytest.raises(ValueError):
-        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=7)
+        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=10)
 
 
 def test_dwt_errors():

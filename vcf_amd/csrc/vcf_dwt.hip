@@ -681,6 +681,271 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
         }
 }
 
+// ---------------------------------------------------------------------------
+// strip kernels (forward, dwt variant 6): one wave per column strip, no barriers
+// ---------------------------------------------------------------------------
+// A wave owns 64 consecutive input columns (one per lane) of a vertical
+// segment of the level's output rows and slides down it: every step takes
+// two new input rows into a circular register window of F samples per
+// channel, forms that column's A and D (axis-0 pass, pywt's tap order) for
+// all three channels, leaves them in a wave-private LDS row, and lanes
+// (A|D, output column) run the axis-1 pass over that row straight into the
+// quantized subband bytes / LL.  Consecutive input rows are loaded once, the
+// window rotates by compile-time indices (the step loop is unrolled by F/2),
+// and nothing waits on a workgroup barrier: a wave reads only what it wrote
+// itself (LDS operations of one wave complete in order).
+// Z0: the first product of a sum starts it instead of 0.0 + product.  That
+// differs only in the sign of a zero sum, and every output is truncated to
+// an integer (zeros of either sign give 0, and a zero sample only ever adds
+// a zero product), so the subband bytes are identical.
+constexpr int kSW = 64;   // input columns per strip (one per lane)
+__host__ __device__ constexpr int strip_tw(int F) { return (kSW - F) / 2 + 1; }
+
+template <int F, unsigned Z, bool Z0>
+__device__ __forceinline__ double nat_sum(const double (&f)[F], const double (&v)[F])
+{
+    // v[k] = sample at logical position i - F + 1 + k, i.e. tap m = F - 1 - k
+    double s = 0.0;
+    bool first = true;
+#pragma unroll
+    for (int m = 0; m < F; ++m) {
+        if ((Z >> m) & 1u) continue;
+        const double p = f[m] * v[F - 1 - m];
+        s = (Z0 && first) ? p : s + p;
+        first = false;
+    }
+    return s;
+}
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// level-1 YCoCg sample (int16 truncation, A4) of channel ch from packed RGB bytes
+__device__ __forceinline__ double ycocg_sample(uint32_t pix, int ch)
+{
+    const int R = pix & 0xFF, G = (pix >> 8) & 0xFF, B = (pix >> 16) & 0xFF;
+    const int iv = ch == 0 ? (R + 2 * G + B) >> 2 : ch == 1 ? (R - B) / 2 : (2 * G - R - B) / 4;
+    return (double)iv;
+}
+
+// the axis-1 pass of a strip's last wave, whose last outputs' taps wrap past
+// the line end (pywt's order through the generic sum); out of line, rare
+template <int F>
+__device__ __forceinline__ void strip_row_generic(const double *row, Filters flt, int w, int ic, int C0,
+                                                            double &lo, double &hi)
+{
+    auto load = [&](int p) -> double { return row[p - C0]; };
+    lo = dwt_tap_sum_logical(flt.dec_lo, F, w, ic, load);
+    hi = dwt_tap_sum_logical(flt.dec_hi, F, w, ic, load);
+}
+
+template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0, bool Z0 = true,
+          bool QP2 = true, int DIAG = 0>
+__global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
+                                                        const double *__restrict__ in, long long plane_stride,
+                                                        double *__restrict__ LLout, uint8_t *__restrict__ packed,
+                                                        long long packed_stride, long long ll_off, long long off_lh,
+                                                        long long off_hl, long long off_hh, int h, int w, int hh,
+                                                        int hw, int Q, int n_strips, int seg_rows, Taps<F> tp,
+                                                        Filters flt)
+{
+    constexpr int TWS = strip_tw(F), P = F / 2;
+    // [channel wave][step of the group][A | D][column]: a buffer per unrolled step, so
+    // one step's axis-1 reads and the next step's writes are independent
+    __shared__ __attribute__((aligned(16))) double rowbuf[3][P][2][kSW];
+    const int lane = threadIdx.x & 63;
+    const int ch = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // one wave per channel (wave-uniform)
+    // 1-D grid over (strip, segment, frame), the last strip -- whose last
+    // outputs take the slow wrapped-tap path -- dispatched first
+    const int n_segs = (hh + seg_rows - 1) / seg_rows;
+    const int per_s = (int)gridDim.x / n_strips;                   // segments x frames
+    const int strip = n_strips - 1 - (int)blockIdx.x / per_s;
+    const int seg = (int)blockIdx.x % per_s % n_segs;
+    const long long frame = (long long)blockIdx.x % per_s / n_segs;
+    const int oc0 = strip * TWS;
+    const int C0 = F / 2 + 2 * oc0 - F + 1;                          // logical column of lane 0
+    const int x = per_wrap(C0 + lane, w);
+    const int o0 = seg * seg_rows, o1 = min(hh, o0 + seg_rows);
+    if (o0 >= o1) return;
+    const int o_tail = min(o1, max(o0, (h - F / 2 + 1) / 2));   // first output row whose taps wrap past h
+    double flo[F], fhi[F];
+#pragma unroll
+    for (int m = 0; m < F; ++m) {
+        flo[m] = CT ? ct_dec(CT, false, m) : tp.lo[m];
+        fhi[m] = CT ? ct_dec(CT, true, m) : tp.hi[m];
+    }
+    const int qsh = __builtin_ctz((unsigned)Q);
+    auto q8 = [&](double v) -> uint8_t {   // (x / Q).astype(int32) + 128, astype(uint8)
+        return (uint8_t)(uint32_t)((int32_t)(QP2 ? __builtin_ldexp(v, -qsh) : v / (double)Q) + 128);
+    };
+    auto q16 = [&](double v) -> uint16_t {
+        return (uint16_t)(uint32_t)((int32_t)(QP2 ? __builtin_ldexp(v, -qsh) : v / (double)Q) + 128);
+    };
+    // axis-1 roles: lanes [0, TWS) take the A row, [TWS, 2 TWS) the D row
+    const int src = lane >= TWS ? 1 : 0, oc = lane - src * TWS, ocg = oc0 + oc;
+    const int nw = min(TWS, hw - oc0);                             // this strip's output columns
+    const bool col_ok = lane < 2 * TWS && oc < nw;
+    const int ic = F / 2 + 2 * ocg;                                  // its centre position on the line
+    // wave-uniform: does this strip hold outputs whose taps wrap past the line end?
+    const bool strip_tail = F / 2 + 2 * (oc0 + nw - 1) >= w;
+    uint8_t *const pk = packed + frame * packed_stride;
+    const uint8_t *const frgb = rgb + frame * rgb_stride;
+    const double *const fin = in + (frame * 3 + ch) * plane_stride;
+    const long long off_r1 = src ? off_lh : off_hl;   // this lane's first run: LH (D) / HL (A)
+    // level 1: this lane's RGB bytes as one (unaligned) dword that starts a byte
+    // early -- or, at x = 0, at the pixel -- so it never leaves the frame
+    const int x3 = 3 * x, xl = x > 0 ? x3 - 1 : x3, xs = x > 0 ? 8 : 0;
+
+    // per_wrap without a division or a branch: the launcher runs strips only on
+    // planes of at least 2F rows and columns, so every row index here lies in
+    // (-Ne, 2 Ne)
+    const int Ne = h + (h & 1);
+    auto row_of = [&](int r) -> long long {
+        int y = r < 0 ? r + Ne : r;
+        y = y >= Ne ? y - Ne : y;
+        return y < h ? y : h - 1;
+    };
+    using Raw = typename std::conditional<FIRST, uint32_t, double>::type;   // a sample before conversion
+    auto load_raw = [&](int r) -> Raw {
+        const long long y = row_of(r);
+        if constexpr (FIRST) {
+            const uint8_t *rowp = frgb + y * w * 3;
+            uint32_t d;
+            __builtin_memcpy(&d, rowp + xl, 4);
+            return (d >> xs) & 0xFFFFFFu;
+        } else {
+            return (fin + y * w)[x];
+        }
+    };
+    auto convert = [&](Raw v) -> double {
+        if constexpr (FIRST) return ycocg_sample(v, ch);
+        else return v;
+    };
+    // the same with the channel a compile-time constant (no branch per sample)
+    auto convert_c = [&](Raw v, auto chc) -> double {
+        if constexpr (FIRST) return ycocg_sample(v, decltype(chc)::value);
+        else return v;
+    };
+    auto load_sample = [&](int r) -> double { return convert(load_raw(r)); };
+
+    // Stores through buffer resources: a lane without an output (col_ok false,
+    // or the other half's subband) stores at an offset past the buffer, which
+    // the hardware drops.  So every store instruction issues unconditionally and
+    // the compiler's vmcnt bookkeeping counts them: the waits for the input rows
+    // loaded P steps ahead are then exact (with stores under an exec branch it
+    // can only count the loads, and waits for far more recent operations).
+    constexpr uint32_t kDrop = 0x80000000u;
+    typedef unsigned int U32x2 __attribute__((__vector_size__(8)));
+    const __amdgpu_buffer_rsrc_t rs_pk = __builtin_amdgcn_make_buffer_rsrc(pk, 0, (int)packed_stride, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_ll = __builtin_amdgcn_make_buffer_rsrc(
+        LLout + (frame * 3 + ch) * plane_stride, 0, (int)((long long)hh * hw * 8), 0x00020000);
+    const int ocr = min(oc, TWS - 1);                                // axis-1 reads stay inside the row
+    const uint32_t e_lane = (uint32_t)(3 * oc + ch);
+    // per-lane drop bits (loop-invariant data, not control flow): OR-ed into an offset
+    const uint32_t drop1 = col_ok ? 0u : kDrop, drop_d = col_ok && src ? 0u : kDrop,
+                   drop_a = col_ok && !src ? 0u : kDrop;
+    // axis-1 pass of output row o over the wave's LDS row, quantize, store
+    // (GENERIC: the strip holding the outputs whose taps wrap past the line end)
+    auto row_pass = [&](int o, int bi, auto generic) {
+        if (decltype(generic)::value) wave_lds_sync();
+        const uint32_t rb = (uint32_t)(((long long)o * hw + oc0) * 3);   // the strip's first byte in a subband row
+        const double *row = rowbuf[ch][bi][src];
+        double lo, hi;
+        if (!decltype(generic)::value) {
+            double v[F];
+#pragma unroll
+            for (int k = 0; k < F; k += 2) {
+                const double2 p = *(const double2 *)(row + 2 * ocr + k);
+                v[k] = p.x;
+                if (k + 1 < F) v[k + 1] = p.y;
+            }
+            lo = nat_sum<F, ZLO, Z0>(flo, v);
+            hi = nat_sum<F, ZHI, Z0>(fhi, v);
+        } else {
+            lo = hi = 0.0;
+            if (col_ok) strip_row_generic<F>(row, flt, w, ic, C0, lo, hi);
+        }
+        // A lanes: ad -> HL, aa -> LL; D lanes: da -> LH, dd -> HH
+        const uint32_t e = rb + e_lane;
+        if (DIAG != 1) {
+            __builtin_amdgcn_raw_buffer_store_b8(q8(src ? lo : hi), rs_pk, ((uint32_t)off_r1 + e) | drop1, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8(q8(hi), rs_pk, ((uint32_t)off_hh + e) | drop_d, 0, 0);
+        }
+        if (LAST)
+            __builtin_amdgcn_raw_buffer_store_b16(q16(lo), rs_pk, ((uint32_t)ll_off + 2 * e) | drop_a, 0, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U32x2, lo), rs_ll,
+                                                  (uint32_t)(((long long)o * hw + ocg) * 8) | drop_a, 0, 0);
+        if (decltype(generic)::value) wave_lds_sync();
+    };
+
+    // rows from direct loads, the axis-0 taps in pywt's order (the rows whose
+    // taps wrap past the bottom; every row of the tail strip)
+    auto direct_rows = [&](int from, auto generic) {
+        for (int o = from; o < o1; ++o) {
+            const int i = F / 2 + 2 * o;
+            wave_lds_sync();
+            rowbuf[ch][0][0][lane] = dwt_tap_sum_logical(flt.dec_lo, F, h, i, load_sample);
+            rowbuf[ch][0][1][lane] = dwt_tap_sum_logical(flt.dec_hi, F, h, i, load_sample);
+            wave_lds_sync();
+            row_pass(o, 0, generic);
+        }
+    };
+    if (strip_tail) {
+        direct_rows(o0, std::true_type());
+        return;
+    }
+
+    // sliding rows: groups of P steps; window slot (2u + k) % F of step u of a
+    // group holds logical input row 2o - F/2 + 1 + k.  Rows are loaded P
+    // steps ahead.  Level 1 runs one copy of the loop per channel (the YCoCg
+    // formula a constant in each).
+    int o = o0;
+    auto slide = [&](auto chc) {
+        double win[F];
+#pragma unroll
+        for (int k = 0; k < F - 2; ++k) win[k] = convert_c(load_raw(2 * o0 - F / 2 + 1 + k), chc);
+        const int o_main = o0 + (o_tail - o0) / P * P;
+        if (o >= o_main) return;
+        // a ring of the next P steps' input rows: step u of a group consumes slot u
+        // and refills it with the rows of the same step of the next group
+        Raw ring[P][2];
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            ring[u][0] = load_raw(2 * (o + u) + F / 2 - 1);
+            ring[u][1] = load_raw(2 * (o + u) + F / 2);
+        }
+        for (; o < o_main; o += P) {
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                win[(2 * u + F - 2) % F] = convert_c(ring[u][0], chc);
+                win[(2 * u + F - 1) % F] = convert_c(ring[u][1], chc);
+                // P steps ahead (past the segment: wrapped rows, unused)
+                ring[u][0] = load_raw(2 * (o + u + P) + F / 2 - 1);
+                ring[u][1] = load_raw(2 * (o + u + P) + F / 2);
+                double v[F];
+#pragma unroll
+                for (int k = 0; k < F; ++k) v[k] = win[(2 * u + k) % F];
+                // LDS operations of a wave complete in order, and the compiler keeps
+                // this lane's write before the reads of the others (same array, no
+                // proof of distinct addresses): no barrier needed
+                rowbuf[ch][u][0][lane] = nat_sum<F, ZLO, Z0>(flo, v);
+                rowbuf[ch][u][1][lane] = nat_sum<F, ZHI, Z0>(fhi, v);
+                row_pass(o + u, u, std::false_type());
+            }
+        }
+    };
+    if (FIRST && ch == 0) slide(std::integral_constant<int, 0>());
+    else if (FIRST && ch == 1) slide(std::integral_constant<int, 1>());
+    else slide(std::integral_constant<int, 2>());
+    wave_lds_sync();
+    direct_rows(o, std::false_type());   // fewer than P rows, and the bottom rows' wrapped taps
+}
+
 // Four consecutive outputs of the inverse from the register windows of the
 // approximation (xa) and detail (xd) inputs: pywt's order for a pair index
 // i >= F/4 (approximation taps j = 0.., then detail taps), tap loop outermost.
@@ -887,6 +1152,7 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
     }
 }
 
+#ifndef VCF_DWT_KERNELS_ONLY   // (micro-experiments compile the kernels alone)
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -1035,6 +1301,67 @@ void launch_fwd_level(const LevelArgs &a, bool first, bool last)
         launch_fwd_kernel<F, 0u, 0u>(a, tp, grid, first, last);
 }
 
+// strip kernels (dwt variant 6; 7 = the same with every sum started at 0.0)
+constexpr int kMaxStripF = 10;   // longest filter with a strip kernel (F samples of window in VGPRs)
+
+template <int F>
+using StripKern = void (*)(const uint8_t *, long long, const double *, long long, double *, uint8_t *, long long,
+                           long long, long long, long long, long long, int, int, int, int, int, int, int, Taps<F>,
+                           Filters);
+
+template <int F, unsigned ZL, unsigned ZH, int CT, bool Z0, bool QP2, int DIAG = 0>
+StripKern<F> strip_kern(bool first, bool last)
+{
+    return first ? (last ? dwt_strip_kernel<F, true, true, ZL, ZH, CT, Z0, QP2, DIAG>
+                         : dwt_strip_kernel<F, true, false, ZL, ZH, CT, Z0, QP2, DIAG>)
+                 : (last ? dwt_strip_kernel<F, false, true, ZL, ZH, CT, Z0, QP2, DIAG>
+                         : dwt_strip_kernel<F, false, false, ZL, ZH, CT, Z0, QP2, DIAG>);
+}
+
+template <int F>
+void launch_strip_level(const LevelArgs &a, bool first, bool last, int mode)
+{
+    const bool z0 = mode != 7;
+    if constexpr (F > kMaxStripF) {
+        return;
+    } else {
+        const Taps<F> tp = taps_of<F>(a.wd->dec_lo, a.wd->dec_hi);
+        constexpr int TWS = strip_tw(F), P = F / 2;
+        const int n_strips = (a.hw + TWS - 1) / TWS;
+        // segments: ~16 waves per SIMD over the chip (three per strip-segment),
+        // at least 2F rows, whole groups of F/2 sliding steps
+        const long long cols = (long long)n_strips * a.n_frames * 3;
+        int seg = (int)std::max<long long>(2 * F, (a.hh * cols + 16383) / 16384);
+        seg = std::min((seg + P - 1) / P * P, a.hh);
+        const long long nblk = (long long)n_strips * ((a.hh + seg - 1) / seg) * a.n_frames;
+        const bool qp2 = (a.Q & (a.Q - 1)) == 0;
+        StripKern<F> kern = qp2 ? strip_kern<F, 0u, 0u, 0, true, true>(first, last)
+                                : strip_kern<F, 0u, 0u, 0, true, false>(first, last);
+        if constexpr (F == 10) {   // bior4.4 (zero taps skipped) / db5: compile-time taps
+            const bool b44 = zero_mask(a.wd->dec_lo, F) == kB44DecLo && zero_mask(a.wd->dec_hi, F) == kB44DecHi;
+            const int id = b44 ? 1 : 2;
+            bool ct = true;
+            for (int m = 0; ct && m < F; ++m) {
+                const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
+                ct = std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
+            }
+            if (ct && b44 && qp2 && mode == 8)   // diagnostic: no detail-subband stores
+                kern = strip_kern<F, kB44DecLo, kB44DecHi, 1, true, true, 1>(first, last);
+
+            else if (ct && b44)
+                kern = qp2 ? (z0 ? strip_kern<F, kB44DecLo, kB44DecHi, 1, true, true>(first, last)
+                                 : strip_kern<F, kB44DecLo, kB44DecHi, 1, false, true>(first, last))
+                           : strip_kern<F, kB44DecLo, kB44DecHi, 1, true, false>(first, last);
+            else if (ct)
+                kern = qp2 ? strip_kern<F, 0u, 0u, 2, true, true>(first, last)
+                           : strip_kern<F, 0u, 0u, 2, true, false>(first, last);
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(192), 0, a.s, a.rgb, a.rgb_stride, a.in,
+                           a.plane_stride, a.LLout, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
+                           a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, n_strips, seg, tp, a.flt);
+    }
+}
+
 // level r of the inverse: subbands a.h x a.w -> outputs a.hh x a.hw (= oh x ow)
 template <int F, unsigned ZLO, unsigned ZHI>
 void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, bool from_packed, bool to_rgb,
@@ -1094,6 +1421,20 @@ void fwd_level(int F, const LevelArgs &a, bool first, bool last)
     }
 }
 
+void strip_level(int F, const LevelArgs &a, bool first, bool last, int mode)
+{
+    switch (F) {
+#define X(n)                                                                                                       \
+    case n:                                                                                                        \
+        launch_strip_level<n>(a, first, last, mode);                                                               \
+        break;
+        VCF_DWT_FOR_EACH_F(X)
+#undef X
+    default:
+        break;
+    }
+}
+
 void inv_level(int F, const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t *rgb_out)
 {
     switch (F) {
@@ -1108,9 +1449,11 @@ void inv_level(int F, const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t
     }
 }
 
+#endif  // VCF_DWT_KERNELS_ONLY
 }  // namespace
 }  // namespace vcf
 
+#ifndef VCF_DWT_KERNELS_ONLY
 using namespace vcf;
 
 extern "C" {
@@ -1152,7 +1495,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 5) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant > 9) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1181,7 +1524,13 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                           g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
                           g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s,
                           variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : 1};
-        fwd_level(F, a, l == 1, l == levels);
+        // strips need planes of at least 2F rows and columns (their row wrap)
+        const bool strip = F <= kMaxStripF && g.hs[l - 1] >= 2 * F && g.ws[l - 1] >= 2 * F &&
+                           ((variant >= 6 && variant <= 8) || (variant == 9 && l > 1 && l < levels));
+        if (strip)
+            strip_level(F, a, l == 1, l == levels, variant);
+        else
+            fwd_level(F, a, l == 1, l == levels);
         in = LLout;
         rc = hip_check(hipGetLastError(), "dwt level launch");
         if (rc != VCF_OK) return rc;
@@ -1288,3 +1637,5 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
 }
 
 }  // extern "C"
+
+#endif  // VCF_DWT_KERNELS_ONLY
