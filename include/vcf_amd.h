@@ -204,14 +204,20 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
                       int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, void *stream);
 
 /* Same, with an explicit kernel choice (for A/B tests and benchmarks):
- * 0 = automatic (1 when its LDS tile fits, else 2), 1 = fused LDS-tiled level
- * kernels (one launch per level; filters up to 18 taps), 2 = separable
- * column/row kernels through float64 workspace planes, 3 = 1 with the
- * earlier three-barrier schedule for bior4.4 (A/B reference; other filters
- * as 1), 4 = 1 with bior4.4's taps as kernel arguments instead of
- * compile-time constants (A/B reference), 5 = 1 with level 1 staging its
- * samples as float at 4 waves/SIMD and no raised wave priority for its
- * loads and copy-out (A/B reference).  vcf_dwt_dz_decode_variant takes
+ * 0 = automatic (9 for filters up to 10 taps, else 1 when its LDS tile fits,
+ * else 2), 1 = fused LDS-tiled level kernels on every level (one launch per
+ * level; filters up to 18 taps), 2 = separable column/row kernels through
+ * float64 workspace planes, 3 = 1 with the earlier three-barrier schedule
+ * for bior4.4 (A/B reference; other filters as 1), 4 = 1 with bior4.4's taps
+ * as kernel arguments instead of compile-time constants (A/B reference),
+ * 5 = 1 with level 1 staging its samples as float at 4 waves/SIMD and no
+ * raised wave priority for its loads and copy-out (A/B reference), 6 = strip
+ * kernels (one wave per channel and 64-column strip sliding down a register
+ * window, no workgroup barriers; filters up to 10 taps, planes of at least
+ * 2F rows and columns) on every level, 7 = 6 with every tap sum started at
+ * 0.0 (A/B), 8 = diagnostic: 6 without the detail-subband stores (outputs
+ * incomplete), 9 = strips for the middle levels, fused kernels for the first
+ * and last.  vcf_dwt_dz_decode_variant takes
  * 0, 1, 2, 4 (bior4.4's reconstruction taps at run time) and 5 (no raised
  * wave priority while the subbands are staged).  Outputs
  * identical. */

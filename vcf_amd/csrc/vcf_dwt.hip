@@ -724,6 +724,20 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// a register copy the compiler cannot see through (see the strip kernel's row prefetch)
+__device__ __forceinline__ uint32_t opaque_mov(uint32_t x)
+{
+    uint32_t r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ double opaque_mov(double x)
+{
+    double r;
+    asm volatile("v_mov_b64 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // level-1 YCoCg sample (int16 truncation, A4) of channel ch from packed RGB bytes
 __device__ __forceinline__ double ycocg_sample(uint32_t pix, int ch)
 {
@@ -756,7 +770,8 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
     constexpr int TWS = strip_tw(F), P = F / 2;
     // [channel wave][step of the group][A | D][column]: a buffer per unrolled step, so
     // one step's axis-1 reads and the next step's writes are independent
-    __shared__ __attribute__((aligned(16))) double rowbuf[3][P][2][kSW];
+    // (the D row starts 2 doubles further on, so A and D lanes' reads fall in different banks)
+    __shared__ __attribute__((aligned(16))) double rowbuf[3][P][2][kSW + 2];
     const int lane = threadIdx.x & 63;
     const int ch = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // one wave per channel (wave-uniform)
     // 1-D grid over (strip, segment, frame), the last strip -- whose last
@@ -816,18 +831,18 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
             const uint8_t *rowp = frgb + y * w * 3;
             uint32_t d;
             __builtin_memcpy(&d, rowp + xl, 4);
-            return (d >> xs) & 0xFFFFFFu;
+            return d;   // the pixel is (d >> xs) & 0xFFFFFF (convert)
         } else {
             return (fin + y * w)[x];
         }
     };
     auto convert = [&](Raw v) -> double {
-        if constexpr (FIRST) return ycocg_sample(v, ch);
+        if constexpr (FIRST) return ycocg_sample((v >> xs) & 0xFFFFFFu, ch);
         else return v;
     };
     // the same with the channel a compile-time constant (no branch per sample)
     auto convert_c = [&](Raw v, auto chc) -> double {
-        if constexpr (FIRST) return ycocg_sample(v, decltype(chc)::value);
+        if constexpr (FIRST) return ycocg_sample((v >> xs) & 0xFFFFFFu, decltype(chc)::value);
         else return v;
     };
     auto load_sample = [&](int r) -> double { return convert(load_raw(r)); };
@@ -911,22 +926,29 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
         for (int k = 0; k < F - 2; ++k) win[k] = convert_c(load_raw(2 * o0 - F / 2 + 1 + k), chc);
         const int o_main = o0 + (o_tail - o0) / P * P;
         if (o >= o_main) return;
-        // a ring of the next P steps' input rows: step u of a group consumes slot u
-        // and refills it with the rows of the same step of the next group
-        Raw ring[P][2];
+        // The next group's 2P input rows are loaded at the top of each group
+        // and handed to the following group through register copies the
+        // compiler cannot fold (opaque_mov): its wait for them then sits at the
+        // end of this group, in straight-line code, and counts exactly the
+        // stores issued since (values loaded in one iteration and first read
+        // in the next make it wait for everything at the loop head).
+        Raw cur[P][2];
 #pragma unroll
         for (int u = 0; u < P; ++u) {
-            ring[u][0] = load_raw(2 * (o + u) + F / 2 - 1);
-            ring[u][1] = load_raw(2 * (o + u) + F / 2);
+            cur[u][0] = load_raw(2 * (o + u) + F / 2 - 1);
+            cur[u][1] = load_raw(2 * (o + u) + F / 2);
         }
         for (; o < o_main; o += P) {
+            Raw nxt[P][2];
+#pragma unroll
+            for (int u = 0; u < P; ++u) {   // past the segment: wrapped rows, unused
+                nxt[u][0] = load_raw(2 * (o + u + P) + F / 2 - 1);
+                nxt[u][1] = load_raw(2 * (o + u + P) + F / 2);
+            }
 #pragma unroll
             for (int u = 0; u < P; ++u) {
-                win[(2 * u + F - 2) % F] = convert_c(ring[u][0], chc);
-                win[(2 * u + F - 1) % F] = convert_c(ring[u][1], chc);
-                // P steps ahead (past the segment: wrapped rows, unused)
-                ring[u][0] = load_raw(2 * (o + u + P) + F / 2 - 1);
-                ring[u][1] = load_raw(2 * (o + u + P) + F / 2);
+                win[(2 * u + F - 2) % F] = convert_c(cur[u][0], chc);
+                win[(2 * u + F - 1) % F] = convert_c(cur[u][1], chc);
                 double v[F];
 #pragma unroll
                 for (int k = 0; k < F; ++k) v[k] = win[(2 * u + k) % F];
@@ -936,6 +958,11 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
                 rowbuf[ch][u][0][lane] = nat_sum<F, ZLO, Z0>(flo, v);
                 rowbuf[ch][u][1][lane] = nat_sum<F, ZHI, Z0>(fhi, v);
                 row_pass(o + u, u, std::false_type());
+            }
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                cur[u][0] = opaque_mov(nxt[u][0]);
+                cur[u][1] = opaque_mov(nxt[u][1]);
             }
         }
     };
@@ -1526,7 +1553,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                           variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : 1};
         // strips need planes of at least 2F rows and columns (their row wrap)
         const bool strip = F <= kMaxStripF && g.hs[l - 1] >= 2 * F && g.ws[l - 1] >= 2 * F &&
-                           ((variant >= 6 && variant <= 8) || (variant == 9 && l > 1 && l < levels));
+                           ((variant >= 6 && variant <= 8) || ((variant == 0 || variant == 9) && l > 1 && l < levels));
         if (strip)
             strip_level(F, a, l == 1, l == levels, variant);
         else

@@ -64,8 +64,9 @@ def _frames(a, what):
 
 def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32, variant: int = 0):
     """HxWx3 u8 (or N of them) -> list of {subband name: indices} per frame.
-    variant: 0 automatic, 1 fused level kernels, 2 separable kernels, 3 fused with the earlier
-    three-barrier schedule (bior4.4; A/B only)."""
+    variant: 0 automatic, 1 fused level kernels, 2 separable kernels, 3-5 fused A/B forms,
+    6 strip kernels on every level, 7 strips with sums started at 0.0, 8 diagnostic,
+    9 strips for the middle levels (what 0 picks for filters up to 10 taps); see vcf_amd.h."""
     f = _frames(rgb, "rgb")
     n, H, W, _ = f.shape
     _, pb, wb = layout(H, W, levels)
