@@ -9,6 +9,9 @@ the reference:
   * src/2D-DCT.py encode_fn/decode_fn (unmodified glue) at -B 1, 2, 3, 4,
     12, 16, 32, 64, 96, 128 (padding, -x, several -q): indices and
     reconstructions bit-exact;
+  * lengths with a prime factor above 5 (pocketfft radfg/radbg) 1..200 vs
+    scipy, and the reference's glue at -B 7, 11, 13, 14, 21, 49, 98, 130, 200
+    (make_golden_radg.py); the Bluestein lengths pocketfft_r picks;
   * the -L search (optimize_block_size, 2D-DCT.py:533-579): the codec's host
     logic (vcf_amd/codec/dct2d.py) with the oracle standing in for the GPU
     transforms reproduces the reference's J for every candidate block size
@@ -43,9 +46,39 @@ def test_oracle_dct_lengths_vs_scipy(N):
     assert np.array_equal(inv.view(np.uint64), g[f"inv_out_{N}"].view(np.uint64))
 
 
-def test_oracle_dct_uncovered_lengths():
-    for N in (7, 11, 14, 49, 77):   # a prime factor > 5: pocketfft radfg/radbg, not restated
-        assert not O.dct_supported(N)
+RADG = json.load(open(os.path.join(GOLDEN, "manifest_radg.json")))
+
+
+@pytest.mark.parametrize("N", RADG["lengths"])
+def test_oracle_dct_radfg_radbg_lengths_vs_scipy(N):
+    """Lengths with a prime factor above 5 (pocketfft's generic radfg/radbg),
+    against scipy.fftpack under the reference's python (make_golden_radg.py)."""
+    g = np.load(os.path.join(GOLDEN, "blocks_radg.npz"))
+    assert O.dct_supported(N)
+    fwd = O.dct_n(g[f"fwd_in_{N}"], 2, np.float32)
+    assert np.array_equal(fwd.view(np.uint32), g[f"fwd_out_{N}"].view(np.uint32))
+    inv = O.dct_n(g[f"inv_in_{N}"].astype(np.float64), 3, np.float64)
+    assert np.array_equal(inv.view(np.uint64), g[f"inv_out_{N}"].view(np.uint64))
+
+
+def test_oracle_dct_bluestein_lengths():
+    """pocketfft_r plans these lengths with Bluestein (not restated); every
+    other length 1..600 is an rfftp plan the restatement covers."""
+    blue = set(RADG["bluestein_lengths"])
+    assert blue and min(blue) == 191
+    for N in range(1, 601):
+        assert O.dct_supported(N) == (N not in blue), N
+
+
+@pytest.mark.parametrize("case", RADG["cases"], ids=lambda c: c["name"])
+def test_oracle_radg_block_sizes_vs_reference(case):
+    d = np.load(os.path.join(GOLDEN, f"dct_{case['name']}.npz"))
+    B, Q, flags = _qf(case["flags"])
+    H, W = d["rgb"].shape[:2]
+    k = O.encode_frame_b(d["rgb"], B, Q, flags)
+    assert k.shape == tuple(case["k_shape"])
+    assert np.array_equal(k, d["k"])
+    assert np.array_equal(O.decode_frame_b(d["k"], H, W, B, Q, flags), d["decoded"])
 
 
 @pytest.mark.parametrize("case", MANIFEST["cases"], ids=lambda c: c["name"])
