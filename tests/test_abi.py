@@ -55,8 +55,8 @@ def test_padded_shape_is_host_only():
 
 @pytest.mark.parametrize("args,status", [
     (dict(H=0), L.VCF_ERR_INVALID),              # not an image
-    (dict(block_size=7), L.VCF_ERR_UNSUPPORTED),   # -B 7: no radix-7 (radfg) transform on the HIP path
-    (dict(block_size=256), L.VCF_ERR_UNSUPPORTED),  # beyond the -L range 2..128
+    (dict(block_size=191), L.VCF_ERR_UNSUPPORTED),  # pocketfft plans length 191 with Bluestein (not restated)
+    (dict(block_size=5000), L.VCF_ERR_UNSUPPORTED),  # beyond the run-time path's 4096
     (dict(block_size=16, flags=2), L.VCF_ERR_UNSUPPORTED),  # -p needs B = 8 (cv2 table resize)
     (dict(Q=0), L.VCF_ERR_INVALID),
     (dict(flags=8), L.VCF_ERR_INVALID),
@@ -96,15 +96,14 @@ def test_product_never_imports_the_oracle():
 
 
 def test_block_size_coverage():
-    """-B sizes with a HIP transform: the 5-smooth B <= 128 (every -L candidate among them)."""
+    """-B sizes with a HIP transform: every length pocketfft plans with rfftp
+    (compiled kernels for the 5-smooth B <= 128, the run-time path for the
+    rest up to 4096); the Bluestein lengths (tests/golden/manifest_radg.json,
+    checked against scipy by tests/test_oracle_dct_general.py) are not."""
+    import json
+    from conftest import GOLDEN
+    blue = set(json.load(open(os.path.join(GOLDEN, "manifest_radg.json")))["bluestein_lengths"])
     lib = L.lib()
-    have = [b for b in range(0, 300) if lib.vcf_dct_block_size_supported(b)]
-    assert have == [b for b in range(1, 129) if _five_smooth(b)]
-    assert len(have) == 38 and all(2 ** i in have for i in range(1, 8))
-
-
-def _five_smooth(n):
-    for p in (2, 3, 5):
-        while n % p == 0:
-            n //= p
-    return n == 1
+    have = [b for b in range(0, 601) if lib.vcf_dct_block_size_supported(b)]
+    assert have == [b for b in range(1, 601) if b not in blue]
+    assert lib.vcf_dct_block_size_supported(4096) and not lib.vcf_dct_block_size_supported(4097)

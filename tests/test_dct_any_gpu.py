@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 
 D = pytest.importorskip("vcf_amd.dct")
 MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest_general.json")))
+RADG = json.load(open(os.path.join(GOLDEN, "manifest_radg.json")))
 LENGTHS = [1, 2, 3, 4, 5, 6, 8, 9, 10, 12, 15, 16, 18, 20, 24, 25, 27, 30, 32, 36, 40, 45, 48, 50, 54, 60, 64, 72, 75, 80, 81, 90, 96, 100, 108, 120, 125, 128]
 
 
@@ -129,9 +130,61 @@ def test_codec_block_size_files_match_reference(case, tmp_path):
 def test_unsupported_block_sizes_raise():
     from vcf_amd._lib import VCFUnsupported
     rgb = _smooth(20, 20, 0)
-    for B in (7, 11, 14, 49, 256):
+    for B in (191, 199, 5000):   # Bluestein lengths (not restated), beyond 4096
         assert not D.block_size_supported(B)
         with pytest.raises(VCFUnsupported):
             D.encode(rgb, 32, 0, block_size=B)
     with pytest.raises(VCFUnsupported):
         D.encode(rgb, 32, 2, block_size=16)   # -p needs B = 8
+
+
+# ---- the run-time-length path (vcf_pocketfft_rt.h): prime factors above 5, B > 128 ----
+
+@pytest.mark.parametrize("case", RADG["cases"], ids=lambda c: c["name"])
+def test_radg_block_size_matches_reference_golden(case):
+    """The reference's own encode_fn/decode_fn at -B 7, 11, 13, 14, 21, 49, 98,
+    130, 200 (tests/golden/make_golden_radg.py), bit for bit."""
+    d = np.load(os.path.join(GOLDEN, f"dct_{case['name']}.npz"))
+    B, Q, flags = _qf(case["flags"])
+    H, W = d["rgb"].shape[:2]
+    k = D.encode(d["rgb"], Q, flags, block_size=B)
+    assert np.array_equal(k, d["k"])
+    assert np.array_equal(D.decode(d["k"], H, W, Q, flags, block_size=B), d["decoded"])
+
+
+RT_LENGTHS = [7, 11, 13, 14, 17, 22, 33, 49, 63, 97, 127, 131, 154, 180, 256, 300, 343]
+
+
+@pytest.mark.parametrize("B", RT_LENGTHS)
+@pytest.mark.parametrize("Q,flags", [(32, 0), (5, 1)])
+def test_runtime_block_size_vs_oracle(B, Q, flags):
+    H, W = B + 3, 2 * B - 1
+    rng = np.random.default_rng(B * 7 + Q)
+    rgb = _smooth(H, W, B) if Q == 32 else rng.integers(0, 256, (H, W, 3), np.uint8)
+    k = D.encode(rgb, Q, flags, block_size=B)
+    assert np.array_equal(k, O.encode_frame_b(rgb, B, Q, flags))
+    assert np.array_equal(D.decode(k, H, W, Q, flags, block_size=B), O.decode_frame_b(k, H, W, B, Q, flags))
+
+
+@pytest.mark.parametrize("B", [7, 49, 130])
+def test_runtime_block_size_int32_and_batches(B):
+    """The int32 (-L style) index type and multi-frame launches on the run-time path."""
+    H, W = 2 * B + 1, B + 4
+    frames = np.stack([_smooth(H, W, s) for s in range(3)])
+    k = D.encode_k32(frames, 32, 0, B) if hasattr(D, "encode_k32") else None
+    for f in range(3):
+        if k is not None:
+            assert np.array_equal(k[f], O.encode_frame_b(frames[f], B, 32, 0, k32=True))
+        ku = D.encode(frames[f], 7, 0, block_size=B)
+        assert np.array_equal(ku, O.encode_frame_b(frames[f], B, 7, 0))
+    ku = D.encode(frames, 7, 0, block_size=B)
+    for f in range(3):
+        assert np.array_equal(ku[f], O.encode_frame_b(frames[f], B, 7, 0))
+        assert np.array_equal(D.decode(ku[f], H, W, 7, 0, block_size=B),
+                              O.decode_frame_b(ku[f], H, W, B, 7, 0))
+
+
+def test_bluestein_length_unsupported():
+    rgb = np.zeros((191, 191, 3), np.uint8)
+    with pytest.raises(NotImplementedError):
+        D.encode(rgb, 32, 0, block_size=191)

@@ -9,11 +9,12 @@ span between reading the image and handing the indices to the entropy codec
 libvcf_amd.so (vcf_dct_dz_encode / vcf_dct_dz_decode); there is no CPU
 implementation of it in the product.
 
--B takes every block size the HIP path has a transform for (the 5-smooth
-B <= 128, vcf_dct_block_size_supported), -L runs optimize_block_size
+-B takes every block size the HIP path has a transform for (every B <= 4096
+that pocketfft plans with rfftp, vcf_dct_block_size_supported; not the
+Bluestein lengths, the first of which is 191), -L runs optimize_block_size
 (2D-DCT.py:533-579) with the GPU doing each candidate's analysis/synthesis.
 Options the HIP path does not implement raise NotImplementedError when the
-codec is constructed (other block sizes, -p with B != 8, colour transforms
+codec is constructed (Bluestein block sizes, -p with B != 8, colour transforms
 other than YCoCg, quantizers other than deadzone, filters other than
 no_filter); entropy codecs come from ENTROPY_CODECS.
 """
@@ -76,8 +77,8 @@ class CoDec(EICCoDec):
         if not self.encoding and filt != "no_filter":
             raise NotImplementedError(f"filter {filt!r}: only no_filter is on the HIP path")
         if not D.block_size_supported(self.block_size):
-            raise NotImplementedError(f"block size {self.block_size}: the HIP path covers the 5-smooth "
-                                      "B <= 128")
+            raise NotImplementedError(f"block size {self.block_size}: the HIP path covers every B <= 4096 "
+                                      "that pocketfft plans with rfftp (not its Bluestein lengths)")
         if self.block_size != 8 and getattr(args, "perceptual_quantization", False):
             # 2D-DCT.py:85-90 resizes the JPEG tables with cv2 for B != 8 (not on the HIP path)
             raise NotImplementedError("-p with a block size other than 8")

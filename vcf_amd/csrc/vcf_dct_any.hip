@@ -4,10 +4,12 @@
 //
 // What is computed is the same frame pipeline as vcf_dct_dz.hip
 // (src/2D-DCT.py:276-361 encode, :399-466 decode; assumptions A1-A5), with the
-// length-B pocketfft transforms of vcf_pocketfft.h.  Supported B: the
-// lengths pocketfft factors into 4, 2, 3 and 5 up to 128 (1, 2, 3, 4, 5, 6,
-// 8, 9, 10, 12, 15, 16, ..., 120, 125, 128: 38 sizes); larger B or a prime
-// factor above 5 (pocketfft's generic radfg/radbg) return VCF_ERR_UNSUPPORTED.
+// length-B pocketfft transforms of vcf_pocketfft.h (compiled in for the 38
+// lengths pocketfft factors into 4, 2, 3 and 5 up to 128: 1, 2, 3, 4, 5, 6, 8,
+// 9, 10, 12, 15, 16, ..., 120, 125, 128) or of vcf_pocketfft_rt.h (any other
+// B <= 4096 that pocketfft plans with rfftp, prime factors above 5 through its
+// generic radfg/radbg passes).  The lengths pocketfft_r plans with Bluestein
+// (the first is 191) return VCF_ERR_UNSUPPORTED.
 //
 // Mapping.  A "unit" is one channel of one BxB block.  A workgroup holds
 // U = 256/B units (encode, fp32) or 128/B units (decode, fp64), B lanes per
@@ -36,11 +38,14 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <map>
 #include <mutex>
+#include <vector>
 
 #include "vcf_amd.h"
 #include "vcf_internal.h"
 #include "vcf_pocketfft.h"
+#include "vcf_pocketfft_rt.h"
 #include "vcf_pocketfft_tables.h"
 
 namespace vcf {
@@ -272,6 +277,324 @@ __global__ __launch_bounds__(256) void dct_any_to_rgb_kernel(const void *__restr
     for (int ch = 0; ch < 3; ++ch) d[ch] = (uint8_t)std::min(255, std::max(0, o3[ch]));   // :466 clip, uint8
 }
 
+// ---- run-time-length path: block sizes without a compiled kernel ----------
+// A workgroup runs one unit at a time (grid-stride): threads take the columns
+// (then the rows) of the unit's block, each on its own scratch line, and the
+// block sits in a scratch tile between the passes.  Same arithmetic as the
+// compiled kernels above, through pfft::RtFft.
+constexpr int kRtThreads = 256;
+constexpr int kRtMaxB = 4096;
+
+__device__ __forceinline__ long long coef_offset_rt(const GeomB &g, int B, int by, int bx, int i, int j)
+{
+    const long long row = g.sub ? (long long)i * g.nby + by : (long long)by * B + i;
+    const long long col = g.sub ? (long long)j * g.nbx + bx : (long long)bx * B + j;
+    return (row * g.Wp + col) * 3;
+}
+
+// scratch per workgroup: the B x B tile, then the threads' two lines of B
+__host__ __device__ constexpr long long rt_ws_per_wg(int B) { return (long long)B * B + 2LL * B * kRtThreads; }
+
+template <bool K32>
+__global__ __launch_bounds__(256) void dct_rt_encode_kernel(const uint8_t *__restrict__ rgb, void *__restrict__ out,
+                                                           GeomB g, int Q, pfft::RtPlan P,
+                                                           const float *__restrict__ mem, float *__restrict__ ws)
+{
+    const int B = P.n, tid = threadIdx.x;
+    float *tile = ws + (long long)blockIdx.x * rt_ws_per_wg(B);
+    float *lines = tile + (long long)B * B;
+    const pfft::Line<float> c{lines + tid, kRtThreads}, ch{lines + (long long)B * kRtThreads + tid, kRtThreads};
+    const pfft::RtFft<float> F{mem};
+    for (long long u = blockIdx.x; u < g.units; u += gridDim.x) {
+        long long f = 0;
+        int by = 0, bx = 0, cc = 0;
+        unit_coords(g, u, f, by, bx, cc);
+        const uint8_t *img = rgb + f * g.in_stride;
+        for (int x = tid; x < B; x += kRtThreads) {
+            // :276 float32, :282 centred zero padding, :292 -= 128, :298 from_RGB (A4)
+            const int sx = bx * B + x - g.left;
+            for (int y = 0; y < B; ++y) {
+                const int sy = by * B + y - g.top;
+                float R = 0.f, G = 0.f, Bl = 0.f;
+                if (sy >= 0 && sy < g.H && sx >= 0 && sx < g.W) {
+                    const uint8_t *p = img + ((long long)sy * g.W + sx) * 3;
+                    R = (float)p[0]; G = (float)p[1]; Bl = (float)p[2];
+                }
+                if constexpr (!K32) { R = R - 128.f; G = G - 128.f; Bl = Bl - 128.f; }
+                float o;
+                if (cc == 0) o = (R / 4.f + G / 2.f) + Bl / 4.f;
+                else if (cc == 1) o = R / 2.f - Bl / 2.f;
+                else o = ((-R) / 4.f + G / 2.f) - Bl / 4.f;
+                c[y] = o;
+            }
+            F.dct2(c, ch, P);   // :303 analyze_image (A1): axis 0 first
+            for (int y = 0; y < B; ++y) tile[(long long)y * B + x] = c[y];
+        }
+        __syncthreads();
+        const float q = (float)Q;
+        for (int y = tid; y < B; y += kRtThreads) {
+            for (int j = 0; j < B; ++j) c[j] = tile[(long long)y * B + j];
+            F.dct2(c, ch, P);
+            // :343 quantize (A5), :348 += 128, :361 uint8
+            for (int j = 0; j < B; ++j) {
+                const int k = (int)__fdiv_rn(c[j], q);
+                const long long o = f * g.out_stride + coef_offset_rt(g, B, by, bx, y, j) + cc;
+                if constexpr (K32) ((int32_t *)out)[o] = k;
+                else ((uint8_t *)out)[o] = (uint8_t)(k + 128);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <bool K32>
+__global__ __launch_bounds__(256) void dct_rt_decode_kernel(const void *__restrict__ kin, void *__restrict__ wsout,
+                                                           GeomB g, int Q, pfft::RtPlan P,
+                                                           const double *__restrict__ mem, double *__restrict__ ws)
+{
+    const int B = P.n, tid = threadIdx.x;
+    double *tile = ws + (long long)blockIdx.x * rt_ws_per_wg(B);
+    double *lines = tile + (long long)B * B;
+    const pfft::Line<double> c{lines + tid, kRtThreads}, ch{lines + (long long)B * kRtThreads + tid, kRtThreads};
+    const pfft::RtFft<double> F{mem};
+    for (long long u = blockIdx.x; u < g.units; u += gridDim.x) {
+        long long f = 0;
+        int by = 0, bx = 0, cc = 0;
+        unit_coords(g, u, f, by, bx, cc);
+        for (int x = tid; x < B; x += kRtThreads) {
+            for (int i = 0; i < B; ++i) {
+                const long long o = f * g.out_stride + coef_offset_rt(g, B, by, bx, i, x) + cc;
+                if constexpr (K32) {
+                    c[i] = (double)(int32_t)((uint32_t)Q * (uint32_t)((const int32_t *)kin)[o]);
+                } else {
+                    const int16_t k = (int16_t)((int)((const uint8_t *)kin)[o] - 128);
+                    c[i] = (double)(int16_t)(Q * (int)k);
+                }
+            }
+            F.dct3(c, ch, P);   // :440 synthesize_image (A2)
+            for (int i = 0; i < B; ++i) tile[(long long)i * B + x] = c[i];
+        }
+        __syncthreads();
+        for (int y = tid; y < B; y += kRtThreads) {
+            for (int j = 0; j < B; ++j) c[j] = tile[(long long)y * B + j];
+            F.dct3(c, ch, P);
+            const long long row = (long long)by * B + y;
+            for (int j = 0; j < B; ++j) {
+                const long long o = f * ((long long)g.Hp * g.Wp * 3) + (row * g.Wp + (long long)bx * B + j) * 3 + cc;
+                if constexpr (K32) ((int32_t *)wsout)[o] = (int32_t)c[j];
+                else ((int16_t *)wsout)[o] = (int16_t)(int32_t)c[j];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- host: run-time plans (pocketfft rfftp + T_dcst23 setup) -------------
+// pocketfft_r<T0>(length)'s plan choice: Bluestein only for lengths >= 50
+// whose largest prime factor p has p*p > length, when its cost guess wins
+// (util::largest_prime_factor, cost_guess, good_size_cmplx)
+size_t rt_largest_prime_factor(size_t n)
+{
+    size_t res = 1;
+    while ((n & 1) == 0) { res = 2; n >>= 1; }
+    for (size_t x = 3; x * x <= n; x += 2)
+        while (n % x == 0) { res = x; n /= x; }
+    if (n > 1) res = n;
+    return res;
+}
+double rt_cost_guess(size_t n)
+{
+    const double lfp = 1.1;   // penalty for non-hardcoded larger factors
+    const size_t ni = n;
+    double result = 0.;
+    while ((n & 1) == 0) { result += 2; n >>= 1; }
+    for (size_t x = 3; x * x <= n; x += 2)
+        while (n % x == 0) { result += (x <= 5) ? double(x) : lfp * double(x); n /= x; }
+    if (n > 1) result += (n <= 5) ? double(n) : lfp * double(n);
+    return result * double(ni);
+}
+size_t rt_good_size_cmplx(size_t n)
+{
+    if (n <= 12) return n;
+    size_t bestfac = 2 * n;
+    for (size_t f11 = 1; f11 < bestfac; f11 *= 11)
+        for (size_t f117 = f11; f117 < bestfac; f117 *= 7)
+            for (size_t f1175 = f117; f1175 < bestfac; f1175 *= 5) {
+                size_t x = f1175;
+                while (x < n) x *= 2;
+                for (;;) {
+                    if (x < n) x *= 3;
+                    else if (x > n) {
+                        if (x < bestfac) bestfac = x;
+                        if (x & 1) break;
+                        x >>= 1;
+                    } else return n;
+                }
+            }
+    return bestfac;
+}
+bool rt_uses_bluestein(size_t n)
+{
+    const size_t tmp = (n < 50) ? 0 : rt_largest_prime_factor(n);
+    if (tmp * tmp <= n) return false;
+    const double comp1 = 0.5 * rt_cost_guess(n);
+    const double comp2 = 2 * rt_cost_guess(rt_good_size_cmplx(2 * n - 1)) * 1.5;   // pocketfft's fudge factor
+    return comp2 < comp1;
+}
+
+// lengths the run-time path covers
+bool rt_covered(int B) { return B >= 1 && B <= kRtMaxB && !rt_uses_bluestein((size_t)B); }
+
+// rfftp factorize + comp_twiddle, T_dcst23's twiddle, pypocketfft's norm_fct
+template <typename T>
+void rt_fill(int n, pfft::RtPlan &P, std::vector<T> &mem)
+{
+    P.n = n;
+    P.nf = 0;
+    int l = n;
+    if (n > 1) {
+        while (l % 4 == 0) { P.fct[P.nf++] = 4; l >>= 2; }
+        if (l % 2 == 0) {
+            l >>= 1;
+            P.fct[P.nf++] = 2;
+            std::swap(P.fct[0], P.fct[P.nf - 1]);
+        }
+        for (int d = 3; d * d <= l; d += 2)
+            while (l % d == 0) { P.fct[P.nf++] = d; l /= d; }
+        if (l > 1) P.fct[P.nf++] = l;
+    }
+    mem.clear();
+    size_t l1 = 1;
+    for (int k = 0; k < P.nf; ++k) {
+        const size_t ip = (size_t)P.fct[k], ido = (size_t)n / (l1 * ip);
+        P.tw[k] = (int)mem.size();
+        if (k < P.nf - 1) {
+            const size_t off = mem.size();
+            mem.resize(off + (ip - 1) * (ido - 1));
+            for (size_t j = 1; j < ip; ++j)
+                for (size_t i = 1; i <= (ido - 1) / 2; ++i) {
+                    T re, im;
+                    sincos_2pibyn<T>((size_t)n, j * l1 * i, re, im);
+                    mem[off + (j - 1) * (ido - 1) + 2 * i - 2] = re;
+                    mem[off + (j - 1) * (ido - 1) + 2 * i - 1] = im;
+                }
+        }
+        P.tws[k] = (int)mem.size();
+        if (ip > 5) {
+            const size_t off = mem.size();
+            mem.resize(off + 2 * ip);
+            mem[off] = T(1);
+            mem[off + 1] = T(0);
+            for (size_t i = 2, ic = 2 * ip - 2; i <= ic; i += 2, ic -= 2) {
+                T re, im;
+                sincos_2pibyn<T>((size_t)n, i / 2 * ((size_t)n / ip), re, im);
+                mem[off + i] = re;
+                mem[off + i + 1] = im;
+                mem[off + ic] = re;
+                mem[off + ic + 1] = -im;
+            }
+        }
+        l1 *= ip;
+    }
+    P.dct_tw = (int)mem.size();
+    for (int i = 0; i < n; ++i) {
+        T re, im;
+        sincos_2pibyn<T>(4 * (size_t)n, (size_t)i + 1, re, im);
+        mem.push_back(re);
+    }
+    P.norm = (int)mem.size();
+    mem.push_back(T(1 / std::sqrt((long double)(2 * n))));
+}
+
+struct RtPlanDev {
+    pfft::RtPlan P;
+    float *f32 = nullptr;
+    double *f64 = nullptr;
+};
+
+// plans per (device, length), uploaded once and kept
+int rt_plan(int n, RtPlanDev &out)
+{
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, RtPlanDev> cache;
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc != VCF_OK) return rc;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find({dev, n});
+    if (it != cache.end()) { out = it->second; return VCF_OK; }
+    RtPlanDev d;
+    std::vector<float> mf;
+    std::vector<double> md;
+    rt_fill<float>(n, d.P, mf);
+    pfft::RtPlan P2;
+    rt_fill<double>(n, P2, md);   // same offsets
+    if ((rc = hip_check(hipMalloc(&d.f32, mf.size() * sizeof(float)), "hipMalloc(rt plan)")) != VCF_OK) return rc;
+    if ((rc = hip_check(hipMalloc(&d.f64, md.size() * sizeof(double)), "hipMalloc(rt plan)")) != VCF_OK) return rc;
+    if ((rc = hip_check(hipMemcpy(d.f32, mf.data(), mf.size() * sizeof(float), hipMemcpyHostToDevice),
+                        "rt plan upload")) != VCF_OK)
+        return rc;
+    if ((rc = hip_check(hipMemcpy(d.f64, md.data(), md.size() * sizeof(double), hipMemcpyHostToDevice),
+                        "rt plan upload")) != VCF_OK)
+        return rc;
+    cache[{dev, n}] = d;
+    out = d;
+    return VCF_OK;
+}
+
+Scratch &rt_scratch_for_current_device()
+{
+    static Scratch per_dev[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    return per_dev[dev];
+}
+
+// workgroups of a run-time-path launch: enough to fill the chip, scratch <= ~1 GiB
+unsigned rt_grid(long long units, int B, size_t esz)
+{
+    const long long per = rt_ws_per_wg(B) * (long long)esz;
+    long long wgs = std::min<long long>(units, 4096);
+    wgs = std::min<long long>(wgs, std::max<long long>(1, (1LL << 30) / per));
+    return (unsigned)std::max<long long>(wgs, 1);
+}
+
+int rt_launch_encode(const uint8_t *rgb, void *out, bool k32, const GeomB &g, int B, int Q, hipStream_t s)
+{
+    RtPlanDev pl;
+    int rc = rt_plan(B, pl);
+    if (rc != VCF_OK) return rc;
+    const unsigned grid = rt_grid(g.units, B, sizeof(float));
+    Scratch &scr = rt_scratch_for_current_device();
+    std::lock_guard<std::mutex> lock(scr.mu);
+    rc = scr.acquire((size_t)grid * rt_ws_per_wg(B) * sizeof(float), s);
+    if (rc != VCF_OK) return rc;
+    float *ws = (float *)scr.ptr;
+    if (k32) hipLaunchKernelGGL((dct_rt_encode_kernel<true>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws);
+    else hipLaunchKernelGGL((dct_rt_encode_kernel<false>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws);
+    rc = hip_check(hipGetLastError(), "dct_rt_encode_kernel launch");
+    const int rc2 = scr.release(s);
+    return rc != VCF_OK ? rc : rc2;
+}
+
+int rt_launch_decode(const void *kin, void *wsout, bool k32, const GeomB &g, int B, int Q, hipStream_t s)
+{
+    RtPlanDev pl;
+    int rc = rt_plan(B, pl);
+    if (rc != VCF_OK) return rc;
+    const unsigned grid = rt_grid(g.units, B, sizeof(double));
+    Scratch &scr = rt_scratch_for_current_device();
+    std::lock_guard<std::mutex> lock(scr.mu);
+    rc = scr.acquire((size_t)grid * rt_ws_per_wg(B) * sizeof(double), s);
+    if (rc != VCF_OK) return rc;
+    double *ws = (double *)scr.ptr;
+    if (k32) hipLaunchKernelGGL((dct_rt_decode_kernel<true>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws);
+    else hipLaunchKernelGGL((dct_rt_decode_kernel<false>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws);
+    rc = hip_check(hipGetLastError(), "dct_rt_decode_kernel launch");
+    const int rc2 = scr.release(s);
+    return rc != VCF_OK ? rc : rc2;
+}
+
 int make_geom_b(int H, int W, int B, uint32_t flags, int64_t n_frames, GeomB &g)
 {
     g.H = H; g.W = W;
@@ -325,7 +648,7 @@ int launch_decode(const void *kin, void *ws, bool k32, const GeomB &g, int Q, hi
     case 80: return CALL(80); case 81: return CALL(81); case 90: return CALL(90);                \
     case 96: return CALL(96); case 100: return CALL(100); case 108: return CALL(108);            \
     case 120: return CALL(120); case 125: return CALL(125); case 128: return CALL(128);          \
-    default: return set_error(VCF_ERR_UNSUPPORTED, "block size %d is not supported", B);         \
+    default: break;                                                                              \
     }
 
 int check_any(const void *a, const void *b, int64_t n_frames, int H, int W, int B, int Q, uint32_t flags,
@@ -336,9 +659,11 @@ int check_any(const void *a, const void *b, int64_t n_frames, int H, int W, int 
     if (H <= 0 || W <= 0)
         return set_error(VCF_ERR_INVALID, "Input image must be a 3D array (height, width, channels).");
     if (B < 1) return set_error(VCF_ERR_INVALID, "block size %d", B);
-    if (slot_of(B) < 0)
+    if (slot_of(B) < 0 && !rt_covered(B))
         return set_error(VCF_ERR_UNSUPPORTED,
-                         "block size %d: the HIP path covers the 5-smooth B <= 128 (pocketfft radix 2/3/4/5)", B);
+                         B > kRtMaxB ? "block size %d: the HIP path covers B <= 4096"
+                                     : "block size %d: pocketfft plans this length with Bluestein (not restated)",
+                         B);
     if (Q < 1 || (decode && !k32 && Q > 32767))
         return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
     if (flags & VCF_DCT_PERCEPTUAL)
@@ -364,6 +689,7 @@ int any_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, i
 #define VCF_ENC_ANY(b) launch_encode<b>(rgb_dev, k_dev, k32, g, Q, s)
     VCF_ANY_SWITCH(B, VCF_ENC_ANY)
 #undef VCF_ENC_ANY
+    return rt_launch_encode(rgb_dev, k_dev, k32, g, B, Q, s);
 }
 
 int any_decode(const void *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t B, int32_t Q, uint32_t flags,
@@ -395,6 +721,7 @@ int any_decode(const void *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_
 #define VCF_DEC_ANY(b) launch_decode<b>(kin, ws, k32, g, Q, s)
             VCF_ANY_SWITCH(B, VCF_DEC_ANY)
 #undef VCF_DEC_ANY
+            return rt_launch_decode(kin, ws, k32, g, B, Q, s);
         };
         rc = pass1();
         if (rc != VCF_OK) break;
@@ -430,7 +757,7 @@ extern "C" {
 
 int vcf_dct_block_size_supported(int32_t block_size)
 {
-    return vcf::slot_of(block_size) >= 0 ? 1 : 0;
+    return vcf::slot_of(block_size) >= 0 || vcf::rt_covered(block_size) ? 1 : 0;
 }
 
 int vcf_dct_dz_encode_k32(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
