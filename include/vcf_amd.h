@@ -92,7 +92,8 @@ int vcf_dct_padded_shape(int32_t H, int32_t W, int32_t block_size, int32_t *Hp, 
  * (Hp x Wp x 3 u8 each, k + 128 modulo 256, subband layout unless
  * VCF_DCT_NO_SUBBANDS).  block_size is the -B option (2D-DCT.py:29): 8 runs
  * the fused 8x8 kernels, the other supported sizes (vcf_dct_block_size_supported)
- * the generic-B kernels; VCF_DCT_PERCEPTUAL needs B = 8.  Q >= 1 is the
+ * the generic-B kernels; VCF_DCT_PERCEPTUAL takes any supported B (B != 8
+ * through vcf_dct_perceptual_tables' resized tables).  Q >= 1 is the
  * deadzone quantization step (-q). */
 int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *k_dev,
@@ -134,11 +135,19 @@ int vcf_dct_dz_decode(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev,
                       void *stream);
 
-/* 1 if block_size has a HIP transform: the 5-smooth B <= 128 (pocketfft's
- * radix 2/3/4/5 passes; 38 sizes, every -L candidate 2, 4, ..., 128 among
- * them, 2D-DCT.py:536).  0 otherwise (a prime factor > 5 needs pocketfft's
- * generic radfg/radbg, not restated). */
+/* 1 if block_size has a HIP transform: every B <= 4096 that pocketfft plans
+ * with rfftp -- compiled kernels for the 38 5-smooth B <= 128 (every -L
+ * candidate 2, 4, ..., 128, 2D-DCT.py:536), run-time-length kernels with the
+ * generic radfg/radbg passes for the rest.  0 for the lengths pocketfft_r
+ * plans with Bluestein (191, 199, 211, ...; not restated) and B > 4096. */
 int vcf_dct_block_size_supported(int32_t block_size);
+
+/* -p's quantization tables for block size B (host only): the JPEG luma /
+ * chroma tables of 2D-DCT.py:66-84 resized to B x B as :85-90 does
+ * (cv2.resize, INTER_AREA for B < 8, INTER_LINEAR otherwise), B*B bytes each.
+ * cv2 is not installed here: OpenCV's scalar resize code paths are restated,
+ * unpinned by any reference output (parity unpinned for -p with B != 8). */
+int vcf_dct_perceptual_tables(int32_t block_size, uint8_t *y_qss, uint8_t *c_qss);
 
 /* The generic-B kernels for any supported block size, B = 8 included (tests
  * and A/B checks against the fused 8x8 kernels); same contract as

@@ -69,6 +69,7 @@ def lib():
         L.vcfo_dct_dz_decode_k32_b.argtypes = [i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_uint, u8p]
         L.vcfo_perceptual_weights.argtypes = [dp]
+        L.vcfo_dct_perceptual_tables.argtypes = [ctypes.c_int, u8p, u8p]
         # 2D-DWT path (vcf_dwt_oracle.cpp)
         ip = ctypes.POINTER(ctypes.c_int)
         u16p = ctypes.POINTER(ctypes.c_uint16)
@@ -141,6 +142,16 @@ def dct_n(x, kind: int = 2, dtype=np.float32):
     if f(b.ctypes.data_as(ctypes.POINTER(ct)), N, b.shape[0]) != 0:
         raise ValueError(f"length {N} not covered by the restatement")
     return b.reshape(a.shape)
+
+
+def perceptual_tables(B: int):
+    """-p's JPEG tables resized to B x B (cv2.resize restated; unpinned for B != 8)."""
+    y = np.empty((B, B), np.uint8)
+    c = np.empty((B, B), np.uint8)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    if lib().vcfo_dct_perceptual_tables(int(B), y.ctypes.data_as(u8p), c.ctypes.data_as(u8p)) != 0:
+        raise ValueError(B)
+    return y, c
 
 
 def encode_frame_b(rgb: np.ndarray, B: int, Q: int = 32, flags: int = 0, k32: bool = False) -> np.ndarray:

@@ -7,6 +7,7 @@ import glob
 import os
 import re
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -57,7 +58,7 @@ def test_padded_shape_is_host_only():
     (dict(H=0), L.VCF_ERR_INVALID),              # not an image
     (dict(block_size=191), L.VCF_ERR_UNSUPPORTED),  # pocketfft plans length 191 with Bluestein (not restated)
     (dict(block_size=5000), L.VCF_ERR_UNSUPPORTED),  # beyond the run-time path's 4096
-    (dict(block_size=16, flags=2), L.VCF_ERR_UNSUPPORTED),  # -p needs B = 8 (cv2 table resize)
+    (dict(block_size=191, flags=2), L.VCF_ERR_UNSUPPORTED),  # -p on a Bluestein length
     (dict(Q=0), L.VCF_ERR_INVALID),
     (dict(flags=8), L.VCF_ERR_INVALID),
     (dict(n_frames=-1), L.VCF_ERR_INVALID),
@@ -107,3 +108,22 @@ def test_block_size_coverage():
     have = [b for b in range(0, 601) if lib.vcf_dct_block_size_supported(b)]
     assert have == [b for b in range(1, 601) if b not in blue]
     assert lib.vcf_dct_block_size_supported(4096) and not lib.vcf_dct_block_size_supported(4097)
+
+
+def test_perceptual_tables_match_the_oracle():
+    """-p's resized JPEG tables (host only): B = 8 is the reference's own
+    table, integer area scales average, and every B the oracle's
+    restatement of cv2.resize gives (unpinned for B != 8: no cv2 here)."""
+    from oracle import oracle as O
+    lib = L.lib()
+    for B in list(range(1, 33)) + [49, 64, 100, 128, 130, 200]:
+        y = np.empty((B, B), np.uint8)
+        c = np.empty((B, B), np.uint8)
+        assert lib.vcf_dct_perceptual_tables(B, y.ctypes.data, c.ctypes.data) == 0
+        yo, co = O.perceptual_tables(B)
+        assert np.array_equal(y, yo) and np.array_equal(c, co), B
+    y8, c8 = O.perceptual_tables(8)
+    assert y8[0].tolist() == [16, 11, 10, 16, 24, 40, 51, 61] and c8[0].tolist() == [17, 18, 24, 47, 99, 99, 99, 99]
+    y4, _ = O.perceptual_tables(4)
+    assert y4[0, 0] == 13   # (16 + 11 + 12 + 12) / 4 = 12.75, rounded
+    assert lib.vcf_dct_perceptual_tables(0, y.ctypes.data, c.ctypes.data) == L.VCF_ERR_INVALID

@@ -134,8 +134,6 @@ def test_unsupported_block_sizes_raise():
         assert not D.block_size_supported(B)
         with pytest.raises(VCFUnsupported):
             D.encode(rgb, 32, 0, block_size=B)
-    with pytest.raises(VCFUnsupported):
-        D.encode(rgb, 32, 2, block_size=16)   # -p needs B = 8
 
 
 # ---- the run-time-length path (vcf_pocketfft_rt.h): prime factors above 5, B > 128 ----
@@ -188,3 +186,34 @@ def test_bluestein_length_unsupported():
     rgb = np.zeros((191, 191, 3), np.uint8)
     with pytest.raises(NotImplementedError):
         D.encode(rgb, 32, 0, block_size=191)
+
+
+@pytest.mark.parametrize("B", [1, 2, 3, 4, 7, 12, 16, 64, 130])
+@pytest.mark.parametrize("flags", [2, 3])
+def test_perceptual_any_block_size_vs_oracle(B, flags):
+    """-p for B != 8 (2D-DCT.py:85-90, :313-327, :421-435) with the resized
+    tables (cv2 restated, unpinned): kernels vs the oracle's pipeline."""
+    H, W = B + 5, 2 * B + 3
+    rgb = _smooth(H, W, B + flags)
+    k = D.encode(rgb, 7, flags, block_size=B)
+    assert np.array_equal(k, O.encode_frame_b(rgb, B, 7, flags))
+    assert np.array_equal(D.decode(k, H, W, 7, flags, block_size=B), O.decode_frame_b(k, H, W, B, 7, flags))
+
+
+def test_perceptual_b8_generic_kernel_equals_fused():
+    """At B = 8 the resize is the identity: the generic kernels' -p equals the fused 8x8 kernels'."""
+    import vcf_amd._lib as L
+    from vcf_amd.device import DeviceBuffer
+    rgb = _smooth(40, 56, 3)
+    Hp, Wp = 40, 56
+    for flags in (2, 3):
+        fused = D.encode(rgb, 32, flags)
+        din, dout = DeviceBuffer.from_array(rgb), DeviceBuffer(Hp * Wp * 3)
+        L.call("vcf_dct_dz_encode_any", din.ptr, 1, 40, 56, 8, 32, flags, dout.ptr, None)
+        anyk = dout.download(np.empty((Hp, Wp, 3), np.uint8))
+        assert np.array_equal(anyk, fused)
+        dec = DeviceBuffer(40 * 56 * 3)
+        L.call("vcf_dct_dz_decode_any", dout.ptr, 1, 40, 56, 8, 32, flags, dec.ptr, None)
+        assert np.array_equal(dec.download(np.empty((40, 56, 3), np.uint8)), D.decode(fused, 40, 56, 32, flags))
+        for b in (din, dout, dec):
+            b.free()

@@ -43,7 +43,7 @@ def test_unsupported_options_raise():
     file or device work."""
     from vcf_amd.codec.dct2d import CoDec
     p = P.dct_parser()
-    for argv in (["encode", "-B", "191"], ["encode", "-B", "5000"], ["encode", "-B", "16", "-p"],
+    for argv in (["encode", "-B", "191"], ["encode", "-B", "5000"],
                  ["encode", "-t", "YCrCb"], ["encode", "-a", "LloydMax"],
                  ["encode", "-c", "PNG"], ["decode", "-f", "gaussian_blur"]):
         with pytest.raises(NotImplementedError):

@@ -80,6 +80,7 @@ SIGNATURES = {
     "vcf_dct_dz_decode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_decode_variant": [ctypes.c_int, _P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_block_size_supported": [_I32],
+    "vcf_dct_perceptual_tables": [_I32, ctypes.c_void_p, ctypes.c_void_p],
     "vcf_dct_dz_encode_any": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_decode_any": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_encode_k32": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],

@@ -14,7 +14,7 @@ that pocketfft plans with rfftp, vcf_dct_block_size_supported; not the
 Bluestein lengths, the first of which is 191), -L runs optimize_block_size
 (2D-DCT.py:533-579) with the GPU doing each candidate's analysis/synthesis.
 Options the HIP path does not implement raise NotImplementedError when the
-codec is constructed (Bluestein block sizes, -p with B != 8, colour transforms
+codec is constructed (Bluestein block sizes, colour transforms
 other than YCoCg, quantizers other than deadzone, filters other than
 no_filter); entropy codecs come from ENTROPY_CODECS.
 """
@@ -79,9 +79,6 @@ class CoDec(EICCoDec):
         if not D.block_size_supported(self.block_size):
             raise NotImplementedError(f"block size {self.block_size}: the HIP path covers every B <= 4096 "
                                       "that pocketfft plans with rfftp (not its Bluestein lengths)")
-        if self.block_size != 8 and getattr(args, "perceptual_quantization", False):
-            # 2D-DCT.py:85-90 resizes the JPEG tables with cv2 for B != 8 (not on the HIP path)
-            raise NotImplementedError("-p with a block size other than 8")
         ec_name = getattr(args, "entropy_image_codec", "TIFF")
         if ec_name not in ENTROPY_CODECS:
             raise NotImplementedError(f"entropy codec {ec_name!r} (have: {sorted(ENTROPY_CODECS)})")

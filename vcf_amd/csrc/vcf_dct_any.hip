@@ -130,7 +130,8 @@ template <int B> constexpr int dec_units() { return B >= 128 ? 1 : 128 / B; }
 // ---- encode: RGB u8 -> k (u8 = k + 128 wrapped, or int32 k) --------------
 template <int B, bool K32>
 __global__ __launch_bounds__(256) void dct_any_encode_kernel(const uint8_t *__restrict__ rgb,
-                                                            void *__restrict__ out, GeomB g, int Q)
+                                                            void *__restrict__ out, GeomB g, int Q,
+                                                            const double *__restrict__ pw)
 {
     constexpr int U = enc_units<B>();
     constexpr int LD = B + 1;   // padded row: row-pass reads stride LD words (no bank conflicts)
@@ -177,6 +178,11 @@ __global__ __launch_bounds__(256) void dct_any_encode_kernel(const uint8_t *__re
 #pragma unroll
         for (int j = 0; j < B; ++j) v[j] = T[y * LD + j];
         pfft::dct2<float, B>(v, tw);
+        if (pw) {   // :313-327 -p: block[..., c] *= QSSs / 121 (or 99), float64 product into float32
+            const double *wr = pw + (c ? B * B : 0) + y * B;
+#pragma unroll
+            for (int j = 0; j < B; ++j) v[j] = (float)((double)v[j] * wr[j]);
+        }
         const float q = (float)Q;
         // :343 quantize (A5: (x / Q).astype(int32)), :348 += 128, :361 uint8
 #pragma unroll
@@ -192,7 +198,8 @@ __global__ __launch_bounds__(256) void dct_any_encode_kernel(const uint8_t *__re
 // ---- decode, pass 1: k -> IDCT'd integers in a padded-frame workspace ------
 template <int B, bool K32>
 __global__ __launch_bounds__(128) void dct_any_decode_kernel(const void *__restrict__ kin,
-                                                            void *__restrict__ ws, GeomB g, int Q)
+                                                            void *__restrict__ ws, GeomB g, int Q,
+                                                            const double *__restrict__ pw)
 {
     constexpr int U = dec_units<B>();
     constexpr int LD = B + 1;
@@ -218,7 +225,12 @@ __global__ __launch_bounds__(128) void dct_any_decode_kernel(const void *__restr
             } else {
                 // :399-411 astype(int16) - 128, Q*k in int16 (A5)
                 const int16_t k = (int16_t)((int)((const uint8_t *)kin)[o] - 128);
-                v[i] = (double)(int16_t)(Q * (int)k);
+                int16_t y16 = (int16_t)(Q * (int)k);
+                if (pw) {   // :421-435 -p: float32 block /= QSSs / 121 (or 99), stored back into int16
+                    const float f = (float)((double)(float)y16 / pw[(c ? B * B : 0) + i * B + x]);
+                    y16 = (int16_t)(int)f;
+                }
+                v[i] = (double)y16;
             }
         }
         // :440 synthesize_image (A2): idct over the integer block -> float64
@@ -298,7 +310,8 @@ __host__ __device__ constexpr long long rt_ws_per_wg(int B) { return (long long)
 template <bool K32>
 __global__ __launch_bounds__(256) void dct_rt_encode_kernel(const uint8_t *__restrict__ rgb, void *__restrict__ out,
                                                            GeomB g, int Q, pfft::RtPlan P,
-                                                           const float *__restrict__ mem, float *__restrict__ ws)
+                                                           const float *__restrict__ mem, float *__restrict__ ws,
+                                                           const double *__restrict__ pw)
 {
     const int B = P.n, tid = threadIdx.x;
     float *tile = ws + (long long)blockIdx.x * rt_ws_per_wg(B);
@@ -335,9 +348,11 @@ __global__ __launch_bounds__(256) void dct_rt_encode_kernel(const uint8_t *__res
         for (int y = tid; y < B; y += kRtThreads) {
             for (int j = 0; j < B; ++j) c[j] = tile[(long long)y * B + j];
             F.dct2(c, ch, P);
-            // :343 quantize (A5), :348 += 128, :361 uint8
+            const double *wr = pw ? pw + (cc ? B * B : 0) + (long long)y * B : nullptr;
+            // :313-327 -p, :343 quantize (A5), :348 += 128, :361 uint8
             for (int j = 0; j < B; ++j) {
-                const int k = (int)__fdiv_rn(c[j], q);
+                const float t = wr ? (float)((double)c[j] * wr[j]) : c[j];
+                const int k = (int)__fdiv_rn(t, q);
                 const long long o = f * g.out_stride + coef_offset_rt(g, B, by, bx, y, j) + cc;
                 if constexpr (K32) ((int32_t *)out)[o] = k;
                 else ((uint8_t *)out)[o] = (uint8_t)(k + 128);
@@ -350,7 +365,8 @@ __global__ __launch_bounds__(256) void dct_rt_encode_kernel(const uint8_t *__res
 template <bool K32>
 __global__ __launch_bounds__(256) void dct_rt_decode_kernel(const void *__restrict__ kin, void *__restrict__ wsout,
                                                            GeomB g, int Q, pfft::RtPlan P,
-                                                           const double *__restrict__ mem, double *__restrict__ ws)
+                                                           const double *__restrict__ mem, double *__restrict__ ws,
+                                                           const double *__restrict__ pw)
 {
     const int B = P.n, tid = threadIdx.x;
     double *tile = ws + (long long)blockIdx.x * rt_ws_per_wg(B);
@@ -368,7 +384,12 @@ __global__ __launch_bounds__(256) void dct_rt_decode_kernel(const void *__restri
                     c[i] = (double)(int32_t)((uint32_t)Q * (uint32_t)((const int32_t *)kin)[o]);
                 } else {
                     const int16_t k = (int16_t)((int)((const uint8_t *)kin)[o] - 128);
-                    c[i] = (double)(int16_t)(Q * (int)k);
+                    int16_t y16 = (int16_t)(Q * (int)k);
+                    if (pw) {   // :421-435 -p
+                        const float f = (float)((double)(float)y16 / pw[(cc ? B * B : 0) + (long long)i * B + x]);
+                        y16 = (int16_t)(int)f;
+                    }
+                    c[i] = (double)y16;
                 }
             }
             F.dct3(c, ch, P);   // :440 synthesize_image (A2)
@@ -506,6 +527,146 @@ void rt_fill(int n, pfft::RtPlan &P, std::vector<T> &mem)
     mem.push_back(T(1 / std::sqrt((long double)(2 * n))));
 }
 
+// cv2.resize of an 8x8 uint8 table to B x B, as src/2D-DCT.py:85-90 calls it
+// (INTER_AREA for B < 8, INTER_LINEAR otherwise), restating OpenCV's scalar
+// code paths (imgproc/src/resize.cpp): for INTER_LINEAR on 8U the
+// fixed-point generic resize (coefficients (1 - f, f) * 2048 rounded to short,
+// horizontal int sums, vertical (s0 b0 + s1 b1 + 2^21) >> 22); for INTER_AREA
+// with an integer scale resizeAreaFast_ (cvRound(sum * (1.f / area))), with a
+// fractional scale resizeArea_ (computeResizeAreaTab float weights,
+// row-then-column float accumulation, cvRound).  cv2 is not installed here,
+// so this is unpinned (OpenCV's SIMD kernels round some ties differently
+// from its scalar code).
+inline int cv_round(double v) { return (int)std::nearbyint(v); }   // cvRound: round half to even
+inline int cv_floor(double v) { int i = (int)v; return i - (i > v); }
+inline int cv_ceil(double v) { int i = (int)v; return i + (i < v); }
+inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+void cv_resize_8x8(const uint8_t *src, int B, uint8_t *dst)
+{
+    const int S = 8;
+    if (B == S) { for (int i = 0; i < S * S; ++i) dst[i] = src[i]; return; }
+    if (B > S) {   // INTER_LINEAR, 8U, fixed point
+        const double inv_scale = (double)B / S, scale = 1. / inv_scale;
+        int ofs[4096];
+        short alpha[2 * 4096];
+        for (int d = 0; d < B; ++d) {
+            float f = (float)((d + 0.5) * scale - 0.5);
+            int s = cv_floor(f);
+            f -= s;
+            if (s < 0) { f = 0.f; s = 0; }
+            if (s >= S - 1) { f = 0.f; s = S - 1; }
+            ofs[d] = s;
+            alpha[2 * d] = (short)cv_round((1.f - f) * 2048);
+            alpha[2 * d + 1] = (short)cv_round(f * 2048);
+        }
+        std::vector<int> rows((size_t)S * B);
+        for (int y = 0; y < S; ++y)
+            for (int d = 0; d < B; ++d) {
+                const int s = ofs[d];
+                rows[(size_t)y * B + d] = s + 1 < S ? src[y * S + s] * alpha[2 * d] + src[y * S + s + 1] * alpha[2 * d + 1]
+                                                    : src[y * S + s] * 2048;
+            }
+        for (int dy = 0; dy < B; ++dy) {
+            const int sy = ofs[dy], sy1 = sy + 1 < S ? sy + 1 : sy;
+            const int b0 = alpha[2 * dy], b1 = alpha[2 * dy + 1];
+            for (int d = 0; d < B; ++d) {
+                const int v = rows[(size_t)sy * B + d] * b0 + rows[(size_t)sy1 * B + d] * b1;
+                dst[dy * B + d] = sat_u8((v + (1 << 21)) >> 22);
+            }
+        }
+        return;
+    }
+    if (S % B == 0) {   // INTER_AREA, integer scale: resizeAreaFast_
+        const int k = S / B, area = k * k;
+        const float sc = 1.f / area;
+        for (int dy = 0; dy < B; ++dy)
+            for (int dx = 0; dx < B; ++dx) {
+                int sum = 0;
+                for (int y = 0; y < k; ++y)
+                    for (int x = 0; x < k; ++x) sum += src[(dy * k + y) * S + dx * k + x];
+                dst[dy * B + dx] = sat_u8(cv_round(sum * sc));
+            }
+        return;
+    }
+    // INTER_AREA, fractional scale: resizeArea_
+    struct Tab { int di, si; float alpha; };
+    auto area_tab = [&](std::vector<Tab> &tab) {
+        const double scale = (double)S / B;
+        for (int dx = 0; dx < B; ++dx) {
+            const double fsx1 = dx * scale, fsx2 = fsx1 + scale;
+            const double cell = std::min(scale, S - fsx1);
+            int sx1 = cv_ceil(fsx1), sx2 = cv_floor(fsx2);
+            sx2 = std::min(sx2, S - 1);
+            sx1 = std::min(sx1, sx2);
+            if (sx1 - fsx1 > 1e-3) tab.push_back({dx, sx1 - 1, (float)((sx1 - fsx1) / cell)});
+            for (int sx = sx1; sx < sx2; ++sx) tab.push_back({dx, sx, (float)(1.0 / cell)});
+            if (fsx2 - sx2 > 1e-3) tab.push_back({dx, sx2, (float)(std::min(std::min(fsx2 - sx2, 1.), cell) / cell)});
+        }
+    };
+    std::vector<Tab> xt, yt;
+    area_tab(xt);
+    area_tab(yt);
+    std::vector<float> buf(B), sum(B, 0.f);
+    int prev = yt[0].di;
+    for (size_t j = 0; j < yt.size(); ++j) {
+        const float beta = yt[j].alpha;
+        const int dy = yt[j].di, sy = yt[j].si;
+        for (int dx = 0; dx < B; ++dx) buf[dx] = 0.f;
+        for (const Tab &t : xt) buf[t.di] += src[sy * S + t.si] * t.alpha;
+        if (dy != prev) {
+            for (int dx = 0; dx < B; ++dx) {
+                dst[prev * B + dx] = sat_u8(cv_round(sum[dx]));
+                sum[dx] = beta * buf[dx];
+            }
+            prev = dy;
+        } else {
+            for (int dx = 0; dx < B; ++dx) sum[dx] += beta * buf[dx];
+        }
+    }
+    for (int dx = 0; dx < B; ++dx) dst[prev * B + dx] = sat_u8(cv_round(sum[dx]));
+}
+
+// the JPEG tables of -p (2D-DCT.py:66-84), uint8
+constexpr uint8_t kJpegY[64] = {16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55,
+                                14, 13, 16, 24, 40, 57, 69, 56, 14, 17, 22, 29, 51, 87, 80, 62,
+                                18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
+                                49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+constexpr uint8_t kJpegC[64] = {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+                                24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
+                                99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+                                99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+
+// -p weights of block size B in HBM: Y_QSSs / 121 then C_QSSs / 99 (float64,
+// numpy's uint8 / int), B*B each, row-major within the block; per device, kept
+int perceptual_weights(int B, const double *&out)
+{
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, double *> cache;
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc != VCF_OK) return rc;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find({dev, B});
+    if (it != cache.end()) { out = it->second; return VCF_OK; }
+    std::vector<uint8_t> ty((size_t)B * B), tc((size_t)B * B);
+    cv_resize_8x8(kJpegY, B, ty.data());
+    cv_resize_8x8(kJpegC, B, tc.data());
+    std::vector<double> w(2 * (size_t)B * B);
+    for (size_t i = 0; i < (size_t)B * B; ++i) {
+        w[i] = (double)ty[i] / 121.0;
+        w[(size_t)B * B + i] = (double)tc[i] / 99.0;
+    }
+    double *d = nullptr;
+    if ((rc = hip_check(hipMalloc(&d, w.size() * sizeof(double)), "hipMalloc(-p weights)")) != VCF_OK) return rc;
+    if ((rc = hip_check(hipMemcpy(d, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice), "-p weights")) !=
+        VCF_OK)
+        return rc;
+    cache[{dev, B}] = d;
+    out = d;
+    return VCF_OK;
+}
+
 struct RtPlanDev {
     pfft::RtPlan P;
     float *f32 = nullptr;
@@ -559,7 +720,8 @@ unsigned rt_grid(long long units, int B, size_t esz)
     return (unsigned)std::max<long long>(wgs, 1);
 }
 
-int rt_launch_encode(const uint8_t *rgb, void *out, bool k32, const GeomB &g, int B, int Q, hipStream_t s)
+int rt_launch_encode(const uint8_t *rgb, void *out, bool k32, const GeomB &g, int B, int Q, const double *pw,
+                     hipStream_t s)
 {
     RtPlanDev pl;
     int rc = rt_plan(B, pl);
@@ -570,14 +732,15 @@ int rt_launch_encode(const uint8_t *rgb, void *out, bool k32, const GeomB &g, in
     rc = scr.acquire((size_t)grid * rt_ws_per_wg(B) * sizeof(float), s);
     if (rc != VCF_OK) return rc;
     float *ws = (float *)scr.ptr;
-    if (k32) hipLaunchKernelGGL((dct_rt_encode_kernel<true>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws);
-    else hipLaunchKernelGGL((dct_rt_encode_kernel<false>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws);
+    if (k32) hipLaunchKernelGGL((dct_rt_encode_kernel<true>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws, pw);
+    else hipLaunchKernelGGL((dct_rt_encode_kernel<false>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws, pw);
     rc = hip_check(hipGetLastError(), "dct_rt_encode_kernel launch");
     const int rc2 = scr.release(s);
     return rc != VCF_OK ? rc : rc2;
 }
 
-int rt_launch_decode(const void *kin, void *wsout, bool k32, const GeomB &g, int B, int Q, hipStream_t s)
+int rt_launch_decode(const void *kin, void *wsout, bool k32, const GeomB &g, int B, int Q, const double *pw,
+                     hipStream_t s)
 {
     RtPlanDev pl;
     int rc = rt_plan(B, pl);
@@ -588,8 +751,8 @@ int rt_launch_decode(const void *kin, void *wsout, bool k32, const GeomB &g, int
     rc = scr.acquire((size_t)grid * rt_ws_per_wg(B) * sizeof(double), s);
     if (rc != VCF_OK) return rc;
     double *ws = (double *)scr.ptr;
-    if (k32) hipLaunchKernelGGL((dct_rt_decode_kernel<true>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws);
-    else hipLaunchKernelGGL((dct_rt_decode_kernel<false>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws);
+    if (k32) hipLaunchKernelGGL((dct_rt_decode_kernel<true>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws, pw);
+    else hipLaunchKernelGGL((dct_rt_decode_kernel<false>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws, pw);
     rc = hip_check(hipGetLastError(), "dct_rt_decode_kernel launch");
     const int rc2 = scr.release(s);
     return rc != VCF_OK ? rc : rc2;
@@ -612,24 +775,24 @@ int make_geom_b(int H, int W, int B, uint32_t flags, int64_t n_frames, GeomB &g)
 }
 
 template <int B>
-int launch_encode(const uint8_t *rgb, void *out, bool k32, const GeomB &g, int Q, hipStream_t s)
+int launch_encode(const uint8_t *rgb, void *out, bool k32, const GeomB &g, int Q, const double *pw, hipStream_t s)
 {
     constexpr int U = enc_units<B>();
     const long long wgs = (g.units + U - 1) / U;
     if (wgs > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "batch too large");
-    if (k32) hipLaunchKernelGGL((dct_any_encode_kernel<B, true>), dim3((unsigned)wgs), dim3(256), 0, s, rgb, out, g, Q);
-    else hipLaunchKernelGGL((dct_any_encode_kernel<B, false>), dim3((unsigned)wgs), dim3(256), 0, s, rgb, out, g, Q);
+    if (k32) hipLaunchKernelGGL((dct_any_encode_kernel<B, true>), dim3((unsigned)wgs), dim3(256), 0, s, rgb, out, g, Q, pw);
+    else hipLaunchKernelGGL((dct_any_encode_kernel<B, false>), dim3((unsigned)wgs), dim3(256), 0, s, rgb, out, g, Q, pw);
     return hip_check(hipGetLastError(), "dct_any_encode_kernel launch");
 }
 
 template <int B>
-int launch_decode(const void *kin, void *ws, bool k32, const GeomB &g, int Q, hipStream_t s)
+int launch_decode(const void *kin, void *ws, bool k32, const GeomB &g, int Q, const double *pw, hipStream_t s)
 {
     constexpr int U = dec_units<B>();
     const long long wgs = (g.units + U - 1) / U;
     if (wgs > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "batch too large");
-    if (k32) hipLaunchKernelGGL((dct_any_decode_kernel<B, true>), dim3((unsigned)wgs), dim3(128), 0, s, kin, ws, g, Q);
-    else hipLaunchKernelGGL((dct_any_decode_kernel<B, false>), dim3((unsigned)wgs), dim3(128), 0, s, kin, ws, g, Q);
+    if (k32) hipLaunchKernelGGL((dct_any_decode_kernel<B, true>), dim3((unsigned)wgs), dim3(128), 0, s, kin, ws, g, Q, pw);
+    else hipLaunchKernelGGL((dct_any_decode_kernel<B, false>), dim3((unsigned)wgs), dim3(128), 0, s, kin, ws, g, Q, pw);
     return hip_check(hipGetLastError(), "dct_any_decode_kernel launch");
 }
 
@@ -666,9 +829,9 @@ int check_any(const void *a, const void *b, int64_t n_frames, int H, int W, int 
                          B);
     if (Q < 1 || (decode && !k32 && Q > 32767))
         return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
-    if (flags & VCF_DCT_PERCEPTUAL)
+    if ((flags & VCF_DCT_PERCEPTUAL) && k32)
         return set_error(VCF_ERR_UNSUPPORTED,
-                         "perceptual quantization is only available for block_size=8 (2D-DCT.py:100-105)");
+                         "the -L search runs without perceptual quantization (2D-DCT.py:100-105)");
     if (flags & ~(VCF_DCT_NO_SUBBANDS | VCF_DCT_PERCEPTUAL))
         return set_error(VCF_ERR_INVALID, "unknown flags 0x%x", flags);
     const long long Hp = (H + B - 1) / B * (long long)B, Wp = (W + B - 1) / B * (long long)B;
@@ -686,10 +849,12 @@ int any_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, i
     GeomB g;
     make_geom_b(H, W, B, flags, n_frames, g);
     const hipStream_t s = (hipStream_t)stream;
-#define VCF_ENC_ANY(b) launch_encode<b>(rgb_dev, k_dev, k32, g, Q, s)
+    const double *pw = nullptr;
+    if ((flags & VCF_DCT_PERCEPTUAL) && (rc = perceptual_weights(B, pw)) != VCF_OK) return rc;
+#define VCF_ENC_ANY(b) launch_encode<b>(rgb_dev, k_dev, k32, g, Q, pw, s)
     VCF_ANY_SWITCH(B, VCF_ENC_ANY)
 #undef VCF_ENC_ANY
-    return rt_launch_encode(rgb_dev, k_dev, k32, g, B, Q, s);
+    return rt_launch_encode(rgb_dev, k_dev, k32, g, B, Q, pw, s);
 }
 
 int any_decode(const void *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t B, int32_t Q, uint32_t flags,
@@ -700,6 +865,8 @@ int any_decode(const void *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_
     rc = ensure_tables();
     if (rc != VCF_OK) return rc;
     const hipStream_t s = (hipStream_t)stream;
+    const double *pw = nullptr;
+    if ((flags & VCF_DCT_PERCEPTUAL) && (rc = perceptual_weights(B, pw)) != VCF_OK) return rc;
     GeomB g0;
     make_geom_b(H, W, B, flags, 1, g0);
     const size_t esz = k32 ? 4 : 2;
@@ -718,10 +885,10 @@ int any_decode(const void *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_
         make_geom_b(H, W, B, flags, n, g);
         const void *kin = (const uint8_t *)k_dev + (size_t)f0 * g.out_stride * kesz;
         auto pass1 = [&]() -> int {
-#define VCF_DEC_ANY(b) launch_decode<b>(kin, ws, k32, g, Q, s)
+#define VCF_DEC_ANY(b) launch_decode<b>(kin, ws, k32, g, Q, pw, s)
             VCF_ANY_SWITCH(B, VCF_DEC_ANY)
 #undef VCF_DEC_ANY
-            return rt_launch_decode(kin, ws, k32, g, B, Q, s);
+            return rt_launch_decode(kin, ws, k32, g, B, Q, pw, s);
         };
         rc = pass1();
         if (rc != VCF_OK) break;
@@ -758,6 +925,15 @@ extern "C" {
 int vcf_dct_block_size_supported(int32_t block_size)
 {
     return vcf::slot_of(block_size) >= 0 || vcf::rt_covered(block_size) ? 1 : 0;
+}
+
+int vcf_dct_perceptual_tables(int32_t block_size, uint8_t *y_qss, uint8_t *c_qss)
+{
+    if (!y_qss || !c_qss) return vcf::set_error(VCF_ERR_INVALID, "null buffer");
+    if (block_size < 1 || block_size > vcf::kRtMaxB) return vcf::set_error(VCF_ERR_INVALID, "block size %d", block_size);
+    vcf::cv_resize_8x8(vcf::kJpegY, block_size, y_qss);
+    vcf::cv_resize_8x8(vcf::kJpegC, block_size, c_qss);
+    return VCF_OK;
 }
 
 int vcf_dct_dz_encode_k32(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
