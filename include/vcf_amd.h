@@ -54,6 +54,7 @@ extern "C" {
 #define VCF_DTYPE_I16 2
 #define VCF_DTYPE_I32 3
 #define VCF_DTYPE_U8 4
+#define VCF_DTYPE_U16 5
 
 /* flags of the DCT path */
 #define VCF_DCT_NO_SUBBANDS 1u   /* -x, --disable_subbands  (2D-DCT.py:40)  */
@@ -171,6 +172,17 @@ int vcf_dct_dz_encode_k32(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, i
                           int32_t Q, uint32_t flags, int32_t *k_dev, void *stream);
 int vcf_dct_dz_decode_k32(const int32_t *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
                           int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream);
+
+/* encode_fn / decode_fn with a quantizer other than deadzone (-a LloydMax):
+ * 2D-DCT.py:106-109 sets self.offset = 0, so there is no -128 before the
+ * colour transform and no +128 on the pixels; the quantizer sees the float32
+ * coefficients (subband layout unless -x, -p weights applied, :313-340) and
+ * hands back int16 coefficients (:399-410).  Replaces the same spans as
+ * vcf_dct_dz_encode/decode minus the deadzone quantizer; any supported B. */
+int vcf_dct_raw_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
+                       uint32_t flags, float *coef_dev, void *stream);
+int vcf_dct_raw_decode(const int16_t *coef_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
+                       uint32_t flags, uint8_t *rgb_dev, void *stream);
 
 /* Same as vcf_dct_dz_decode with an explicit kernel choice (A/B tests and
  * benchmarks): 0 = automatic (2), 1 = lane-per-block (one block's 64 float64
@@ -387,6 +399,41 @@ int vcf_deadzone_quantize(const void *x_dev, int32_t x_dtype, int64_t n, int32_t
  * Replaces deadzone.CoDec.dequantize_fn (deadzone.py:107-117). */
 int vcf_deadzone_dequantize(const void *k_dev, int32_t k_dtype, int64_t n, int32_t Q, void *y_dev,
                             void *stream);
+
+/* ---- §8(f) row 4: the YCrCb and LloydMax plug-ins ------------------------------
+ * YCrCb (src/YCrCb.py:25-72): the stand-alone pixel codec.  Its transform,
+ * color_transforms.YCrCb, is not vendored: OpenCV's integer RGB<->YCrCb on
+ * uint8 is assumed (A11; parity unpinned).  n_px pixels of 3 interleaved
+ * channels.  Note: 2D-DCT.py / 2D-DWT.py with -t YCrCb still convert with
+ * YCoCg (they bind from_RGB/to_RGB from color_transforms.YCoCg, 2D-DCT.py:22-23,
+ * 2D-DWT.py:19-20), so they use the YCoCg entry points above. */
+int vcf_ycrcb_from_rgb(const uint8_t *rgb_dev, int64_t n_px, uint8_t *ycrcb_dev, void *stream);
+int vcf_ycrcb_to_rgb(const uint8_t *ycrcb_dev, int64_t n_px, uint8_t *rgb_dev, void *stream);
+/* YCrCb.encode (:33-51) with -a deadzone: from_RGB, int16, (x / Q) truncated, uint16. */
+int vcf_ycrcb_dz_encode(const uint8_t *rgb_dev, int64_t n_px, int32_t Q, uint16_t *k_dev, void *stream);
+/* YCrCb.decode (:53-72): Q * k in uint16, int16, uint8, to_RGB, clip. */
+int vcf_ycrcb_dz_decode(const uint16_t *k_dev, int64_t n_px, int32_t Q, uint8_t *rgb_dev, void *stream);
+
+/* LloydMax (src/LloydMax.py:75-143).  Per channel c of an n_px x channels
+ * array: counts = numpy.histogram(x[..., c], bins=max-min+1, range=(min, max))
+ * (numpy 1.26's arithmetic; int64 counts, channel-major, zeroed here), the
+ * glue's +1, the Lloyd-Max design of scalar_quantization's LloydMax_Quantizer
+ * (un-vendored; A12, unpinned: the textbook design, oracle/plugins.py),
+ * k = searchsorted(thresholds, x, 'right') stored with a C cast into k's type,
+ * y = centroids[k] truncated into y's integer type.  dtypes: VCF_DTYPE_U8,
+ * I16, U16, F32 (histogram/encode input, encode output).  vcf_lm_levels returns
+ * the number of levels N = ceil((max - min + 1) / Q) or an error (< 0). */
+int vcf_lm_levels(int32_t Q_step, int32_t min_val, int32_t max_val);
+int vcf_lm_histogram(const void *x_dev, int32_t x_dtype, int64_t n_px, int32_t channels, int32_t min_val,
+                     int32_t max_val, int64_t *counts_dev, void *stream);
+/* Host memory: counts (n_bins, already +1) -> centroids (N doubles); returns N or an error. */
+int vcf_lm_design(const int64_t *counts, int32_t n_bins, int32_t Q_step, int32_t min_val, double *centroids);
+/* centroids_dev: channels x n_levels doubles (channel-major). */
+int vcf_lm_encode(const void *x_dev, int32_t x_dtype, int64_t n_px, int32_t channels, const double *centroids_dev,
+                  int32_t n_levels, void *k_dev, int32_t k_dtype, void *stream);
+/* *bad_dev is set to 1 when an index is outside [-N, N) (numpy's IndexError); the caller zeroes it. */
+int vcf_lm_decode(const void *k_dev, int32_t k_dtype, int64_t n_px, int32_t channels, const double *centroids_dev,
+                  int32_t n_levels, void *y_dev, int32_t y_dtype, int32_t *bad_dev, void *stream);
 
 /* ---- cross-rank exchange on RCCL over xGMI -------------------
  * Frames shard across one process per GPU with no collective on the data

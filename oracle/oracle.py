@@ -68,6 +68,9 @@ def lib():
                                          ctypes.c_double, u8p, dp]
         L.vcfo_dct_dz_decode_k32_b.argtypes = [i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_uint, u8p]
+        L.vcfo_dct_raw_encode_b.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint, fp]
+        L.vcfo_dct_raw_decode_b.argtypes = [ctypes.POINTER(ctypes.c_int16), ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_uint, u8p]
         L.vcfo_perceptual_weights.argtypes = [dp]
         L.vcfo_dct_perceptual_tables.argtypes = [ctypes.c_int, u8p, u8p]
         # 2D-DWT path (vcf_dwt_oracle.cpp)
@@ -184,6 +187,32 @@ def decode_frame_b(k: np.ndarray, H: int, W: int, B: int, Q: int = 32, flags: in
     else:
         k = np.ascontiguousarray(k, dtype=np.uint8)
         rc = lib().vcfo_dct_dz_decode_b(_u8(k), H, W, B, int(Q), flags, _u8(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle decode failed ({rc})")
+    return out
+
+
+def dct_raw_encode_b(rgb: np.ndarray, B: int, flags: int = 0) -> np.ndarray:
+    """encode_fn with a quantizer other than deadzone (offset 0, 2D-DCT.py:106-109): the
+    float32 HpxWpx3 coefficients (subband layout unless -x) handed to quantize_decom."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    H, W = rgb.shape[:2]
+    Hp, Wp = padded_shape(H, W, B)
+    out = np.empty((Hp, Wp, 3), np.float32)
+    rc = lib().vcfo_dct_raw_encode_b(_u8(rgb), H, W, B, flags, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    if rc != 0:
+        raise RuntimeError(f"oracle encode failed ({rc})")
+    return out
+
+
+def dct_raw_decode_b(y: np.ndarray, H: int, W: int, B: int, flags: int = 0) -> np.ndarray:
+    """decode_fn after another quantizer's dequantize_decom: int16 HpxWpx3 coefficients -> u8 HxWx3."""
+    Hp, Wp = padded_shape(H, W, B)
+    y = np.ascontiguousarray(y, dtype=np.int16)
+    if y.shape != (Hp, Wp, 3):
+        raise ValueError(f"coefficient array shape {y.shape} != {(Hp, Wp, 3)}")
+    out = np.empty((H, W, 3), np.uint8)
+    rc = lib().vcfo_dct_raw_decode_b(y.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)), H, W, B, flags, _u8(out))
     if rc != 0:
         raise RuntimeError(f"oracle decode failed ({rc})")
     return out

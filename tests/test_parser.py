@@ -44,7 +44,7 @@ def test_unsupported_options_raise():
     from vcf_amd.codec.dct2d import CoDec
     p = P.dct_parser()
     for argv in (["encode", "-B", "191"], ["encode", "-B", "5000"],
-                 ["encode", "-t", "YCrCb"], ["encode", "-a", "LloydMax"],
+                 ["encode", "-t", "color-DCT"], ["encode", "-a", "VQ"],
                  ["encode", "-c", "PNG"], ["decode", "-f", "gaussian_blur"]):
         with pytest.raises(NotImplementedError):
             CoDec(P.parse(p, argv))

@@ -22,6 +22,7 @@ VCF_DTYPE_F64 = 1
 VCF_DTYPE_I16 = 2
 VCF_DTYPE_I32 = 3
 VCF_DTYPE_U8 = 4
+VCF_DTYPE_U16 = 5
 
 VCF_DCT_NO_SUBBANDS = 1
 VCF_DCT_PERCEPTUAL = 2
@@ -85,6 +86,17 @@ SIGNATURES = {
     "vcf_dct_dz_decode_any": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_encode_k32": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_decode_k32": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dct_raw_encode": [_P, _I64, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dct_raw_decode": [_P, _I64, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_ycrcb_from_rgb": [_P, _I64, _P, _P],
+    "vcf_ycrcb_to_rgb": [_P, _I64, _P, _P],
+    "vcf_ycrcb_dz_encode": [_P, _I64, _I32, _P, _P],
+    "vcf_ycrcb_dz_decode": [_P, _I64, _I32, _P, _P],
+    "vcf_lm_levels": [_I32, _I32, _I32],
+    "vcf_lm_histogram": [_P, _I32, _I64, _I32, _I32, _I32, _P, _P],
+    "vcf_lm_design": [_P, _I32, _I32, _I32, _P],
+    "vcf_lm_encode": [_P, _I32, _I64, _I32, _P, _I32, _P, _I32, _P],
+    "vcf_lm_decode": [_P, _I32, _I64, _I32, _P, _I32, _P, _I32, _P, _P],
     "vcf_wavelet_index": [ctypes.c_char_p, _PI32],
     "vcf_dwt_layout": [_I32, _I32, _I32, _PI32, _PI32, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     "vcf_dwt_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
@@ -163,9 +175,11 @@ def lib():
     return _lib
 
 
-def check(status: int) -> None:
-    if status == VCF_OK:
-        return
+def check(status: int) -> int:
+    """Raise for a negative status; a non-negative one (VCF_OK, or a count such as
+    vcf_lm_levels' N) is returned."""
+    if status >= VCF_OK:
+        return status
     msg = lib().vcf_last_error().decode(errors="replace")
     if status == VCF_ERR_INVALID:
         raise VCFInvalidArgument(status, msg)
@@ -174,5 +188,5 @@ def check(status: int) -> None:
     raise VCFError(status, msg)
 
 
-def call(name: str, *args) -> None:
-    check(getattr(lib(), name)(*args))
+def call(name: str, *args) -> int:
+    return check(getattr(lib(), name)(*args))

@@ -13,10 +13,16 @@ implementation of it in the product.
 that pocketfft plans with rfftp, vcf_dct_block_size_supported; not the
 Bluestein lengths, the first of which is 191), -L runs optimize_block_size
 (2D-DCT.py:533-579) with the GPU doing each candidate's analysis/synthesis.
-Options the HIP path does not implement raise NotImplementedError when the
-codec is constructed (Bluestein block sizes, colour transforms
-other than YCoCg, quantizers other than deadzone, filters other than
-no_filter); entropy codecs come from ENTROPY_CODECS.
+-t YCrCb runs exactly as -t YCoCg: 2D-DCT.py binds from_RGB/to_RGB from
+color_transforms.YCoCg at import (:22-23) and -t only picks the base class
+(:54-56), whose encode/decode it overrides.  -a LloydMax (LloydMax.py) sets
+the offset to 0 (:106-109): the GPU hands the float32 coefficients to the
+Lloyd-Max quantizer (histogram, design, encoder on the GPU,
+codec/quantizers.py) and decodes from its int16 output.  Options the HIP
+path does not implement raise NotImplementedError when the codec is
+constructed (Bluestein block sizes, other colour transforms, quantizers
+other than deadzone and LloydMax, filters other than no_filter, -L with
+LloydMax); entropy codecs come from ENTROPY_CODECS.
 """
 from __future__ import annotations
 
@@ -27,7 +33,9 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 from .. import dct as D
+from ..device import DeviceBuffer
 from .eic import CoDec as EICCoDec
+from .quantizers import LloydMaxQuantizer
 from .tiff import TIFFCodec
 
 
@@ -55,6 +63,26 @@ def register_entropy_codec(name, cls):
     ENTROPY_CODECS[name] = cls
 
 
+def make_entropy(args):
+    """The entropy codec named by -c (no_filter.py:14-21)."""
+    ec_name = getattr(args, "entropy_image_codec", "TIFF")
+    if ec_name not in ENTROPY_CODECS:
+        raise NotImplementedError(f"entropy codec {ec_name!r} (have: {sorted(ENTROPY_CODECS)})")
+    maker = ENTROPY_CODECS[ec_name]
+    return maker(args) if maker in (_cbaac, _cbahc, _tcbaac) else maker()
+
+
+def make_quantizer(args):
+    """None for -a deadzone (fused into the transform kernels), else the LloydMax plug-in."""
+    quant = getattr(args, "quantizer", "deadzone")
+    if quant == "deadzone":
+        return None
+    if quant == "LloydMax":
+        return LloydMaxQuantizer(int(getattr(args, "QSS", 32)), int(getattr(args, "min_val", 0)),
+                                 int(getattr(args, "max_val", 255)))
+    raise NotImplementedError(f"quantizer {quant!r}: deadzone and LloydMax are on the HIP path")
+
+
 def _flags(args) -> int:
     return D.flags_from(bool(getattr(args, "disable_subbands", False)),
                         bool(getattr(args, "perceptual_quantization", False)))
@@ -68,28 +96,25 @@ class CoDec(EICCoDec):
         super().__init__(args)
         self.block_size = int(getattr(args, "block_size_DCT", 8))
         ct = getattr(args, "color_transform", "YCoCg")
-        if ct != "YCoCg":
-            raise NotImplementedError(f"color transform {ct!r}: only YCoCg is on the HIP path")
-        quant = getattr(args, "quantizer", "deadzone")
-        if quant != "deadzone":
-            raise NotImplementedError(f"quantizer {quant!r}: only deadzone is on the HIP path")
+        if ct not in ("YCoCg", "YCrCb"):
+            raise NotImplementedError(f"color transform {ct!r}: YCoCg (and YCrCb, which 2D-DCT.py runs as "
+                                      "YCoCg) are on the HIP path")
+        self.lm = make_quantizer(args)
         filt = getattr(args, "filter", "no_filter")
         if not self.encoding and filt != "no_filter":
             raise NotImplementedError(f"filter {filt!r}: only no_filter is on the HIP path")
         if not D.block_size_supported(self.block_size):
             raise NotImplementedError(f"block size {self.block_size}: the HIP path covers every B <= 4096 "
                                       "that pocketfft plans with rfftp (not its Bluestein lengths)")
-        ec_name = getattr(args, "entropy_image_codec", "TIFF")
-        if ec_name not in ENTROPY_CODECS:
-            raise NotImplementedError(f"entropy codec {ec_name!r} (have: {sorted(ENTROPY_CODECS)})")
-        maker = ENTROPY_CODECS[ec_name]
-        self.entropy = maker(args) if maker in (_cbaac, _cbahc, _tcbaac) else maker()
+        self.entropy = make_entropy(args)
         self.file_extension = self.entropy.file_extension
         self.QSS = int(getattr(args, "QSS", 32))
-        self.offset = 128            # 2D-DCT.py:102-105 (quantizer == deadzone)
+        self.offset = 128 if self.lm is None else 0    # 2D-DCT.py:106-109
         self.flags = _flags(args)
         self.original_shape = None
         self.Lambda = None
+        if self.encoding and getattr(args, "Lambda", None) is not None and self.lm is not None:
+            raise NotImplementedError("-L with -a LloydMax: the search's quantizer calls are not on the HIP path")
         if self.encoding and getattr(args, "Lambda", None) is not None:
             # 2D-DCT.py:99-105
             if not getattr(args, "perceptual_quantization", False):
@@ -180,21 +205,65 @@ class CoDec(EICCoDec):
         if img.dtype != np.uint8 or img.shape[2] != 3:
             raise NotImplementedError(f"{img.dtype} x{img.shape[2]} images: the HIP path takes u8 RGB")
 
+    def _deadzone_only(self, what):
+        if self.lm is not None:
+            raise NotImplementedError(f"{what} with -a LloydMax (use encode_fn/decode_fn)")
+
+    def encode_lm(self, img: np.ndarray) -> np.ndarray:
+        """2D-DCT.py:276-361 with -a LloydMax: offset 0, the float32 coefficients
+        (subbands, -p) on the GPU, LloydMax.quantize_fn (side files at
+        /tmp/encoded, as quantize_decom's default), k = float32 indices -> uint8 (:361)."""
+        self._check_frame(img)
+        self.original_shape = img.shape
+        H, W = img.shape[:2]
+        Hp, Wp = D.padded_shape(H, W, self.block_size)
+        src = DeviceBuffer.from_array(img)
+        coef = D.raw_encode_device(src, 1, H, W, self.flags, block_size=self.block_size)
+        src.free()
+        k = self.lm.quantize_device(coef, np.float32, Hp * Wp, 3, np.uint8)
+        coef.free()
+        self.total_output_size += self.lm.codebook_bytes   # LloydMax.py:107-108
+        self.lm.codebook_bytes = 0
+        out = k.download(np.empty((Hp, Wp, 3), np.uint8))
+        k.free()
+        return out
+
+    def decode_lm(self, k: np.ndarray, shape) -> np.ndarray:
+        """2D-DCT.py:399-466 with -a LloydMax: uint8 k -> int16, centroids (from /tmp/encoded's
+        side files, LloydMax.dequantize_fn) truncated into int16, then the GPU synthesis, offset 0."""
+        H, W = int(shape[0]), int(shape[1])
+        Hp, Wp = D.padded_shape(H, W, self.block_size)
+        k = np.ascontiguousarray(k, dtype=np.uint8)
+        if k.shape != (Hp, Wp, 3):
+            raise ValueError(f"index frame {k.shape} does not match {(Hp, Wp, 3)} for {H}x{W}")
+        dk = DeviceBuffer.from_array(k)
+        y = self.lm.dequantize_device(dk, np.uint8, Hp * Wp, 3, np.int16)
+        dk.free()
+        rgb = D.raw_decode_device(y, 1, H, W, self.flags, block_size=self.block_size)
+        y.free()
+        out = rgb.download(np.empty((H, W, 3), np.uint8))
+        rgb.free()
+        return out
+
     def encode_indices(self, img: np.ndarray) -> np.ndarray:
         """2D-DCT.py:276-361 on the GPU: u8 RGB -> u8 indices (k + 128, wrapped)."""
+        self._deadzone_only("encode_indices")
         self._check_frame(img)
         self.original_shape = img.shape
         return D.encode(img, self.QSS, self.flags, self.block_size)
 
     def decode_indices(self, k: np.ndarray, shape) -> np.ndarray:
         """2D-DCT.py:399-466 on the GPU: u8 indices -> u8 RGB (padding removed)."""
+        self._deadzone_only("decode_indices")
         H, W = int(shape[0]), int(shape[1])
         return D.decode(np.ascontiguousarray(k, dtype=np.uint8), H, W, self.QSS, self.flags,
                         self.block_size)
 
     def encode_fn(self, in_fn, out_fn):
         img = self.encode_read_fn(in_fn)
-        if hasattr(self.entropy, "compress_device"):
+        if self.lm is not None:
+            cs = self.compress(self.encode_lm(img))
+        elif hasattr(self.entropy, "compress_device"):
             cs = self._encode_compress_device(img)
         else:
             cs = self.compress(self.encode_indices(img))
@@ -226,7 +295,10 @@ class CoDec(EICCoDec):
         with open(f"{in_fn}_shape.bin", "rb") as f:
             self.original_shape = struct.unpack("iii", f.read(12))
         k = self.decompress(codestream)
-        y = self.decode_indices(k, self.original_shape)
+        if self.lm is not None:
+            y = self.decode_lm(k, self.original_shape)
+        else:
+            y = self.decode_indices(k, self.original_shape)
         return self.decode_write_fn(y, out_fn)
 
     def decode(self, in_fn="/tmp/encoded", out_fn="/tmp/decoded.png"):
@@ -245,6 +317,8 @@ class CoDec(EICCoDec):
         pairs = list(pairs)
         if not pairs:
             return []
+        if self.lm is not None:   # one histogram and design per frame: frame by frame
+            return [self.encode_fn(i, o) for i, o in pairs]
         staged = self._encode_fns_staged(pairs, batch, io_threads)
         if staged is not None:
             return staged
@@ -353,6 +427,8 @@ class CoDec(EICCoDec):
         pairs = list(pairs)
         if not pairs:
             return []
+        if self.lm is not None:
+            return [self.decode_fn(i, o) for i, o in pairs]
         sizes = [0] * len(pairs)
         batches = [pairs[b0:b0 + batch] for b0 in range(0, len(pairs), batch)]
 
@@ -394,9 +470,13 @@ class CoDec(EICCoDec):
         return self.dequantize(decom_k)
 
     def quantize(self, img, fn="/tmp/encoded"):
+        if self.lm is not None:
+            return self.lm.quantize(img, fn)
         from .. import quant
         return quant.deadzone_quantize(img, self.QSS)
 
     def dequantize(self, k, fn="/tmp/encoded"):
+        if self.lm is not None:
+            return self.lm.dequantize(k, fn)
         from .. import quant
         return quant.deadzone_dequantize(k, self.QSS)

@@ -29,8 +29,12 @@ class CoDec(EICCoDec):
         self.wavelet = str(getattr(args, "wavelet", "db5"))
         DW.wavelet_index(self.wavelet)            # ValueError for names pywt does not know
         ct = getattr(args, "color_transform", "YCoCg")
-        if ct != "YCoCg":
-            raise NotImplementedError(f"color transform {ct!r}: only YCoCg is on the HIP path")
+        # -t YCrCb only changes the base class: 2D-DWT.py binds from_RGB/to_RGB from
+        # color_transforms.YCoCg at import (:19-20), so the arithmetic stays YCoCg's
+        # (tests/golden/manifest_plugins.json "same_as_ycocg")
+        if ct not in ("YCoCg", "YCrCb"):
+            raise NotImplementedError(f"color transform {ct!r}: YCoCg (and YCrCb, which 2D-DWT.py runs as "
+                                      "YCoCg) are on the HIP path")
         quant = getattr(args, "quantizer", "deadzone")
         if quant != "deadzone":
             raise NotImplementedError(f"quantizer {quant!r}: only deadzone is on the HIP path")

@@ -91,6 +91,9 @@ class _IPP:
 
     def __init__(self, args, group=None):
         super().__init__(args)
+        if getattr(self, "lm", None) is not None:
+            # the GOP loop keeps indices in HBM through the fused deadzone kernels
+            raise NotImplementedError("IPP with -a LloydMax: only deadzone is on the HIP path")
         self.gop_size = getattr(args, "gop_size", 10) or 10
         self.block_size_ME = getattr(args, "block_size_ME", 16) or 16
         self.search_range = getattr(args, "search_range", 8)

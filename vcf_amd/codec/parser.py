@@ -98,6 +98,29 @@ def add_deadzone(enc, dec):
                      help=f"Denoising filter (default: {DEFAULT_FILTER})", default=DEFAULT_FILTER)
 
 
+def add_lloydmax(enc, dec):
+    """LloydMax.py:27-35: -q as deadzone's, plus -m/--min_val and -n/--max_val (and -f on decode)."""
+    add_deadzone(enc, dec)
+    for p in (enc, dec):
+        p.add_argument("-m", "--min_val", type=int_or_str, help="Default min_val (default: 0)", default=0)
+        p.add_argument("-n", "--max_val", type=int_or_str, help="Default max_val (default: 255)", default=255)
+
+
+def add_quantizer(enc, dec, quantizer: str = DEFAULT_QUANTIZER):
+    """The options of the module -a names (YCoCg.py:21 imports it)."""
+    if quantizer == "LloydMax":
+        add_lloydmax(enc, dec)
+    else:
+        add_deadzone(enc, dec)
+
+
+def quantizer_of(argv) -> str:
+    """Pre-parse -a/--quantizer, as the reference's import chain does (YCoCg.py:20-21)."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("-a", "--quantizer", default=DEFAULT_QUANTIZER)
+    return pre.parse_known_args(argv)[0].quantizer
+
+
 def add_ycocg(enc, dec):
     """YCoCg.py:17-19."""
     enc.add_argument("-a", "--quantizer", help=f"Quantizer (default: {DEFAULT_QUANTIZER})",
@@ -147,12 +170,12 @@ def add_iii(enc, dec):
 
 
 def dct_parser(description: str = "Exploiting spatial redundancy with the 2D Discrete Cosine "
-                                  "Transform of constant block size."):
-    """The parser `python 2D-DCT.py ...` ends up with (default codec chain)."""
+                                  "Transform of constant block size.", quantizer: str = DEFAULT_QUANTIZER):
+    """The parser `python 2D-DCT.py ...` ends up with (the codec chain -a names)."""
     p, enc, dec = base_parser(description)
     add_dct(enc, dec)
     add_ycocg(enc, dec)
-    add_deadzone(enc, dec)
+    add_quantizer(enc, dec, quantizer)
     add_filter(enc, dec)
     add_eic(enc, dec)
     return p
@@ -181,6 +204,26 @@ def iii_parser(description: str = "III coding: runs a 2D image codec for each im
         add_dct(enc, dec)
     add_ycocg(enc, dec)
     add_deadzone(enc, dec)
+    add_filter(enc, dec)
+    add_eic(enc, dec)
+    return p
+
+
+def lloydmax_parser(description: str = "Image quantization using a LloydMax quantizer."):
+    """`python LloydMax.py ...` (LloydMax.py -> no_filter.py -> TIFF.py)."""
+    p, enc, dec = base_parser(description)
+    add_lloydmax(enc, dec)
+    add_filter(enc, dec)
+    add_eic(enc, dec)
+    return p
+
+
+def ycrcb_parser(description: str = "Exploiting color (perceptual) redundancy with the YCrCb transform.",
+                 quantizer: str = DEFAULT_QUANTIZER):
+    """`python YCrCb.py ...` (YCrCb.py -> <quantizer>.py -> no_filter.py -> TIFF.py)."""
+    p, enc, dec = base_parser(description)
+    add_ycocg(enc, dec)        # YCrCb.py:17-19 adds the same -a option
+    add_quantizer(enc, dec, quantizer)
     add_filter(enc, dec)
     add_eic(enc, dec)
     return p

@@ -30,7 +30,11 @@
 //     int32, the IDCT stored into int32, to_RGB in int32).  The search runs
 //     from CoDec.__init__ (:99-103) before the deadzone offset of 128 is set
 //     (:106-109), so self.offset is still YCoCg's [0, 0, 0] (YCoCg.py:28-29):
-//     no -128 before the colour transform and no +128 on k or the pixels.
+//     no -128 before the colour transform and no +128 on k or the pixels;
+//   float32 / int16 coefficients ("raw": encode_fn/decode_fn with a quantizer
+//     other than deadzone, e.g. -a LloydMax: offset 0 (:106-109), the float32
+//     coefficients handed to quantize_decom (:340) and the int16 ones its
+//     dequantize_decom returns (:410); the quantizer runs in vcf_plugins.hip).
 // These are not the headline kernels (the 8x8 path is); they favour a small,
 // uniform implementation over peak bandwidth.
 #include <hip/hip_runtime.h>
@@ -125,10 +129,13 @@ __device__ __forceinline__ void unit_coords(const GeomB &g, long long u, long lo
 }
 
 template <int B> constexpr int enc_units() { return B >= 256 ? 1 : 256 / B; }
+
+// index type of a launch: encode_fn's u8 (k + 128), the -L search's int32, or raw coefficients
+enum Mode : int { kU8 = 0, kK32 = 1, kRaw = 2 };
 template <int B> constexpr int dec_units() { return B >= 128 ? 1 : 128 / B; }
 
-// ---- encode: RGB u8 -> k (u8 = k + 128 wrapped, or int32 k) --------------
-template <int B, bool K32>
+// ---- encode: RGB u8 -> k (u8 = k + 128 wrapped, int32 k, or float32 coefficients) --
+template <int B, int M>
 __global__ __launch_bounds__(256) void dct_any_encode_kernel(const uint8_t *__restrict__ rgb,
                                                             void *__restrict__ out, GeomB g, int Q,
                                                             const double *__restrict__ pw)
@@ -159,7 +166,7 @@ __global__ __launch_bounds__(256) void dct_any_encode_kernel(const uint8_t *__re
                 const uint8_t *p = img + ((long long)sy * g.W + sx) * 3;
                 R = (float)p[0]; G = (float)p[1]; Bl = (float)p[2];
             }
-            if constexpr (!K32) { R = R - 128.f; G = G - 128.f; Bl = Bl - 128.f; }
+            if constexpr (M == kU8) { R = R - 128.f; G = G - 128.f; Bl = Bl - 128.f; }
             float o;
             if (c == 0) o = (R / 4.f + G / 2.f) + Bl / 4.f;
             else if (c == 1) o = R / 2.f - Bl / 2.f;
@@ -187,16 +194,20 @@ __global__ __launch_bounds__(256) void dct_any_encode_kernel(const uint8_t *__re
         // :343 quantize (A5: (x / Q).astype(int32)), :348 += 128, :361 uint8
 #pragma unroll
         for (int j = 0; j < B; ++j) {
-            const int k = (int)__fdiv_rn(v[j], q);
             const long long o = f * g.out_stride + coef_offset<B>(g, by, bx, y, j) + c;
-            if constexpr (K32) ((int32_t *)out)[o] = k;
-            else ((uint8_t *)out)[o] = (uint8_t)(k + 128);
+            if constexpr (M == kRaw) {
+                ((float *)out)[o] = v[j];
+            } else {
+                const int k = (int)__fdiv_rn(v[j], q);
+                if constexpr (M == kK32) ((int32_t *)out)[o] = k;
+                else ((uint8_t *)out)[o] = (uint8_t)(k + 128);
+            }
         }
     }
 }
 
 // ---- decode, pass 1: k -> IDCT'd integers in a padded-frame workspace ------
-template <int B, bool K32>
+template <int B, int M>
 __global__ __launch_bounds__(128) void dct_any_decode_kernel(const void *__restrict__ kin,
                                                             void *__restrict__ ws, GeomB g, int Q,
                                                             const double *__restrict__ pw)
@@ -219,13 +230,18 @@ __global__ __launch_bounds__(128) void dct_any_decode_kernel(const void *__restr
 #pragma unroll
         for (int i = 0; i < B; ++i) {
             const long long o = f * g.out_stride + coef_offset<B>(g, by, bx, i, x) + c;
-            if constexpr (K32) {
+            if constexpr (M == kK32) {
                 // :560-562 decom_k (int32) -> dequantize Q*k in int32
                 v[i] = (double)(int32_t)((uint32_t)Q * (uint32_t)((const int32_t *)kin)[o]);
             } else {
-                // :399-411 astype(int16) - 128, Q*k in int16 (A5)
-                const int16_t k = (int16_t)((int)((const uint8_t *)kin)[o] - 128);
-                int16_t y16 = (int16_t)(Q * (int)k);
+                int16_t y16;
+                if constexpr (M == kRaw) {
+                    y16 = ((const int16_t *)kin)[o];   // :410 the other quantizer's int16 output
+                } else {
+                    // :399-411 astype(int16) - 128, Q*k in int16 (A5)
+                    const int16_t k = (int16_t)((int)((const uint8_t *)kin)[o] - 128);
+                    y16 = (int16_t)(Q * (int)k);
+                }
                 if (pw) {   // :421-435 -p: float32 block /= QSSs / 121 (or 99), stored back into int16
                     const float f = (float)((double)(float)y16 / pw[(c ? B * B : 0) + i * B + x]);
                     y16 = (int16_t)(int)f;
@@ -250,14 +266,14 @@ __global__ __launch_bounds__(128) void dct_any_decode_kernel(const void *__restr
 #pragma unroll
         for (int j = 0; j < B; ++j) {
             const long long o = f * ((long long)g.Hp * g.Wp * 3) + (row * g.Wp + (long long)bx * B + j) * 3 + c;
-            if constexpr (K32) ((int32_t *)ws)[o] = (int32_t)v[j];
+            if constexpr (M == kK32) ((int32_t *)ws)[o] = (int32_t)v[j];
             else ((int16_t *)ws)[o] = (int16_t)(int32_t)v[j];
         }
     }
 }
 
-// ---- decode, pass 2: crop, to_RGB, += 128, clip, uint8 ---------------------
-template <bool K32>
+// ---- decode, pass 2: crop, to_RGB, += 128 (0 in raw mode), clip, uint8 -----
+template <int M>
 __global__ __launch_bounds__(256) void dct_any_to_rgb_kernel(const void *__restrict__ ws, uint8_t *__restrict__ rgb,
                                                              GeomB g, long long n_px)
 {
@@ -269,7 +285,7 @@ __global__ __launch_bounds__(256) void dct_any_to_rgb_kernel(const void *__restr
     const int y = (int)(r / g.W), x = (int)(r % g.W);
     const long long o = f * ((long long)g.Hp * g.Wp * 3) + ((long long)(y + g.top) * g.Wp + x + g.left) * 3;
     int o3[3];
-    if constexpr (K32) {
+    if constexpr (M == kK32) {
         // int32 arithmetic, offset 0 (optimize_block_size: to_RGB of the int32 array, :567-568)
         const int32_t *s = (const int32_t *)ws + o;
         const uint32_t Y = (uint32_t)s[0], Co = (uint32_t)s[1], Cg = (uint32_t)s[2];
@@ -277,12 +293,13 @@ __global__ __launch_bounds__(256) void dct_any_to_rgb_kernel(const void *__restr
         o3[1] = (int32_t)(Y + Cg);
         o3[2] = (int32_t)(Y - Co - Cg);
     } else {
-        // :449 to_RGB in int16 (wrapping), :454 += 128 in int16
+        // :449 to_RGB in int16 (wrapping), :454 += self.offset in int16 (128; 0 for other quantizers)
         const int16_t *s = (const int16_t *)ws + o;
         const int Y = s[0], Co = s[1], Cg = s[2];
-        o3[0] = (int16_t)((int16_t)(Y + Co - Cg) + 128);
-        o3[1] = (int16_t)((int16_t)(Y + Cg) + 128);
-        o3[2] = (int16_t)((int16_t)(Y - Co - Cg) + 128);
+        constexpr int off = M == kRaw ? 0 : 128;
+        o3[0] = (int16_t)((int16_t)(Y + Co - Cg) + off);
+        o3[1] = (int16_t)((int16_t)(Y + Cg) + off);
+        o3[2] = (int16_t)((int16_t)(Y - Co - Cg) + off);
     }
     uint8_t *d = rgb + p * 3;
 #pragma unroll
@@ -307,7 +324,7 @@ __device__ __forceinline__ long long coef_offset_rt(const GeomB &g, int B, int b
 // scratch per workgroup: the B x B tile, then the threads' two lines of B
 __host__ __device__ constexpr long long rt_ws_per_wg(int B) { return (long long)B * B + 2LL * B * kRtThreads; }
 
-template <bool K32>
+template <int M>
 __global__ __launch_bounds__(256) void dct_rt_encode_kernel(const uint8_t *__restrict__ rgb, void *__restrict__ out,
                                                            GeomB g, int Q, pfft::RtPlan P,
                                                            const float *__restrict__ mem, float *__restrict__ ws,
@@ -333,7 +350,7 @@ __global__ __launch_bounds__(256) void dct_rt_encode_kernel(const uint8_t *__res
                     const uint8_t *p = img + ((long long)sy * g.W + sx) * 3;
                     R = (float)p[0]; G = (float)p[1]; Bl = (float)p[2];
                 }
-                if constexpr (!K32) { R = R - 128.f; G = G - 128.f; Bl = Bl - 128.f; }
+                if constexpr (M == kU8) { R = R - 128.f; G = G - 128.f; Bl = Bl - 128.f; }
                 float o;
                 if (cc == 0) o = (R / 4.f + G / 2.f) + Bl / 4.f;
                 else if (cc == 1) o = R / 2.f - Bl / 2.f;
@@ -352,17 +369,21 @@ __global__ __launch_bounds__(256) void dct_rt_encode_kernel(const uint8_t *__res
             // :313-327 -p, :343 quantize (A5), :348 += 128, :361 uint8
             for (int j = 0; j < B; ++j) {
                 const float t = wr ? (float)((double)c[j] * wr[j]) : c[j];
-                const int k = (int)__fdiv_rn(t, q);
                 const long long o = f * g.out_stride + coef_offset_rt(g, B, by, bx, y, j) + cc;
-                if constexpr (K32) ((int32_t *)out)[o] = k;
-                else ((uint8_t *)out)[o] = (uint8_t)(k + 128);
+                if constexpr (M == kRaw) {
+                    ((float *)out)[o] = t;
+                } else {
+                    const int k = (int)__fdiv_rn(t, q);
+                    if constexpr (M == kK32) ((int32_t *)out)[o] = k;
+                    else ((uint8_t *)out)[o] = (uint8_t)(k + 128);
+                }
             }
         }
         __syncthreads();
     }
 }
 
-template <bool K32>
+template <int M>
 __global__ __launch_bounds__(256) void dct_rt_decode_kernel(const void *__restrict__ kin, void *__restrict__ wsout,
                                                            GeomB g, int Q, pfft::RtPlan P,
                                                            const double *__restrict__ mem, double *__restrict__ ws,
@@ -380,11 +401,16 @@ __global__ __launch_bounds__(256) void dct_rt_decode_kernel(const void *__restri
         for (int x = tid; x < B; x += kRtThreads) {
             for (int i = 0; i < B; ++i) {
                 const long long o = f * g.out_stride + coef_offset_rt(g, B, by, bx, i, x) + cc;
-                if constexpr (K32) {
+                if constexpr (M == kK32) {
                     c[i] = (double)(int32_t)((uint32_t)Q * (uint32_t)((const int32_t *)kin)[o]);
                 } else {
-                    const int16_t k = (int16_t)((int)((const uint8_t *)kin)[o] - 128);
-                    int16_t y16 = (int16_t)(Q * (int)k);
+                    int16_t y16;
+                    if constexpr (M == kRaw) {
+                        y16 = ((const int16_t *)kin)[o];
+                    } else {
+                        const int16_t k = (int16_t)((int)((const uint8_t *)kin)[o] - 128);
+                        y16 = (int16_t)(Q * (int)k);
+                    }
                     if (pw) {   // :421-435 -p
                         const float f = (float)((double)(float)y16 / pw[(cc ? B * B : 0) + (long long)i * B + x]);
                         y16 = (int16_t)(int)f;
@@ -402,7 +428,7 @@ __global__ __launch_bounds__(256) void dct_rt_decode_kernel(const void *__restri
             const long long row = (long long)by * B + y;
             for (int j = 0; j < B; ++j) {
                 const long long o = f * ((long long)g.Hp * g.Wp * 3) + (row * g.Wp + (long long)bx * B + j) * 3 + cc;
-                if constexpr (K32) ((int32_t *)wsout)[o] = (int32_t)c[j];
+                if constexpr (M == kK32) ((int32_t *)wsout)[o] = (int32_t)c[j];
                 else ((int16_t *)wsout)[o] = (int16_t)(int32_t)c[j];
             }
         }
@@ -720,7 +746,7 @@ unsigned rt_grid(long long units, int B, size_t esz)
     return (unsigned)std::max<long long>(wgs, 1);
 }
 
-int rt_launch_encode(const uint8_t *rgb, void *out, bool k32, const GeomB &g, int B, int Q, const double *pw,
+int rt_launch_encode(const uint8_t *rgb, void *out, int mode, const GeomB &g, int B, int Q, const double *pw,
                      hipStream_t s)
 {
     RtPlanDev pl;
@@ -732,14 +758,15 @@ int rt_launch_encode(const uint8_t *rgb, void *out, bool k32, const GeomB &g, in
     rc = scr.acquire((size_t)grid * rt_ws_per_wg(B) * sizeof(float), s);
     if (rc != VCF_OK) return rc;
     float *ws = (float *)scr.ptr;
-    if (k32) hipLaunchKernelGGL((dct_rt_encode_kernel<true>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws, pw);
-    else hipLaunchKernelGGL((dct_rt_encode_kernel<false>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws, pw);
+    if (mode == kK32) hipLaunchKernelGGL((dct_rt_encode_kernel<kK32>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws, pw);
+    else if (mode == kRaw) hipLaunchKernelGGL((dct_rt_encode_kernel<kRaw>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws, pw);
+    else hipLaunchKernelGGL((dct_rt_encode_kernel<kU8>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws, pw);
     rc = hip_check(hipGetLastError(), "dct_rt_encode_kernel launch");
     const int rc2 = scr.release(s);
     return rc != VCF_OK ? rc : rc2;
 }
 
-int rt_launch_decode(const void *kin, void *wsout, bool k32, const GeomB &g, int B, int Q, const double *pw,
+int rt_launch_decode(const void *kin, void *wsout, int mode, const GeomB &g, int B, int Q, const double *pw,
                      hipStream_t s)
 {
     RtPlanDev pl;
@@ -751,8 +778,9 @@ int rt_launch_decode(const void *kin, void *wsout, bool k32, const GeomB &g, int
     rc = scr.acquire((size_t)grid * rt_ws_per_wg(B) * sizeof(double), s);
     if (rc != VCF_OK) return rc;
     double *ws = (double *)scr.ptr;
-    if (k32) hipLaunchKernelGGL((dct_rt_decode_kernel<true>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws, pw);
-    else hipLaunchKernelGGL((dct_rt_decode_kernel<false>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws, pw);
+    if (mode == kK32) hipLaunchKernelGGL((dct_rt_decode_kernel<kK32>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws, pw);
+    else if (mode == kRaw) hipLaunchKernelGGL((dct_rt_decode_kernel<kRaw>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws, pw);
+    else hipLaunchKernelGGL((dct_rt_decode_kernel<kU8>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws, pw);
     rc = hip_check(hipGetLastError(), "dct_rt_decode_kernel launch");
     const int rc2 = scr.release(s);
     return rc != VCF_OK ? rc : rc2;
@@ -775,24 +803,26 @@ int make_geom_b(int H, int W, int B, uint32_t flags, int64_t n_frames, GeomB &g)
 }
 
 template <int B>
-int launch_encode(const uint8_t *rgb, void *out, bool k32, const GeomB &g, int Q, const double *pw, hipStream_t s)
+int launch_encode(const uint8_t *rgb, void *out, int mode, const GeomB &g, int Q, const double *pw, hipStream_t s)
 {
     constexpr int U = enc_units<B>();
     const long long wgs = (g.units + U - 1) / U;
     if (wgs > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "batch too large");
-    if (k32) hipLaunchKernelGGL((dct_any_encode_kernel<B, true>), dim3((unsigned)wgs), dim3(256), 0, s, rgb, out, g, Q, pw);
-    else hipLaunchKernelGGL((dct_any_encode_kernel<B, false>), dim3((unsigned)wgs), dim3(256), 0, s, rgb, out, g, Q, pw);
+    if (mode == kK32) hipLaunchKernelGGL((dct_any_encode_kernel<B, kK32>), dim3((unsigned)wgs), dim3(256), 0, s, rgb, out, g, Q, pw);
+    else if (mode == kRaw) hipLaunchKernelGGL((dct_any_encode_kernel<B, kRaw>), dim3((unsigned)wgs), dim3(256), 0, s, rgb, out, g, Q, pw);
+    else hipLaunchKernelGGL((dct_any_encode_kernel<B, kU8>), dim3((unsigned)wgs), dim3(256), 0, s, rgb, out, g, Q, pw);
     return hip_check(hipGetLastError(), "dct_any_encode_kernel launch");
 }
 
 template <int B>
-int launch_decode(const void *kin, void *ws, bool k32, const GeomB &g, int Q, const double *pw, hipStream_t s)
+int launch_decode(const void *kin, void *ws, int mode, const GeomB &g, int Q, const double *pw, hipStream_t s)
 {
     constexpr int U = dec_units<B>();
     const long long wgs = (g.units + U - 1) / U;
     if (wgs > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "batch too large");
-    if (k32) hipLaunchKernelGGL((dct_any_decode_kernel<B, true>), dim3((unsigned)wgs), dim3(128), 0, s, kin, ws, g, Q, pw);
-    else hipLaunchKernelGGL((dct_any_decode_kernel<B, false>), dim3((unsigned)wgs), dim3(128), 0, s, kin, ws, g, Q, pw);
+    if (mode == kK32) hipLaunchKernelGGL((dct_any_decode_kernel<B, kK32>), dim3((unsigned)wgs), dim3(128), 0, s, kin, ws, g, Q, pw);
+    else if (mode == kRaw) hipLaunchKernelGGL((dct_any_decode_kernel<B, kRaw>), dim3((unsigned)wgs), dim3(128), 0, s, kin, ws, g, Q, pw);
+    else hipLaunchKernelGGL((dct_any_decode_kernel<B, kU8>), dim3((unsigned)wgs), dim3(128), 0, s, kin, ws, g, Q, pw);
     return hip_check(hipGetLastError(), "dct_any_decode_kernel launch");
 }
 
@@ -815,8 +845,9 @@ int launch_decode(const void *kin, void *ws, bool k32, const GeomB &g, int Q, co
     }
 
 int check_any(const void *a, const void *b, int64_t n_frames, int H, int W, int B, int Q, uint32_t flags,
-              bool decode, bool k32)
+              bool decode, int mode)
 {
+    const bool k32 = mode == kK32;
     if (!a || !b) return set_error(VCF_ERR_INVALID, "null buffer");
     if (n_frames < 0) return set_error(VCF_ERR_INVALID, "n_frames < 0");
     if (H <= 0 || W <= 0)
@@ -827,7 +858,7 @@ int check_any(const void *a, const void *b, int64_t n_frames, int H, int W, int 
                          B > kRtMaxB ? "block size %d: the HIP path covers B <= 4096"
                                      : "block size %d: pocketfft plans this length with Bluestein (not restated)",
                          B);
-    if (Q < 1 || (decode && !k32 && Q > 32767))
+    if (Q < 1 || (decode && mode == kU8 && Q > 32767))
         return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
     if ((flags & VCF_DCT_PERCEPTUAL) && k32)
         return set_error(VCF_ERR_UNSUPPORTED,
@@ -840,9 +871,9 @@ int check_any(const void *a, const void *b, int64_t n_frames, int H, int W, int 
 }
 
 int any_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t B, int32_t Q,
-               uint32_t flags, void *k_dev, bool k32, void *stream)
+               uint32_t flags, void *k_dev, int mode, void *stream)
 {
-    int rc = check_any(rgb_dev, k_dev, n_frames, H, W, B, Q, flags, false, k32);
+    int rc = check_any(rgb_dev, k_dev, n_frames, H, W, B, Q, flags, false, mode);
     if (rc != VCF_OK || n_frames == 0) return rc;
     rc = ensure_tables();
     if (rc != VCF_OK) return rc;
@@ -851,16 +882,16 @@ int any_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, i
     const hipStream_t s = (hipStream_t)stream;
     const double *pw = nullptr;
     if ((flags & VCF_DCT_PERCEPTUAL) && (rc = perceptual_weights(B, pw)) != VCF_OK) return rc;
-#define VCF_ENC_ANY(b) launch_encode<b>(rgb_dev, k_dev, k32, g, Q, pw, s)
+#define VCF_ENC_ANY(b) launch_encode<b>(rgb_dev, k_dev, mode, g, Q, pw, s)
     VCF_ANY_SWITCH(B, VCF_ENC_ANY)
 #undef VCF_ENC_ANY
-    return rt_launch_encode(rgb_dev, k_dev, k32, g, B, Q, pw, s);
+    return rt_launch_encode(rgb_dev, k_dev, mode, g, B, Q, pw, s);
 }
 
 int any_decode(const void *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t B, int32_t Q, uint32_t flags,
-               uint8_t *rgb_dev, bool k32, void *stream)
+               uint8_t *rgb_dev, int mode, void *stream)
 {
-    int rc = check_any(k_dev, rgb_dev, n_frames, H, W, B, Q, flags, true, k32);
+    int rc = check_any(k_dev, rgb_dev, n_frames, H, W, B, Q, flags, true, mode);
     if (rc != VCF_OK || n_frames == 0) return rc;
     rc = ensure_tables();
     if (rc != VCF_OK) return rc;
@@ -869,7 +900,7 @@ int any_decode(const void *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_
     if ((flags & VCF_DCT_PERCEPTUAL) && (rc = perceptual_weights(B, pw)) != VCF_OK) return rc;
     GeomB g0;
     make_geom_b(H, W, B, flags, 1, g0);
-    const size_t esz = k32 ? 4 : 2;
+    const size_t esz = mode == kK32 ? 4 : 2;
     const size_t frame_ws = (size_t)g0.Hp * g0.Wp * 3 * esz;
     // workspace in chunks of frames, at most ~1 GiB at a time
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n_frames, (int64_t)((1ull << 30) / frame_ws)));
@@ -878,25 +909,26 @@ int any_decode(const void *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_
     rc = scr.acquire(frame_ws * chunk, s);
     if (rc != VCF_OK) return rc;
     void *ws = scr.ptr;
-    const size_t kesz = k32 ? 4 : 1;
+    const size_t kesz = mode == kK32 ? 4 : (mode == kRaw ? 2 : 1);
     for (int64_t f0 = 0; f0 < n_frames && rc == VCF_OK; f0 += chunk) {
         const int64_t n = std::min(chunk, n_frames - f0);
         GeomB g;
         make_geom_b(H, W, B, flags, n, g);
         const void *kin = (const uint8_t *)k_dev + (size_t)f0 * g.out_stride * kesz;
         auto pass1 = [&]() -> int {
-#define VCF_DEC_ANY(b) launch_decode<b>(kin, ws, k32, g, Q, pw, s)
+#define VCF_DEC_ANY(b) launch_decode<b>(kin, ws, mode, g, Q, pw, s)
             VCF_ANY_SWITCH(B, VCF_DEC_ANY)
 #undef VCF_DEC_ANY
-            return rt_launch_decode(kin, ws, k32, g, B, Q, pw, s);
+            return rt_launch_decode(kin, ws, mode, g, B, Q, pw, s);
         };
         rc = pass1();
         if (rc != VCF_OK) break;
         const long long npx = (long long)n * H * W;
         const unsigned grid = (unsigned)((npx + 255) / 256);
         uint8_t *out = rgb_dev + (size_t)f0 * g.in_stride;
-        if (k32) hipLaunchKernelGGL((dct_any_to_rgb_kernel<true>), dim3(grid), dim3(256), 0, s, ws, out, g, npx);
-        else hipLaunchKernelGGL((dct_any_to_rgb_kernel<false>), dim3(grid), dim3(256), 0, s, ws, out, g, npx);
+        if (mode == kK32) hipLaunchKernelGGL((dct_any_to_rgb_kernel<kK32>), dim3(grid), dim3(256), 0, s, ws, out, g, npx);
+        else if (mode == kRaw) hipLaunchKernelGGL((dct_any_to_rgb_kernel<kRaw>), dim3(grid), dim3(256), 0, s, ws, out, g, npx);
+        else hipLaunchKernelGGL((dct_any_to_rgb_kernel<kU8>), dim3(grid), dim3(256), 0, s, ws, out, g, npx);
         rc = hip_check(hipGetLastError(), "dct_any_to_rgb_kernel launch");
     }
     const int rc2 = scr.release(s);
@@ -909,13 +941,13 @@ int any_decode(const void *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_
 int dct_any_encode_u8(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t B, int32_t Q,
                       uint32_t flags, uint8_t *k_dev, void *stream)
 {
-    return any_encode(rgb_dev, n_frames, H, W, B, Q, flags, k_dev, false, stream);
+    return any_encode(rgb_dev, n_frames, H, W, B, Q, flags, k_dev, kU8, stream);
 }
 
 int dct_any_decode_u8(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t B, int32_t Q,
                       uint32_t flags, uint8_t *rgb_dev, void *stream)
 {
-    return any_decode(k_dev, n_frames, H, W, B, Q, flags, rgb_dev, false, stream);
+    return any_decode(k_dev, n_frames, H, W, B, Q, flags, rgb_dev, kU8, stream);
 }
 
 }  // namespace vcf
@@ -939,25 +971,37 @@ int vcf_dct_perceptual_tables(int32_t block_size, uint8_t *y_qss, uint8_t *c_qss
 int vcf_dct_dz_encode_k32(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
                           int32_t Q, uint32_t flags, int32_t *k_dev, void *stream)
 {
-    return vcf::any_encode(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, true, stream);
+    return vcf::any_encode(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, vcf::kK32, stream);
 }
 
 int vcf_dct_dz_decode_k32(const int32_t *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
                           int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream)
 {
-    return vcf::any_decode(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, true, stream);
+    return vcf::any_decode(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, vcf::kK32, stream);
 }
 
 int vcf_dct_dz_encode_any(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
                           int32_t Q, uint32_t flags, uint8_t *k_dev, void *stream)
 {
-    return vcf::any_encode(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, false, stream);
+    return vcf::any_encode(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, vcf::kU8, stream);
 }
 
 int vcf_dct_dz_decode_any(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
                           int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream)
 {
-    return vcf::any_decode(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, false, stream);
+    return vcf::any_decode(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, vcf::kU8, stream);
+}
+
+int vcf_dct_raw_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
+                       uint32_t flags, float *coef_dev, void *stream)
+{
+    return vcf::any_encode(rgb_dev, n_frames, H, W, block_size, 1, flags, coef_dev, vcf::kRaw, stream);
+}
+
+int vcf_dct_raw_decode(const int16_t *coef_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
+                       uint32_t flags, uint8_t *rgb_dev, void *stream)
+{
+    return vcf::any_decode(coef_dev, n_frames, H, W, block_size, 1, flags, rgb_dev, vcf::kRaw, stream);
 }
 
 }  // extern "C"

@@ -18,7 +18,8 @@ from ._lib import VCF_DCT_NO_SUBBANDS, VCF_DCT_PERCEPTUAL, call
 from .device import DeviceBuffer, _h
 
 __all__ = ["padded_shape", "flags_from", "encode_device", "decode_device", "encode", "decode",
-           "block_size_supported", "encode_k32", "decode_k32", "VCF_DCT_NO_SUBBANDS", "VCF_DCT_PERCEPTUAL"]
+           "block_size_supported", "encode_k32", "decode_k32", "raw_encode_device", "raw_decode_device",
+           "VCF_DCT_NO_SUBBANDS", "VCF_DCT_PERCEPTUAL"]
 
 
 def block_size_supported(block_size: int) -> bool:
@@ -156,3 +157,32 @@ def decode_k32(k: np.ndarray, H: int, W: int, Q: int = 32, flags: int = 0, block
     din.free()
     dout.free()
     return res[0] if single else res
+
+
+def raw_encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, flags: int = 0,
+                      out: DeviceBuffer | None = None, stream=None, block_size: int = 8) -> DeviceBuffer:
+    """encode_fn up to the quantizer for -a other than deadzone (offset 0, 2D-DCT.py:106-109):
+    u8 RGB frames -> float32 HpxWpx3 coefficient frames (subband layout unless -x, -p applied)."""
+    Hp, Wp = padded_shape(H, W, block_size)
+    if rgb.nbytes < n_frames * H * W * 3:
+        raise ValueError("input buffer too small")
+    if out is None:
+        out = DeviceBuffer(n_frames * Hp * Wp * 3 * 4)
+    elif out.nbytes < n_frames * Hp * Wp * 3 * 4:
+        raise ValueError("output buffer too small")
+    call("vcf_dct_raw_encode", rgb.ptr, n_frames, H, W, block_size, flags, out.ptr, _h(stream))
+    return out
+
+
+def raw_decode_device(coef: DeviceBuffer, n_frames: int, H: int, W: int, flags: int = 0,
+                      out: DeviceBuffer | None = None, stream=None, block_size: int = 8) -> DeviceBuffer:
+    """decode_fn after another quantizer's dequantize_decom: int16 HpxWpx3 coefficient frames -> u8 RGB."""
+    Hp, Wp = padded_shape(H, W, block_size)
+    if coef.nbytes < n_frames * Hp * Wp * 3 * 2:
+        raise ValueError("input buffer too small")
+    if out is None:
+        out = DeviceBuffer(n_frames * H * W * 3)
+    elif out.nbytes < n_frames * H * W * 3:
+        raise ValueError("output buffer too small")
+    call("vcf_dct_raw_decode", coef.ptr, n_frames, H, W, block_size, flags, out.ptr, _h(stream))
+    return out
