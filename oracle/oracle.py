@@ -79,6 +79,8 @@ def lib():
         L.vcfo_wavelet_index.argtypes = [ctypes.c_char_p]
         L.vcfo_wavelet_len.argtypes = [ctypes.c_int]
         L.vcfo_dwt_shapes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ip]
+        L.vcfo_dwt1_per_w.argtypes = [dp, ctypes.c_int, ctypes.c_int, dp, dp]
+        L.vcfo_idwt1_per_w.argtypes = [dp, dp, ctypes.c_int, ctypes.c_int, dp]
         L.vcfo_wavedec2.argtypes = [dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]
         L.vcfo_waverec2.argtypes = [dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]
         L.vcfo_dwt_dz_encode.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -297,6 +299,30 @@ def _dp(a):
 def _coeff_count(H, W, levels):
     sh = dwt_shapes(H, W, levels)
     return sh[-1][0] * sh[-1][1] + sum(3 * h * w for h, w in sh)
+
+
+def dwt1(x: np.ndarray, wavelet: str):
+    """pywt.dwt(x, wavelet, mode='periodization') of one float64 line."""
+    x = np.ascontiguousarray(x, np.float64)
+    n = (x.size + 1) // 2
+    cA, cD = np.empty(n), np.empty(n)
+    dp = ctypes.POINTER(ctypes.c_double)
+    if lib().vcfo_dwt1_per_w(x.ctypes.data_as(dp), x.size, wavelet_index(wavelet), cA.ctypes.data_as(dp),
+                             cD.ctypes.data_as(dp)) != 0:
+        raise ValueError(wavelet)
+    return cA, cD
+
+
+def idwt1(a: np.ndarray, d: np.ndarray, wavelet: str):
+    """pywt.idwt(a, d, wavelet, mode='periodization') of one pair of float64 lines."""
+    a = np.ascontiguousarray(a, np.float64)
+    d = np.ascontiguousarray(d, np.float64)
+    out = np.empty(2 * a.size)
+    dp = ctypes.POINTER(ctypes.c_double)
+    if lib().vcfo_idwt1_per_w(a.ctypes.data_as(dp), d.ctypes.data_as(dp), a.size, wavelet_index(wavelet),
+                              out.ctypes.data_as(dp)) != 0:
+        raise ValueError(wavelet)
+    return out
 
 
 def wavedec2(x: np.ndarray, wavelet: str, levels: int):

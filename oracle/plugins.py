@@ -131,5 +131,8 @@ def ycrcb_dz_encode(rgb: np.ndarray, Q: int) -> np.ndarray:
 
 def ycrcb_dz_decode(k: np.ndarray, Q: int) -> np.ndarray:
     """YCrCb.decode (:53-72): Q*k in uint16, int16, uint8, to_RGB, clip."""
-    y = (np.asarray(k, np.uint16) * np.uint16(Q)).astype(np.int16).astype(np.uint8)
+    # numpy 1.26: uint16 array * int -> uint16 (wrapping) for Q < 2**16, a wider type otherwise;
+    # either way the uint8 cast keeps the low byte of Q * k
+    y = ((np.asarray(k, np.uint16).astype(np.int64) * int(Q)) & 0xFFFF).astype(np.uint16)
+    y = y.astype(np.int16).astype(np.uint8)
     return ycrcb_to_rgb(y)

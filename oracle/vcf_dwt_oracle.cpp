@@ -33,9 +33,13 @@
  *     zeroed output): out[(2i + p + 1 - F/2) mod 2N] += f[2j + p] * c[(i - j)
  *     mod N], one product at a time, j ascending; for the first
  *     ceil((F/2 - 1) / 2) values of i (whose outputs wrap to the end) the
- *     taps j <= i come first in descending j, then j > i ascending.
- *   Inputs shorter than F/2 take a separate path in pywt that this does not
- *   restate (only reachable for subbands of < F/2 samples).
+ *     taps j <= top come first in descending j, then j > top ascending
+ *     (top = i for lines of at least F/2 samples).
+ *   For lines shorter than the taps (pywt's short-input branch, which wraps
+ *   the coefficients around more than once) the reordered indices are
+ *   i < ceil((F/2 - 1) / 2) still, with top = the largest i + kN below that
+ *   bound instead of i (found against pywt 1.1.1 for all 106 discrete wavelets,
+ *   N = 1 .. F/2 + 3, make_golden_dwt_short.py).
  *   2D: wavedec2 = per level dwt along axis 0 then axis 1 (keys aa, da, ad,
  *   dd -> cA, (cH, cV, cD)); waverec2 = per level trim cA to the detail
  *   shape, idwt along axis 1 (aa+ad -> a, da+dd -> d), then along axis 0.
@@ -107,7 +111,8 @@ void vcfo_idwt1_per(const double *a, const double *d, int N, int cs, const doubl
             for (int t = 0; t < F2; ++t) {
                 int j;
                 if (i < T) {
-                    const int top = i < F2 - 1 ? i : F2 - 1;
+                    /* the largest i + kN below T: i itself unless N < T (pywt's short-input branch) */
+                    const int top = i + N * ((T - 1 - i) / N);
                     j = t <= top ? top - t : t;   /* top..0, then top+1.. */
                 } else {
                     j = t;
@@ -118,6 +123,24 @@ void vcfo_idwt1_per(const double *a, const double *d, int N, int cs, const doubl
             }
         }
     }
+}
+
+/* 1-D lines by wavelet id (pywt.dwt / pywt.idwt, mode 'periodization') */
+int vcfo_dwt1_per_w(const double *x, int N, int wavelet, double *cA, double *cD)
+{
+    if (wavelet < 0 || wavelet >= kNumWavelets || N < 1) return -1;
+    const vcf::WaveletDef &wd = kWavelets[wavelet];
+    vcfo_dwt1_per(x, N, 1, wd.dec_lo, wd.len, cA, 1);
+    vcfo_dwt1_per(x, N, 1, wd.dec_hi, wd.len, cD, 1);
+    return 0;
+}
+
+int vcfo_idwt1_per_w(const double *a, const double *d, int N, int wavelet, double *out)
+{
+    if (wavelet < 0 || wavelet >= kNumWavelets || N < 1) return -1;
+    const vcf::WaveletDef &wd = kWavelets[wavelet];
+    vcfo_idwt1_per(a, d, N, 1, wd.rec_lo, wd.rec_hi, wd.len, out, 1);
+    return 0;
 }
 
 static int half(int n) { return (n + 1) / 2; }

@@ -11,6 +11,7 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 _MAN = json.load(open(os.path.join(GOLDEN, "manifest_dwt.json")))
+_SHORT = json.load(open(os.path.join(GOLDEN, "manifest_dwt_short.json")))
 
 
 def _params(case):
@@ -32,6 +33,36 @@ def test_dwt_encode_decode_vs_reference(case):
     assert np.array_equal(out, d["decoded"])
 
 
+@pytest.mark.parametrize("case", _SHORT["cases"], ids=lambda c: c["name"])
+def test_dwt_short_subbands_vs_reference(case):
+    """Frames whose last levels' subbands are shorter than F/2 (pywt's short-input
+    branch in the inverse) against the reference's own files and decoded frame."""
+    import vcf_amd.dwt as DW
+    d = np.load(os.path.join(GOLDEN, case["file"]))
+    w, L, Q = _params(case)
+    sb = DW.encode(d["rgb"], w, L, Q)[0]
+    for name in case["subbands"]:
+        assert np.array_equal(sb[name], d[name]), name
+    for variant in (0, 2):
+        out = DW.decode({n: d[n] for n in case["subbands"]}, case["H"], case["W"], w, L, Q, variant=variant)
+        assert np.array_equal(out, d["decoded"]), variant
+
+
+@pytest.mark.parametrize("wavelet", ["db5", "bior4.4", "db10", "sym8", "coif5", "rbio3.9", "db20"])
+@pytest.mark.parametrize("H,W,L", [(5, 7, 3), (23, 2, 2), (1, 1, 4), (40, 9, 5), (3, 64, 6)])
+def test_dwt_short_lines_vs_oracle(wavelet, H, W, L):
+    import vcf_amd.dwt as DW
+    rng = np.random.Generator(np.random.PCG64(H * 131 + W * 7 + L))
+    frames = rng.integers(0, 256, (2, H, W, 3), dtype=np.uint8)
+    got = DW.encode(frames, wavelet, L, 5, variant=2)
+    out = DW.decode(got, H, W, wavelet, L, 5)
+    for f in range(2):
+        ref = O.dwt_encode_frame(frames[f], wavelet, L, 5)
+        for name, arr in ref.items():
+            assert np.array_equal(got[f][name], arr), (f, name)
+        assert np.array_equal(out[f], O.dwt_decode_frame(got[f], H, W, wavelet, L, 5))
+
+
 @pytest.mark.parametrize("variant", [1, 2, 6], ids=["fused", "separable", "strip"])
 @pytest.mark.parametrize("wavelet", ["db5", "bior4.4", "haar", "sym4", "coif2", "db9", "db10"])
 @pytest.mark.parametrize("H,W,L,Q", [(96, 128, 3, 32), (67, 45, 2, 7), (256, 160, 5, 16), (8, 10, 1, 1),
@@ -51,11 +82,15 @@ def test_dwt_vs_oracle(wavelet, H, W, L, Q, variant):
         for name, arr in ref.items():
             assert np.array_equal(got[f][name], arr), (f, name)
     half = O.lib().vcfo_wavelet_len(O.wavelet_index(wavelet)) // 2
+    dec_variant = {6: 1}.get(variant, variant)
     if min(shapes[-1]) < half:
-        with pytest.raises(NotImplementedError):
-            DW.decode(got[0], H, W, wavelet, L, Q)
-        return
-    out = DW.decode(got, H, W, wavelet, L, Q, variant={6: 1}.get(variant, variant))
+        # pywt's short-input branch: the separable kernels (automatic choice) run it,
+        # an explicit request for the fused tiles is refused
+        if dec_variant == 1:
+            with pytest.raises(NotImplementedError):
+                DW.decode(got[0], H, W, wavelet, L, Q, variant=1)
+        dec_variant = 0
+    out = DW.decode(got, H, W, wavelet, L, Q, variant=dec_variant)
     for f in range(2):
         assert np.array_equal(out[f], O.dwt_decode_frame(got[f], H, W, wavelet, L, Q))
 

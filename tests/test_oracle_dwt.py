@@ -16,6 +16,7 @@ from conftest import GOLDEN
 from oracle import oracle as O
 
 _MAN = json.load(open(os.path.join(GOLDEN, "manifest_dwt.json")))
+_SHORT = json.load(open(os.path.join(GOLDEN, "manifest_dwt_short.json")))
 
 
 def _params(case):
@@ -65,3 +66,33 @@ def test_wavelet_table():
     assert O.wavelet_index("db5") >= 0 and O.wavelet_index("bior4.4") >= 0
     with pytest.raises(ValueError):
         O.wavelet_index("nope")
+
+
+def test_lines_shorter_than_the_filter_vs_pywt():
+    """pywt's short-input branch: idwt/dwt of every line length 1 .. F/2 + 3 for all
+    106 discrete wavelets, bit for bit (dwt_short_pywt.npz, make_golden_dwt_short.py)."""
+    d = np.load(os.path.join(GOLDEN, "dwt_short_pywt.npz"))
+    names = [str(n) for n in d["names"]]
+    assert len(names) == 106
+    n = 0
+    for w in names:
+        N = 1
+        while f"inv_{w}_{N}" in d.files:
+            y = O.idwt1(d[f"inv_a_{w}_{N}"], d[f"inv_d_{w}_{N}"], w)
+            assert np.array_equal(y.view(np.uint64), d[f"inv_{w}_{N}"].view(np.uint64)), (w, N)
+            cA, cD = O.dwt1(d[f"fwd_x_{w}_{N}"], w)
+            assert np.array_equal(cA, d[f"fwd_a_{w}_{N}"]) and np.array_equal(cD, d[f"fwd_d_{w}_{N}"]), (w, N)
+            N += 1
+            n += 1
+    assert n > 1000
+
+
+@pytest.mark.parametrize("case", _SHORT["cases"], ids=lambda c: c["name"])
+def test_dwt_codec_short_subbands_vs_reference(case):
+    d = np.load(os.path.join(GOLDEN, case["file"]))
+    w, L, Q = _params(case)
+    sb = O.dwt_encode_frame(d["rgb"], w, L, Q)
+    for name in case["subbands"]:
+        assert np.array_equal(sb[name], d[name]), name
+    out = O.dwt_decode_frame({n: d[n] for n in case["subbands"]}, case["H"], case["W"], w, L, Q)
+    assert np.array_equal(out, d["decoded"])

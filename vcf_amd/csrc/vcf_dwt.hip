@@ -105,6 +105,17 @@ __device__ __forceinline__ double dwt_tap_sum(const double *__restrict__ f, int 
     return s;
 }
 
+// pywt's order of the taps of input index i (0 <= i < N) in the inverse: the
+// first T = F2/2 indices take taps top..0 descending, then top+1..F2-1; the
+// others ascending.  top = the largest i + kN below T -- i itself unless the
+// line is shorter than T (pywt's short-input branch wraps the input around
+// more than once; checked against pywt 1.1.1 for every discrete wavelet and
+// every N <= F2 + 3, tests/golden/make_golden_dwt_short.py)
+__host__ __device__ __forceinline__ int idwt_top(int i, int N, int T)
+{
+    return i + N * ((T - 1 - i) / N);
+}
+
 // inverse 'per': output n (0 <= n < 2N) of idwt(a, d): the one input index i
 // feeding it, then approximation taps and detail taps accumulated one product
 // at a time (pywt: output zeroed, += per product, cA pass then cD pass)
@@ -117,7 +128,7 @@ __device__ __forceinline__ double idwt_out(const double *__restrict__ lo, const 
     q %= 2 * N;
     if (q < 0) q += 2 * N;
     const int p = q & 1, i = q >> 1;
-    const int top = i < F2 - 1 ? i : F2 - 1;
+    const int top = i < T ? idwt_top(i, N, T) : 0;
     double s = 0.0;
     for (int pass = 0; pass < 2; ++pass) {
         const double *f = pass ? hi : lo;
@@ -374,7 +385,7 @@ __device__ __forceinline__ double idwt_out_logical(const double *__restrict__ lo
     const int qq = n + F2 - 1;            // n - shift, >= 0
     const int q = qq % (2 * N);
     const int p = q & 1, i = q >> 1, ii = qq >> 1;
-    const int top = i < F2 - 1 ? i : F2 - 1;
+    const int top = i < T ? idwt_top(i, N, T) : 0;
     double s = 0.0;
     for (int pass = 0; pass < 2; ++pass) {
         const double *f = pass ? hi : lo;
@@ -1227,14 +1238,6 @@ int check_dwt(const void *a, const void *b, int64_t n_frames, int32_t H, int32_t
     if (Q < 1 || (decode && Q > 32767)) return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
     if ((long long)H * W * 3 >= (1LL << 31)) return set_error(VCF_ERR_INVALID, "frame too large");
     if (n_frames > 0 && (!a || !b)) return set_error(VCF_ERR_INVALID, "null buffer");
-    // pywt takes a different code path for lines shorter than F/2 (not restated)
-    DwtGeom g;
-    dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
-    const int F2 = kWavelets[wavelet].len / 2;
-    if (decode && (g.hs[levels] < F2 || g.ws[levels] < F2))
-        return set_error(VCF_ERR_UNSUPPORTED,
-                         "level-%d subbands of %d x %d are shorter than the %s filter half-length %d",
-                         levels, g.hs[levels], g.ws[levels], kWavelets[wavelet].name, F2);
     return VCF_OK;
 }
 
@@ -1617,10 +1620,19 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *prev = nullptr;
     int lda = 0;
-    const bool fused = variant == 1 || variant >= 4 || (variant == 0 && fast_filter(F));
+    // subbands shorter than F/2 (pywt's short-input branch: the coefficients
+    // wrap around more than once) run on the separable kernels, whose loads
+    // take any index modulo the line length; the fused tiles wrap once
+    const bool short_lines = g.hs[levels] < F / 2 || g.ws[levels] < F / 2;
+    const bool fused = variant == 1 || variant >= 4 || (variant == 0 && fast_filter(F) && !short_lines);
     if (fused && !fast_filter(F))
         return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
                          kMaxFastF);
+    if (fused && short_lines)
+        return set_error(VCF_ERR_UNSUPPORTED,
+                         "level-%d subbands of %d x %d are shorter than the %s filter half-length %d: the fused "
+                         "kernels wrap once (variant 0 or 2 runs them)",
+                         levels, g.hs[levels], g.ws[levels], kWavelets[wavelet].name, F / 2);
     if (fused) {
         for (int r = levels; r >= 1; --r) {
             const int h = g.hs[r], w = g.ws[r];
