@@ -403,7 +403,7 @@ int vcf_deadzone_dequantize(const void *k_dev, int32_t k_dtype, int64_t n, int32
 /* ---- §8(f) row 4: the YCrCb and LloydMax plug-ins ------------------------------
  * YCrCb (src/YCrCb.py:25-72): the stand-alone pixel codec.  Its transform,
  * color_transforms.YCrCb, is not vendored: OpenCV's integer RGB<->YCrCb on
- * uint8 is assumed (A11; parity unpinned).  n_px pixels of 3 interleaved
+ * uint8 is assumed (A12; parity unpinned).  n_px pixels of 3 interleaved
  * channels.  Note: 2D-DCT.py / 2D-DWT.py with -t YCrCb still convert with
  * YCoCg (they bind from_RGB/to_RGB from color_transforms.YCoCg, 2D-DCT.py:22-23,
  * 2D-DWT.py:19-20), so they use the YCoCg entry points above. */
@@ -418,7 +418,7 @@ int vcf_ycrcb_dz_decode(const uint16_t *k_dev, int64_t n_px, int32_t Q, uint8_t 
  * array: counts = numpy.histogram(x[..., c], bins=max-min+1, range=(min, max))
  * (numpy 1.26's arithmetic; int64 counts, channel-major, zeroed here), the
  * glue's +1, the Lloyd-Max design of scalar_quantization's LloydMax_Quantizer
- * (un-vendored; A12, unpinned: the textbook design, oracle/plugins.py),
+ * (un-vendored; A13, unpinned: the textbook design, oracle/plugins.py),
  * k = searchsorted(thresholds, x, 'right') stored with a C cast into k's type,
  * y = centroids[k] truncated into y's integer type.  dtypes: VCF_DTYPE_U8,
  * I16, U16, F32 (histogram/encode input, encode output).  vcf_lm_levels returns

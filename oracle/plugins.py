@@ -4,17 +4,17 @@ imports it.
 
 * YCrCb.py (src/YCrCb.py:25-72): the stand-alone pixel codec.  Its colour
   transform is color_transforms.YCrCb (un-vendored), assumed to be OpenCV's
-  integer RGB<->YCrCb (A11, tests/golden/shims/color_transforms/YCrCb.py).
+  integer RGB<->YCrCb (A12, tests/golden/shims/color_transforms/YCrCb.py).
 * LloydMax.py (src/LloydMax.py:75-143): numpy.histogram of each channel with
   bins = max_val - min_val + 1 over range=(min_val, max_val) (restated from
   numpy 1.26, the reference's numpy: lib/histograms.py's uniform-bin path),
   +1, and scalar_quantization's LloydMax_Quantizer (un-vendored), assumed to
   be the textbook Lloyd-Max design of tests/golden/shims/scalar_quantization/
-  LloydMax_quantization.py (A12).
+  LloydMax_quantization.py (A13).
 
 Parity: the glue is pinned by tests/golden/plug_*.npz (the reference's own
 modules run under python3.9 with those shims, make_golden_plugins.py); the
-A11/A12 arithmetic is unpinned (neither package nor OpenCV is available).
+A12/A13 arithmetic is unpinned (neither package nor OpenCV is available).
 """
 from __future__ import annotations
 
@@ -25,7 +25,7 @@ import numpy as np
 MAX_ITERS = 100
 
 
-# ---- A11: OpenCV RGB<->YCrCb on uint8 (yuv_shift 14, CV_DESCALE, saturate) ----
+# ---- A12: OpenCV RGB<->YCrCb on uint8 (yuv_shift 14, CV_DESCALE, saturate) ----
 def ycrcb_from_rgb(rgb: np.ndarray) -> np.ndarray:
     a = np.asarray(rgb).astype(np.int64)
     r, g, b = a[..., 0], a[..., 1], a[..., 2]
@@ -70,7 +70,7 @@ def histogram(x: np.ndarray, lo: int, hi: int) -> np.ndarray:
     return np.bincount(idx, minlength=n).astype(np.int64)
 
 
-# ---- A12: Lloyd-Max design over an integer histogram ----
+# ---- A13: Lloyd-Max design over an integer histogram ----
 def levels(Q: int, lo: int, hi: int) -> int:
     L = hi - lo + 1
     return -(-L // Q)

@@ -1,8 +1,8 @@
 """Golden fixtures for the §8(f) row-4 plug-ins: YCrCb (src/YCrCb.py) and
 LloydMax (src/LloydMax.py), run through the reference's own, unmodified glue
 under /opt/conda/bin/python3.9 (numpy 1.26, tifffile 2021.7.2) with the
-tests/golden/shims stand-ins (A11: color_transforms.YCrCb as OpenCV's integer
-RGB<->YCrCb; A12: scalar_quantization.LloydMax_quantization as the textbook
+tests/golden/shims stand-ins (A12: color_transforms.YCrCb as OpenCV's integer
+RGB<->YCrCb; A13: scalar_quantization.LloydMax_quantization as the textbook
 Lloyd-Max design).  Build container only:
 
     python tests/golden/make_golden_plugins.py
@@ -171,8 +171,8 @@ def main():
         sys.exit("needs /opt/conda/bin/python3.9 and /root/reference (build container only)")
     manifest = dict(generator="tests/golden/make_golden_plugins.py",
                     reference="src/YCrCb.py, src/LloydMax.py, src/2D-DCT.py, src/2D-DWT.py (unmodified glue)",
-                    assumptions="A11 (color_transforms.YCrCb = OpenCV integer RGB<->YCrCb), "
-                                "A12 (LloydMax_Quantizer, textbook Lloyd-Max): unpinned",
+                    assumptions="A12 (color_transforms.YCrCb = OpenCV integer RGB<->YCrCb), "
+                                "A13 (LloydMax_Quantizer, textbook Lloyd-Max): unpinned",
                     cases=[], same_as_ycocg=[])
     make_hist()
     with tempfile.TemporaryDirectory() as tmp:

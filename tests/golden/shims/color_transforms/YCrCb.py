@@ -1,4 +1,4 @@
-"""A11: color_transforms.YCrCb = cv2.cvtColor(RGB2YCrCb / YCrCb2RGB) on uint8.
+"""A12: color_transforms.YCrCb = cv2.cvtColor(RGB2YCrCb / YCrCb2RGB) on uint8.
 
 OpenCV's integer path (yuv_shift = 14, CV_DESCALE rounding, saturate_cast):
   Y  = (4899 R + 9617 G + 1868 B + 2^13) >> 14

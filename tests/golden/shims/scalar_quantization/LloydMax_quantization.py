@@ -1,4 +1,4 @@
-"""A12: scalar_quantization.LloydMax_quantization (un-vendored), restated as the
+"""A13: scalar_quantization.LloydMax_quantization (un-vendored), restated as the
 textbook Lloyd-Max design over the integer histogram it is given.
 
   L = max_val - min_val + 1 histogram bins (value v = min_val + i), N = ceil(L / Q_step)

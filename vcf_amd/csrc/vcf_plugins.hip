@@ -4,14 +4,14 @@
 // * YCrCb (src/YCrCb.py:25-72), the stand-alone pixel codec: RGB -> YCrCb,
 //   int16, deadzone quantizer, uint16 indices (and back).  The transform is
 //   color_transforms.YCrCb, which the reference does not vendor; it is taken
-//   to be OpenCV's integer RGB<->YCrCb (assumption A11: yuv_shift 14,
+//   to be OpenCV's integer RGB<->YCrCb (assumption A12: yuv_shift 14,
 //   CV_DESCALE rounding, saturate_cast; parity unpinned).
 // * LloydMax (src/LloydMax.py:75-143), the quantizer plug-in of 2D-DCT.py,
 //   YCrCb.py and the stand-alone LloydMax.py: per channel
 //   numpy.histogram(x, bins=max_val-min_val+1, range=(min_val, max_val))
 //   (numpy 1.26's uniform-bin arithmetic, pinned by tests/golden/
 //   plug_histograms.npz), +1, scalar_quantization's LloydMax_Quantizer
-//   (un-vendored; assumption A12: the textbook Lloyd-Max design, restated in
+//   (un-vendored; assumption A13: the textbook Lloyd-Max design, restated in
 //   oracle/plugins.py), encode = searchsorted(thresholds, x, 'right'),
 //   decode = centroids[k].
 //
@@ -44,7 +44,7 @@ unsigned grid_for(int64_t n, int64_t per_thread = 4)
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 256 * 32));
 }
 
-// ---- A11: OpenCV's RGB2YCrCb_i / YCrCb2RGB_i for uint8 ---------------------
+// ---- A12: OpenCV's RGB2YCrCb_i / YCrCb2RGB_i for uint8 ---------------------
 __device__ __forceinline__ int sat8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 
 __device__ __forceinline__ void rgb_to_ycrcb(int r, int g, int b, int &y, int &cr, int &cb)

@@ -4,11 +4,11 @@ YCrCb (src/YCrCb.py:25-72): ycrcb_dz_encode / ycrcb_dz_decode run the
 stand-alone pixel codec's span between reading the image and the entropy
 codec in one kernel each (vcf_ycrcb_dz_*); ycrcb_from_rgb / ycrcb_to_rgb
 are the colour transform alone (for the LloydMax quantizer).  The
-transform is OpenCV's integer RGB<->YCrCb (assumption A11, unpinned).
+transform is OpenCV's integer RGB<->YCrCb (assumption A12, unpinned).
 
 LloydMax (src/LloydMax.py:75-143): lm_quantize_device runs, per channel,
 numpy.histogram (vcf_lm_histogram), the glue's +1, the Lloyd-Max design
-(vcf_lm_design, host, A12 unpinned) and the encoder (vcf_lm_encode);
+(vcf_lm_design, host, A13 unpinned) and the encoder (vcf_lm_encode);
 lm_dequantize_device the centroid lookup (vcf_lm_decode).  There is no CPU
 path: the arithmetic runs in libvcf_amd.so.
 """
@@ -56,7 +56,7 @@ def _px_map(fn: str, a: np.ndarray, out_dtype) -> np.ndarray:
 
 
 def ycrcb_from_rgb(rgb: np.ndarray) -> np.ndarray:
-    """color_transforms.YCrCb.from_RGB (A11) on a u8 H x W x 3 frame."""
+    """color_transforms.YCrCb.from_RGB (A12) on a u8 H x W x 3 frame."""
     rgb = _rgb(rgb, "rgb")
     if rgb.dtype != np.uint8:
         raise TypeError("from_RGB takes uint8 frames")
@@ -64,7 +64,7 @@ def ycrcb_from_rgb(rgb: np.ndarray) -> np.ndarray:
 
 
 def ycrcb_to_rgb(ycc: np.ndarray) -> np.ndarray:
-    """color_transforms.YCrCb.to_RGB (A11) on a u8 H x W x 3 frame."""
+    """color_transforms.YCrCb.to_RGB (A12) on a u8 H x W x 3 frame."""
     ycc = _rgb(ycc, "ycrcb")
     if ycc.dtype != np.uint8:
         raise TypeError("to_RGB takes uint8 frames")
@@ -134,7 +134,7 @@ def lm_histogram_device(x: DeviceBuffer, dtype, n_px: int, channels: int, min_va
 
 
 def lm_design(counts: np.ndarray, Q: int, min_val: int) -> np.ndarray:
-    """LloydMax_Quantizer(Q_step=Q, counts, min_val, ...).get_representation_levels() (A12)."""
+    """LloydMax_Quantizer(Q_step=Q, counts, min_val, ...).get_representation_levels() (A13)."""
     c = np.ascontiguousarray(counts, dtype=np.int64)
     n_bins = c.shape[0]
     cent = np.empty(-(-n_bins // int(Q)) if Q >= 1 else 1, np.float64)
