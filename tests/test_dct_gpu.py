@@ -136,14 +136,15 @@ def test_unknown_variant_rejected():
 
 
 @pytest.mark.parametrize("shape", SHAPES + [(2160, 3840), (1080, 1920)])
-@pytest.mark.parametrize("Q,flags", [(32, 0), (7, 1), (1, 0), (5, 3), (64, 2)])
+@pytest.mark.parametrize("Q,flags", [(32, 0), (7, 1), (1, 0), (5, 3), (64, 2), (30001, 0)])
 def test_decode_variants_vs_oracle(shape, Q, flags):
-    """Both decode kernels (1 lane-per-block, 2 column-per-lane) are bit-exact."""
+    """The decode kernels (0 automatic: column-per-lane with the dequantization
+    table, 1 lane-per-block, 2 column-per-lane with the 32-bit multiply) are bit-exact."""
     H, W = shape
     rgb = _rand((H, W, 3), seed=H * 31 + W + Q, kind="smooth" if W % 2 else "rand")
     k = O.encode_frame(rgb, Q, flags) if H * W <= 1 << 20 else D.encode(rgb, Q, flags)
     want = O.decode_frame(k, H, W, Q, flags)
-    for v in (1, 2):
+    for v in (0, 1, 2):
         assert np.array_equal(D.decode(k, H, W, Q, flags, variant=v), want), v
 
 
@@ -152,7 +153,7 @@ def test_decode_variants_batched():
     k = D.encode(frames, 32, 0)
     a = D.decode(k, 72, 4104, 32, 0, variant=1)
     b = D.decode(k, 72, 4104, 32, 0, variant=2)
-    for v in (3, 4, 5):   # load/store-hint and priority A/B variants of 2
+    for v in (0, 3, 4, 5, 6, 7):   # the table default and the A/B variants of 2
         assert np.array_equal(D.decode(k, 72, 4104, 32, 0, variant=v), b), v
     assert np.array_equal(a, b)
     assert np.array_equal(a[2], O.decode_frame(k[2], 72, 4104, 32, 0))

@@ -513,6 +513,7 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_encode_cols(const uint8_t *__re
 template <int TB>
 struct DecColsSmem {
     double tr[TB][8][9];   // per-block transpose tile, pitch 9
+    double lut[256];       // DQ 1: the dequantized int16 value of each index byte, / 16
     uint8_t stage[64 * TB * 3 + 8 * 32];
 };
 
@@ -520,7 +521,13 @@ struct DecColsSmem {
 // 1.7 % faster than non-temporal ones; the store hint does not matter
 // (decode variants 3 and 4 are the A/B records).  PRIO: wave
 // priority while the index loads issue (3: 1 % faster than 0, variant 5).
-template <int TB, bool SUB, bool PERC, bool PAD, bool NTL = false, bool NTS = true, int PRIO = 3>
+// DQ: how an index byte becomes the column pass's input.  0: (int16)(Q*(k-128))
+// with a 32-bit multiply, converted, the transform's 1/16 applied to each
+// output (ldexp); 2: the same with a 24-bit multiply (full rate); 1: one LDS
+// table of the 256 possible values, already divided by 16 -- a power of two
+// commutes with every rounding of the transform (no value comes near the
+// subnormal range), so the outputs are bit-identical and need no scaling.
+template <int TB, bool SUB, bool PERC, bool PAD, bool NTL = false, bool NTS = true, int PRIO = 3, int DQ = 0>
 __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__restrict__ kin,
                                                               uint8_t *__restrict__ rgb, Geom g, int Q,
                                                               int tiles_per_row)
@@ -562,6 +569,10 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
         }
     }
     if (PRIO) __builtin_amdgcn_s_setprio(0);
+    if constexpr (DQ == 1 && !PERC) {
+        static_assert(TB * 8 >= 256, "one table entry per thread");
+        if (tid < 256) sm.lut[tid] = (double)(int16_t)__mul24(Q, tid - 128) * 0.0625;
+    }
     __syncthreads();
     if (lb >= nvalid) return;
 
@@ -575,7 +586,11 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
         for (int i = 0; i < 8; ++i) {
             const int kb = SUB ? sm.stage[cols_stage_off<TB, SUB>(i * 8 + x) + lb * 3 + C]
                                : sm.stage[cols_stage_off<TB, SUB>(i) + lb * 24 + x * 3 + C];
-            int16_t yv = (int16_t)(Q * (kb - 128));
+            if constexpr (DQ == 1 && !PERC) {
+                col[i] = sm.lut[kb];
+                continue;
+            }
+            int16_t yv = (int16_t)(DQ ? __mul24(Q, kb - 128) : Q * (kb - 128));
             if (PERC) {
                 const float f = (float)((double)(float)yv / pweight_rt(C, i * 8 + x));
                 yv = (int16_t)(int)f;
@@ -593,7 +608,8 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
         wave_lds_fence();   // the tile is rewritten by the next channel
         dct3_8r(row);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) out[C][j] = (int16_t)(int)(row[j] * 0.0625);   // fct 1/4 per pass; int16
+        for (int j = 0; j < 8; ++j)   // fct 1/4 per pass (already in the inputs for DQ 1); int16
+            out[C][j] = (int16_t)(int)(DQ == 1 && !PERC ? row[j] : row[j] * 0.0625);
     }
     // :444 remove_padding, :449 to_RGB (int16), :454 += 128, :466 clip, uint8
     uint32_t px[24];
@@ -637,9 +653,10 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
     }
 }
 
+// dq: the dequantization of dct_dz_decode_cols (1, the table, by default; 0 for A/B)
 template <int TB>
 int launch_decode_cols(const uint8_t *k_dev, int64_t n_frames, uint8_t *rgb_dev, const Geom &g, int Q, bool sub,
-                       bool perc, bool pad, void *stream)
+                       bool perc, bool pad, void *stream, int dq = 1)
 {
     const int tpr = (g.nbx + TB - 1) / TB;
     for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
@@ -647,9 +664,14 @@ int launch_decode_cols(const uint8_t *k_dev, int64_t n_frames, uint8_t *rgb_dev,
         const uint8_t *in = k_dev + f0 * g.out_stride;
         uint8_t *out = rgb_dev + f0 * g.in_stride;
 #define VCF_DEC2(SB, PC, PD) \
-        if (sub == SB && perc == PC && pad == PD) \
-            hipLaunchKernelGGL((dct_dz_decode_cols<TB, SB, PC, PD>), grid, dim3(TB * 8), 0, \
-                               (hipStream_t)stream, in, out, g, Q, tpr);
+        if (sub == SB && perc == PC && pad == PD) { \
+            if (dq == 1) \
+                hipLaunchKernelGGL((dct_dz_decode_cols<TB, SB, PC, PD, false, true, 3, 1>), grid, dim3(TB * 8), 0, \
+                                   (hipStream_t)stream, in, out, g, Q, tpr); \
+            else \
+                hipLaunchKernelGGL((dct_dz_decode_cols<TB, SB, PC, PD>), grid, dim3(TB * 8), 0, \
+                                   (hipStream_t)stream, in, out, g, Q, tpr); \
+        }
         VCF_DEC2(true, false, false) else VCF_DEC2(true, false, true)
         else VCF_DEC2(true, true, false) else VCF_DEC2(true, true, true)
         else VCF_DEC2(false, false, false) else VCF_DEC2(false, false, true)
@@ -970,7 +992,7 @@ int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frame
         return dct_any_decode_u8(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, stream);
     int rc = check_args(k_dev, rgb_dev, n_frames, H, W, block_size, Q, flags, true);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 5) return set_error(VCF_ERR_INVALID, "unknown decode variant %d", variant);
+    if (variant < 0 || variant > 7) return set_error(VCF_ERR_INVALID, "unknown decode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -988,12 +1010,19 @@ int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frame
         else if (variant == 4)   // plain pixel stores
             hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, false>), grid, dim3(256), 0,
                                (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
-        else   // no wave priority for the load phase
+        else if (variant == 5)   // no wave priority for the load phase
             hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 0>), grid, dim3(256), 0,
+                               (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
+        else if (variant == 6)   // dequantization table in LDS, 1/16 folded in
+            hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 1>), grid, dim3(256), 0,
+                               (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
+        else   // 24-bit multiply for the dequantization
+            hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 2>), grid, dim3(256), 0,
                                (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
         return hip_check(hipGetLastError(), "decode variant 3/4 launch");
     }
-    if (variant != 1) return launch_decode_cols<32>(k_dev, n_frames, rgb_dev, g, (int)Q, sub, perc, pad, stream);
+    if (variant != 1)
+        return launch_decode_cols<32>(k_dev, n_frames, rgb_dev, g, (int)Q, sub, perc, pad, stream, variant == 2 ? 0 : 1);
     for (int64_t f0 = 0; f0 < n_frames; f0 += 65535) {
         const dim3 grid(g.tiles_per_frame, (unsigned)std::min<int64_t>(65535, n_frames - f0));
         VCF_DEC_CASE(true, false, false) else VCF_DEC_CASE(true, false, true)
