@@ -185,14 +185,16 @@ int vcf_dct_raw_decode(const int16_t *coef_dev, int64_t n_frames, int32_t H, int
                        uint32_t flags, uint8_t *rgb_dev, void *stream);
 
 /* Same as vcf_dct_dz_decode with an explicit kernel choice (A/B tests and
- * benchmarks): 0 = automatic (column-per-lane with the dequantization table,
- * any flags), 1 = lane-per-block (one block's 64 float64 samples per lane),
+ * benchmarks): 0 = automatic (column-per-lane with the dequantization table
+ * and, for aligned frames, the packed int16 epilogue; any flags), 1 = lane-per-block (one block's 64 float64 samples per lane),
  * 2 = column-per-lane (8 lanes per block, LDS transpose) dequantizing with a
  * 32-bit multiply and scaling each output by 1/16 (the round-1 default),
  * 3, 4, 5 = variant 2 with non-temporal index loads (3, the earlier policy),
  * plain pixel stores (4) or no raised wave priority for the load phase (5),
- * 6 = the automatic kernel (an LDS table of the 256 dequantized values / 16),
- * 7 = variant 2 with a 24-bit multiply (3-7: A/B references; aligned frames,
+ * 6 = the LDS table of the 256 dequantized values / 16 alone, 7 = variant 2
+ * with a 24-bit multiply, 8 = the automatic kernel: the table plus to_RGB,
+ * += 128 and the clamp on pixel pairs in packed int16 arithmetic, bytes by
+ * permutes, 24-bit staging offsets (3-8: A/B references; aligned frames,
  * subbands, no -p).
  * Outputs identical. */
 int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,

@@ -527,7 +527,11 @@ struct DecColsSmem {
 // table of the 256 possible values, already divided by 16 -- a power of two
 // commutes with every rounding of the transform (no value comes near the
 // subnormal range), so the outputs are bit-identical and need no scaling.
-template <int TB, bool SUB, bool PERC, bool PAD, bool NTL = false, bool NTS = true, int PRIO = 3, int DQ = 0>
+// EPI 1 (aligned frames): to_RGB, += 128 and the clamp on pixel pairs in packed
+// int16 arithmetic (v_pk_add/sub/max/min_i16 wrap exactly as numpy's int16),
+// the 24 bytes formed with byte permutes; 0: one pixel at a time.
+template <int TB, bool SUB, bool PERC, bool PAD, bool NTL = false, bool NTS = true, int PRIO = 3, int DQ = 0,
+          int EPI = 0>
 __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__restrict__ kin,
                                                               uint8_t *__restrict__ rgb, Geom g, int Q,
                                                               int tiles_per_row)
@@ -548,14 +552,32 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
         return (uint32_t)(SUB ? seg_offset_sub(g, by, bx0, seg) : seg_offset_nosub(g, by, bx0, seg));
     };
     if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+    // EPI 1 also takes the staging offsets in 24-bit arithmetic when the frame
+    // allows it (wave-uniform): seg = q / cps by a multiply-shift, the run
+    // offset from per-workgroup constants (no 32-bit multiplies per lane)
+    const uint32_t runA = (uint32_t)g.nby * (uint32_t)g.Wp * 3u, runB = (uint32_t)g.nbx * 3u;
+    const bool fast24 = EPI == 1 && SUB && runA < (1u << 24) && runB * 8u < (1u << 24);
+    const uint32_t runBase = ((uint32_t)by * (uint32_t)g.Wp + (uint32_t)bx0) * 3u;
     if (g.vec && nvalid == TB && (TB * 3) % 16 == 0) {
         constexpr int cps = (SUB ? 3 * TB : 24 * TB) / 16, total = nseg * cps;
+        constexpr uint32_t kDivM = ((1u << 18) + cps - 1) / cps;   // q / cps for q < total
+        static_assert(total < 4096, "multiply-shift division range");
 #pragma unroll
         for (int q0 = 0; q0 < total; q0 += TB * 8) {
             const int q = q0 + tid;
             if (total % (TB * 8) == 0 || q < total) {
-                const int seg = q / cps, off = (q - seg * cps) << 4;
-                const u32x4 *gp = reinterpret_cast<const u32x4 *>(src + seg_off(seg) + off);
+                int seg, off;
+                uint32_t so;
+                if (fast24) {
+                    seg = (int)(__umul24((uint32_t)q, kDivM) >> 18);
+                    off = (q - seg * cps) << 4;
+                    so = __umul24((uint32_t)(seg >> 3), runA) + __umul24((uint32_t)(seg & 7), runB) + runBase;
+                } else {
+                    seg = q / cps;
+                    off = (q - seg * cps) << 4;
+                    so = seg_off(seg);
+                }
+                const u32x4 *gp = reinterpret_cast<const u32x4 *>(src + so + off);
                 *reinterpret_cast<u32x4 *>(sm.stage + cols_stage_off<TB, SUB>(seg) + off) =
                     NTL ? __builtin_nontemporal_load(gp) : *gp;
             }
@@ -612,6 +634,45 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
             out[C][j] = (int16_t)(int)(DQ == 1 && !PERC ? row[j] : row[j] * 0.0625);
     }
     // :444 remove_padding, :449 to_RGB (int16), :454 += 128, :466 clip, uint8
+    if constexpr (EPI == 1 && !PAD) {
+        typedef short s2 __attribute__((ext_vector_type(2)));
+        const s2 off = {128, 128}, zero = {0, 0}, top = {255, 255};
+        uint32_t RG[4], Bq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const s2 Y = {(short)out[0][2 * q], (short)out[0][2 * q + 1]};
+            const s2 Co = {(short)out[1][2 * q], (short)out[1][2 * q + 1]};
+            const s2 Cg = {(short)out[2][2 * q], (short)out[2][2 * q + 1]};
+            s2 R = Y + Co - Cg + off, G = Y + Cg + off, B = Y - Co - Cg + off;
+            R = __builtin_elementwise_min(__builtin_elementwise_max(R, zero), top);
+            G = __builtin_elementwise_min(__builtin_elementwise_max(G, zero), top);
+            B = __builtin_elementwise_min(__builtin_elementwise_max(B, zero), top);
+            // R(2q) G(2q) R(2q+1) G(2q+1); B(2q) and B(2q+1) sit in bytes 0 and 2 of Bq
+            RG[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, G), __builtin_bit_cast(uint32_t, R),
+                                          0x06020400u);
+            Bq[q] = __builtin_bit_cast(uint32_t, B);
+        }
+        uint32_t w[6];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {   // pixels 4h .. 4h+3: 12 bytes
+            const uint32_t a = RG[2 * h], b = Bq[2 * h], c = RG[2 * h + 1], d = Bq[2 * h + 1];
+            w[3 * h + 0] = __builtin_amdgcn_perm(b, a, 0x02040100u);                 // R G B R
+            const uint32_t t = __builtin_amdgcn_perm(b, a, 0x0c0c0603u);             // G B
+            w[3 * h + 1] = __builtin_amdgcn_perm(c, t, 0x05040100u);                 // G B R G
+            w[3 * h + 2] = __builtin_amdgcn_perm(d, c, 0x06030204u);                 // B R G B
+        }
+        u32x2 *p = reinterpret_cast<u32x2 *>(dst + ((uint32_t)(by * 8 + x) * (uint32_t)g.W + (uint32_t)bx * 8) * 3);
+        if (NTS) {
+            __builtin_nontemporal_store(u32x2{w[0], w[1]}, p);
+            __builtin_nontemporal_store(u32x2{w[2], w[3]}, p + 1);
+            __builtin_nontemporal_store(u32x2{w[4], w[5]}, p + 2);
+        } else {
+            p[0] = u32x2{w[0], w[1]};
+            p[1] = u32x2{w[2], w[3]};
+            p[2] = u32x2{w[4], w[5]};
+        }
+        return;
+    }
     uint32_t px[24];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -653,7 +714,8 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
     }
 }
 
-// dq: the dequantization of dct_dz_decode_cols (1, the table, by default; 0 for A/B)
+// dq: 1 (default) = the dequantization table with the packed int16 epilogue; 0 = the
+// round-1 kernel (decode variant 2, A/B)
 template <int TB>
 int launch_decode_cols(const uint8_t *k_dev, int64_t n_frames, uint8_t *rgb_dev, const Geom &g, int Q, bool sub,
                        bool perc, bool pad, void *stream, int dq = 1)
@@ -666,7 +728,7 @@ int launch_decode_cols(const uint8_t *k_dev, int64_t n_frames, uint8_t *rgb_dev,
 #define VCF_DEC2(SB, PC, PD) \
         if (sub == SB && perc == PC && pad == PD) { \
             if (dq == 1) \
-                hipLaunchKernelGGL((dct_dz_decode_cols<TB, SB, PC, PD, false, true, 3, 1>), grid, dim3(TB * 8), 0, \
+                hipLaunchKernelGGL((dct_dz_decode_cols<TB, SB, PC, PD, false, true, 3, 1, 1>), grid, dim3(TB * 8), 0, \
                                    (hipStream_t)stream, in, out, g, Q, tpr); \
             else \
                 hipLaunchKernelGGL((dct_dz_decode_cols<TB, SB, PC, PD>), grid, dim3(TB * 8), 0, \
@@ -992,7 +1054,7 @@ int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frame
         return dct_any_decode_u8(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, stream);
     int rc = check_args(k_dev, rgb_dev, n_frames, H, W, block_size, Q, flags, true);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 7) return set_error(VCF_ERR_INVALID, "unknown decode variant %d", variant);
+    if (variant < 0 || variant > 8) return set_error(VCF_ERR_INVALID, "unknown decode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -1016,9 +1078,12 @@ int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frame
         else if (variant == 6)   // dequantization table in LDS, 1/16 folded in
             hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 1>), grid, dim3(256), 0,
                                (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
-        else   // 24-bit multiply for the dequantization
+        else if (variant == 7)   // 24-bit multiply for the dequantization
             hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 2>), grid, dim3(256), 0,
                                (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
+        else   // the table and the packed int16 epilogue
+            hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 1, 1>), grid, dim3(256),
+                               0, (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
         return hip_check(hipGetLastError(), "decode variant 3/4 launch");
     }
     if (variant != 1)
