@@ -507,7 +507,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
                                                         long long packed_stride, long long ll_off, long long off_lh,
                                                         long long off_hl, long long off_hh, int h, int w, int hh,
-                                                        int hw, int Q, Taps<F> tp, Filters flt)
+                                                        int hw, int Q, Taps<F> tp, Filters flt, int cw)
 {
     constexpr int TW = fwd_tile_w(F), IH = 2 * (kFTH - 1) + F, IW = kFIW;
     constexpr int NWIN = 2 * (kG - 1) + F;
@@ -520,7 +520,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                             double>::type;
     __shared__ Stage tin[IH * IW];
     __shared__ double tA[kFTH * RS + 8], tD[kFTH * RS + 8];   // +8: the last row group's window overhang
-    __shared__ uint8_t stage[3 * SB];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[3 * SB];
     __shared__ uint8_t stage16[LAST ? 2 * SB : 1];
     __shared__ double stageLL[LAST || PIPE ? 1 : kFTH * TW];
     const int o0 = blockIdx.y * kFTH, c0 = blockIdx.x * TW;
@@ -676,15 +676,32 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
     }
     if (PIPE) __syncthreads();   // the byte image is complete
     if (PRI) __builtin_amdgcn_s_setprio(PRI);
-    // copy-out: each subband row of the tile is one contiguous byte run
+    // copy-out: each subband row of the tile is one contiguous byte run, moved
+    // as dwords when every run start is 4-byte aligned (cw 4; cw 1 = bytes, the
+    // earlier copy kept for A/B as dwt variant 10)
     const int rows = min(kFTH, hh - o0), nb = min(TW, hw - c0) * 3;
     uint8_t *pk = packed + frame * packed_stride;
     const long long offs[3] = {off_lh, off_hl, off_hh};
-    for (int sb = 0; sb < 3; ++sb)
-        for (int t = tid; t < rows * TW * 3; t += 256) {
-            const int o = t / (TW * 3), b = t - o * (TW * 3);
-            if (b < nb) pk[offs[sb] + ((long long)(o0 + o) * hw + c0) * 3 + b] = stage[sb * SB + t];
+    constexpr int TWW = TW * 3 / 4;   // dwords per staged subband row
+    const bool dw = (TW * 3) % 4 == 0 && cw == 4 &&
+                    ((reinterpret_cast<uintptr_t>(pk) | (uintptr_t)(off_lh | off_hl | off_hh | (long long)hw * 3 |
+                                                                    (long long)c0 * 3 | nb)) & 3u) == 0;
+    if (dw) {
+        const int nw = nb >> 2;
+        for (int t = tid; t < 3 * rows * TWW; t += 256) {
+            const int sb = t / (rows * TWW), r = t - sb * (rows * TWW);
+            const int o = r / TWW, b = r - o * TWW;
+            if (b < nw)
+                *reinterpret_cast<uint32_t *>(pk + offs[sb] + ((long long)(o0 + o) * hw + c0) * 3 + 4 * b) =
+                    *reinterpret_cast<const uint32_t *>(stage + sb * SB + o * (TW * 3) + 4 * b);
         }
+    } else {
+        for (int sb = 0; sb < 3; ++sb)
+            for (int t = tid; t < rows * TW * 3; t += 256) {
+                const int o = t / (TW * 3), b = t - o * (TW * 3);
+                if (b < nb) pk[offs[sb] + ((long long)(o0 + o) * hw + c0) * 3 + b] = stage[sb * SB + t];
+            }
+    }
     if (LAST)
         for (int t = tid; t < rows * TW * 6; t += 256) {
             const int o = t / (TW * 6), b = t - o * (TW * 6);
@@ -1271,6 +1288,7 @@ struct LevelArgs {
     hipStream_t s;
     int pipe = 1;   // fused levels, bior4.4/db5: 0 = the three-barrier schedule (variant 3), 2 = run-time taps (4),
                     // 3 = level 1 staged as float (5)
+    int copy_w = 4; // fused forward levels' copy-out: 4 = dwords when aligned, 1 = bytes (variant 10)
 };
 
 // bit m set = tap m is exactly 0.0
@@ -1316,7 +1334,8 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
         }
     }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed,
-                       a.packed_stride, a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt);
+                       a.packed_stride, a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt,
+                       a.copy_w);
 }
 
 template <int F>
@@ -1525,7 +1544,9 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 9) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant > 10) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    const int copy_w = variant == 10 ? 1 : 4;   // 10: variant 0 with the byte-wise copy-out (A/B)
+    if (variant == 10) variant = 0;
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1553,7 +1574,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
                           g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
                           g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s,
-                          variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : 1};
+                          variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : 1, copy_w};
         // strips need planes of at least 2F rows and columns (their row wrap)
         const bool strip = F <= kMaxStripF && g.hs[l - 1] >= 2 * F && g.ws[l - 1] >= 2 * F &&
                            ((variant >= 6 && variant <= 8) || ((variant == 0 || variant == 9) && l > 1 && l < levels));
