@@ -78,7 +78,8 @@ def dwt(args):
                          "one 4K S-smooth frame, oracle/vcf_dwt_oracle.cpp (pywt 1.1.1 'per' restated)")
     cpu_d, _ = cpu_port(lambda: O.dwt_decode_frame(sb, H, W, "bior4.4", L_, Q), H * W,
                         "one 4K frame's subbands, oracle/vcf_dwt_oracle.cpp")
-    for variant, vname in ((1, "fused level kernels"), (2, "separable kernels")):
+    for variant, vname in ((0, "default (fused level 1 and last level, strips for the middle levels)"),
+                           (1, "fused level kernels"), (2, "separable kernels")):
         enc = lambda: L.call("vcf_dwt_dz_encode_variant", variant, din.ptr, F, H, W, w, L_, Q, dpk.ptr, dws.ptr,
                              s.handle)
         dec = lambda: L.call("vcf_dwt_dz_decode_variant", variant, dpk.ptr, F, H, W, w, L_, Q, dout.ptr, dws.ptr,
@@ -108,7 +109,8 @@ def dct_decode(args):
     from oracle import oracle as O
     k0 = O.encode_frame(frames[0], Q)
     cpu, _ = cpu_port(lambda: O.decode_frame(k0, H, W, Q), H * W, "one 4K frame, oracle/vcf_oracle.c")
-    for variant, vname in ((2, "column-per-lane"), (1, "lane-per-block")):
+    for variant, vname in ((0, "default (column-per-lane, dequantization table, packed int16 epilogue)"),
+                           (2, "column-per-lane, round-1 form"), (1, "lane-per-block")):
         t = timed(s, lambda: D.decode_device(dk, F, H, W, Q, out=dout, stream=s, variant=variant), args.steps, 3)
         print(json.dumps({"metric": "Mpixels/s dct_decode 4K Q=32", "variant": vname,
                           "value": round(F * H * W / t / 1e3, 1),

@@ -1,6 +1,4 @@
 set -u
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u scripts/ab_dwt.py 10,0 > gpurun_out/ab_dwt.log 2>&1
-rc=$?; echo "ab rc=$rc"; tail -4 gpurun_out/ab_dwt.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u -m pytest tests/test_dwt_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_dwt.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_dwt.log
+timeout -k 10 500 python -u scripts/bench_paths.py --only dwt,dct_decode,dct_encode_pcie,ipp > gpurun_out/paths.jsonl 2> gpurun_out/paths.err
+rc=$?; echo "paths rc=$rc"; cat gpurun_out/paths.jsonl | cut -c1-400
