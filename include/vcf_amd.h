@@ -124,8 +124,10 @@ int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
  * 12-16 = variant 5 with wave priority 3 for the load issue and copy-out
  *      (12, the default's setting), 1 for both (13), the copy-out only (14),
  *      the loads only (15), none (16) (A/B references, aligned frames with
- *      subbands).
- * Variants 1, 3, 4, 5, 7 and 11-16 produce identical bytes. */
+ *      subbands),
+ * 17 = variant 5 with the earlier address arithmetic (32-bit divisions and
+ *      multiplies per copy-out chunk, a 64-bit multiply per input row; A/B).
+ * Variants 1, 3, 4, 5, 7 and 11-17 produce identical bytes. */
 int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H,
                               int32_t W, int32_t block_size, int32_t Q, uint32_t flags,
                               uint8_t *k_dev, void *stream);

@@ -182,6 +182,6 @@ def test_store_policy_ab_variant_equal():
     as the default; it only exists for A/B timing."""
     frames = np.stack([_rand((1080, 1920, 3), s, "smooth") for s in range(3)])
     want = D.encode(frames, 32, 0, variant=1)
-    for v in (0, 5, 7, 11, 12, 13, 14, 15, 16):
+    for v in (0, 5, 7, 11, 12, 13, 14, 15, 16, 17):
         assert np.array_equal(D.encode(frames, 32, 0, variant=v), want), v
     assert np.array_equal(want[1], O.encode_frame(frames[1], 32, 0))

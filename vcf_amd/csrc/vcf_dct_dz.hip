@@ -133,7 +133,12 @@ __device__ __forceinline__ void move_runs_tab(const Geom &g, uint8_t *stage, con
 // in the XCD's L2 until the neighbour's half arrives (the tile order keeps
 // neighbours on one XCD, see dct_dz_encode_kernel); non-temporal stores
 // wrote those lines twice, half at a time (2 % slower).
-template <bool SUB, int NT = 1>   // NT: 1 non-temporal stores, 0 plain, 2 plain within 128 B of a run's ends
+// FA: the chunk -> (run, offset, block) divisions as 24-bit multiply-shifts and
+// the run bases from two per-launch constants (full-rate v_mul_u32_u24 instead
+// of quarter-rate 32-bit multiplies and 64-bit address arithmetic) whenever the
+// frame's subband stride fits 24 bits; FA = false is the earlier code (encode
+// variant 17, A/B).
+template <bool SUB, int NT = 1, bool FA = false>   // NT: 1 non-temporal stores, 0 plain, 2 plain within 128 B of a run's ends
 __device__ __forceinline__ void move_runs_full(const Geom &g, const uint8_t *stage, const uint32_t *rowbase,
                                                uint8_t *frame)
 {
@@ -147,15 +152,31 @@ __device__ __forceinline__ void move_runs_full(const Geom &g, const uint8_t *sta
     u32x4 v[per_lane];
     uint32_t go[per_lane];
     bool edge[per_lane];
+    const uint32_t segA = (uint32_t)g.nby * (uint32_t)g.Wp * 3u, segB = (uint32_t)g.nbx * 3u;
+    if (FA && SUB && segA < (1u << 24)) {
+        static_assert(!SUB || (cps == 48 && bpb == 3), "multiply-shift constants");
 #pragma unroll
-    for (int r = 0; r < per_lane; ++r) {
-        const int q = tid + r * kTile;
-        const int seg = q / cps;
-        const int off = (q - seg * cps) << 4;
-        const int blk = off / bpb;
-        go[r] = rowbase[blk] + seg_base<SUB>(g, seg) + (uint32_t)(off - blk * bpb);
-        v[r] = *reinterpret_cast<const u32x4 *>(stage + seg * lds_stride + off);
-        edge[r] = off < 128 || off + 16 > cps * 16 - 128;
+        for (int r = 0; r < per_lane; ++r) {
+            const int q = tid + r * kTile;                                   // < 3072
+            const int seg = (int)(__umul24((uint32_t)q, 21846u) >> 20);      // q / 48
+            const int off = (q - seg * cps) << 4;                            // < 768
+            const int blk = (int)(__umul24((uint32_t)off, 43691u) >> 17);    // off / 3
+            go[r] = rowbase[blk] + __umul24((uint32_t)(seg >> 3), segA) + __umul24((uint32_t)(seg & 7), segB) +
+                    (uint32_t)(off - blk * bpb);
+            v[r] = *reinterpret_cast<const u32x4 *>(stage + seg * lds_stride + off);
+            edge[r] = off < 128 || off + 16 > cps * 16 - 128;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < per_lane; ++r) {
+            const int q = tid + r * kTile;
+            const int seg = q / cps;
+            const int off = (q - seg * cps) << 4;
+            const int blk = off / bpb;
+            go[r] = rowbase[blk] + seg_base<SUB>(g, seg) + (uint32_t)(off - blk * bpb);
+            v[r] = *reinterpret_cast<const u32x4 *>(stage + seg * lds_stride + off);
+            edge[r] = off < 128 || off + 16 > cps * 16 - 128;
+        }
     }
 #pragma unroll
     for (int r = 0; r < per_lane; ++r) {
@@ -182,15 +203,17 @@ __device__ __forceinline__ void opaque(uint32_t (&raw)[8][6], uint32_t dep)
 // LD: 1 plain loads (default), 0 non-temporal loads (encode variant 11, an
 // A/B record: 2.7 % slower).  The compiler merges each row's
 // three 8-byte loads into one 16-byte and one 8-byte load either way.
-template <bool PAD, int LD = 1>
+template <bool PAD, int LD = 1, bool FA = false>
 __device__ __forceinline__ void load_block(const Geom &g, const uint8_t *src, int by, int bx,
                                            uint32_t (&raw)[8][6])
 {
     if (!PAD) {
+        // FA: one 64-bit block address, the rows at uniform (scalar) offsets y * 3W
+        const uint8_t *blk = src + ((long long)by * 8 * g.W + bx * 8) * 3;
 #pragma unroll
         for (int y = 0; y < 8; ++y) {
             const u32x2 *p = reinterpret_cast<const u32x2 *>(
-                src + ((long long)(by * 8 + y) * g.W + bx * 8) * 3);
+                FA ? blk + (long long)y * (3LL * g.W) : src + ((long long)(by * 8 + y) * g.W + bx * 8) * 3);
             const u32x2 a = LD == 0 ? __builtin_nontemporal_load(p) : p[0];
             const u32x2 b = LD == 0 ? __builtin_nontemporal_load(p + 1) : p[1];
             const u32x2 c = LD == 0 ? __builtin_nontemporal_load(p + 2) : p[2];
@@ -264,7 +287,7 @@ __device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncCon
 // workgroups' VALU streams (15, the default, measured 1-2.5 % faster than 0
 // over three boxes, ABBA; variants 12-15 and 16 = PRIO 0 are the A/B records).
 template <bool POW2, bool SUB, bool PERC, bool PAD, bool SDWA = true, bool PK = false, bool MEMONLY = false,
-          int STREAMS = 0, int NT = 0, bool XCD = true, int LD = 1, int PRIO = 15>
+          int STREAMS = 0, int NT = 0, bool XCD = true, int LD = 1, int PRIO = 15, bool FA = true>
 __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
                                                               uint8_t *__restrict__ kout, Geom g,
                                                               EncConsts K, FinalK rowk)
@@ -290,7 +313,7 @@ __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__r
         rowbase[tid] = block_rowbase<SUB>(g, by, bx);
         uint32_t raw[8][6];
         if (PRIO & 3) __builtin_amdgcn_s_setprio(PRIO & 3);
-        load_block<PAD, LD>(g, rgb + frame * g.in_stride, by, bx, raw);
+        load_block<PAD, LD, FA>(g, rgb + frame * g.in_stride, by, bx, raw);
         if (PRIO & 3) __builtin_amdgcn_s_setprio(0);
         encode_block<POW2, SUB, PERC, SDWA, PK, MEMONLY>(raw, K, rowk, stage, tid);
     }
@@ -310,7 +333,7 @@ __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__r
             }
         return;
     }
-    if (nvalid == kTile && g.vec) move_runs_full<SUB, NT>(g, stage, rowbase, kout + frame * g.out_stride);
+    if (nvalid == kTile && g.vec) move_runs_full<SUB, NT, FA>(g, stage, rowbase, kout + frame * g.out_stride);
     else move_runs_tab<SUB, true>(g, stage, rowbase, kout + frame * g.out_stride, nvalid);
 }
 
@@ -934,7 +957,7 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         return dct_any_encode_u8(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, stream);
     int rc = check_args(rgb_dev, k_dev, n_frames, H, W, block_size, Q, flags, false);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 16) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
+    if (variant < 0 || variant > 17) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -994,6 +1017,14 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         VCF_ENC_PRIO(12, 15) VCF_ENC_PRIO(13, 5) VCF_ENC_PRIO(14, 12) VCF_ENC_PRIO(15, 3) VCF_ENC_PRIO(16, 0)
 #undef VCF_ENC_PRIO
         return hip_check(hipGetLastError(), "variant 12-16 launch");
+    }
+    if (variant == 17) {   // A/B: the default with the earlier address arithmetic (FA = false)
+        if (!(pow2 && !perc && sub && !pad)) return set_error(VCF_ERR_INVALID, "variant 17: pow2 Q, aligned, default flags");
+        if (n_frames > 65535) return set_error(VCF_ERR_INVALID, "variant 17: <= 65535 frames");
+        const dim3 grid(g.tiles_per_frame, (unsigned)n_frames);
+        hipLaunchKernelGGL((dct_dz_encode_kernel<true, true, false, false, true, true, false, 0, 0, true, 1, 15, false>),
+                           grid, dim3(kTile), 0, (hipStream_t)stream, rgb_dev, k_dev, g, K, rowk);
+        return hip_check(hipGetLastError(), "variant 17 launch");
     }
     if (variant == 11) {   // A/B: variant 5 with the earlier non-temporal input loads
         if (!(pow2 && !perc && sub && !pad)) return set_error(VCF_ERR_INVALID, "variant 11: pow2 Q, aligned, default flags");
