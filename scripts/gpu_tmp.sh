@@ -1,4 +1,6 @@
 set -u
 cd $GRAFT_REPO_ROOT
-ROUNDS=16 timeout -k 10 300 python -u scripts/bench_variants.py 17,0 > gpurun_out/ab_enc.log 2>&1
-rc=$?; echo "ab rc=$rc"; tail -3 gpurun_out/ab_enc.log
+timeout -k 10 300 python -u scripts/ab_dwt.py 0,1,6 > gpurun_out/ab_dwt.log 2>&1
+rc=$?; echo "ab rc=$rc"; tail -3 gpurun_out/ab_dwt.log; [ $rc -eq 0 ] || exit $rc
+true
+

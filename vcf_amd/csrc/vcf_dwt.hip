@@ -629,11 +629,29 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
         auto ll_dst = [&](int o, int oc) -> double * {
             return PIPE ? llp + (long long)o * hw + oc : stageLL + (o * TW + oc);
         };
-        // row pass (axis 1): (A or D) x kFTH rows x NG groups of 4 outputs
+        // row pass (axis 1): (A or D) x kFTH rows x NG groups of 4 outputs.  Mapping
+        // (cw & 8 == 0, default): 16 group slots per row, so a lane's (src, o, gq)
+        // are bit fields and every half-wave reads two whole rows -- conflict-free
+        // LDS banks -- with the slots past NG idle; cw & 8: NG slots per row (the
+        // earlier mapping, dwt variant 11)
         const int first_tail = row_tail ? max(0, (w - F / 2 + 1) / 2 - c0) : TW;   // first column with i >= w
-        for (int t = tid; t < 2 * kFTH * NG; t += 256) {
-            const int src = t / (kFTH * NG), rest = t % (kFTH * NG);
-            const int o = rest / NG, gq = rest % NG, oc0 = kG * gq;
+        constexpr int NGP = 16;
+        static_assert(NG <= NGP && 2 * kFTH * NGP == 256, "row-pass slots");
+        const bool slots16 = (cw & 8) == 0;
+        for (int t = tid; t < (slots16 ? 256 : 2 * kFTH * NG); t += 256) {
+            int src, o, gq;
+            if (slots16) {
+                src = t >> 7;
+                o = (t >> 4) & (kFTH - 1);
+                gq = t & (NGP - 1);
+                if (gq >= NG) continue;
+            } else {
+                src = t / (kFTH * NG);
+                const int rest = t % (kFTH * NG);
+                o = rest / NG;
+                gq = rest % NG;
+            }
+            const int oc0 = kG * gq;
             const double *row = (src ? tD : tA) + o * RS;
             double v[NWIN];
 #pragma unroll
@@ -683,7 +701,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
     uint8_t *pk = packed + frame * packed_stride;
     const long long offs[3] = {off_lh, off_hl, off_hh};
     constexpr int TWW = TW * 3 / 4;   // dwords per staged subband row
-    const bool dw = (TW * 3) % 4 == 0 && cw == 4 &&
+    const bool dw = (TW * 3) % 4 == 0 && (cw & 7) == 4 &&
                     ((reinterpret_cast<uintptr_t>(pk) | (uintptr_t)(off_lh | off_hl | off_hh | (long long)hw * 3 |
                                                                     (long long)c0 * 3 | nb)) & 3u) == 0;
     if (dw) {
@@ -1544,9 +1562,10 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 10) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
-    const int copy_w = variant == 10 ? 1 : 4;   // 10: variant 0 with the byte-wise copy-out (A/B)
-    if (variant == 10) variant = 0;
+    if (variant < 0 || variant > 11) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    // 10: variant 0 with the byte-wise copy-out, 11: with the earlier row-pass mapping (A/B)
+    const int copy_w = variant == 10 ? 1 : variant == 11 ? 4 | 8 : 4;
+    if (variant >= 10) variant = 0;
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
