@@ -248,7 +248,9 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
  * incomplete), 9 = strips for the middle levels, fused kernels for the first
  * and last, 10 = 0 with the fused levels' subband copy-out byte by byte
  * instead of in dwords, 11 = 0 with the fused levels' earlier row-pass work
- * mapping (NG group slots per row instead of 16; A/B references).  vcf_dwt_dz_decode_variant takes
+ * mapping (NG group slots per row instead of 16), 12 = 0 with no raised wave
+ * priority on any fused level and the staging unchanged (A/B references;
+ * 5 changes level 1's priority and, for db5, its staging together).  vcf_dwt_dz_decode_variant takes
  * 0, 1, 2, 4 (bior4.4's reconstruction taps at run time) and 5 (no raised
  * wave priority while the subbands are staged).  Outputs
  * identical. */

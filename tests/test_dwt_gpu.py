@@ -133,7 +133,7 @@ def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
 def test_dwt_unknown_variant():
     import vcf_amd.dwt as DW
     with pytest.raises(ValueError):
-        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=12)
+        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=13)
 
 
 def test_dwt_errors():

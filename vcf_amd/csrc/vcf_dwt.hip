@@ -1329,7 +1329,7 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
                       : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI> : dwt_level_kernel<F, false, false, ZLO, ZHI>);
     if constexpr (F == 10) {   // bior4.4 / db5: constant taps (pipe 2: run-time taps, dwt variant 4)
         constexpr int id = ZLO != 0 ? 1 : 2;
-        bool ct = a.pipe == 1 || a.pipe == 3;
+        bool ct = a.pipe == 1 || a.pipe == 3 || a.pipe == 5;
         for (int m = 0; m < F; ++m) {
             const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
             ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
@@ -1343,6 +1343,11 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
         if (ct && a.pipe == 3 && first)   // level 1 staged as float, no wave priority (dwt variant 5, A/B)
             kern = last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, 0, 0>
                         : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, 0, 0>;
+        if (ct && a.pipe == 5)   // no raised wave priority on any fused level, staging unchanged (variant 12, A/B)
+            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, stg, 0>
+                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, stg, 0>)
+                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, id, 0, 0>
+                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, true, id, 0, 0>);
         if constexpr (ZLO != 0) {   // bior4.4: the earlier three-barrier schedule for A/B (variant 3)
             if (a.pipe == 0)
                 kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, false>
@@ -1562,9 +1567,11 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 11) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
-    // 10: variant 0 with the byte-wise copy-out, 11: with the earlier row-pass mapping (A/B)
+    if (variant < 0 || variant > 12) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    // 10: variant 0 with the byte-wise copy-out, 11: with the earlier row-pass mapping,
+    // 12: with no raised wave priority on the fused levels (A/B)
     const int copy_w = variant == 10 ? 1 : variant == 11 ? 4 | 8 : 4;
+    const int pipe0 = variant == 12 ? 5 : 1;
     if (variant >= 10) variant = 0;
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
@@ -1593,7 +1600,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
                           g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
                           g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s,
-                          variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : 1, copy_w};
+                          variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : pipe0, copy_w};
         // strips need planes of at least 2F rows and columns (their row wrap)
         const bool strip = F <= kMaxStripF && g.hs[l - 1] >= 2 * F && g.ws[l - 1] >= 2 * F &&
                            ((variant >= 6 && variant <= 8) || ((variant == 0 || variant == 9) && l > 1 && l < levels));
