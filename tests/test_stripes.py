@@ -1,0 +1,108 @@
+"""Single-frame row-stripe sharding on the CPU (vcf_amd/codec/stripes.py):
+the stripe cut, the subband-row scatter and the gather, with the oracle's
+per-frame coder standing in for the HIP kernels -- striped results must be
+the oracle's whole-frame results exactly, for every rank count, ragged
+heights (ranks with no block rows included), -x, -p and other block sizes.
+The real kernels under the same driver: tests/test_stripes_gpu.py."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from vcf_amd.codec import stripes as S
+from vcf_amd.dct import VCF_DCT_NO_SUBBANDS, VCF_DCT_PERCEPTUAL
+
+
+def _enc(x, q, f, b):
+    return O.encode_frame_b(x, b, q, f)
+
+
+def _dec(k, h, w, q, f, b):
+    return O.decode_frame_b(k, h, w, b, q, f)
+
+
+def _img(H, W, seed):
+    return np.random.Generator(np.random.PCG64(seed)).integers(0, 256, (H, W, 3), dtype=np.uint8)
+
+
+def _striped(rgb, P, Q, flags, B):
+    """Every rank's stripe coded on its own, then rank 0's scatter -- the driver minus the transport."""
+    H, W = rgb.shape[:2]
+    Hp, Wp = O.padded_shape(H, W, B)
+    k = np.full((Hp, Wp, 3), 77, np.uint8)
+    seen = []
+    for r in range(P):
+        by0, by1 = S.block_rows(H, B, r, P)
+        seen += range(by0, by1)
+        if by1 > by0:
+            S.place_stripe(k, _enc(S.stripe_pixels(rgb, by0, by1, B), Q, flags, B), by0, by1, B, flags)
+    assert seen == list(range(Hp // B))
+    return k
+
+
+def _unstriped(k, H, W, P, Q, flags, B):
+    parts = []
+    for r in range(P):
+        by0, by1 = S.block_rows(H, B, r, P)
+        if by1 > by0:
+            parts.append(_dec(S.take_stripe(k, by0, by1, B, flags), B * (by1 - by0), W, Q, flags, B))
+    top = (O.padded_shape(H, W, B)[0] - H) // 2
+    return np.concatenate(parts)[top:top + H]
+
+
+@pytest.mark.parametrize("H,W,B", [(64, 48, 8), (61, 45, 8), (7, 13, 8), (100, 36, 16), (50, 22, 6)])
+@pytest.mark.parametrize("flags", [0, VCF_DCT_NO_SUBBANDS, VCF_DCT_PERCEPTUAL])
+@pytest.mark.parametrize("P", [1, 2, 3, 8])
+def test_stripes_equal_whole_frame(H, W, B, flags, P):
+    if flags & VCF_DCT_PERCEPTUAL and B != 8:
+        pytest.skip("-p tables are pinned at B = 8")
+    rgb = _img(H, W, H * 131 + W + P)
+    k = _striped(rgb, P, 32, flags, B)
+    assert np.array_equal(k, O.encode_frame_b(rgb, B, 32, flags))
+    assert np.array_equal(_unstriped(k, H, W, P, 32, flags, B), O.decode_frame_b(k, H, W, B, 32, flags))
+
+
+def test_stripe_pixels_padding():
+    rgb = _img(13, 5, 1)                         # Hp 16: 1 zero row on top, 2 at the bottom
+    s0 = S.stripe_pixels(rgb, 0, 1, 8)
+    s1 = S.stripe_pixels(rgb, 1, 2, 8)
+    assert s0.shape == s1.shape == (8, 5, 3)
+    assert not s0[0].any() and np.array_equal(s0[1:], rgb[:7])
+    assert np.array_equal(s1[:6], rgb[7:]) and not s1[6:].any()
+    assert S.stripe_pixels(rgb, 1, 1, 8).shape == (0, 5, 3)
+
+
+def _worker(rank, world, rgb, Q, flags, B):
+    from vcf_amd.codec import shard
+    g = shard.Group("host")
+    k = S.encode_frame(rgb, g, Q, flags, B, encode=_enc)
+    H, W = rgb.shape[:2]
+    kk = O.encode_frame_b(rgb, B, Q, flags)       # every rank is handed the frame's indices
+    y = S.decode_frame(kk, H, W, g, Q, flags, B, decode=_dec)
+    g.close()
+    return k, y
+
+
+@pytest.mark.parametrize("world,H,W,flags", [(2, 77, 40, 0), (3, 16, 24, VCF_DCT_NO_SUBBANDS)])
+def test_stripes_host_group(world, H, W, flags):
+    """world ranks over the host group: rank 0 gets the whole frame's indices and pixels."""
+    from _dist import run_ranks
+    rgb = _img(H, W, 5)
+    res = run_ranks(_worker, world, rgb, 40, flags, 8)
+    k, y = res[0]
+    assert np.array_equal(k, O.encode_frame_b(rgb, 8, 40, flags))
+    assert np.array_equal(y, O.decode_frame_b(k, H, W, 8, 40, flags))
+    assert all(res[r] == (None, None) for r in range(1, world))
+
+
+def test_single_rank_group_and_errors():
+    from vcf_amd.codec import shard
+    g = shard.Group("host")
+    rgb = _img(20, 12, 9)
+    k = S.encode_frame(rgb, g, 32, 0, 8, encode=_enc)
+    assert np.array_equal(k, O.encode_frame_b(rgb, 8, 32, 0))
+    with pytest.raises(ValueError):
+        S.encode_frame(rgb.astype(np.int16), g, encode=_enc)
+    with pytest.raises(ValueError):
+        S.decode_frame(k[:8], 20, 12, g, decode=_dec)
+    with pytest.raises(NotImplementedError):
+        S.encode_frame(rgb, g, block_size=191, encode=_enc)
