@@ -226,9 +226,9 @@ int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
 
 /* Inverse: packed subbands -> RGB frames of 2*ceil(H/2) x 2*ceil(W/2) x 3
  * (what pywt.waverec2 returns; the reference writes that size too).
- * Replaces 2D-DWT.py:80-101 after the TIFF reader.  1 <= Q <= 32767; the
- * coarsest subbands must be at least filter_length/2 samples on each side
- * (pywt's short-input code path is not restated: VCF_ERR_UNSUPPORTED). */
+ * Replaces 2D-DWT.py:80-101 after the TIFF reader.  1 <= Q <= 32767.
+ * Coarsest subbands shorter than filter_length/2 (pywt's short-input code
+ * path) run on the separable kernels. */
 int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                       int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, void *stream);
 
@@ -250,9 +250,20 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
  * instead of in dwords, 11 = 0 with the fused levels' earlier row-pass work
  * mapping (NG group slots per row instead of 16), 12 = 0 with no raised wave
  * priority on any fused level and the staging unchanged (A/B references;
- * 5 changes level 1's priority and, for db5, its staging together).  vcf_dwt_dz_decode_variant takes
- * 0, 1, 2, 4 (bior4.4's reconstruction taps at run time) and 5 (no raised
- * wave priority while the subbands are staged).  Outputs
+ * 5 changes level 1's priority and, for db5, its staging together),
+ * 13-19 = 0 with the batch cut into chunks of consecutive frames whose
+ * level chains run on the library's streams, forked from and joined to the
+ * caller's stream (13: two streams, two chunks; 14: 13 staggered -- chunk k's
+ * level 1 waits for chunk k-1's -- ; 15 / 16: two streams, four / eight
+ * chunks, staggered; 18: three streams, four chunks, staggered; 19: four
+ * streams, four chunks), 17 = 0 on the caller's stream alone, 20 / 21 / 22 =
+ * 0 with the levels whose input planes have at most 40 k / 140 k / 600 k
+ * samples on the separable kernels.  Variant 0 pipelines (as 13) when the
+ * batch has at least 2 frames of at least 2^20 pixels.  vcf_dwt_dz_decode_variant takes 0, 1, 2, 4 (bior4.4's
+ * reconstruction taps at run time), 5 (no raised wave priority while the
+ * subbands are staged), 6 / 7 / 8 / 10 / 11 (0 pipelined as the encode's
+ * 13 / 14 / 15 / 16 / 18; staggering orders the chunks' last levels) and 9
+ * (0 on the caller's stream alone; 0 does not pipeline).  Outputs
  * identical. */
 int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,

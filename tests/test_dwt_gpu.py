@@ -130,10 +130,53 @@ def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
     assert np.abs(da.astype(int) - frames.astype(int)).mean() < 8     # a sane reconstruction
 
 
+@pytest.mark.parametrize("wavelet", ["bior4.4", "db5"])
+def test_dwt_4k_frame_pipeline(wavelet):
+    """Frame chunks on the library's streams (encode variants 0/13-22, decode 0/6-11) give the bytes of the
+    single-stream chain (encode 17, decode 9) on an odd batch of 4K frames; the last frame equals the oracle."""
+    import vcf_amd.dwt as DW
+    H, W, L, Q = 2160, 3840, 5, 32
+    rng = np.random.Generator(np.random.PCG64(11))
+    frames = rng.integers(0, 256, (5, H, W, 3), dtype=np.uint8)
+    ref = DW.encode(frames, wavelet, L, Q, variant=17)
+    for v in (0, 13, 14, 15, 16, 18, 19, 20, 21, 22):
+        got = DW.encode(frames, wavelet, L, Q, variant=v)
+        for f in range(5):
+            for name in ref[f]:
+                assert np.array_equal(got[f][name], ref[f][name]), (v, f, name)
+    oref = O.dwt_encode_frame(frames[4], wavelet, L, Q)
+    for name in oref:
+        assert np.array_equal(ref[4][name], oref[name]), name
+    dref = DW.decode(ref, H, W, wavelet, L, Q, variant=9)
+    for v in (0, 6, 7, 8, 10, 11):
+        assert np.array_equal(DW.decode(ref, H, W, wavelet, L, Q, variant=v), dref), v
+    assert np.array_equal(dref[4], O.dwt_decode_frame(ref[4], H, W, wavelet, L, Q))
+
+
+@pytest.mark.parametrize("H,W,L,Q", [(67, 45, 2, 7), (141, 301, 4, 3)])
+def test_dwt_frame_pipeline_small(H, W, L, Q):
+    """The forced pipeline variants on small odd frames (the default keeps them on the caller's stream)."""
+    import vcf_amd.dwt as DW
+    rng = np.random.Generator(np.random.PCG64(H + W))
+    frames = rng.integers(0, 256, (3, H, W, 3), dtype=np.uint8)
+    for wavelet in ("bior4.4", "sym4"):
+        ref = DW.encode(frames, wavelet, L, Q, variant=0)
+        for v in (13, 14, 16, 19, 20, 22):
+            got = DW.encode(frames, wavelet, L, Q, variant=v)
+            for f in range(3):
+                for name in ref[f]:
+                    assert np.array_equal(got[f][name], ref[f][name]), (wavelet, v, f, name)
+        dref = DW.decode(ref, H, W, wavelet, L, Q, variant=0)
+        for v in (6, 7, 10):
+            assert np.array_equal(DW.decode(ref, H, W, wavelet, L, Q, variant=v), dref), (wavelet, v)
+
+
 def test_dwt_unknown_variant():
     import vcf_amd.dwt as DW
     with pytest.raises(ValueError):
-        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=13)
+        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=23)
+    with pytest.raises(ValueError):
+        DW.decode(DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32), 16, 16, "db5", 2, 32, variant=12)
 
 
 def test_dwt_errors():

@@ -1521,6 +1521,113 @@ void inv_level(int F, const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t
     }
 }
 
+// ---------------------------------------------------------------------------
+// Frame pipeline over library streams (dwt encode variants 13-16, decode 6-8)
+// ---------------------------------------------------------------------------
+// A 4K level 1 fills the chip; levels 3 .. l hold a few thousand waves or a
+// few hundred workgroups each, whose serial chains leave most SIMDs idle
+// (C3: levels 4 and 5 take 0.09 ms for 1/300 of level 1's samples).  Frames
+// are independent, so a batch is cut into chunks of frames whose level
+// chains run on several streams: one chunk's small levels overlap another's
+// large ones.  The caller's stream forks to the library's streams through an
+// event and joins them again, so the call keeps its stream semantics; each
+// chunk touches only its own frames' input, output and workspace planes.
+constexpr int kAuxStreams = 4, kMaxChunks = 16;
+
+// stagger: the level that fills the chip (level 1 of either direction) of
+// chunk k waits for chunk k-1's to finish, so those kernels run one after
+// another at full width while the small levels fill in beside them
+struct PipeHook {
+    hipEvent_t wait = nullptr;   // before the big level (null: none)
+    hipEvent_t rec = nullptr;    // recorded after it
+};
+
+struct AuxStreams {
+    std::mutex mu;
+    bool ready = false;
+    hipStream_t s[kAuxStreams] = {};
+    hipEvent_t fork = nullptr, join[kAuxStreams] = {}, big[kMaxChunks] = {};
+
+    int init()
+    {
+        if (ready) return VCF_OK;
+        int rc = hip_check(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "hipEventCreate");
+        for (int j = 0; rc == VCF_OK && j < kAuxStreams; ++j) {
+            rc = hip_check(hipStreamCreateWithFlags(&s[j], hipStreamNonBlocking), "hipStreamCreate");
+            if (rc == VCF_OK) rc = hip_check(hipEventCreateWithFlags(&join[j], hipEventDisableTiming), "hipEventCreate");
+        }
+        for (int j = 0; rc == VCF_OK && j < kMaxChunks; ++j)
+            rc = hip_check(hipEventCreateWithFlags(&big[j], hipEventDisableTiming), "hipEventCreate");
+        ready = rc == VCF_OK;
+        return rc;
+    }
+};
+
+AuxStreams &aux_for_current_device()
+{
+    static AuxStreams per_dev[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    return per_dev[dev];
+}
+
+// how a batch is pipelined: `chunks` chunks of consecutive frames round-robin
+// over `streams` library streams, staggered or not; streams == 0: no pipeline
+struct PipeShape {
+    int streams = 0, chunks = 0;
+    bool stagger = false;
+};
+
+// run chain(first_frame, n, stream, hook) per chunk, ordered after and before
+// the caller's stream s
+template <typename Chain>
+int run_pipelined(long long n_frames, PipeShape ps, hipStream_t s, Chain &&chain)
+{
+    AuxStreams &ax = aux_for_current_device();
+    std::lock_guard<std::mutex> lock(ax.mu);
+    int rc = ax.init();
+    if (rc != VCF_OK) return rc;
+    const int ns = std::max(1, std::min(ps.streams, kAuxStreams));
+    const long long nc = std::max(1LL, std::min<long long>({(long long)ps.chunks, (long long)kMaxChunks, n_frames}));
+    const long long chunk = (n_frames + nc - 1) / nc;
+    if ((rc = hip_check(hipEventRecord(ax.fork, s), "hipEventRecord")) != VCF_OK) return rc;
+    for (int j = 0; j < ns; ++j)
+        if ((rc = hip_check(hipStreamWaitEvent(ax.s[j], ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
+    int k = 0;
+    for (long long f0 = 0; f0 < n_frames; f0 += chunk, ++k) {
+        PipeHook hook;
+        if (ps.stagger) {
+            hook.wait = k > 0 ? ax.big[k - 1] : nullptr;
+            hook.rec = ax.big[k];
+        }
+        if ((rc = chain(f0, std::min(chunk, n_frames - f0), ax.s[k % ns], ps.stagger ? &hook : nullptr)) != VCF_OK)
+            break;
+    }
+    // join every stream even after an error, so the caller's stream never runs ahead
+    for (int j = 0; j < ns; ++j) {
+        int r2 = hip_check(hipEventRecord(ax.join[j], ax.s[j]), "hipEventRecord");
+        if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(s, ax.join[j], 0), "hipStreamWaitEvent");
+        if (rc == VCF_OK) rc = r2;
+    }
+    return rc;
+}
+
+int hook_wait(const PipeHook *h, hipStream_t s)
+{
+    return h && h->wait ? hip_check(hipStreamWaitEvent(s, h->wait, 0), "hipStreamWaitEvent") : VCF_OK;
+}
+int hook_rec(const PipeHook *h, hipStream_t s)
+{
+    return h && h->rec ? hip_check(hipEventRecord(h->rec, s), "hipEventRecord") : VCF_OK;
+}
+
+// the default: batches of at least two frames of at least 2^20 pixels
+// (smaller frames stay on the caller's stream)
+bool pipeline_default(long long n_frames, int H, int W) { return n_frames >= 2 && (long long)H * W >= (1LL << 20); }
+// (measured on C3, ABBA: encode two unstaggered chunks -7.8 %; staggering, more chunks or
+// streams, and every decode pipeline were slower -- DESIGN.md §6)
+constexpr PipeShape kEncodePipe{2, 2, false}, kDecodePipe{0, 0, false};
+
 #endif  // VCF_DWT_KERNELS_ONLY
 }  // namespace
 }  // namespace vcf
@@ -1563,21 +1670,18 @@ int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
                                      stream);
 }
 
-int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
-                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
-                              void *stream)
+// one stream's level chain of the encode (variants 0-12; the pipelined forms
+// call it per chunk of frames with their hook)
+static int encode_chain(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
+                        int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, hipStream_t s,
+                        const PipeHook *hook, long long sep_area = 0)
 {
-    if (variant < 0 || variant > 12) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    int rc = VCF_OK;
     // 10: variant 0 with the byte-wise copy-out, 11: with the earlier row-pass mapping,
     // 12: with no raised wave priority on the fused levels (A/B)
     const int copy_w = variant == 10 ? 1 : variant == 11 ? 4 | 8 : 4;
     const int pipe0 = variant == 12 ? 5 : 1;
     if (variant >= 10) variant = 0;
-    int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
-    if (rc != VCF_OK) return rc;
-    if (n_frames == 0) return VCF_OK;
-    if (!workspace_dev) return set_error(VCF_ERR_INVALID, "null workspace");
-    if (n_frames * 3 > 65535) return set_error(VCF_ERR_INVALID, "at most 21845 frames per call");
     Filters flt;
     if ((rc = device_filters(wavelet, flt)) != VCF_OK) return rc;
     DwtGeom g;
@@ -1588,31 +1692,14 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
     const long long ws_stride = pd;                          // per plane
     double *A = base, *D = base + std::max<long long>((long long)g.hs[1] * g.ws[0], (long long)g.hs[1] * 2 * g.ws[1]);
     double *LL0 = D + (D - A), *LL1 = LL0 + 4LL * g.hs[1] * g.ws[1];
-    hipStream_t s = (hipStream_t)stream;
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *in = nullptr;
     const bool fused = variant == 1 || variant >= 3 || (variant == 0 && fast_filter(F));
     if (fused && !fast_filter(F))
         return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
                          kMaxFastF);
-    for (int l = 1; fused && l <= levels; ++l) {
-        double *LLout = (l & 1) ? LL0 : LL1;
-        const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
-                          g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
-                          g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s,
-                          variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : pipe0, copy_w};
-        // strips need planes of at least 2F rows and columns (their row wrap)
-        const bool strip = F <= kMaxStripF && g.hs[l - 1] >= 2 * F && g.ws[l - 1] >= 2 * F &&
-                           ((variant >= 6 && variant <= 8) || ((variant == 0 || variant == 9) && l > 1 && l < levels));
-        if (strip)
-            strip_level(F, a, l == 1, l == levels, variant);
-        else
-            fwd_level(F, a, l == 1, l == levels);
-        in = LLout;
-        rc = hip_check(hipGetLastError(), "dwt level launch");
-        if (rc != VCF_OK) return rc;
-    }
-    for (int l = 1; !fused && l <= levels; ++l) {
+    // one level on the separable kernels (column pass, then the row pass into the subbands / LL)
+    auto sep_level = [&](int l) {
         const int h = g.hs[l - 1], w = g.ws[l - 1], hh = g.hs[l], hw = g.ws[l];
         if (l == 1)
             hipLaunchKernelGGL(dwt_cols_kernel<true>, dim3(gx(w), hh, planes), dim3(256), 0, s, rgb_dev,
@@ -1629,11 +1716,75 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
             hipLaunchKernelGGL(dwt_rows_kernel<false>, dim3(gx(hw), hh, planes), dim3(256), 0, s, A, D, ws_stride,
                                LLout, ws_stride, packed_dev, g.packed_bytes, g.ll_off, g.sb_off[l][0],
                                g.sb_off[l][1], g.sb_off[l][2], hh, w, hw, F, Q, flt);
+    };
+    for (int l = 1; fused && l <= levels; ++l) {
+        double *LLout = (l & 1) ? LL0 : LL1;
+        const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
+                          g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
+                          g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s,
+                          variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : pipe0, copy_w};
+        // strips need planes of at least 2F rows and columns (their row wrap)
+        const bool strip = F <= kMaxStripF && g.hs[l - 1] >= 2 * F && g.ws[l - 1] >= 2 * F &&
+                           ((variant >= 6 && variant <= 8) || ((variant == 0 || variant == 9) && l > 1 && l < levels));
+        if (l == 1 && (rc = hook_wait(hook, s)) != VCF_OK) return rc;
+        if (l > 1 && (long long)g.hs[l - 1] * g.ws[l - 1] <= sep_area)
+            sep_level(l);   // small levels on the separable kernels (A/B: variants 20-22)
+        else if (strip)
+            strip_level(F, a, l == 1, l == levels, variant);
+        else
+            fwd_level(F, a, l == 1, l == levels);
         in = LLout;
+        rc = hip_check(hipGetLastError(), "dwt level launch");
+        if (rc != VCF_OK) return rc;
+        if (l == 1 && (rc = hook_rec(hook, s)) != VCF_OK) return rc;
+    }
+    for (int l = 1; !fused && l <= levels; ++l) {
+        sep_level(l);
+        in = (l & 1) ? LL0 : LL1;
         rc = hip_check(hipGetLastError(), "dwt encode launch");
         if (rc != VCF_OK) return rc;
     }
     return VCF_OK;
+}
+
+int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
+                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
+                              void *stream)
+{
+    if (variant < 0 || variant > 22) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
+    if (rc != VCF_OK) return rc;
+    if (n_frames == 0) return VCF_OK;
+    if (!workspace_dev) return set_error(VCF_ERR_INVALID, "null workspace");
+    if (n_frames * 3 > 65535) return set_error(VCF_ERR_INVALID, "at most 21845 frames per call");
+    // frame pipeline (A/B: 13 = two streams and two chunks; 14 = the same staggered; 15 / 16 =
+    // two streams, four / eight chunks, staggered; 18 = three streams, four chunks, staggered;
+    // 19 = four streams, four chunks; 17 = variant 0 on the caller's stream alone)
+    hipStream_t s = (hipStream_t)stream;
+    PipeShape ps;
+    if (variant == 0 && pipeline_default(n_frames, H, W)) ps = kEncodePipe;
+    if (variant == 13) ps = {2, 2, false};
+    if (variant == 14) ps = {2, 2, true};
+    if (variant == 15) ps = {2, 4, true};
+    if (variant == 16) ps = {2, 8, true};
+    if (variant == 18) ps = {3, 4, true};
+    if (variant == 19) ps = {4, 4, false};
+    // 20 / 21 / 22: variant 0 with levels whose input planes have at most 40 k / 140 k / 600 k
+    // samples on the separable kernels (at 4K: level 5 / levels 4-5 / levels 3-5)
+    const long long sep_area = variant == 20 ? 40000 : variant == 21 ? 140000 : variant == 22 ? 600000 : 0;
+    if (variant >= 20 && pipeline_default(n_frames, H, W)) ps = kEncodePipe;
+    if (variant >= 13) variant = 0;
+    if (ps.streams > 0 && fast_filter(kWavelets[wavelet].len)) {
+        DwtGeom g;
+        dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
+        const long long fpx = (long long)H * W * 3, wsf = 3 * plane_doubles(g);
+        return run_pipelined(n_frames, ps, s, [&](long long f0, long long n, hipStream_t cs, const PipeHook *hook) {
+            return encode_chain(0, rgb_dev + f0 * fpx, n, H, W, wavelet, levels, Q, packed_dev + f0 * g.packed_bytes,
+                                (double *)workspace_dev + f0 * wsf, cs, hook, sep_area);
+        });
+    }
+    return encode_chain(variant, rgb_dev, n_frames, H, W, wavelet, levels, Q, packed_dev, workspace_dev, s, nullptr,
+                        sep_area);
 }
 
 int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
@@ -1643,16 +1794,12 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
                                      stream);
 }
 
-int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W,
-                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
-                              void *stream)
+// one stream's level chain of the decode (variants 0-5)
+static int decode_chain(int variant, const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W,
+                        int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
+                        hipStream_t s, const PipeHook *hook)
 {
-    if (variant < 0 || (variant > 2 && variant != 4 && variant != 5)) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
-    int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
-    if (rc != VCF_OK) return rc;
-    if (n_frames == 0) return VCF_OK;
-    if (!workspace_dev) return set_error(VCF_ERR_INVALID, "null workspace");
-    if (n_frames * 3 > 65535) return set_error(VCF_ERR_INVALID, "at most 21845 frames per call");
+    int rc = VCF_OK;
     Filters flt;
     if ((rc = device_filters(wavelet, flt)) != VCF_OK) return rc;
     DwtGeom g;
@@ -1663,7 +1810,6 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
     const long long ws_stride = pd;
     double *A = base, *D = base + std::max<long long>((long long)g.hs[1] * g.ws[0], (long long)g.hs[1] * 2 * g.ws[1]);
     double *P0 = D + (D - A), *P1 = P0 + 4LL * g.hs[1] * g.ws[1];
-    hipStream_t s = (hipStream_t)stream;
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *prev = nullptr;
     int lda = 0;
@@ -1689,11 +1835,13 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
                               g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], h, w, oh, ow, Q, lda,
                               (unsigned)n_frames, flt, &kWavelets[wavelet], s,
                               variant == 4 ? 2 : variant == 5 ? 3 : 1};
+            if (r == 1 && (rc = hook_wait(hook, s)) != VCF_OK) return rc;
             inv_level(F, a, r == levels, r == 1, rgb_dev);
             prev = out;
             lda = ow;
             rc = hip_check(hipGetLastError(), "idwt level launch");
             if (rc != VCF_OK) return rc;
+            if (r == 1 && (rc = hook_rec(hook, s)) != VCF_OK) return rc;
         }
         return VCF_OK;
     }
@@ -1720,6 +1868,45 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
     hipLaunchKernelGGL(dwt_to_rgb_kernel, dim3((unsigned)((npx + 255) / 256), (unsigned)n_frames), dim3(256), 0, s,
                        prev, ws_stride, rgb_dev, npx, npx * 3);
     return hip_check(hipGetLastError(), "dwt to_rgb launch");
+}
+
+int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W,
+                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
+                              void *stream)
+{
+    if (variant < 0 || variant == 3 || variant > 11) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
+    if (rc != VCF_OK) return rc;
+    if (n_frames == 0) return VCF_OK;
+    if (!workspace_dev) return set_error(VCF_ERR_INVALID, "null workspace");
+    if (n_frames * 3 > 65535) return set_error(VCF_ERR_INVALID, "at most 21845 frames per call");
+    // frame pipeline as in the encode (A/B: 6 = two streams and two chunks; 7 = the same
+    // staggered; 8 / 10 = two streams, four / eight chunks, staggered; 11 = three streams, four
+    // chunks, staggered; 9 = variant 0 on the caller's stream alone)
+    PipeShape ps;
+    if (variant == 0 && pipeline_default(n_frames, H, W)) ps = kDecodePipe;
+    if (variant == 6) ps = {2, 2, false};
+    if (variant == 7) ps = {2, 2, true};
+    if (variant == 8) ps = {2, 4, true};
+    if (variant == 10) ps = {2, 8, true};
+    if (variant == 11) ps = {3, 4, true};
+    if (variant >= 6) variant = 0;
+    {
+        DwtGeom g;
+        dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
+        const int F = g.F;
+        if (ps.streams > 0 && fast_filter(F) && !(g.hs[levels] < F / 2 || g.ws[levels] < F / 2)) {
+            const long long fpx = (long long)2 * g.hs[1] * 2 * g.ws[1] * 3, wsf = 3 * plane_doubles(g);
+            return run_pipelined(n_frames, ps, (hipStream_t)stream,
+                                 [&](long long f0, long long n, hipStream_t cs, const PipeHook *hook) {
+                                     return decode_chain(0, packed_dev + f0 * g.packed_bytes, n, H, W, wavelet,
+                                                         levels, Q, rgb_dev + f0 * fpx,
+                                                         (double *)workspace_dev + f0 * wsf, cs, hook);
+                                 });
+        }
+    }
+    return decode_chain(variant, packed_dev, n_frames, H, W, wavelet, levels, Q, rgb_dev, workspace_dev,
+                        (hipStream_t)stream, nullptr);
 }
 
 }  // extern "C"
