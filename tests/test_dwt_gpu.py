@@ -132,14 +132,14 @@ def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
 
 @pytest.mark.parametrize("wavelet", ["bior4.4", "db5"])
 def test_dwt_4k_frame_pipeline(wavelet):
-    """Frame chunks on the library's streams (encode variants 0/13-22, decode 0/6-11) give the bytes of the
+    """Frame chunks on the library's streams (encode variants 0/13-25, decode 0/6-11) give the bytes of the
     single-stream chain (encode 17, decode 9) on an odd batch of 4K frames; the last frame equals the oracle."""
     import vcf_amd.dwt as DW
     H, W, L, Q = 2160, 3840, 5, 32
     rng = np.random.Generator(np.random.PCG64(11))
     frames = rng.integers(0, 256, (5, H, W, 3), dtype=np.uint8)
     ref = DW.encode(frames, wavelet, L, Q, variant=17)
-    for v in (0, 13, 14, 15, 16, 18, 19, 20, 21, 22):
+    for v in (0, 13, 14, 15, 16, 18, 19, 20, 21, 22, 23, 24, 25):
         got = DW.encode(frames, wavelet, L, Q, variant=v)
         for f in range(5):
             for name in ref[f]:
@@ -161,7 +161,7 @@ def test_dwt_frame_pipeline_small(H, W, L, Q):
     frames = rng.integers(0, 256, (3, H, W, 3), dtype=np.uint8)
     for wavelet in ("bior4.4", "sym4"):
         ref = DW.encode(frames, wavelet, L, Q, variant=0)
-        for v in (13, 14, 16, 19, 20, 22):
+        for v in (13, 14, 16, 19, 20, 22, 23, 24, 25):
             got = DW.encode(frames, wavelet, L, Q, variant=v)
             for f in range(3):
                 for name in ref[f]:
@@ -174,7 +174,7 @@ def test_dwt_frame_pipeline_small(H, W, L, Q):
 def test_dwt_unknown_variant():
     import vcf_amd.dwt as DW
     with pytest.raises(ValueError):
-        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=23)
+        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=26)
     with pytest.raises(ValueError):
         DW.decode(DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32), 16, 16, "db5", 2, 32, variant=12)
 

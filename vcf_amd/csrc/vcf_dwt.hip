@@ -415,10 +415,22 @@ __device__ __forceinline__ int pad_col(int e) { return e + (e >> 3); }
 // never -0, so the outputs are bit-identical (tests/test_dwt_gpu.py).  A
 // run-time branch per tap measured 15-20 % slower; the masks are template
 // arguments for the filters that have zeros and matter (bior4.4 = CDF 9/7).
-template <int F, unsigned ZLO = 0, unsigned ZHI = 0>
+// Z0: each sum starts with its first nonzero product instead of 0.0 + that
+// product -- the strip kernels' argument: only the sign of a zero sum can
+// differ, a zero only ever contributes zero products downstream, and every
+// output the codec keeps is truncated to an integer, so the bytes are equal.
+__host__ __device__ constexpr int first_nonzero_tap(unsigned Z, int F)
+{
+    int m = 0;
+    while (m < F && ((Z >> m) & 1u)) ++m;
+    return m;
+}
+
+template <int F, unsigned ZLO = 0, unsigned ZHI = 0, bool Z0 = false>
 __device__ __forceinline__ void fwd_group(const double (&flo)[F], const double (&fhi)[F],
                                           const double (&v)[2 * (kG - 1) + F], double (&lo)[kG], double (&hi)[kG])
 {
+    constexpr int m0lo = Z0 ? first_nonzero_tap(ZLO, F) : -1, m0hi = Z0 ? first_nonzero_tap(ZHI, F) : -1;
 #pragma unroll
     for (int u = 0; u < kG; ++u) {
         lo[u] = 0.0;
@@ -430,8 +442,8 @@ __device__ __forceinline__ void fwd_group(const double (&flo)[F], const double (
 #pragma unroll
         for (int u = 0; u < kG; ++u) {
             const double x = v[2 * u + F - 1 - m];
-            if (!((ZLO >> m) & 1u)) lo[u] = lo[u] + fl * x;
-            if (!((ZHI >> m) & 1u)) hi[u] = hi[u] + fh * x;
+            if (!((ZLO >> m) & 1u)) lo[u] = m == m0lo ? fl * x : lo[u] + fl * x;
+            if (!((ZHI >> m) & 1u)) hi[u] = m == m0hi ? fh * x : hi[u] + fh * x;
         }
     }
 }
@@ -500,8 +512,8 @@ __host__ __device__ constexpr double ct_dec(int id, bool hi, int m)
 // bior4.4 the register cap spills (+2 %), so it keeps 0 (dwt variant 5
 // flips db5 back to 0 for A/B).
 template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true, int CT = 0,
-          int STG = 0, int PRI = 3>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIRST && STG ? 5 : 1)))
+          int STG = 0, int PRI = 3, bool Z0 = false, int NT = 256>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FIRST && STG && NT == 256 ? 5 : 1)))
 void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
@@ -509,26 +521,27 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         long long off_hl, long long off_hh, int h, int w, int hh,
                                                         int hw, int Q, Taps<F> tp, Filters flt, int cw)
 {
-    constexpr int TW = fwd_tile_w(F), IH = 2 * (kFTH - 1) + F, IW = kFIW;
+    constexpr int FTH = NT / kFIW * kG;   // output rows per tile (kFTH at 256 threads)
+    constexpr int TW = fwd_tile_w(F), IH = 2 * (FTH - 1) + F, IW = kFIW;
     constexpr int NWIN = 2 * (kG - 1) + F;
     constexpr int NG = (TW + kG - 1) / kG;
-    constexpr int SB = kFTH * TW * 3;
-    static_assert(kFTH == 2 * kG && 2 * (TW - 1) + F == IW, "tile geometry");
+    constexpr int SB = FTH * TW * 3;
+    static_assert(NT % kFIW == 0 && 2 * (TW - 1) + F == IW, "tile geometry");
     constexpr int RS = IW + IW / 8;                  // A/D rows padded one double per 8 (bank spread)
     // level 1 stages int16-valued YCoCg samples (as int16, or exact in float)
     using Stage = typename std::conditional<FIRST, typename std::conditional<STG == 1, int16_t, float>::type,
                                             double>::type;
     __shared__ Stage tin[IH * IW];
-    __shared__ double tA[kFTH * RS + 8], tD[kFTH * RS + 8];   // +8: the last row group's window overhang
+    __shared__ double tA[FTH * RS + 8], tD[FTH * RS + 8];   // +8: the last row group's window overhang
     __shared__ __attribute__((aligned(16))) uint8_t stage[3 * SB];
     __shared__ uint8_t stage16[LAST ? 2 * SB : 1];
-    __shared__ double stageLL[LAST || PIPE ? 1 : kFTH * TW];
-    const int o0 = blockIdx.y * kFTH, c0 = blockIdx.x * TW;
+    __shared__ double stageLL[LAST || PIPE ? 1 : FTH * TW];
+    const int o0 = blockIdx.y * FTH, c0 = blockIdx.x * TW;
     const long long frame = blockIdx.z;
     const int R0 = F / 2 + 2 * o0 - F + 1, C0 = F / 2 + 2 * c0 - F + 1;
     const int tid = threadIdx.x;
     const bool rows_in = R0 >= 0 && R0 + IH <= h, cols_in = C0 >= 0 && C0 + IW <= w;
-    const bool col_tail = F / 2 + 2 * (o0 + kFTH - 1) >= h, row_tail = F / 2 + 2 * (c0 + TW - 1) >= w;
+    const bool col_tail = F / 2 + 2 * (o0 + FTH - 1) >= h, row_tail = F / 2 + 2 * (c0 + TW - 1) >= w;
     // taps into VGPRs through LDS (kernel-argument taps would sit in scalar
     // registers, which the pass loops exhaust)
     double flo[F], fhi[F];
@@ -541,14 +554,14 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
     // ahead into registers: level 1 reads its RGB bytes once for all three
     // channels, later levels prefetch the next channel's plane during the
     // current channel's passes
-    constexpr int PER = IH * IW / 256;
-    static_assert(PER * 256 == IH * IW, "staging split");
+    constexpr int PER = IH * IW / NT;
+    static_assert(PER * NT == IH * IW, "staging split");
     uint32_t pix[FIRST ? PER : 1];
     double nxt[FIRST ? 1 : PER];
     auto fetch = [&](int ch) {
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            const int t = tid + 256 * j;
+            const int t = tid + NT * j;
             const int r = t / IW, c = t % IW;
             const int y = rows_in ? R0 + r : per_wrap(R0 + r, h);
             const int x = cols_in ? C0 + c : per_wrap(C0 + c, w);
@@ -573,10 +586,10 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                 if (ch == 0) iv = (R + 2 * G + B) >> 2;
                 else if (ch == 1) iv = (R - B) / 2;
                 else iv = (2 * G - R - B) / 4;
-                tin[tid + 256 * j] = (Stage)iv;
+                tin[tid + NT * j] = (Stage)iv;
             } else {
                 v = nxt[FIRST ? 0 : j];
-                tin[tid + 256 * j] = (Stage)v;
+                tin[tid + NT * j] = (Stage)v;
             }
         }
     };
@@ -601,7 +614,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
 #pragma unroll
             for (int k = 0; k < NWIN; ++k) v[k] = (double)tin[(2 * kG * g + k) * IW + c];
             double a[kG], d[kG];
-            fwd_group<F, ZLO, ZHI>(flo, fhi, v, a, d);
+            fwd_group<F, ZLO, ZHI, Z0>(flo, fhi, v, a, d);
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
                 tA[(kG * g + u) * RS + pad_col(c)] = a[u];
@@ -611,7 +624,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
         if (col_tail) {   // tile-uniform: rows whose taps wrap past the end take pywt's order
             __syncthreads();
             const int first = max(0, (h - F / 2 + 1) / 2 - o0);   // first tile row with i >= h
-            for (int t = tid; t < (kFTH - first) * IW; t += 256) {
+            for (int t = tid; t < (FTH - first) * IW; t += NT) {
                 const int o = first + t / IW, c = t % IW;
                 const int i = F / 2 + 2 * (o0 + o);
                 auto load = [&](int p) -> double { return (double)tin[(p - R0) * IW + c]; };
@@ -629,25 +642,25 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
         auto ll_dst = [&](int o, int oc) -> double * {
             return PIPE ? llp + (long long)o * hw + oc : stageLL + (o * TW + oc);
         };
-        // row pass (axis 1): (A or D) x kFTH rows x NG groups of 4 outputs.  Mapping
+        // row pass (axis 1): (A or D) x FTH rows x NG groups of 4 outputs.  Mapping
         // (cw & 8 == 0, default): 16 group slots per row, so a lane's (src, o, gq)
         // are bit fields and every half-wave reads two whole rows -- conflict-free
         // LDS banks -- with the slots past NG idle; cw & 8: NG slots per row (the
         // earlier mapping, dwt variant 11)
         const int first_tail = row_tail ? max(0, (w - F / 2 + 1) / 2 - c0) : TW;   // first column with i >= w
         constexpr int NGP = 16;
-        static_assert(NG <= NGP && 2 * kFTH * NGP == 256, "row-pass slots");
+        static_assert(NG <= NGP && 2 * FTH * NGP == NT, "row-pass slots");
         const bool slots16 = (cw & 8) == 0;
-        for (int t = tid; t < (slots16 ? 256 : 2 * kFTH * NG); t += 256) {
+        for (int t = tid; t < (slots16 ? NT : 2 * FTH * NG); t += NT) {
             int src, o, gq;
             if (slots16) {
-                src = t >> 7;
-                o = (t >> 4) & (kFTH - 1);
+                src = t / (FTH * NGP);
+                o = (t >> 4) & (FTH - 1);
                 gq = t & (NGP - 1);
                 if (gq >= NG) continue;
             } else {
-                src = t / (kFTH * NG);
-                const int rest = t % (kFTH * NG);
+                src = t / (FTH * NG);
+                const int rest = t % (FTH * NG);
                 o = rest / NG;
                 gq = rest % NG;
             }
@@ -657,7 +670,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
 #pragma unroll
             for (int k = 0; k < NWIN; ++k) v[k] = row[9 * gq + k + (k >> 3)];   // pad_col(8 gq + k)
             double lo[kG], hi[kG];
-            fwd_group<F, ZLO, ZHI>(flo, fhi, v, lo, hi);
+            fwd_group<F, ZLO, ZHI, Z0>(flo, fhi, v, lo, hi);
             const bool rv = o0 + o < hh;
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
@@ -669,8 +682,8 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
         }
         if (row_tail) {   // tile-uniform: outputs whose taps wrap past the line end
             const int n = min(TW, hw - c0) - first_tail;
-            for (int t = tid; t < 2 * kFTH * max(n, 0); t += 256) {
-                const int src = t / (kFTH * n), rest = t % (kFTH * n);
+            for (int t = tid; t < 2 * FTH * max(n, 0); t += NT) {
+                const int src = t / (FTH * n), rest = t % (FTH * n);
                 const int o = rest / n, oc = first_tail + rest % n;
                 if (o0 + o >= hh) continue;
                 const int i = F / 2 + 2 * (c0 + oc);
@@ -684,8 +697,8 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
         if (!PIPE) {
             __syncthreads();
             if (!LAST) {   // LL rows leave as contiguous runs of doubles
-                const int rows = min(kFTH, hh - o0), nw = min(TW, hw - c0);
-                for (int t = tid; t < rows * TW; t += 256) {
+                const int rows = min(FTH, hh - o0), nw = min(TW, hw - c0);
+                for (int t = tid; t < rows * TW; t += NT) {
                     const int o = t / TW, oc = t - o * TW;
                     if (oc < nw) llp[(long long)o * hw + oc] = stageLL[t];
                 }
@@ -697,7 +710,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
     // copy-out: each subband row of the tile is one contiguous byte run, moved
     // as dwords when every run start is 4-byte aligned (cw 4; cw 1 = bytes, the
     // earlier copy kept for A/B as dwt variant 10)
-    const int rows = min(kFTH, hh - o0), nb = min(TW, hw - c0) * 3;
+    const int rows = min(FTH, hh - o0), nb = min(TW, hw - c0) * 3;
     uint8_t *pk = packed + frame * packed_stride;
     const long long offs[3] = {off_lh, off_hl, off_hh};
     constexpr int TWW = TW * 3 / 4;   // dwords per staged subband row
@@ -706,7 +719,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                                     (long long)c0 * 3 | nb)) & 3u) == 0;
     if (dw) {
         const int nw = nb >> 2;
-        for (int t = tid; t < 3 * rows * TWW; t += 256) {
+        for (int t = tid; t < 3 * rows * TWW; t += NT) {
             const int sb = t / (rows * TWW), r = t - sb * (rows * TWW);
             const int o = r / TWW, b = r - o * TWW;
             if (b < nw)
@@ -715,13 +728,13 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
         }
     } else {
         for (int sb = 0; sb < 3; ++sb)
-            for (int t = tid; t < rows * TW * 3; t += 256) {
+            for (int t = tid; t < rows * TW * 3; t += NT) {
                 const int o = t / (TW * 3), b = t - o * (TW * 3);
                 if (b < nb) pk[offs[sb] + ((long long)(o0 + o) * hw + c0) * 3 + b] = stage[sb * SB + t];
             }
     }
     if (LAST)
-        for (int t = tid; t < rows * TW * 6; t += 256) {
+        for (int t = tid; t < rows * TW * 6; t += NT) {
             const int o = t / (TW * 6), b = t - o * (TW * 6);
             if (b < 2 * nb) pk[ll_off + ((long long)(o0 + o) * hw + c0) * 6 + b] = stage16[t];
         }
@@ -760,6 +773,22 @@ __device__ __forceinline__ double nat_sum(const double (&f)[F], const double (&v
         s = (Z0 && first) ? p : s + p;
         first = false;
     }
+    return s;
+}
+
+// nat_sum's taps in pywt's order for an output whose taps wrap past the line
+// end (i >= N: the wrapped taps first, descending, then the others; as
+// dwt_tap_sum_logical), over the same window v; zero taps skipped as in nat_sum
+template <int F, unsigned Z>
+__device__ __forceinline__ double wrap_sum(const double (&f)[F], const double (&v)[F], int i, int N)
+{
+    double s = 0.0;
+#pragma unroll
+    for (int m = F - 1; m >= 0; --m)
+        if (!((Z >> m) & 1u) && i - m >= N) s = s + f[m] * v[F - 1 - m];
+#pragma unroll
+    for (int m = 0; m < F; ++m)
+        if (!((Z >> m) & 1u) && i - m < N) s = s + f[m] * v[F - 1 - m];
     return s;
 }
 
@@ -803,8 +832,12 @@ __device__ __forceinline__ void strip_row_generic(const double *row, Filters flt
     hi = dwt_tap_sum_logical(flt.dec_hi, F, w, ic, load);
 }
 
+// TAILFAST: the strip holding the outputs whose taps wrap past the line end
+// slides like the others (its wrapping lanes reorder their row-pass taps from
+// the same window, wrap_sum) instead of running every row through the generic
+// sums with per-tap global loads -- the slowest wave of a small level
 template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0, bool Z0 = true,
-          bool QP2 = true, int DIAG = 0>
+          bool QP2 = true, int DIAG = 0, bool TAILFAST = true>
 __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
@@ -926,6 +959,10 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
             }
             lo = nat_sum<F, ZLO, Z0>(flo, v);
             hi = nat_sum<F, ZHI, Z0>(fhi, v);
+            if (TAILFAST && strip_tail && ic >= w) {   // this lane's taps wrap past the line end
+                lo = wrap_sum<F, ZLO>(flo, v, ic, w);
+                hi = wrap_sum<F, ZHI>(fhi, v, ic, w);
+            }
         } else {
             lo = hi = 0.0;
             if (col_ok) strip_row_generic<F>(row, flt, w, ic, C0, lo, hi);
@@ -956,7 +993,7 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
             row_pass(o, 0, generic);
         }
     };
-    if (strip_tail) {
+    if (strip_tail && !TAILFAST) {   // the earlier tail strip: every row through the generic sums
         direct_rows(o0, std::true_type());
         return;
     }
@@ -1329,17 +1366,22 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
                       : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI> : dwt_level_kernel<F, false, false, ZLO, ZHI>);
     if constexpr (F == 10) {   // bior4.4 / db5: constant taps (pipe 2: run-time taps, dwt variant 4)
         constexpr int id = ZLO != 0 ? 1 : 2;
-        bool ct = a.pipe == 1 || a.pipe == 3 || a.pipe == 5;
+        bool ct = a.pipe == 1 || a.pipe == 3 || a.pipe == 5 || a.pipe == 6 || a.pipe == 7 || a.pipe == 8;
         for (int m = 0; m < F; ++m) {
             const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
             ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
         }
         constexpr int stg = id == 2 ? 1 : 0;
-        if (ct)
+        if (ct && a.pipe == 6)   // sums started at 0.0 (dwt variant 23, A/B)
             kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, stg>
                                  : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, stg>)
                          : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, id>
                                  : dwt_level_kernel<F, false, false, ZLO, ZHI, true, id>);
+        else if (ct)
+            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, stg, 3, true>
+                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, stg, 3, true>)
+                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, id, 0, 3, true>
+                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, true, id, 0, 3, true>);
         if (ct && a.pipe == 3 && first)   // level 1 staged as float, no wave priority (dwt variant 5, A/B)
             kern = last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, 0, 0>
                         : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, 0, 0>;
@@ -1354,6 +1396,22 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
                                      : dwt_level_kernel<F, true, false, ZLO, ZHI, false>)
                              : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, false>
                                      : dwt_level_kernel<F, false, false, ZLO, ZHI, false>);
+        }
+    }
+    if constexpr (F == 10) {
+        constexpr int id = ZLO != 0 ? 1 : 2;
+        bool ct = a.pipe == 7;
+        for (int m = 0; m < F; ++m) {
+            const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
+            ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
+        }
+        if (ct && first && !last) {   // level 1 in 512-thread tiles of 16 output rows, int16 staging (variant 24)
+            constexpr int NT = 512, FTH = NT / kFIW * kG;
+            const dim3 g2(grid.x, (a.hh + FTH - 1) / FTH, grid.z);
+            hipLaunchKernelGGL((dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, 1, 3, true, NT>), g2, dim3(NT),
+                               0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed, a.packed_stride,
+                               a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, a.copy_w);
+            return;
         }
     }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed,
@@ -1381,13 +1439,13 @@ using StripKern = void (*)(const uint8_t *, long long, const double *, long long
                            long long, long long, long long, long long, int, int, int, int, int, int, int, Taps<F>,
                            Filters);
 
-template <int F, unsigned ZL, unsigned ZH, int CT, bool Z0, bool QP2, int DIAG = 0>
+template <int F, unsigned ZL, unsigned ZH, int CT, bool Z0, bool QP2, int DIAG = 0, bool TF = true>
 StripKern<F> strip_kern(bool first, bool last)
 {
-    return first ? (last ? dwt_strip_kernel<F, true, true, ZL, ZH, CT, Z0, QP2, DIAG>
-                         : dwt_strip_kernel<F, true, false, ZL, ZH, CT, Z0, QP2, DIAG>)
-                 : (last ? dwt_strip_kernel<F, false, true, ZL, ZH, CT, Z0, QP2, DIAG>
-                         : dwt_strip_kernel<F, false, false, ZL, ZH, CT, Z0, QP2, DIAG>);
+    return first ? (last ? dwt_strip_kernel<F, true, true, ZL, ZH, CT, Z0, QP2, DIAG, TF>
+                         : dwt_strip_kernel<F, true, false, ZL, ZH, CT, Z0, QP2, DIAG, TF>)
+                 : (last ? dwt_strip_kernel<F, false, true, ZL, ZH, CT, Z0, QP2, DIAG, TF>
+                         : dwt_strip_kernel<F, false, false, ZL, ZH, CT, Z0, QP2, DIAG, TF>);
 }
 
 template <int F>
@@ -1420,6 +1478,8 @@ void launch_strip_level(const LevelArgs &a, bool first, bool last, int mode)
             if (ct && b44 && qp2 && mode == 8)   // diagnostic: no detail-subband stores
                 kern = strip_kern<F, kB44DecLo, kB44DecHi, 1, true, true, 1>(first, last);
 
+            else if (ct && b44 && qp2 && z0 && a.pipe == 8)   // the earlier all-generic tail strip (variant 25)
+                kern = strip_kern<F, kB44DecLo, kB44DecHi, 1, true, true, 0, false>(first, last);
             else if (ct && b44)
                 kern = qp2 ? (z0 ? strip_kern<F, kB44DecLo, kB44DecHi, 1, true, true>(first, last)
                                  : strip_kern<F, kB44DecLo, kB44DecHi, 1, false, true>(first, last))
@@ -1680,7 +1740,7 @@ static int encode_chain(int variant, const uint8_t *rgb_dev, int64_t n_frames, i
     // 10: variant 0 with the byte-wise copy-out, 11: with the earlier row-pass mapping,
     // 12: with no raised wave priority on the fused levels (A/B)
     const int copy_w = variant == 10 ? 1 : variant == 11 ? 4 | 8 : 4;
-    const int pipe0 = variant == 12 ? 5 : 1;
+    const int pipe0 = variant == 12 ? 5 : variant == 23 ? 6 : variant == 24 ? 7 : variant == 25 ? 8 : 1;
     if (variant >= 10) variant = 0;
     Filters flt;
     if ((rc = device_filters(wavelet, flt)) != VCF_OK) return rc;
@@ -1751,7 +1811,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 22) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant > 25) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1773,13 +1833,17 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
     // samples on the separable kernels (at 4K: level 5 / levels 4-5 / levels 3-5)
     const long long sep_area = variant == 20 ? 40000 : variant == 21 ? 140000 : variant == 22 ? 600000 : 0;
     if (variant >= 20 && pipeline_default(n_frames, H, W)) ps = kEncodePipe;
-    if (variant >= 13) variant = 0;
+    // 23: variant 0 with the fused levels' sums started at 0.0 (no Z0, A/B)
+    // 24: variant 0 with level 1 in 512-thread tiles of 16 output rows (int16 staging)
+    // 25: variant 0 with the earlier tail strip (every row through the generic sums)
+    const int cv = variant >= 23 && variant <= 25 ? variant : 0;
+    if (variant >= 13) variant = cv;
     if (ps.streams > 0 && fast_filter(kWavelets[wavelet].len)) {
         DwtGeom g;
         dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
         const long long fpx = (long long)H * W * 3, wsf = 3 * plane_doubles(g);
         return run_pipelined(n_frames, ps, s, [&](long long f0, long long n, hipStream_t cs, const PipeHook *hook) {
-            return encode_chain(0, rgb_dev + f0 * fpx, n, H, W, wavelet, levels, Q, packed_dev + f0 * g.packed_bytes,
+            return encode_chain(cv, rgb_dev + f0 * fpx, n, H, W, wavelet, levels, Q, packed_dev + f0 * g.packed_bytes,
                                 (double *)workspace_dev + f0 * wsf, cs, hook, sep_area);
         });
     }
