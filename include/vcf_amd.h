@@ -256,14 +256,17 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
  * caller's stream (13: two streams, two chunks; 14: 13 staggered -- chunk k's
  * level 1 waits for chunk k-1's -- ; 15 / 16: two streams, four / eight
  * chunks, staggered; 18: three streams, four chunks, staggered; 19: four
- * streams, four chunks), 17 = 0 on the caller's stream alone, 20 / 21 / 22 =
- * 0 with the levels whose input planes have at most 40 k / 140 k / 600 k
- * samples on the separable kernels, 23 = 0 with the fused levels' tap sums
+ * streams, four chunks), 17 = 0 on the caller's stream alone, 20 = 0 with
+ * every level after the first on the fused/strip kernels (variant 0 runs the
+ * levels whose input planes have at most 40 k samples -- at 4K level 5 -- on
+ * the separable kernels), 21 / 22 = 0 with up to 140 k / 600 k samples on
+ * them, 23 = 0 with the fused levels' tap sums
  * started at 0.0 instead of their first nonzero product (the earlier
  * arithmetic; variants 3-5 and 12 keep it too), 24 = 0 with level 1 in
  * 512-thread tiles of 16 output rows, 25 = 0 with the strip levels' last
  * strip (whose outputs' taps wrap past the line end) running every row
- * through the generic sums (the earlier form).  Variant 0 pipelines (as 13) when the
+ * through the generic sums (the earlier form), 26 = 13 with chunk 0 on the
+ * caller's stream.  Variant 0 pipelines (as 13) when the
  * batch has at least 2 frames of at least 2^20 pixels.  vcf_dwt_dz_decode_variant takes 0, 1, 2, 4 (bior4.4's
  * reconstruction taps at run time), 5 (no raised wave priority while the
  * subbands are staged), 6 / 7 / 8 / 10 / 11 (0 pipelined as the encode's

@@ -63,7 +63,7 @@ def test_dwt_short_lines_vs_oracle(wavelet, H, W, L):
         assert np.array_equal(out[f], O.dwt_decode_frame(got[f], H, W, wavelet, L, 5))
 
 
-@pytest.mark.parametrize("variant", [1, 2, 6], ids=["fused", "separable", "strip"])
+@pytest.mark.parametrize("variant", [0, 1, 2, 6, 20], ids=["default", "fused", "separable", "strip", "hybrid"])
 @pytest.mark.parametrize("wavelet", ["db5", "bior4.4", "haar", "sym4", "coif2", "db9", "db10"])
 @pytest.mark.parametrize("H,W,L,Q", [(96, 128, 3, 32), (67, 45, 2, 7), (256, 160, 5, 16), (8, 10, 1, 1),
                                      (141, 301, 4, 3), (17, 200, 3, 32)])
@@ -82,7 +82,7 @@ def test_dwt_vs_oracle(wavelet, H, W, L, Q, variant):
         for name, arr in ref.items():
             assert np.array_equal(got[f][name], arr), (f, name)
     half = O.lib().vcfo_wavelet_len(O.wavelet_index(wavelet)) // 2
-    dec_variant = {6: 1}.get(variant, variant)
+    dec_variant = {6: 1, 20: 0}.get(variant, variant)
     if min(shapes[-1]) < half:
         # pywt's short-input branch: the separable kernels (automatic choice) run it,
         # an explicit request for the fused tiles is refused
@@ -132,14 +132,14 @@ def test_dwt_4k_fused_equals_separable_and_oracle(wavelet):
 
 @pytest.mark.parametrize("wavelet", ["bior4.4", "db5"])
 def test_dwt_4k_frame_pipeline(wavelet):
-    """Frame chunks on the library's streams (encode variants 0/13-25, decode 0/6-11) give the bytes of the
+    """Frame chunks on the library's streams (encode variants 0/13-26, decode 0/6-11) give the bytes of the
     single-stream chain (encode 17, decode 9) on an odd batch of 4K frames; the last frame equals the oracle."""
     import vcf_amd.dwt as DW
     H, W, L, Q = 2160, 3840, 5, 32
     rng = np.random.Generator(np.random.PCG64(11))
     frames = rng.integers(0, 256, (5, H, W, 3), dtype=np.uint8)
     ref = DW.encode(frames, wavelet, L, Q, variant=17)
-    for v in (0, 13, 14, 15, 16, 18, 19, 20, 21, 22, 23, 24, 25):
+    for v in (0, 13, 14, 15, 16, 18, 19, 20, 21, 22, 23, 24, 25, 26):
         got = DW.encode(frames, wavelet, L, Q, variant=v)
         for f in range(5):
             for name in ref[f]:
@@ -161,7 +161,7 @@ def test_dwt_frame_pipeline_small(H, W, L, Q):
     frames = rng.integers(0, 256, (3, H, W, 3), dtype=np.uint8)
     for wavelet in ("bior4.4", "sym4"):
         ref = DW.encode(frames, wavelet, L, Q, variant=0)
-        for v in (13, 14, 16, 19, 20, 22, 23, 24, 25):
+        for v in (13, 14, 16, 19, 20, 22, 23, 24, 25, 26):
             got = DW.encode(frames, wavelet, L, Q, variant=v)
             for f in range(3):
                 for name in ref[f]:
@@ -174,7 +174,7 @@ def test_dwt_frame_pipeline_small(H, W, L, Q):
 def test_dwt_unknown_variant():
     import vcf_amd.dwt as DW
     with pytest.raises(ValueError):
-        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=26)
+        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=27)
     with pytest.raises(ValueError):
         DW.decode(DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32), 16, 16, "db5", 2, 32, variant=12)
 

@@ -1636,6 +1636,7 @@ AuxStreams &aux_for_current_device()
 struct PipeShape {
     int streams = 0, chunks = 0;
     bool stagger = false;
+    bool caller = false;   // the caller's stream is stream 0 (no fork wait or join on it)
 };
 
 // run chain(first_frame, n, stream, hook) per chunk, ordered after and before
@@ -1650,9 +1651,13 @@ int run_pipelined(long long n_frames, PipeShape ps, hipStream_t s, Chain &&chain
     const int ns = std::max(1, std::min(ps.streams, kAuxStreams));
     const long long nc = std::max(1LL, std::min<long long>({(long long)ps.chunks, (long long)kMaxChunks, n_frames}));
     const long long chunk = (n_frames + nc - 1) / nc;
+    // stream j of the pipeline: the caller's own for j = 0 when ps.caller, else a library stream
+    const int j0 = ps.caller ? 1 : 0;
+    auto stream_of = [&](int j) { return ps.caller && j == 0 ? s : ax.s[j - j0]; };
     if ((rc = hip_check(hipEventRecord(ax.fork, s), "hipEventRecord")) != VCF_OK) return rc;
-    for (int j = 0; j < ns; ++j)
-        if ((rc = hip_check(hipStreamWaitEvent(ax.s[j], ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
+    for (int j = j0; j < ns; ++j)
+        if ((rc = hip_check(hipStreamWaitEvent(stream_of(j), ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK)
+            return rc;
     int k = 0;
     for (long long f0 = 0; f0 < n_frames; f0 += chunk, ++k) {
         PipeHook hook;
@@ -1660,11 +1665,12 @@ int run_pipelined(long long n_frames, PipeShape ps, hipStream_t s, Chain &&chain
             hook.wait = k > 0 ? ax.big[k - 1] : nullptr;
             hook.rec = ax.big[k];
         }
-        if ((rc = chain(f0, std::min(chunk, n_frames - f0), ax.s[k % ns], ps.stagger ? &hook : nullptr)) != VCF_OK)
+        if ((rc = chain(f0, std::min(chunk, n_frames - f0), stream_of(k % ns), ps.stagger ? &hook : nullptr)) !=
+            VCF_OK)
             break;
     }
-    // join every stream even after an error, so the caller's stream never runs ahead
-    for (int j = 0; j < ns; ++j) {
+    // join every library stream even after an error, so the caller's stream never runs ahead
+    for (int j = 0; j < ns - j0; ++j) {
         int r2 = hip_check(hipEventRecord(ax.join[j], ax.s[j]), "hipEventRecord");
         if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(s, ax.join[j], 0), "hipStreamWaitEvent");
         if (rc == VCF_OK) rc = r2;
@@ -1811,7 +1817,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 25) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant > 26) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1829,9 +1835,15 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
     if (variant == 16) ps = {2, 8, true};
     if (variant == 18) ps = {3, 4, true};
     if (variant == 19) ps = {4, 4, false};
-    // 20 / 21 / 22: variant 0 with levels whose input planes have at most 40 k / 140 k / 600 k
-    // samples on the separable kernels (at 4K: level 5 / levels 4-5 / levels 3-5)
-    const long long sep_area = variant == 20 ? 40000 : variant == 21 ? 140000 : variant == 22 ? 600000 : 0;
+    if (variant == 26) ps = {2, 2, false, true};   // 13 with chunk 0 on the caller's stream
+    // levels after the first whose input planes have at most 40 k samples (at 4K: level 5) run on
+    // the separable kernels: one thread per output beats the fused tile's three serial channels
+    // there (-2.2 % on C3, ABBA); 20 = none of them (the earlier schedule), 21 / 22 = up to
+    // 140 k / 600 k samples (at 4K: levels 4-5 / 3-5)
+    const long long sep_area = variant == 20 || (variant >= 1 && variant <= 12) ? 0
+                               : variant == 21                                    ? 140000
+                               : variant == 22                                    ? 600000
+                                                                                  : 40000;
     if (variant >= 20 && pipeline_default(n_frames, H, W)) ps = kEncodePipe;
     // 23: variant 0 with the fused levels' sums started at 0.0 (no Z0, A/B)
     // 24: variant 0 with level 1 in 512-thread tiles of 16 output rows (int16 staging)
