@@ -127,7 +127,10 @@ int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
  *      subbands),
  * 17 = variant 5 with the earlier address arithmetic (32-bit divisions and
  *      multiplies per copy-out chunk, a 64-bit multiply per input row; A/B).
- * Variants 1, 3, 4, 5, 7 and 11-17 produce identical bytes. */
+ * 18, 19 = variant 0 with the frames cut into two / four chunks whose
+ *      launches run on two library streams (forked from and joined to the
+ *      caller's stream; A/B).
+ * Variants 1, 3, 4, 5, 7 and 11-19 produce identical bytes. */
 int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H,
                               int32_t W, int32_t block_size, int32_t Q, uint32_t flags,
                               uint8_t *k_dev, void *stream);

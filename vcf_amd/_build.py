@@ -16,7 +16,8 @@ LIB = os.path.join(PKG, "libvcf_amd.so")
 SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_dct_any.hip", "vcf_quant.hip", "vcf_dwt.hip", "vcf_cbaac.cpp",
            "vcf_cbahc.cpp", "vcf_ipp.hip", "vcf_ipp_rdo.hip",
            "vcf_png.cpp", "vcf_comm.cpp", "vcf_cbaac_gpu.hip", "vcf_plugins.hip"]
-HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h", "vcf_wavelets.h", "vcf_pocketfft.h", "vcf_pocketfft_tables.h"]
+HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h", "vcf_wavelets.h", "vcf_pocketfft.h", "vcf_pocketfft_tables.h",
+           "vcf_pocketfft_rt.h", "vcf_pipeline.h"]
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("VCF_OFFLOAD_ARCH", "gfx950")
 

@@ -31,6 +31,7 @@
 #include "vcf_dct8.h"
 #include "vcf_dct_block.h"
 #include "vcf_internal.h"
+#include "vcf_pipeline.h"
 
 namespace vcf {
 namespace {
@@ -957,10 +958,18 @@ int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         return dct_any_encode_u8(rgb_dev, n_frames, H, W, block_size, Q, flags, k_dev, stream);
     int rc = check_args(rgb_dev, k_dev, n_frames, H, W, block_size, Q, flags, false);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 17) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
+    if (variant < 0 || variant > 19) return set_error(VCF_ERR_INVALID, "unknown encode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
+    if (variant == 18 || variant == 19) {   // A/B: variant 0 over two / four chunks of frames on two library streams
+        const PipeShape ps{2, variant == 18 ? 2 : 4, false};
+        return run_pipelined(n_frames, ps, (hipStream_t)stream,
+                             [&](long long f0, long long n, hipStream_t cs, const PipeHook *) {
+                                 return vcf_dct_dz_encode_variant(0, rgb_dev + f0 * g.in_stride, n, H, W, block_size,
+                                                                  Q, flags, k_dev + f0 * g.out_stride, cs);
+                             });
+    }
     const bool pow2 = (Q & (Q - 1)) == 0;
     const bool sub = !(flags & VCF_DCT_NO_SUBBANDS);
     const bool perc = (flags & VCF_DCT_PERCEPTUAL) != 0;

@@ -34,6 +34,7 @@
 
 #include "vcf_amd.h"
 #include "vcf_internal.h"
+#include "vcf_pipeline.h"
 #include "vcf_wavelets.h"
 
 namespace vcf {
@@ -1592,101 +1593,7 @@ void inv_level(int F, const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t
 // large ones.  The caller's stream forks to the library's streams through an
 // event and joins them again, so the call keeps its stream semantics; each
 // chunk touches only its own frames' input, output and workspace planes.
-constexpr int kAuxStreams = 4, kMaxChunks = 16;
-
-// stagger: the level that fills the chip (level 1 of either direction) of
-// chunk k waits for chunk k-1's to finish, so those kernels run one after
-// another at full width while the small levels fill in beside them
-struct PipeHook {
-    hipEvent_t wait = nullptr;   // before the big level (null: none)
-    hipEvent_t rec = nullptr;    // recorded after it
-};
-
-struct AuxStreams {
-    std::mutex mu;
-    bool ready = false;
-    hipStream_t s[kAuxStreams] = {};
-    hipEvent_t fork = nullptr, join[kAuxStreams] = {}, big[kMaxChunks] = {};
-
-    int init()
-    {
-        if (ready) return VCF_OK;
-        int rc = hip_check(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "hipEventCreate");
-        for (int j = 0; rc == VCF_OK && j < kAuxStreams; ++j) {
-            rc = hip_check(hipStreamCreateWithFlags(&s[j], hipStreamNonBlocking), "hipStreamCreate");
-            if (rc == VCF_OK) rc = hip_check(hipEventCreateWithFlags(&join[j], hipEventDisableTiming), "hipEventCreate");
-        }
-        for (int j = 0; rc == VCF_OK && j < kMaxChunks; ++j)
-            rc = hip_check(hipEventCreateWithFlags(&big[j], hipEventDisableTiming), "hipEventCreate");
-        ready = rc == VCF_OK;
-        return rc;
-    }
-};
-
-AuxStreams &aux_for_current_device()
-{
-    static AuxStreams per_dev[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    return per_dev[dev];
-}
-
-// how a batch is pipelined: `chunks` chunks of consecutive frames round-robin
-// over `streams` library streams, staggered or not; streams == 0: no pipeline
-struct PipeShape {
-    int streams = 0, chunks = 0;
-    bool stagger = false;
-    bool caller = false;   // the caller's stream is stream 0 (no fork wait or join on it)
-};
-
-// run chain(first_frame, n, stream, hook) per chunk, ordered after and before
-// the caller's stream s
-template <typename Chain>
-int run_pipelined(long long n_frames, PipeShape ps, hipStream_t s, Chain &&chain)
-{
-    AuxStreams &ax = aux_for_current_device();
-    std::lock_guard<std::mutex> lock(ax.mu);
-    int rc = ax.init();
-    if (rc != VCF_OK) return rc;
-    const int ns = std::max(1, std::min(ps.streams, kAuxStreams));
-    const long long nc = std::max(1LL, std::min<long long>({(long long)ps.chunks, (long long)kMaxChunks, n_frames}));
-    const long long chunk = (n_frames + nc - 1) / nc;
-    // stream j of the pipeline: the caller's own for j = 0 when ps.caller, else a library stream
-    const int j0 = ps.caller ? 1 : 0;
-    auto stream_of = [&](int j) { return ps.caller && j == 0 ? s : ax.s[j - j0]; };
-    if ((rc = hip_check(hipEventRecord(ax.fork, s), "hipEventRecord")) != VCF_OK) return rc;
-    for (int j = j0; j < ns; ++j)
-        if ((rc = hip_check(hipStreamWaitEvent(stream_of(j), ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK)
-            return rc;
-    int k = 0;
-    for (long long f0 = 0; f0 < n_frames; f0 += chunk, ++k) {
-        PipeHook hook;
-        if (ps.stagger) {
-            hook.wait = k > 0 ? ax.big[k - 1] : nullptr;
-            hook.rec = ax.big[k];
-        }
-        if ((rc = chain(f0, std::min(chunk, n_frames - f0), stream_of(k % ns), ps.stagger ? &hook : nullptr)) !=
-            VCF_OK)
-            break;
-    }
-    // join every library stream even after an error, so the caller's stream never runs ahead
-    for (int j = 0; j < ns - j0; ++j) {
-        int r2 = hip_check(hipEventRecord(ax.join[j], ax.s[j]), "hipEventRecord");
-        if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(s, ax.join[j], 0), "hipStreamWaitEvent");
-        if (rc == VCF_OK) rc = r2;
-    }
-    return rc;
-}
-
-int hook_wait(const PipeHook *h, hipStream_t s)
-{
-    return h && h->wait ? hip_check(hipStreamWaitEvent(s, h->wait, 0), "hipStreamWaitEvent") : VCF_OK;
-}
-int hook_rec(const PipeHook *h, hipStream_t s)
-{
-    return h && h->rec ? hip_check(hipEventRecord(h->rec, s), "hipEventRecord") : VCF_OK;
-}
-
+// (helpers in vcf_pipeline.h)
 // the default: batches of at least two frames of at least 2^20 pixels
 // (smaller frames stay on the caller's stream)
 bool pipeline_default(long long n_frames, int H, int W) { return n_frames >= 2 && (long long)H * W >= (1LL << 20); }
@@ -1873,7 +1780,7 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
 // one stream's level chain of the decode (variants 0-5)
 static int decode_chain(int variant, const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W,
                         int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
-                        hipStream_t s, const PipeHook *hook)
+                        hipStream_t s, const PipeHook *hook, long long sep_area = 0)
 {
     int rc = VCF_OK;
     Filters flt;
@@ -1911,6 +1818,22 @@ static int decode_chain(int variant, const uint8_t *packed_dev, int64_t n_frames
                               g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], h, w, oh, ow, Q, lda,
                               (unsigned)n_frames, flt, &kWavelets[wavelet], s,
                               variant == 4 ? 2 : variant == 5 ? 3 : 1};
+            if (r > 1 && (long long)h * w <= sep_area) {   // a small level on the separable kernels (A/B)
+                if (r == levels)
+                    hipLaunchKernelGGL(idwt_rows_kernel<true>, dim3(gx(2 * w), h, planes), dim3(256), 0, s, packed_dev,
+                                       g.packed_bytes, g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2],
+                                       nullptr, 0LL, 0, A, D, ws_stride, h, w, F, Q, flt);
+                else
+                    hipLaunchKernelGGL(idwt_rows_kernel<false>, dim3(gx(2 * w), h, planes), dim3(256), 0, s,
+                                       packed_dev, g.packed_bytes, g.ll_off, g.sb_off[r][0], g.sb_off[r][1],
+                                       g.sb_off[r][2], prev, ws_stride, lda, A, D, ws_stride, h, w, F, Q, flt);
+                hipLaunchKernelGGL(idwt_cols_kernel, dim3(gx(2 * w), 2 * h, planes), dim3(256), 0, s, A, D,
+                                   ws_stride, out, ws_stride, h, 2 * w, F, flt);
+                prev = out;
+                lda = 2 * w;
+                if ((rc = hip_check(hipGetLastError(), "idwt level launch")) != VCF_OK) return rc;
+                continue;
+            }
             if (r == 1 && (rc = hook_wait(hook, s)) != VCF_OK) return rc;
             inv_level(F, a, r == levels, r == 1, rgb_dev);
             prev = out;
@@ -1950,7 +1873,7 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant == 3 || variant > 11) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant == 3 || variant > 14) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1966,6 +1889,9 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
     if (variant == 8) ps = {2, 4, true};
     if (variant == 10) ps = {2, 8, true};
     if (variant == 11) ps = {3, 4, true};
+    // 12 / 13 / 14: variant 0 with the levels after the coarsest-first order's big one whose subbands
+    // have at most 10 k / 40 k / 140 k samples on the separable kernels (4K: level 5 / 4-5 / 3-5)
+    const long long sep_area = variant == 12 ? 10000 : variant == 13 ? 40000 : variant == 14 ? 140000 : 0;
     if (variant >= 6) variant = 0;
     {
         DwtGeom g;
@@ -1982,7 +1908,7 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
         }
     }
     return decode_chain(variant, packed_dev, n_frames, H, W, wavelet, levels, Q, rgb_dev, workspace_dev,
-                        (hipStream_t)stream, nullptr);
+                        (hipStream_t)stream, nullptr, sep_area);
 }
 
 }  // extern "C"
