@@ -78,8 +78,11 @@ def dwt(args):
                          "one 4K S-smooth frame, oracle/vcf_dwt_oracle.cpp (pywt 1.1.1 'per' restated)")
     cpu_d, _ = cpu_port(lambda: O.dwt_decode_frame(sb, H, W, "bior4.4", L_, Q), H * W,
                         "one 4K frame's subbands, oracle/vcf_dwt_oracle.cpp")
-    for variant, vname in ((0, "default (fused level 1 and last level, strips for the middle levels)"),
-                           (1, "fused level kernels"), (2, "separable kernels")):
+    names = {0: "default (two-chunk frame pipeline; fused level 1, strips for the middle levels, "
+                "separable last level)",
+             1: "fused level kernels", 2: "separable kernels"}
+    for variant in [int(v) for v in args.dwt_variants.split(",")]:
+        vname = names.get(variant, f"variant {variant}")
         enc = lambda: L.call("vcf_dwt_dz_encode_variant", variant, din.ptr, F, H, W, w, L_, Q, dpk.ptr, dws.ptr,
                              s.handle)
         dec = lambda: L.call("vcf_dwt_dz_decode_variant", variant, dpk.ptr, F, H, W, w, L_, Q, dout.ptr, dws.ptr,
@@ -260,6 +263,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--only", default="dwt,dct_decode,dct_encode_pcie,ipp,entropy,configs")
+    ap.add_argument("--dwt-variants", default="0,1,2")
     args = ap.parse_args()
     set_device(0)
     for name in args.only.split(","):

@@ -2,7 +2,7 @@
 # PMC passes over the DWT bench (fused level kernels): scripts/pmc_dwt.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-ROOT=$(pwd); OUT=$ROOT/gpurun_out/pmc_dwt; mkdir -p "$OUT"; export TMPDIR=/tmp; cd /tmp
+ROOT=$(pwd); OUT=/tmp/pmc_dwt; rm -rf "$OUT"; mkdir -p "$OUT"; export TMPDIR=/tmp; cd /tmp   # raw counters stay on the box
 i=0
 for grp in "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS" \
            "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES" \
@@ -10,7 +10,7 @@ for grp in "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_WAIT_INST_
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o pmc \
-      -- python3 "$ROOT/scripts/bench_paths.py" --only dwt --steps 1 > "$OUT/p$i.log" 2>&1
+      -- python3 "$ROOT/scripts/bench_paths.py" --only dwt --dwt-variants 0 --steps 1 > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"
   case $rc in 0) ;; 124|134|137|139) exit $rc;; *) tail -3 "$OUT/p$i.log";; esac
 done
