@@ -274,8 +274,9 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
  * reconstruction taps at run time), 5 (no raised wave priority while the
  * subbands are staged), 6 / 7 / 8 / 10 / 11 (0 pipelined as the encode's
  * 13 / 14 / 15 / 16 / 18; staggering orders the chunks' last levels) and 9
- * (0 on the caller's stream alone; 0 does not pipeline).  Outputs
- * identical. */
+ * (0 on the caller's stream alone; 0 does not pipeline), 12 / 13 / 14 (small
+ * levels on the separable kernels) and 15 / 16 (bior4.4 / db5 inverse levels
+ * in 32 x 32 / 128 x 8 output tiles instead of 64 x 16).  Outputs identical. */
 int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream);

@@ -148,7 +148,7 @@ def test_dwt_4k_frame_pipeline(wavelet):
     for name in oref:
         assert np.array_equal(ref[4][name], oref[name]), name
     dref = DW.decode(ref, H, W, wavelet, L, Q, variant=9)
-    for v in (0, 6, 7, 8, 10, 11, 12, 13, 14):
+    for v in (0, 6, 7, 8, 10, 11, 12, 13, 14, 15, 16):
         assert np.array_equal(DW.decode(ref, H, W, wavelet, L, Q, variant=v), dref), v
     assert np.array_equal(dref[4], O.dwt_decode_frame(ref[4], H, W, wavelet, L, Q))
 
@@ -167,7 +167,7 @@ def test_dwt_frame_pipeline_small(H, W, L, Q):
                 for name in ref[f]:
                     assert np.array_equal(got[f][name], ref[f][name]), (wavelet, v, f, name)
         dref = DW.decode(ref, H, W, wavelet, L, Q, variant=0)
-        for v in (6, 7, 10, 12, 14):
+        for v in (6, 7, 10, 12, 14, 15, 16):   # 15 / 16: 32 x 32 / 128 x 8 inverse tiles (bior4.4)
             assert np.array_equal(DW.decode(ref, H, W, wavelet, L, Q, variant=v), dref), (wavelet, v)
 
 
@@ -176,7 +176,7 @@ def test_dwt_unknown_variant():
     with pytest.raises(ValueError):
         DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=27)
     with pytest.raises(ValueError):
-        DW.decode(DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32), 16, 16, "db5", 2, 32, variant=15)
+        DW.decode(DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32), 16, 16, "db5", 2, 32, variant=17)
 
 
 def test_dwt_errors():

@@ -1085,10 +1085,10 @@ __device__ __forceinline__ void inv_group(const double (&flo)[F], const double (
 
 // the column pass's reordered outputs (rare: first / last rows of a plane)
 __device__ __attribute__((noinline)) double inv_col_generic(Filters flt, int F, int h, int n, const double *ta,
-                                                            const double *td, int K0r, int nc)
+                                                            const double *td, int K0r, int nc, int itw)
 {
-    auto la = [&](int k) -> double { return ta[(k - K0r) * kITW + nc]; };
-    auto ld = [&](int k) -> double { return td[(k - K0r) * kITW + nc]; };
+    auto la = [&](int k) -> double { return ta[(k - K0r) * itw + nc]; };
+    auto ld = [&](int k) -> double { return td[(k - K0r) * itw + nc]; };
     return idwt_out_logical(flt.rec_lo, flt.rec_hi, F, h, n, la, ld);
 }
 
@@ -1121,7 +1121,10 @@ __host__ __device__ constexpr double ct_rec(int id, bool hi, int m)
 
 // CT: reconstruction taps of wavelet CT (ct_rec) as compile-time constants
 // (no tap registers: 40 fewer VGPRs than taps staged through LDS)
-template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0, int PRI = 3>
+// ITW: output tile width (the tile is 1024 / ITW rows; 64 x 16 the default, 32 x 32 / 128 x 8 = dwt decode
+// variants 15 / 16, A/B: +3 % / +21 % on C3, profiles/r02_dwt_decode_ab_tiles.log)
+template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0, int PRI = 3,
+          int ITW = kITW>
 __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
                                                          long long ll_off, long long off_lh, long long off_hl,
                                                          long long off_hh, const double *__restrict__ prev,
@@ -1129,29 +1132,30 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
                                                          int h, int w, int oh, int ow, int Q, Taps<F> tp,
                                                          Filters flt, uint8_t *__restrict__ rgb, long long rgb_stride)
 {
+    constexpr int ITH = 1024 / ITW;
     constexpr int F2 = F / 2, T = F2 / 2;
-    constexpr int KHm = kITH / 2 + F2, KWm = kITW / 2 + F2;
+    constexpr int KHm = ITH / 2 + F2, KWm = ITW / 2 + F2;
     constexpr int P0 = (F2 - 1) & 1;                 // parity of n + F2 - 1 for even n
     constexpr int NW = F2 + ((P0 + kG - 1) >> 1);    // window of a 4-output group
-    constexpr int NGC = kITW / kG, NGR = kITH / kG;
-    static_assert(NGC * NGR * kG * kG == kITH * kITW && kITW * NGR == 256, "tile geometry");
+    constexpr int NGC = ITW / kG, NGR = ITH / kG;
+    static_assert(NGC * NGR * kG * kG == ITH * ITW && ITW * NGR == 256, "tile geometry");
     constexpr int S = (KHm * KWm + 1) & ~1;          // even, so the offsets below are odd apart (bank spread)
     __shared__ double sub[4 * S + 4];
-    __shared__ double ta[KHm * kITW], td[KHm * kITW];
+    __shared__ double ta[KHm * ITW], td[KHm * ITW];
     double *sAA = sub, *sDA = sub + S + 1, *sAD = sub + 2 * S + 2, *sDD = sub + 3 * S + 3;
-    const int n0r = blockIdx.y * kITH, n0c = blockIdx.x * kITW;
+    const int n0r = blockIdx.y * ITH, n0c = blockIdx.x * ITW;
     const int K0r = ((n0r + F2 - 1) >> 1) - F2 + 1, K0c = ((n0c + F2 - 1) >> 1) - F2 + 1;
-    const int KH = ((n0r + kITH - 1 + F2 - 1) >> 1) - K0r + 1;
-    const int KW = ((n0c + kITW - 1 + F2 - 1) >> 1) - K0c + 1;
+    const int KH = ((n0r + ITH - 1 + F2 - 1) >> 1) - K0r + 1;
+    const int KW = ((n0c + ITW - 1 + F2 - 1) >> 1) - K0c + 1;
     const bool rows_in = K0r >= 0 && K0r + KH <= h, cols_in = K0c >= 0 && K0c + KW <= w;
-    const bool row_tail = n0c == 0 || n0c + kITW + F2 - 2 >= 2 * w;
-    const bool col_tail = n0r == 0 || n0r + kITH + F2 - 2 >= 2 * h;
+    const bool row_tail = n0c == 0 || n0c + ITW + F2 - 2 >= 2 * w;
+    const bool col_tail = n0r == 0 || n0r + ITH + F2 - 2 >= 2 * h;
     const int tid = threadIdx.x;
     const long long frame = TO_RGB ? blockIdx.z : blockIdx.z / 3;
     const uint8_t *pk = packed + frame * packed_stride;
     double acc[TO_RGB ? 3 : 1][kG];
     const int ch_lo = TO_RGB ? 0 : (int)(blockIdx.z % 3), ch_hi = TO_RGB ? 3 : ch_lo + 1;
-    const int nc = tid % kITW, gr = tid / kITW;      // column-pass item
+    const int nc = tid % ITW, gr = tid / ITW;      // column-pass item
     __shared__ double taps[CT ? 1 : 2 * F];
     if (!CT) {
         if (tid < F) {
@@ -1203,20 +1207,20 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
             }
             double sum[kG];
             inv_group<F, ZLO, ZHI>(flo, fhi, xa, xd, sum);
-            double *dst = (src ? td : ta) + r * kITW + kG * g;
+            double *dst = (src ? td : ta) + r * ITW + kG * g;
 #pragma unroll
             for (int u = 0; u < kG; ++u) dst[u] = sum[u];
         }
         if (row_tail) {   // tile-uniform: outputs whose wrapped pair index is below F/4
             __syncthreads();
-            for (int t = tid; t < KH * kITW * 2; t += 256) {
-                const int src = t & 1, r = (t >> 1) / kITW, nc2 = (t >> 1) % kITW;
+            for (int t = tid; t < KH * ITW * 2; t += 256) {
+                const int src = t & 1, r = (t >> 1) / ITW, nc2 = (t >> 1) % ITW;
                 const int n = n0c + nc2, q = n + F2 - 1;
                 if (n >= ow || ((q % (2 * w)) >> 1) >= T) continue;
                 const double *Xr = (src ? sDA : sAA) + r * KWm - K0c, *Yr = (src ? sDD : sAD) + r * KWm - K0c;
                 auto la = [&](int k) -> double { return Xr[k]; };
                 auto ld = [&](int k) -> double { return Yr[k]; };
-                (src ? td : ta)[r * kITW + nc2] = idwt_out_logical(flt.rec_lo, flt.rec_hi, F, w, n, la, ld);
+                (src ? td : ta)[r * ITW + nc2] = idwt_out_logical(flt.rec_lo, flt.rec_hi, F, w, n, la, ld);
             }
         }
         __syncthreads();
@@ -1226,8 +1230,8 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
             double xa[NW], xd[NW];
 #pragma unroll
             for (int k = 0; k < NW; ++k) {
-                xa[k] = ta[(base + k) * kITW + nc];
-                xd[k] = td[(base + k) * kITW + nc];
+                xa[k] = ta[(base + k) * ITW + nc];
+                xd[k] = td[(base + k) * ITW + nc];
             }
             double sum[kG];
             inv_group<F, ZLO, ZHI>(flo, fhi, xa, xd, sum);
@@ -1235,7 +1239,7 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
 #pragma unroll
                 for (int u = 0; u < kG; ++u) {
                     const int n = n0 + u, q = n + F2 - 1;
-                    if (((q % (2 * h)) >> 1) < T) sum[u] = inv_col_generic(flt, F, h, n, ta, td, K0r, nc);
+                    if (((q % (2 * h)) >> 1) < T) sum[u] = inv_col_generic(flt, F, h, n, ta, td, K0r, nc, ITW);
                 }
             }
 #pragma unroll
@@ -1497,7 +1501,7 @@ void launch_strip_level(const LevelArgs &a, bool first, bool last, int mode)
 
 // level r of the inverse: subbands a.h x a.w -> outputs a.hh x a.hw (= oh x ow)
 template <int F, unsigned ZLO, unsigned ZHI>
-void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, bool from_packed, bool to_rgb,
+void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, dim3 grid, bool from_packed, bool to_rgb,
                        uint8_t *rgb_out)
 {
     auto kern = from_packed
@@ -1505,7 +1509,7 @@ void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
                     : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI> : idwt_level_kernel<F, false, false, ZLO, ZHI>);
     if constexpr (F == 10) {   // bior4.4 / db5: constant taps (run-time taps for A/B: dwt decode variant 4)
         constexpr int id = ZLO != 0 ? 1 : 2;
-        bool ct = a.pipe == 1 || a.pipe == 3;
+        bool ct = a.pipe == 1 || a.pipe == 3 || a.pipe == 4 || a.pipe == 5;
         for (int m = 0; m < F; ++m) {
             const double l = ct_rec(id, false, m), h = ct_rec(id, true, m);
             ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
@@ -1520,6 +1524,22 @@ void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
                                          : idwt_level_kernel<F, true, false, ZLO, ZHI, id, 0>)
                                : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id, 0>
                                          : idwt_level_kernel<F, false, false, ZLO, ZHI, id, 0>);
+        if (ct && a.pipe == 4) {   // 32 x 32 output tiles (dwt decode variant 15, A/B)
+            kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI, id, 3, 32>
+                                         : idwt_level_kernel<F, true, false, ZLO, ZHI, id, 3, 32>)
+                               : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id, 3, 32>
+                                         : idwt_level_kernel<F, false, false, ZLO, ZHI, id, 3, 32>);
+            grid.x = (unsigned)((a.hw + 31) / 32);
+            grid.y = (unsigned)((a.hh + 31) / 32);
+        }
+        if (ct && a.pipe == 5) {   // 128 x 8 output tiles (dwt decode variant 16, A/B)
+            kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI, id, 3, 128>
+                                         : idwt_level_kernel<F, true, false, ZLO, ZHI, id, 3, 128>)
+                               : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id, 3, 128>
+                                         : idwt_level_kernel<F, false, false, ZLO, ZHI, id, 3, 128>);
+            grid.x = (unsigned)((a.hw + 127) / 128);
+            grid.y = (unsigned)((a.hh + 7) / 8);
+        }
     }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
                        a.off_hh, a.in, a.plane_stride, a.lda, a.LLout, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, rgb_out,
@@ -1817,7 +1837,7 @@ static int decode_chain(int variant, const uint8_t *packed_dev, int64_t n_frames
             const LevelArgs a{nullptr, 0, prev, ws_stride, out, const_cast<uint8_t *>(packed_dev), g.packed_bytes,
                               g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], h, w, oh, ow, Q, lda,
                               (unsigned)n_frames, flt, &kWavelets[wavelet], s,
-                              variant == 4 ? 2 : variant == 5 ? 3 : 1};
+                              variant == 4 ? 2 : variant == 5 ? 3 : variant == 15 ? 4 : variant == 16 ? 5 : 1};
             if (r > 1 && (long long)h * w <= sep_area) {   // a small level on the separable kernels (A/B)
                 if (r == levels)
                     hipLaunchKernelGGL(idwt_rows_kernel<true>, dim3(gx(2 * w), h, planes), dim3(256), 0, s, packed_dev,
@@ -1873,7 +1893,7 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant == 3 || variant > 14) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant == 3 || variant > 16) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
     int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1892,7 +1912,7 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
     // 12 / 13 / 14: variant 0 with the levels after the coarsest-first order's big one whose subbands
     // have at most 10 k / 40 k / 140 k samples on the separable kernels (4K: level 5 / 4-5 / 3-5)
     const long long sep_area = variant == 12 ? 10000 : variant == 13 ? 40000 : variant == 14 ? 140000 : 0;
-    if (variant >= 6) variant = 0;
+    if (variant >= 6 && variant < 15) variant = 0;
     {
         DwtGeom g;
         dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
