@@ -6,7 +6,8 @@
 - III and IPP at world size 2, both ranks on this box's GPU running the real
   HIP codec, the exchange on the host group: decoded frames equal the
   oracle's, rank 0's gathered code-streams equal every frame's file;
-- `bench.py --gpus 2` without a launcher (the parent spawns the ranks).
+- `bench.py --gpus 2` without a launcher (the parent spawns the ranks) and
+  under `torch.distributed.run`, the driver's command for N > 1.
 """
 import json
 import os
@@ -132,4 +133,24 @@ def test_bench_two_ranks_without_launcher():
                        env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-2000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 8 and line["value"] > 0
+
+
+def test_bench_two_ranks_under_torchrun():
+    """The driver's own N>1 command: torch.distributed.run starts the ranks (the launcher
+    process never touches the GPU), bench.py takes RANK/WORLD_SIZE/MASTER_* from it and
+    keeps its host group off torchrun's store port."""
+    from vcf_amd.comm import free_port
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "VCF_STORE_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--frames", "4", "--steps", "3",
+                        "--warmup", "1", "--settle-max-s", "0", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 8 and line["value"] > 0
