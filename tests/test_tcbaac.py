@@ -1,6 +1,8 @@
 """Tiled CBAAC container (vcf_amd/tcbaac.py) on the host: layout, index
 checks and the reference's malformed-header behaviour (CBAAC.py:101-102).
 The coding itself runs on the GPU (tests/test_tcbaac_gpu.py)."""
+import struct
+
 import numpy as np
 import pytest
 
@@ -29,3 +31,45 @@ def test_segment_count():
     assert T.n_segments(1, 256) == 1
     assert T.n_segments(1080 * 1920 * 3, T.DEFAULT_SEG) == 48
     assert T.n_segments(2160 * 3840 * 3, T.DEFAULT_SEG) == 190
+
+
+def test_container_version_2_carries_the_prior():
+    prior = (np.arange(256) % 50 + 1).astype(np.uint16)
+    data = T.pack((4, 70), 0, 256, [3, 2], b"abcde", prior)
+    assert struct.unpack_from("<I", data, 16)[0] == T.VERSION_PRIOR
+    shape, order, seg_len, sb, pl, pr = T._parse(data)
+    assert shape == (4, 70) and list(sb) == [3, 2] and pl == b"abcde" and np.array_equal(pr, prior)
+    assert T.unpack(data)[:3] == ((4, 70), 0, 256)
+    with pytest.raises(ValueError):
+        T.pack((4, 70), 0, 256, [3, 2], b"abcde", np.zeros(256, np.uint16))    # a zero frequency
+    with pytest.raises(ValueError):
+        T.pack((4, 70), 0, 256, [3, 2], b"abcde", np.full(256, 64, np.uint16))  # total >= max_freq
+
+
+def test_prior_formula():
+    sym = np.array([0] * 900 + [5] * 90 + [255] * 10, np.uint8)
+    p = T.prior_of(sym)
+    assert p[0] == 1 + 900 * 8192 // 1000 and p[5] == 1 + 90 * 8192 // 1000 and p[255] == 1 + 10 * 8192 // 1000
+    assert p[1] == 1 and int(p.sum()) < 16384
+    assert np.array_equal(T.prior_of(np.zeros(0, np.uint8)), np.ones(256, np.uint16))
+
+
+def test_host_coder_with_prior():
+    """vcf_cbaac_encode_prior: all-ones prior == the reference's model; a
+    skewed prior round-trips and codes a skewed segment in fewer bytes."""
+    rng = np.random.Generator(np.random.PCG64(4))
+    sym = np.where(rng.random(20000) < 0.97, 128, rng.integers(0, 256, 20000)).astype(np.uint8)
+    ones = np.ones(256, np.uint16)
+    assert T.host_segments_prior(sym, ones, 4096) == T.host_segments(sym, 0, 4096)
+    p = T.prior_of(sym)
+    segs = T.host_segments_prior(sym, p, 4096)
+    assert sum(map(len, segs)) < sum(map(len, T.host_segments(sym, 0, 4096)))
+    for i, s in enumerate(segs):
+        part = sym[i * 4096:(i + 1) * 4096]
+        assert np.array_equal(T.host_decode_prior(s, part.size, p), part)
+
+
+def test_prior_codec_is_registered():
+    from vcf_amd.codec.dct2d import ENTROPY_CODECS
+    c = ENTROPY_CODECS["TCBAACP"]()
+    assert c.prior and c.ORDER == 0 and c.seg_len == T.PRIOR_SEG and c.file_extension == ".tadpt_arith"

@@ -106,3 +106,61 @@ def test_dct_codec_with_tcbaac_frame(tmp_path):
     dec.decode_fn(str(tmp_path / "enc"), str(tmp_path / "out.png"))
     out = np.asarray(Image.open(str(tmp_path / "out.png")))
     assert np.array_equal(out, O.decode_frame(k, 1080, 1920, 32, 0))
+
+
+@pytest.mark.parametrize("seg_len", [256, 4096, 32768])
+def test_prior_segments_equal_host_coder_and_round_trip(seg_len):
+    """Container version 2: the GPU prior equals the host formula; every
+    segment's bytes equal vcf_cbaac_encode_prior of that segment; the GPU
+    decoder inverts them."""
+    coder = T.TiledCoder(0, seg_len, prior=True)
+    for name, sym in _streams().items():
+        if seg_len == 256 and sym.size > 50_000:
+            sym = sym[:50_000 + 77]
+        sizes, payload = coder.encode(sym)
+        prior = T.prior_of(sym)
+        assert np.array_equal(coder.last_prior, prior), name
+        host = T.host_segments_prior(sym, prior, seg_len)
+        assert list(sizes) == [len(h) for h in host], name
+        assert payload == b"".join(host), name
+        assert np.array_equal(coder.decode(payload, sizes, sym.size, prior), sym), name
+
+
+def test_prior_codec_on_dct_indices():
+    """A 1080p frame's indices through the version-2 codec: round trip, and
+    short segments cost less rate than with fresh models."""
+    from bench import synth_frame
+    from oracle import oracle as O
+    k = O.encode_frame(synth_frame(1080, 1920, 3), 32, 0)
+    c = T.TiledCBAACCodec(order=0, seg_len=8192, prior=True)
+    data = c.compress(k).getvalue()
+    assert np.array_equal(T.TiledCBAACCodec().decompress(data), k)
+    fresh = T.TiledCBAACCodec(order=0, seg_len=8192).compress(k).getvalue()
+    assert len(data) < 0.7 * len(fresh)
+    with pytest.raises(NotImplementedError):
+        T.TiledCoder(1, 4096, prior=True)
+
+
+def test_dct_codec_with_tcbaacp_frame(tmp_path):
+    """-c TCBAACP: the DCT indices coded on the GPU with prior-seeded models;
+    the file's segments equal the host coder's, decoding gives the oracle frame."""
+    from PIL import Image
+
+    from bench import synth_frame
+    from oracle import oracle as O
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec.dct2d import CoDec
+    rgb = synth_frame(1080, 1920, 4)
+    src = str(tmp_path / "f.png")
+    Image.fromarray(rgb).save(src)
+    CoDec(P.parse(P.dct_parser(), ["encode", "-c", "TCBAACP"])).encode_fn(src, str(tmp_path / "enc"))
+    data = open(str(tmp_path / "enc.tadpt_arith"), "rb").read()
+    k = O.encode_frame(rgb, 32, 0)
+    shape, order, seg_len, sizes, payload, prior = T._parse(data)
+    assert shape == k.shape and order == 0 and seg_len == T.PRIOR_SEG
+    assert np.array_equal(prior, T.prior_of(k))
+    assert payload == b"".join(T.host_segments_prior(k, prior, seg_len))
+    CoDec(P.parse(P.dct_parser(), ["decode", "-c", "TCBAACP"])).decode_fn(str(tmp_path / "enc"),
+                                                                         str(tmp_path / "out.png"))
+    out = np.asarray(Image.open(str(tmp_path / "out.png")))
+    assert np.array_equal(out, O.decode_frame(k, 1080, 1920, 32, 0))

@@ -55,8 +55,15 @@ def _tcbaac(args=None):
                            getattr(args, "segment_symbols", DEFAULT_SEG) if args is not None else DEFAULT_SEG)
 
 
-# TCBAAC: CBAAC in independent segments on the GPU (vcf_amd/tcbaac.py, a new container)
-ENTROPY_CODECS = {"TIFF": TIFFCodec, "CBAAC": _cbaac, "CBAHC": _cbahc, "TCBAAC": _tcbaac}
+def _tcbaac_prior(args=None):
+    from ..tcbaac import PRIOR_SEG, TiledCBAACCodec
+    return TiledCBAACCodec(0, getattr(args, "segment_symbols", PRIOR_SEG) if args is not None else PRIOR_SEG,
+                           prior=True)
+
+
+# TCBAAC: CBAAC in independent segments on the GPU (vcf_amd/tcbaac.py, a new container);
+# TCBAACP: the same with every segment's order-0 model seeded by the frame's prior (container version 2)
+ENTROPY_CODECS = {"TIFF": TIFFCodec, "CBAAC": _cbaac, "CBAHC": _cbahc, "TCBAAC": _tcbaac, "TCBAACP": _tcbaac_prior}
 
 
 def register_entropy_codec(name, cls):

@@ -55,6 +55,11 @@ struct Model {
             for (int k = i + 1; k <= kSymbols; k += k & -k) tree[k] += freq[i];
         }
     }
+    void init(const uint16_t *prior)   // the tiled container's prior-initialised model (order 0)
+    {
+        for (int i = 0; i < kSymbols; ++i) freq[i] = prior[i];
+        rebuild();
+    }
     uint32_t cum(int s) const   // sum of freq[0..s)
     {
         uint32_t r = 0;
@@ -163,13 +168,14 @@ int64_t vcf_cbaac_bound(int64_t n_symbols)
     return n_symbols < 0 ? 0 : (n_symbols * 17 + 7) / 8 + 16;
 }
 
-int vcf_cbaac_encode(const uint8_t *symbols, int64_t n, int32_t order, uint8_t *out, int64_t out_capacity,
-                     int64_t *out_bytes, int64_t *out_bits)
+static int cbaac_encode(const uint8_t *symbols, int64_t n, int32_t order, uint8_t *out, int64_t out_capacity,
+                        int64_t *out_bytes, int64_t *out_bits, const uint16_t *prior)
 {
     if (n < 0 || order < 0 || order > 8) return set_error(VCF_ERR_INVALID, "bad n or order (0..8)");
     if ((n > 0 && !symbols) || !out || !out_bytes) return set_error(VCF_ERR_INVALID, "null buffer");
     try {
         Contexts ctx(order);
+        if (prior) ctx.get(0).init(prior);
         BitWriter bw{out, out_capacity};
         uint32_t low = 0, high = 0xFFFFFFFFu;
         uint64_t pending = 0, key = 0;
@@ -216,12 +222,30 @@ int vcf_cbaac_encode(const uint8_t *symbols, int64_t n, int32_t order, uint8_t *
     return VCF_OK;
 }
 
-int vcf_cbaac_decode(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t order, uint8_t *symbols_out)
+int vcf_cbaac_encode(const uint8_t *symbols, int64_t n, int32_t order, uint8_t *out, int64_t out_capacity,
+                     int64_t *out_bytes, int64_t *out_bits)
+{
+    return cbaac_encode(symbols, n, order, out, out_capacity, out_bytes, out_bits, nullptr);
+}
+
+// order 0 from the tiled container's prior frequencies (vcf_cbaac_gpu.hip)
+int vcf_cbaac_encode_prior(const uint8_t *symbols, int64_t n, const uint16_t *prior, uint8_t *out,
+                           int64_t out_capacity, int64_t *out_bytes, int64_t *out_bits)
+{
+    if (!prior) return set_error(VCF_ERR_INVALID, "null prior");
+    for (int i = 0; i < kSymbols; ++i)
+        if (prior[i] == 0) return set_error(VCF_ERR_INVALID, "prior frequency 0 (symbol %d)", i);
+    return cbaac_encode(symbols, n, 0, out, out_capacity, out_bytes, out_bits, prior);
+}
+
+static int cbaac_decode(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t order, uint8_t *symbols_out,
+                        const uint16_t *prior)
 {
     if (n < 0 || nbytes < 0 || order < 0 || order > 8) return set_error(VCF_ERR_INVALID, "bad arguments");
     if ((n > 0 && !symbols_out) || (nbytes > 0 && !bytes)) return set_error(VCF_ERR_INVALID, "null buffer");
     try {
         Contexts ctx(order);
+        if (prior) ctx.get(0).init(prior);
         BitReader br{bytes, nbytes * 8};
         uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
         for (int k = 0; k < 32; ++k) value = (value << 1) | (uint32_t)br.get();
@@ -261,6 +285,20 @@ int vcf_cbaac_decode(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t or
         return set_error(VCF_ERR_INVALID, "out of host memory (context order %d)", order);
     }
     return VCF_OK;
+}
+
+int vcf_cbaac_decode(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t order, uint8_t *symbols_out)
+{
+    return cbaac_decode(bytes, nbytes, n, order, symbols_out, nullptr);
+}
+
+int vcf_cbaac_decode_prior(const uint8_t *bytes, int64_t nbytes, int64_t n, const uint16_t *prior,
+                           uint8_t *symbols_out)
+{
+    if (!prior) return set_error(VCF_ERR_INVALID, "null prior");
+    for (int i = 0; i < kSymbols; ++i)
+        if (prior[i] == 0) return set_error(VCF_ERR_INVALID, "prior frequency 0 (symbol %d)", i);
+    return cbaac_decode(bytes, nbytes, n, 0, symbols_out, prior);
 }
 
 // The model alone, for parity tests: (low, high, total) handed to the coder

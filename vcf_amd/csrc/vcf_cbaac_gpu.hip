@@ -35,6 +35,8 @@
 // copy), so only the compressed bytes need to leave HBM.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "vcf_amd.h"
 #include "vcf_internal.h"
 
@@ -64,6 +66,26 @@ __device__ __forceinline__ void model_reset(Model &m, uint32_t lane)
     m.p0 = (4 * lane) | ((4 * lane + 1) << 16);   // all frequencies 1
     m.p1 = (4 * lane + 2) | ((4 * lane + 3) << 16);
     m.total = 256;
+}
+
+// Prior-initialised model (order 0, the `.tadpt_arith` version-2 container):
+// every segment starts from the frame's prior frequencies f[s] = 1 +
+// floor(hist[s] * kPriorScale / n) instead of 256 ones, then adapts by the
+// reference's rules (CBAAC.py:32-36).  Short segments then stop paying the
+// model's learning cost.
+constexpr uint32_t kPriorScale = 8192;   // prior total <= 256 + 8192 < max_freq
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane);
+
+__device__ __forceinline__ void model_reset_prior(Model &m, const uint16_t *__restrict__ prior, uint32_t lane)
+{
+    const uint2 q = *reinterpret_cast<const uint2 *>(prior + 4 * lane);   // f[4l .. 4l+3]
+    const uint32_t f0 = q.x & 0xFFFFu, f1 = q.x >> 16, f2 = q.y & 0xFFFFu, f3 = q.y >> 16;
+    const uint32_t sum = f0 + f1 + f2 + f3;
+    const uint32_t ex = wave_excl_scan(sum, lane);
+    m.p0 = ex | ((ex + f0) << 16);
+    m.p1 = (ex + f0 + f1) | ((ex + f0 + f1 + f2) << 16);
+    m.total = rl(ex + sum, 63);
 }
 
 // C[4L..4L+4] of lane L as one 64-bit word + C[4L+4]
@@ -289,7 +311,8 @@ template <int ORDER, bool TRACE>
 __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *__restrict__ sym, int64_t n,
                                                                 int64_t seg_len, uint32_t *__restrict__ slots,
                                                                 int64_t slot_words, int64_t *__restrict__ seg_bits,
-                                                                int32_t *__restrict__ trace)
+                                                                int32_t *__restrict__ trace,
+                                                                const uint16_t *__restrict__ prior)
 {
     Tables *tabs = Lds<ORDER>::get();
     const int64_t seg = blockIdx.x;
@@ -299,7 +322,8 @@ __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *_
     const uint8_t *src = sym + start;
 
     Model m;
-    model_reset(m, lane);
+    if (ORDER == 0 && prior) model_reset_prior(m, prior, lane);
+    else model_reset(m, lane);
     if constexpr (ORDER == 1) tables_reset(tabs[0], lane);
     uint32_t ctx = 0;
 
@@ -392,7 +416,8 @@ struct BitReader {
 template <int ORDER>
 __global__ __launch_bounds__(64) void cbaac_tiled_decode_kernel(const uint8_t *__restrict__ in,
                                                                 const int64_t *__restrict__ offs, int64_t n,
-                                                                int64_t seg_len, uint8_t *__restrict__ out)
+                                                                int64_t seg_len, uint8_t *__restrict__ out,
+                                                                const uint16_t *__restrict__ prior)
 {
     Tables *tabs = Lds<ORDER>::get();
     const int64_t seg = blockIdx.x;
@@ -402,7 +427,8 @@ __global__ __launch_bounds__(64) void cbaac_tiled_decode_kernel(const uint8_t *_
     uint8_t *dst = out + start;
 
     Model m;
-    model_reset(m, lane);
+    if (ORDER == 0 && prior) model_reset_prior(m, prior, lane);
+    else model_reset(m, lane);
     if constexpr (ORDER == 1) tables_reset(tabs[0], lane);
     uint32_t ctx = 0;
 
@@ -518,6 +544,26 @@ __global__ __launch_bounds__(256) void cbaac_tiled_pack_kernel(const uint32_t *_
         if (o + i < capacity) out[o + i] = src[i];
 }
 
+// order-0 histogram of the frame's symbols (LDS bins, one global atomic per bin and workgroup)
+__global__ __launch_bounds__(256) void cbaac_hist_kernel(const uint8_t *__restrict__ sym, int64_t n,
+                                                         uint32_t *__restrict__ hist)
+{
+    __shared__ uint32_t bins[256];
+    bins[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        atomicAdd(&bins[sym[i]], 1u);
+    __syncthreads();
+    if (bins[threadIdx.x]) atomicAdd(&hist[threadIdx.x], bins[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void cbaac_prior_kernel(const uint32_t *__restrict__ hist, int64_t n,
+                                                          uint16_t *__restrict__ prior)
+{
+    const uint32_t t = threadIdx.x;
+    prior[t] = (uint16_t)(1u + (n > 0 ? (uint32_t)((uint64_t)hist[t] * kPriorScale / (uint64_t)n) : 0u));
+}
+
 int64_t slot_words_for(int64_t seg_len) { return (vcf_cbaac_bound(seg_len) + 3) / 4; }
 
 int check_args(int64_t n, int32_t order, int64_t seg_len)
@@ -557,9 +603,10 @@ int64_t vcf_cbaac_tiled_bound(int64_t n, int64_t seg_len)
 
 static int tiled_encode(const uint8_t *sym_dev, int64_t n, int32_t order, int64_t seg_len, uint8_t *out_dev,
                         int64_t out_capacity, int64_t *seg_bytes_dev, int32_t *trace_dev, void *ws_dev,
-                        void *stream)
+                        void *stream, const uint16_t *prior_dev = nullptr)
 {
     if (int s = check_args(n, order, seg_len)) return s;
+    if (prior_dev && order != 0) return set_error(VCF_ERR_UNSUPPORTED, "prior-initialised models: order 0 only");
     const int64_t ns = vcf_cbaac_tiled_segments(n, seg_len);
     if (!seg_bytes_dev) return set_error(VCF_ERR_INVALID, "null seg_bytes");
     hipStream_t st = (hipStream_t)stream;
@@ -572,11 +619,11 @@ static int tiled_encode(const uint8_t *sym_dev, int64_t n, int32_t order, int64_
     int64_t *offs = bits + ns;
     const dim3 grid((unsigned)ns);
     if (trace_dev) {
-        if (order == 0) cbaac_tiled_encode_kernel<0, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev);
-        else cbaac_tiled_encode_kernel<1, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev);
+        if (order == 0) cbaac_tiled_encode_kernel<0, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev, prior_dev);
+        else cbaac_tiled_encode_kernel<1, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev, nullptr);
     } else {
-        if (order == 0) cbaac_tiled_encode_kernel<0, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr);
-        else cbaac_tiled_encode_kernel<1, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr);
+        if (order == 0) cbaac_tiled_encode_kernel<0, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr, prior_dev);
+        else cbaac_tiled_encode_kernel<1, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr, nullptr);
     }
     if (int s = hip_check(hipGetLastError(), "cbaac_tiled_encode_kernel")) return s;
     cbaac_tiled_scan_kernel<<<1, 1024, 0, st>>>(bits, ns, offs, seg_bytes_dev);
@@ -603,19 +650,58 @@ int vcf_cbaac_tiled_trace(const uint8_t *sym_dev, int64_t n, int32_t order, int6
     return tiled_encode(sym_dev, n, order, seg_len, nullptr, 0, seg_bytes_dev, triples_dev, ws_dev, stream);
 }
 
-int vcf_cbaac_tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
-                           int64_t seg_len, uint8_t *sym_dev, void *stream)
+static int tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
+                        int64_t seg_len, uint8_t *sym_dev, void *stream, const uint16_t *prior_dev)
 {
     if (int s = check_args(n, order, seg_len)) return s;
+    if (prior_dev && order != 0) return set_error(VCF_ERR_UNSUPPORTED, "prior-initialised models: order 0 only");
     const int64_t ns = vcf_cbaac_tiled_segments(n, seg_len);
     if (ns == 0) return VCF_OK;
     if (!in_dev || !seg_offsets_dev || !sym_dev) return set_error(VCF_ERR_INVALID, "null buffer");
     if (ns > 0x7FFFFFFF) return set_error(VCF_ERR_INVALID, "too many segments");
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((unsigned)ns);
-    if (order == 0) cbaac_tiled_decode_kernel<0><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev);
-    else cbaac_tiled_decode_kernel<1><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev);
+    if (order == 0) cbaac_tiled_decode_kernel<0><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev, prior_dev);
+    else cbaac_tiled_decode_kernel<1><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev, nullptr);
     return hip_check(hipGetLastError(), "cbaac_tiled_decode_kernel");
+}
+
+int vcf_cbaac_tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
+                           int64_t seg_len, uint8_t *sym_dev, void *stream)
+{
+    return tiled_decode(in_dev, seg_offsets_dev, n, order, seg_len, sym_dev, stream, nullptr);
+}
+
+int vcf_cbaac_tiled_prior(const uint8_t *sym_dev, int64_t n, uint16_t *prior_dev, uint32_t *hist_dev, void *stream)
+{
+    if (n < 0) return set_error(VCF_ERR_INVALID, "negative symbol count");
+    if (!prior_dev || !hist_dev || (n > 0 && !sym_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    if (int s = hip_check(hipMemsetAsync(hist_dev, 0, 256 * sizeof(uint32_t), st), "hipMemsetAsync")) return s;
+    if (n > 0) {
+        const int64_t blocks = std::min<int64_t>((n + 4095) / 4096, 2048);
+        cbaac_hist_kernel<<<(unsigned)blocks, 256, 0, st>>>(sym_dev, n, hist_dev);
+        if (int s = hip_check(hipGetLastError(), "cbaac_hist_kernel")) return s;
+    }
+    cbaac_prior_kernel<<<1, 256, 0, st>>>(hist_dev, n, prior_dev);
+    return hip_check(hipGetLastError(), "cbaac_prior_kernel");
+}
+
+int vcf_cbaac_tiled_encode_prior(const uint8_t *sym_dev, int64_t n, const uint16_t *prior_dev, int64_t seg_len,
+                                 uint8_t *out_dev, int64_t out_capacity, int64_t *seg_bytes_dev, void *ws_dev,
+                                 void *stream)
+{
+    if (out_capacity < 0) return set_error(VCF_ERR_INVALID, "negative capacity");
+    if (n > 0 && (!out_dev || !prior_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
+    return tiled_encode(sym_dev, n, 0, seg_len, out_dev, out_capacity, seg_bytes_dev, nullptr, ws_dev, stream,
+                        prior_dev);
+}
+
+int vcf_cbaac_tiled_decode_prior(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n,
+                                 const uint16_t *prior_dev, int64_t seg_len, uint8_t *sym_dev, void *stream)
+{
+    if (n > 0 && !prior_dev) return set_error(VCF_ERR_INVALID, "null prior");
+    return tiled_decode(in_dev, seg_offsets_dev, n, 0, seg_len, sym_dev, stream, prior_dev);
 }
 
 }  // extern "C"

@@ -17,6 +17,11 @@ no segment index):
     b"VCFT", uint32 version = 1, uint32 order, uint32 seg_len,
     uint32 n_segments, uint32 segment_bytes[n_segments]
     the segments' bit streams, back to back (each MSB-first, zero padded)
+Version 2 (`prior=True`, order 0 only; not in the reference) adds, after
+n_segments, 256 uint16 prior frequencies f[s] = 1 + floor(hist[s] * 8192 / n)
+of the frame's symbols, before the segment sizes: every segment's model starts
+from them instead of 256 ones and adapts by the reference's rules, so short
+segments (many waves per frame) stop paying the model's learning cost.
 decompress() of a malformed header returns zeros((10, 10)) like
 CBAAC.py:101-102.
 """
@@ -33,7 +38,9 @@ from .device import DeviceBuffer, Stream
 FILE_EXTENSION = ".tadpt_arith"
 MAGIC = b"VCFT"
 VERSION = 1
+VERSION_PRIOR = 2
 DEFAULT_SEG = 1 << 17     # 48 segments for a 1080p frame, 190 for 4K
+PRIOR_SEG = 1 << 15       # version 2: 190 segments for 1080p at +2.3 % rate (profiles/r02_tcbaac_prior.jsonl)
 
 
 def n_segments(n: int, seg_len: int = DEFAULT_SEG) -> int:
@@ -57,21 +64,34 @@ class _Scratch:
 class TiledCoder:
     """The GPU calls, with reusable scratch and a stream."""
 
-    def __init__(self, order: int = 0, seg_len: int = DEFAULT_SEG, stream: Stream | None = None):
-        self.order, self.seg_len = int(order), int(seg_len)
+    def __init__(self, order: int = 0, seg_len: int = DEFAULT_SEG, stream: Stream | None = None,
+                 prior: bool = False):
+        self.order, self.seg_len, self.prior = int(order), int(seg_len), bool(prior)
+        if self.prior and self.order != 0:
+            raise NotImplementedError("prior-initialised tiled CBAAC: order 0 only")
         self.stream = stream if stream is not None else Stream()
         self.scratch = _Scratch()
+        self.last_prior = None     # the prior table of the last encode (prior=True)
 
     def encode_device(self, sym: DeviceBuffer, n: int, offset: int = 0):
-        """Symbols already in HBM -> (segment byte counts, payload bytes)."""
+        """Symbols already in HBM -> (segment byte counts, payload bytes);
+        with prior=True the frame's prior table is left in self.last_prior."""
         lib = L.lib()
         ns = n_segments(n, self.seg_len)
         ws = self.scratch.get("ws", int(lib.vcf_cbaac_tiled_workspace(n, self.seg_len)))
         cap = int(lib.vcf_cbaac_tiled_bound(n, self.seg_len))
         out = self.scratch.get("out", cap)
         sb = self.scratch.get("sizes", 8 * (ns + 1))
-        L.call("vcf_cbaac_tiled_encode", sym.address(offset), int(n), self.order, self.seg_len, out.ptr, cap,
-               sb.ptr, ws.ptr, self.stream.handle)
+        if self.prior:
+            pr, hist = self.scratch.get("prior", 512), self.scratch.get("hist", 1024)
+            L.call("vcf_cbaac_tiled_prior", sym.address(offset), int(n), pr.ptr, hist.ptr, self.stream.handle)
+            L.call("vcf_cbaac_tiled_encode_prior", sym.address(offset), int(n), pr.ptr, self.seg_len, out.ptr, cap,
+                   sb.ptr, ws.ptr, self.stream.handle)
+            self.last_prior = np.empty(256, np.uint16)
+            pr.download(self.last_prior, self.stream)
+        else:
+            L.call("vcf_cbaac_tiled_encode", sym.address(offset), int(n), self.order, self.seg_len, out.ptr, cap,
+                   sb.ptr, ws.ptr, self.stream.handle)
         sizes = np.empty(ns + 1, np.int64)
         sb.download(sizes, self.stream)
         self.stream.synchronize()
@@ -109,7 +129,7 @@ class TiledCoder:
         self.stream.synchronize()
         return out
 
-    def decode_to_device(self, payload: bytes, seg_bytes, n: int, out: DeviceBuffer):
+    def decode_to_device(self, payload: bytes, seg_bytes, n: int, out: DeviceBuffer, prior=None):
         seg_bytes = np.asarray(seg_bytes, np.int64)
         offs = np.zeros(seg_bytes.size + 1, np.int64)
         np.cumsum(seg_bytes, out=offs[1:])
@@ -120,12 +140,19 @@ class TiledCoder:
             src.upload(np.frombuffer(payload, np.uint8), self.stream)
         ob = self.scratch.get("offs", offs.nbytes)
         ob.upload(offs, self.stream)
-        L.call("vcf_cbaac_tiled_decode", src.ptr, ob.ptr, int(n), self.order, self.seg_len, out.ptr,
-               self.stream.handle)
+        if prior is not None:
+            prior = check_prior(prior)
+            pr = self.scratch.get("prior_in", 512)
+            pr.upload(prior, self.stream)
+            L.call("vcf_cbaac_tiled_decode_prior", src.ptr, ob.ptr, int(n), pr.ptr, self.seg_len, out.ptr,
+                   self.stream.handle)
+        else:
+            L.call("vcf_cbaac_tiled_decode", src.ptr, ob.ptr, int(n), self.order, self.seg_len, out.ptr,
+                   self.stream.handle)
 
-    def decode(self, payload: bytes, seg_bytes, n: int) -> np.ndarray:
+    def decode(self, payload: bytes, seg_bytes, n: int, prior=None) -> np.ndarray:
         out = self.scratch.get("dec", n)
-        self.decode_to_device(payload, seg_bytes, n, out)
+        self.decode_to_device(payload, seg_bytes, n, out, prior)
         res = np.empty(n, np.uint8)
         if n:
             out.download(res, self.stream)
@@ -133,16 +160,33 @@ class TiledCoder:
         return res
 
 
-def pack(shape, order: int, seg_len: int, seg_bytes, payload: bytes) -> bytes:
+def check_prior(prior) -> np.ndarray:
+    """256 uint16 frequencies, each >= 1, total below the model's max_freq
+    (so the packed 16-bit cumulative counts of the GPU model cannot overflow)."""
+    prior = np.ascontiguousarray(prior, np.uint16)
+    if prior.shape != (256,) or int(prior.min()) < 1 or int(prior.sum(dtype=np.int64)) >= 16384:
+        raise ValueError("bad prior table")
+    return prior
+
+
+def pack(shape, order: int, seg_len: int, seg_bytes, payload: bytes, prior=None) -> bytes:
     seg_bytes = np.asarray(seg_bytes, np.int64)
     head = np.array([len(shape), *shape], np.uint32).tobytes()
-    head += MAGIC + struct.pack("<IIII", VERSION, order, seg_len, seg_bytes.size)
+    version = VERSION if prior is None else VERSION_PRIOR
+    head += MAGIC + struct.pack("<IIII", version, order, seg_len, seg_bytes.size)
+    if prior is not None:
+        head += check_prior(prior).astype("<u2").tobytes()
     head += seg_bytes.astype(np.uint32).tobytes()
     return head + payload
 
 
 def unpack(data: bytes):
     """-> (shape, order, seg_len, seg_bytes, payload); ValueError if malformed."""
+    return _parse(data)[:5]
+
+
+def _parse(data: bytes):
+    """-> (shape, order, seg_len, seg_bytes, payload, prior or None)."""
     nd = struct.unpack_from("<I", data, 0)[0]
     if nd > 16:
         raise ValueError("ndims")
@@ -151,16 +195,20 @@ def unpack(data: bytes):
     if data[p:p + 4] != MAGIC:
         raise ValueError("not a tiled CBAAC stream")
     version, order, seg_len, ns = struct.unpack_from("<IIII", data, p + 4)
-    if version != VERSION:
+    if version not in (VERSION, VERSION_PRIOR) or (version == VERSION_PRIOR and order != 0):
         raise ValueError(f"version {version}")
     p += 20
+    prior = None
+    if version == VERSION_PRIOR:
+        prior = check_prior(np.frombuffer(data, "<u2", 256, p))
+        p += 512
     seg_bytes = np.frombuffer(data, np.uint32, ns, p).astype(np.int64)
     p += 4 * ns
     payload = data[p:]
     n = int(np.prod(shape)) if nd else 1
     if n_segments(n, seg_len) != ns or int(seg_bytes.sum()) != len(payload):
         raise ValueError("segment index does not match the payload")
-    return tuple(int(s) for s in shape), int(order), int(seg_len), seg_bytes, payload
+    return tuple(int(s) for s in shape), int(order), int(seg_len), seg_bytes, payload, prior
 
 
 class TiledCBAACCodec:
@@ -169,15 +217,16 @@ class TiledCBAACCodec:
 
     file_extension = FILE_EXTENSION
 
-    def __init__(self, order: int = 0, seg_len: int = DEFAULT_SEG):
+    def __init__(self, order: int = 0, seg_len: int = DEFAULT_SEG, prior: bool = False):
         self.ORDER = int(order)
         self.seg_len = int(seg_len)
+        self.prior = bool(prior)
         self._coder = None
 
     @property
     def coder(self) -> TiledCoder:
         if self._coder is None:
-            self._coder = TiledCoder(self.ORDER, self.seg_len)
+            self._coder = TiledCoder(self.ORDER, self.seg_len, prior=self.prior)
         return self._coder
 
     def compress(self, img: np.ndarray, fn=None) -> io.BytesIO:
@@ -186,7 +235,8 @@ class TiledCBAACCodec:
         if flat.size and (flat.min() < 0 or flat.max() > 255):
             raise ValueError("CBAAC codes byte symbols (0..255)")
         sizes, payload = self.coder.encode(flat.astype(np.uint8))
-        b = io.BytesIO(pack(img.shape, self.ORDER, self.seg_len, sizes, payload))
+        b = io.BytesIO(pack(img.shape, self.ORDER, self.seg_len, sizes, payload,
+                            self.coder.last_prior if self.prior else None))
         b.seek(0)
         return b
 
@@ -195,7 +245,8 @@ class TiledCBAACCodec:
         compressed bytes cross PCIe."""
         n = int(np.prod(shape))
         sizes, payload = self.coder.encode_device(k, n, offset)
-        b = io.BytesIO(pack(tuple(shape), self.ORDER, self.seg_len, sizes, payload))
+        b = io.BytesIO(pack(tuple(shape), self.ORDER, self.seg_len, sizes, payload,
+                            self.coder.last_prior if self.prior else None))
         b.seek(0)
         return b
 
@@ -204,12 +255,12 @@ class TiledCBAACCodec:
             data = data.getvalue()
         data = bytes(data)
         try:
-            shape, order, seg_len, seg_bytes, payload = unpack(data)
+            shape, order, seg_len, seg_bytes, payload, prior = _parse(data)
         except (ValueError, struct.error):
             return np.zeros((10, 10), np.uint8)      # CBAAC.py:101-102
         coder = self.coder if (order, seg_len) == (self.ORDER, self.seg_len) else TiledCoder(order, seg_len)
         n = int(np.prod(shape))
-        return coder.decode(payload, seg_bytes, n).reshape(shape)
+        return coder.decode(payload, seg_bytes, n, prior).reshape(shape)
 
 
 def host_segments(sym: np.ndarray, order: int = 0, seg_len: int = DEFAULT_SEG):
@@ -218,3 +269,40 @@ def host_segments(sym: np.ndarray, order: int = 0, seg_len: int = DEFAULT_SEG):
     from .cbaac import encode_symbols
     sym = np.ascontiguousarray(sym, np.uint8).ravel()
     return [encode_symbols(sym[i:i + seg_len], order) for i in range(0, sym.size, seg_len)]
+
+
+def prior_of(sym: np.ndarray) -> np.ndarray:
+    """The version-2 prior of a frame's symbols, on the host (what
+    vcf_cbaac_tiled_prior computes on the GPU)."""
+    sym = np.ascontiguousarray(sym, np.uint8).ravel()
+    hist = np.bincount(sym, minlength=256).astype(np.uint64)
+    n = max(sym.size, 1)
+    return (1 + hist * 8192 // n).astype(np.uint16)
+
+
+def host_segments_prior(sym: np.ndarray, prior, seg_len: int = DEFAULT_SEG):
+    """vcf_cbaac_encode_prior on every segment: what each segment of a
+    version-2 stream must equal."""
+    import ctypes
+    prior = check_prior(prior)
+    sym = np.ascontiguousarray(sym, np.uint8).ravel()
+    lib = L.lib()
+    res = []
+    for i in range(0, sym.size, seg_len):
+        seg = np.ascontiguousarray(sym[i:i + seg_len])
+        cap = int(lib.vcf_cbaac_bound(seg.size))
+        out = np.empty(cap, np.uint8)
+        nb, bits = ctypes.c_int64(), ctypes.c_int64()
+        L.call("vcf_cbaac_encode_prior", seg.ctypes.data, seg.size, prior.ctypes.data, out.ctypes.data, cap,
+               ctypes.byref(nb), ctypes.byref(bits))
+        res.append(out[:nb.value].tobytes())
+    return res
+
+
+def host_decode_prior(data: bytes, n: int, prior) -> np.ndarray:
+    prior = check_prior(prior)
+    out = np.empty(n, np.uint8)
+    buf = np.frombuffer(data, np.uint8)
+    L.call("vcf_cbaac_decode_prior", buf.ctypes.data if buf.size else None, buf.size, n, prior.ctypes.data,
+           out.ctypes.data)
+    return out
