@@ -127,7 +127,7 @@ def c2_end_to_end(reps=5):
     with tempfile.TemporaryDirectory() as d:
         src = os.path.join(d, "f.png")
         Image.fromarray(synth_frame(1080, 1920, 0)).save(src)
-        for ec in ("TCBAAC", "CBAAC"):
+        for ec in ("TCBAAC", "TCBAACP", "CBAAC"):
             c = CoDec(P.parse(P.dct_parser(), ["encode", "-c", ec]))
             c.encode_fn(src, os.path.join(d, "e"))        # warm (allocations, first launch)
             t0 = time.perf_counter()
@@ -142,6 +142,10 @@ def c2_end_to_end(reps=5):
 def main():
     from vcf_amd.device import set_device
     set_device(0)
+    if "--c2" in sys.argv:
+        for r in c2_end_to_end():
+            print(json.dumps(r), flush=True)
+        return
     if "--prior" in sys.argv:
         for H, W in ((1080, 1920), (2160, 3840)):
             for seg in (1 << 12, 1 << 13, 1 << 14, 1 << 15, 1 << 17):
