@@ -380,22 +380,23 @@ int vcf_cbaac_tiled_trace(const uint8_t *sym_dev, int64_t n, int32_t order, int6
  * int64 byte offsets, device); n symbols out. */
 int vcf_cbaac_tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
                            int64_t seg_len, uint8_t *sym_dev, void *stream);
-/* Prior-initialised order-0 segments (container version 2; not in the
- * reference, which starts every model from 256 ones): the frame's prior
- * f[s] = 1 + floor(hist[s] * 8192 / n) (256 uint16 in prior_dev, 8-byte
- * aligned; hist_dev = 256 uint32 of scratch) seeds every segment's model,
- * which then adapts by CBAAC.py:32-36.  Each segment's bytes equal
- * vcf_cbaac_encode_prior of that segment alone. */
+/* Prior-seeded segments, orders 0 and 1 (container version 2; not in the
+ * reference, which starts every model from 256 ones): the frame's order-0
+ * prior f[s] = 1 + floor(hist[s] * 8192 / n) (256 uint16 in prior_dev,
+ * 8-byte aligned; hist_dev = 256 uint32 of scratch) seeds every model of
+ * every segment (order 1: all 256 contexts), which then adapts by
+ * CBAAC.py:32-36.  Each segment's bytes equal vcf_cbaac_encode_prior of that
+ * segment alone. */
 int vcf_cbaac_tiled_prior(const uint8_t *sym_dev, int64_t n, uint16_t *prior_dev, uint32_t *hist_dev, void *stream);
-int vcf_cbaac_tiled_encode_prior(const uint8_t *sym_dev, int64_t n, const uint16_t *prior_dev, int64_t seg_len,
-                                 uint8_t *out_dev, int64_t out_capacity, int64_t *seg_bytes_dev, void *ws_dev,
-                                 void *stream);
-int vcf_cbaac_tiled_decode_prior(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n,
+int vcf_cbaac_tiled_encode_prior(const uint8_t *sym_dev, int64_t n, int32_t order, const uint16_t *prior_dev,
+                                 int64_t seg_len, uint8_t *out_dev, int64_t out_capacity, int64_t *seg_bytes_dev,
+                                 void *ws_dev, void *stream);
+int vcf_cbaac_tiled_decode_prior(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
                                  const uint16_t *prior_dev, int64_t seg_len, uint8_t *sym_dev, void *stream);
-/* host, order 0: vcf_cbaac_encode / _decode with the model seeded by prior (256 uint16, each >= 1) */
-int vcf_cbaac_encode_prior(const uint8_t *symbols, int64_t n, const uint16_t *prior, uint8_t *out,
+/* host, orders 0 / 1: vcf_cbaac_encode / _decode with every model seeded by prior (256 uint16, each >= 1) */
+int vcf_cbaac_encode_prior(const uint8_t *symbols, int64_t n, int32_t order, const uint16_t *prior, uint8_t *out,
                            int64_t out_capacity, int64_t *out_bytes, int64_t *out_bits);
-int vcf_cbaac_decode_prior(const uint8_t *bytes, int64_t nbytes, int64_t n, const uint16_t *prior,
+int vcf_cbaac_decode_prior(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t order, const uint16_t *prior,
                            uint8_t *symbols_out);
 
 /* ---- CBAHC entropy codec (CBAHC.py), host code --------------------------------- */

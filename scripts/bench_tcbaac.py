@@ -79,7 +79,7 @@ def case(H, W, order, seg_len, reps=5):
                 host_serial_ms=round(host_ms, 2), round_trip=bool(np.array_equal(back, k.ravel())))
 
 
-def case_prior(H, W, seg_len, reps=5):
+def case_prior(H, W, seg_len, order=0, reps=5):
     """Container version 2 (order 0, models seeded by the frame's prior):
     rate vs the serial stream and GPU time per frame (prior + encode)."""
     from vcf_amd import _lib as L
@@ -87,7 +87,7 @@ def case_prior(H, W, seg_len, reps=5):
     from vcf_amd.device import DeviceBuffer
     k = frame_indices(H, W)
     n = k.size
-    coder = tcbaac.TiledCoder(0, seg_len, prior=True)
+    coder = tcbaac.TiledCoder(order, seg_len, prior=True)
     sizes, payload = coder.encode(k)
     lib = L.lib()
     sym = DeviceBuffer.from_array(k.ravel(), coder.stream)
@@ -98,20 +98,20 @@ def case_prior(H, W, seg_len, reps=5):
 
     def enc():
         L.call("vcf_cbaac_tiled_prior", sym.ptr, n, pr.ptr, hist.ptr, coder.stream.handle)
-        L.call("vcf_cbaac_tiled_encode_prior", sym.ptr, n, pr.ptr, seg_len, out.ptr, cap, sb.ptr, ws.ptr,
+        L.call("vcf_cbaac_tiled_encode_prior", sym.ptr, n, order, pr.ptr, seg_len, out.ptr, cap, sb.ptr, ws.ptr,
                coder.stream.handle)
     enc_ms = time_gpu(enc, coder.stream, reps)
     dec_out = DeviceBuffer(n)
     offs = DeviceBuffer.from_array(np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64), coder.stream)
     src = DeviceBuffer.from_array(np.frombuffer(payload, np.uint8), coder.stream)
     prd = DeviceBuffer.from_array(coder.last_prior, coder.stream)
-    dec_ms = time_gpu(lambda: L.call("vcf_cbaac_tiled_decode_prior", src.ptr, offs.ptr, n, prd.ptr, seg_len,
+    dec_ms = time_gpu(lambda: L.call("vcf_cbaac_tiled_decode_prior", src.ptr, offs.ptr, n, order, prd.ptr, seg_len,
                                      dec_out.ptr, coder.stream.handle), coder.stream, reps)
     back = np.empty(n, np.uint8)
     dec_out.download(back)
-    serial = cbaac.encode_symbols(k, 0)
+    serial = cbaac.encode_symbols(k, order)
     total = len(payload) + 512   # the prior table travels in the container
-    return dict(case="tcbaac_prior", frame=[H, W, 3], order=0, seg_len=seg_len, segments=len(sizes), symbols=n,
+    return dict(case="tcbaac_prior", frame=[H, W, 3], order=order, seg_len=seg_len, segments=len(sizes), symbols=n,
                 serial_bytes=len(serial), tiled_bytes=total, rate_overhead=round(total / len(serial) - 1, 4),
                 gpu_encode_ms=round(enc_ms, 3), gpu_decode_ms=round(dec_ms, 3),
                 round_trip=bool(np.array_equal(back, k.ravel())))
@@ -147,9 +147,11 @@ def main():
             print(json.dumps(r), flush=True)
         return
     if "--prior" in sys.argv:
-        for H, W in ((1080, 1920), (2160, 3840)):
-            for seg in (1 << 12, 1 << 13, 1 << 14, 1 << 15, 1 << 17):
-                print(json.dumps(case_prior(H, W, seg)), flush=True)
+        orders = (1,) if "--order1" in sys.argv else (0, 1)
+        for order in orders:
+            for H, W in ((1080, 1920), (2160, 3840)):
+                for seg in (1 << 12, 1 << 13, 1 << 14, 1 << 15, 1 << 17):
+                    print(json.dumps(case_prior(H, W, seg, order)), flush=True)
         return
     for H, W in ((1080, 1920), (2160, 3840)):
         for order in (0, 1):

@@ -67,6 +67,10 @@ def test_host_coder_with_prior():
     for i, s in enumerate(segs):
         part = sym[i * 4096:(i + 1) * 4096]
         assert np.array_equal(T.host_decode_prior(s, part.size, p), part)
+    assert T.host_segments_prior(sym, ones, 4096, 1) == T.host_segments(sym, 1, 4096)   # order 1, all contexts
+    for i, s in enumerate(T.host_segments_prior(sym, p, 4096, 1)):
+        part = sym[i * 4096:(i + 1) * 4096]
+        assert np.array_equal(T.host_decode_prior(s, part.size, p, 1), part)
 
 
 def test_prior_codec_is_registered():

@@ -108,19 +108,20 @@ def test_dct_codec_with_tcbaac_frame(tmp_path):
     assert np.array_equal(out, O.decode_frame(k, 1080, 1920, 32, 0))
 
 
+@pytest.mark.parametrize("order", [0, 1])
 @pytest.mark.parametrize("seg_len", [256, 4096, 32768])
-def test_prior_segments_equal_host_coder_and_round_trip(seg_len):
+def test_prior_segments_equal_host_coder_and_round_trip(order, seg_len):
     """Container version 2: the GPU prior equals the host formula; every
     segment's bytes equal vcf_cbaac_encode_prior of that segment; the GPU
     decoder inverts them."""
-    coder = T.TiledCoder(0, seg_len, prior=True)
+    coder = T.TiledCoder(order, seg_len, prior=True)
     for name, sym in _streams().items():
         if seg_len == 256 and sym.size > 50_000:
             sym = sym[:50_000 + 77]
         sizes, payload = coder.encode(sym)
         prior = T.prior_of(sym)
         assert np.array_equal(coder.last_prior, prior), name
-        host = T.host_segments_prior(sym, prior, seg_len)
+        host = T.host_segments_prior(sym, prior, seg_len, order)
         assert list(sizes) == [len(h) for h in host], name
         assert payload == b"".join(host), name
         assert np.array_equal(coder.decode(payload, sizes, sym.size, prior), sym), name
@@ -138,7 +139,7 @@ def test_prior_codec_on_dct_indices():
     fresh = T.TiledCBAACCodec(order=0, seg_len=8192).compress(k).getvalue()
     assert len(data) < 0.7 * len(fresh)
     with pytest.raises(NotImplementedError):
-        T.TiledCoder(1, 4096, prior=True)
+        T.TiledCoder(2, 4096, prior=True)
 
 
 def test_dct_codec_with_tcbaacp_frame(tmp_path):

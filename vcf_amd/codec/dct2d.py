@@ -57,12 +57,12 @@ def _tcbaac(args=None):
 
 def _tcbaac_prior(args=None):
     from ..tcbaac import PRIOR_SEG, TiledCBAACCodec
-    return TiledCBAACCodec(0, getattr(args, "segment_symbols", PRIOR_SEG) if args is not None else PRIOR_SEG,
-                           prior=True)
+    return TiledCBAACCodec(getattr(args, "order", 0) if args is not None else 0,
+                           getattr(args, "segment_symbols", PRIOR_SEG) if args is not None else PRIOR_SEG, prior=True)
 
 
 # TCBAAC: CBAAC in independent segments on the GPU (vcf_amd/tcbaac.py, a new container);
-# TCBAACP: the same with every segment's order-0 model seeded by the frame's prior (container version 2)
+# TCBAACP: the same with every segment's models seeded by the frame's order-0 prior (container version 2)
 ENTROPY_CODECS = {"TIFF": TIFFCodec, "CBAAC": _cbaac, "CBAHC": _cbahc, "TCBAAC": _tcbaac, "TCBAACP": _tcbaac_prior}
 
 

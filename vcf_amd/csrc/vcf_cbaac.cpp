@@ -175,7 +175,8 @@ static int cbaac_encode(const uint8_t *symbols, int64_t n, int32_t order, uint8_
     if ((n > 0 && !symbols) || !out || !out_bytes) return set_error(VCF_ERR_INVALID, "null buffer");
     try {
         Contexts ctx(order);
-        if (prior) ctx.get(0).init(prior);
+        if (prior)   // orders 0 / 1: every context's model (1 or 256, all created up front) from the prior
+            for (uint64_t c = 0; c < (order == 0 ? 1u : 256u); ++c) ctx.get(c).init(prior);
         BitWriter bw{out, out_capacity};
         uint32_t low = 0, high = 0xFFFFFFFFu;
         uint64_t pending = 0, key = 0;
@@ -228,14 +229,15 @@ int vcf_cbaac_encode(const uint8_t *symbols, int64_t n, int32_t order, uint8_t *
     return cbaac_encode(symbols, n, order, out, out_capacity, out_bytes, out_bits, nullptr);
 }
 
-// order 0 from the tiled container's prior frequencies (vcf_cbaac_gpu.hip)
-int vcf_cbaac_encode_prior(const uint8_t *symbols, int64_t n, const uint16_t *prior, uint8_t *out,
+// orders 0 / 1 from the tiled container's prior frequencies (vcf_cbaac_gpu.hip)
+int vcf_cbaac_encode_prior(const uint8_t *symbols, int64_t n, int32_t order, const uint16_t *prior, uint8_t *out,
                            int64_t out_capacity, int64_t *out_bytes, int64_t *out_bits)
 {
     if (!prior) return set_error(VCF_ERR_INVALID, "null prior");
+    if (order < 0 || order > 1) return set_error(VCF_ERR_UNSUPPORTED, "prior-seeded models: orders 0 and 1");
     for (int i = 0; i < kSymbols; ++i)
         if (prior[i] == 0) return set_error(VCF_ERR_INVALID, "prior frequency 0 (symbol %d)", i);
-    return cbaac_encode(symbols, n, 0, out, out_capacity, out_bytes, out_bits, prior);
+    return cbaac_encode(symbols, n, order, out, out_capacity, out_bytes, out_bits, prior);
 }
 
 static int cbaac_decode(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t order, uint8_t *symbols_out,
@@ -245,7 +247,8 @@ static int cbaac_decode(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t
     if ((n > 0 && !symbols_out) || (nbytes > 0 && !bytes)) return set_error(VCF_ERR_INVALID, "null buffer");
     try {
         Contexts ctx(order);
-        if (prior) ctx.get(0).init(prior);
+        if (prior)   // orders 0 / 1: every context's model (1 or 256, all created up front) from the prior
+            for (uint64_t c = 0; c < (order == 0 ? 1u : 256u); ++c) ctx.get(c).init(prior);
         BitReader br{bytes, nbytes * 8};
         uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
         for (int k = 0; k < 32; ++k) value = (value << 1) | (uint32_t)br.get();
@@ -292,13 +295,14 @@ int vcf_cbaac_decode(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t or
     return cbaac_decode(bytes, nbytes, n, order, symbols_out, nullptr);
 }
 
-int vcf_cbaac_decode_prior(const uint8_t *bytes, int64_t nbytes, int64_t n, const uint16_t *prior,
+int vcf_cbaac_decode_prior(const uint8_t *bytes, int64_t nbytes, int64_t n, int32_t order, const uint16_t *prior,
                            uint8_t *symbols_out)
 {
     if (!prior) return set_error(VCF_ERR_INVALID, "null prior");
+    if (order < 0 || order > 1) return set_error(VCF_ERR_UNSUPPORTED, "prior-seeded models: orders 0 and 1");
     for (int i = 0; i < kSymbols; ++i)
         if (prior[i] == 0) return set_error(VCF_ERR_INVALID, "prior frequency 0 (symbol %d)", i);
-    return cbaac_decode(bytes, nbytes, n, 0, symbols_out, prior);
+    return cbaac_decode(bytes, nbytes, n, order, symbols_out, prior);
 }
 
 // The model alone, for parity tests: (low, high, total) handed to the coder

@@ -68,7 +68,7 @@ __device__ __forceinline__ void model_reset(Model &m, uint32_t lane)
     m.total = 256;
 }
 
-// Prior-initialised model (order 0, the `.tadpt_arith` version-2 container):
+// Prior-initialised models (orders 0 and 1, the `.tadpt_arith` version-2 container):
 // every segment starts from the frame's prior frequencies f[s] = 1 +
 // floor(hist[s] * kPriorScale / n) instead of 256 ones, then adapts by the
 // reference's rules (CBAAC.py:32-36).  Short segments then stop paying the
@@ -176,6 +176,16 @@ __device__ __forceinline__ void tables_reset(Tables &t, uint32_t lane)
     model_reset(m, lane);
     for (uint32_t r = 0; r < 256; ++r) t.c[r * 64 + lane] = make_uint2(m.p0, m.p1);
     for (uint32_t r = lane; r < 256; r += 64) t.total[r] = 256;
+    __syncthreads();
+}
+
+// order 1 with a prior: every context's model starts from the frame's order-0 prior
+__device__ __forceinline__ void tables_reset_prior(Tables &t, const uint16_t *__restrict__ prior, uint32_t lane)
+{
+    Model m;
+    model_reset_prior(m, prior, lane);
+    for (uint32_t r = 0; r < 256; ++r) t.c[r * 64 + lane] = make_uint2(m.p0, m.p1);
+    for (uint32_t r = lane; r < 256; r += 64) t.total[r] = m.total;
     __syncthreads();
 }
 
@@ -322,9 +332,12 @@ __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *_
     const uint8_t *src = sym + start;
 
     Model m;
-    if (ORDER == 0 && prior) model_reset_prior(m, prior, lane);
+    if (prior) model_reset_prior(m, prior, lane);
     else model_reset(m, lane);
-    if constexpr (ORDER == 1) tables_reset(tabs[0], lane);
+    if constexpr (ORDER == 1) {
+        if (prior) tables_reset_prior(tabs[0], prior, lane);
+        else tables_reset(tabs[0], lane);
+    }
     uint32_t ctx = 0;
 
     BitWriter w;
@@ -427,9 +440,12 @@ __global__ __launch_bounds__(64) void cbaac_tiled_decode_kernel(const uint8_t *_
     uint8_t *dst = out + start;
 
     Model m;
-    if (ORDER == 0 && prior) model_reset_prior(m, prior, lane);
+    if (prior) model_reset_prior(m, prior, lane);
     else model_reset(m, lane);
-    if constexpr (ORDER == 1) tables_reset(tabs[0], lane);
+    if constexpr (ORDER == 1) {
+        if (prior) tables_reset_prior(tabs[0], prior, lane);
+        else tables_reset(tabs[0], lane);
+    }
     uint32_t ctx = 0;
 
     BitReader br;
@@ -606,7 +622,6 @@ static int tiled_encode(const uint8_t *sym_dev, int64_t n, int32_t order, int64_
                         void *stream, const uint16_t *prior_dev = nullptr)
 {
     if (int s = check_args(n, order, seg_len)) return s;
-    if (prior_dev && order != 0) return set_error(VCF_ERR_UNSUPPORTED, "prior-initialised models: order 0 only");
     const int64_t ns = vcf_cbaac_tiled_segments(n, seg_len);
     if (!seg_bytes_dev) return set_error(VCF_ERR_INVALID, "null seg_bytes");
     hipStream_t st = (hipStream_t)stream;
@@ -620,10 +635,10 @@ static int tiled_encode(const uint8_t *sym_dev, int64_t n, int32_t order, int64_
     const dim3 grid((unsigned)ns);
     if (trace_dev) {
         if (order == 0) cbaac_tiled_encode_kernel<0, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev, prior_dev);
-        else cbaac_tiled_encode_kernel<1, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev, nullptr);
+        else cbaac_tiled_encode_kernel<1, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev, prior_dev);
     } else {
         if (order == 0) cbaac_tiled_encode_kernel<0, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr, prior_dev);
-        else cbaac_tiled_encode_kernel<1, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr, nullptr);
+        else cbaac_tiled_encode_kernel<1, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr, prior_dev);
     }
     if (int s = hip_check(hipGetLastError(), "cbaac_tiled_encode_kernel")) return s;
     cbaac_tiled_scan_kernel<<<1, 1024, 0, st>>>(bits, ns, offs, seg_bytes_dev);
@@ -654,7 +669,6 @@ static int tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, i
                         int64_t seg_len, uint8_t *sym_dev, void *stream, const uint16_t *prior_dev)
 {
     if (int s = check_args(n, order, seg_len)) return s;
-    if (prior_dev && order != 0) return set_error(VCF_ERR_UNSUPPORTED, "prior-initialised models: order 0 only");
     const int64_t ns = vcf_cbaac_tiled_segments(n, seg_len);
     if (ns == 0) return VCF_OK;
     if (!in_dev || !seg_offsets_dev || !sym_dev) return set_error(VCF_ERR_INVALID, "null buffer");
@@ -662,7 +676,7 @@ static int tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, i
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((unsigned)ns);
     if (order == 0) cbaac_tiled_decode_kernel<0><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev, prior_dev);
-    else cbaac_tiled_decode_kernel<1><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev, nullptr);
+    else cbaac_tiled_decode_kernel<1><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev, prior_dev);
     return hip_check(hipGetLastError(), "cbaac_tiled_decode_kernel");
 }
 
@@ -687,21 +701,21 @@ int vcf_cbaac_tiled_prior(const uint8_t *sym_dev, int64_t n, uint16_t *prior_dev
     return hip_check(hipGetLastError(), "cbaac_prior_kernel");
 }
 
-int vcf_cbaac_tiled_encode_prior(const uint8_t *sym_dev, int64_t n, const uint16_t *prior_dev, int64_t seg_len,
-                                 uint8_t *out_dev, int64_t out_capacity, int64_t *seg_bytes_dev, void *ws_dev,
-                                 void *stream)
+int vcf_cbaac_tiled_encode_prior(const uint8_t *sym_dev, int64_t n, int32_t order, const uint16_t *prior_dev,
+                                 int64_t seg_len, uint8_t *out_dev, int64_t out_capacity, int64_t *seg_bytes_dev,
+                                 void *ws_dev, void *stream)
 {
     if (out_capacity < 0) return set_error(VCF_ERR_INVALID, "negative capacity");
     if (n > 0 && (!out_dev || !prior_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
-    return tiled_encode(sym_dev, n, 0, seg_len, out_dev, out_capacity, seg_bytes_dev, nullptr, ws_dev, stream,
+    return tiled_encode(sym_dev, n, order, seg_len, out_dev, out_capacity, seg_bytes_dev, nullptr, ws_dev, stream,
                         prior_dev);
 }
 
-int vcf_cbaac_tiled_decode_prior(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n,
+int vcf_cbaac_tiled_decode_prior(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
                                  const uint16_t *prior_dev, int64_t seg_len, uint8_t *sym_dev, void *stream)
 {
     if (n > 0 && !prior_dev) return set_error(VCF_ERR_INVALID, "null prior");
-    return tiled_decode(in_dev, seg_offsets_dev, n, 0, seg_len, sym_dev, stream, prior_dev);
+    return tiled_decode(in_dev, seg_offsets_dev, n, order, seg_len, sym_dev, stream, prior_dev);
 }
 
 }  // extern "C"

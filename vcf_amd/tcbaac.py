@@ -17,10 +17,10 @@ no segment index):
     b"VCFT", uint32 version = 1, uint32 order, uint32 seg_len,
     uint32 n_segments, uint32 segment_bytes[n_segments]
     the segments' bit streams, back to back (each MSB-first, zero padded)
-Version 2 (`prior=True`, order 0 only; not in the reference) adds, after
+Version 2 (`prior=True`, orders 0 and 1; not in the reference) adds, after
 n_segments, 256 uint16 prior frequencies f[s] = 1 + floor(hist[s] * 8192 / n)
-of the frame's symbols, before the segment sizes: every segment's model starts
-from them instead of 256 ones and adapts by the reference's rules, so short
+of the frame's symbols, before the segment sizes: every model of every
+segment (order 1: all 256 contexts) starts from them instead of 256 ones and adapts by the reference's rules, so short
 segments (many waves per frame) stop paying the model's learning cost.
 decompress() of a malformed header returns zeros((10, 10)) like
 CBAAC.py:101-102.
@@ -67,8 +67,8 @@ class TiledCoder:
     def __init__(self, order: int = 0, seg_len: int = DEFAULT_SEG, stream: Stream | None = None,
                  prior: bool = False):
         self.order, self.seg_len, self.prior = int(order), int(seg_len), bool(prior)
-        if self.prior and self.order != 0:
-            raise NotImplementedError("prior-initialised tiled CBAAC: order 0 only")
+        if self.prior and self.order > 1:
+            raise NotImplementedError("prior-seeded tiled CBAAC: orders 0 and 1")
         self.stream = stream if stream is not None else Stream()
         self.scratch = _Scratch()
         self.last_prior = None     # the prior table of the last encode (prior=True)
@@ -85,8 +85,8 @@ class TiledCoder:
         if self.prior:
             pr, hist = self.scratch.get("prior", 512), self.scratch.get("hist", 1024)
             L.call("vcf_cbaac_tiled_prior", sym.address(offset), int(n), pr.ptr, hist.ptr, self.stream.handle)
-            L.call("vcf_cbaac_tiled_encode_prior", sym.address(offset), int(n), pr.ptr, self.seg_len, out.ptr, cap,
-                   sb.ptr, ws.ptr, self.stream.handle)
+            L.call("vcf_cbaac_tiled_encode_prior", sym.address(offset), int(n), self.order, pr.ptr, self.seg_len,
+                   out.ptr, cap, sb.ptr, ws.ptr, self.stream.handle)
             self.last_prior = np.empty(256, np.uint16)
             pr.download(self.last_prior, self.stream)
         else:
@@ -144,8 +144,8 @@ class TiledCoder:
             prior = check_prior(prior)
             pr = self.scratch.get("prior_in", 512)
             pr.upload(prior, self.stream)
-            L.call("vcf_cbaac_tiled_decode_prior", src.ptr, ob.ptr, int(n), pr.ptr, self.seg_len, out.ptr,
-                   self.stream.handle)
+            L.call("vcf_cbaac_tiled_decode_prior", src.ptr, ob.ptr, int(n), self.order, pr.ptr, self.seg_len,
+                   out.ptr, self.stream.handle)
         else:
             L.call("vcf_cbaac_tiled_decode", src.ptr, ob.ptr, int(n), self.order, self.seg_len, out.ptr,
                    self.stream.handle)
@@ -195,7 +195,7 @@ def _parse(data: bytes):
     if data[p:p + 4] != MAGIC:
         raise ValueError("not a tiled CBAAC stream")
     version, order, seg_len, ns = struct.unpack_from("<IIII", data, p + 4)
-    if version not in (VERSION, VERSION_PRIOR) or (version == VERSION_PRIOR and order != 0):
+    if version not in (VERSION, VERSION_PRIOR) or (version == VERSION_PRIOR and order > 1):
         raise ValueError(f"version {version}")
     p += 20
     prior = None
@@ -280,7 +280,7 @@ def prior_of(sym: np.ndarray) -> np.ndarray:
     return (1 + hist * 8192 // n).astype(np.uint16)
 
 
-def host_segments_prior(sym: np.ndarray, prior, seg_len: int = DEFAULT_SEG):
+def host_segments_prior(sym: np.ndarray, prior, seg_len: int = DEFAULT_SEG, order: int = 0):
     """vcf_cbaac_encode_prior on every segment: what each segment of a
     version-2 stream must equal."""
     import ctypes
@@ -293,16 +293,16 @@ def host_segments_prior(sym: np.ndarray, prior, seg_len: int = DEFAULT_SEG):
         cap = int(lib.vcf_cbaac_bound(seg.size))
         out = np.empty(cap, np.uint8)
         nb, bits = ctypes.c_int64(), ctypes.c_int64()
-        L.call("vcf_cbaac_encode_prior", seg.ctypes.data, seg.size, prior.ctypes.data, out.ctypes.data, cap,
+        L.call("vcf_cbaac_encode_prior", seg.ctypes.data, seg.size, order, prior.ctypes.data, out.ctypes.data, cap,
                ctypes.byref(nb), ctypes.byref(bits))
         res.append(out[:nb.value].tobytes())
     return res
 
 
-def host_decode_prior(data: bytes, n: int, prior) -> np.ndarray:
+def host_decode_prior(data: bytes, n: int, prior, order: int = 0) -> np.ndarray:
     prior = check_prior(prior)
     out = np.empty(n, np.uint8)
     buf = np.frombuffer(data, np.uint8)
-    L.call("vcf_cbaac_decode_prior", buf.ctypes.data if buf.size else None, buf.size, n, prior.ctypes.data,
+    L.call("vcf_cbaac_decode_prior", buf.ctypes.data if buf.size else None, buf.size, n, order, prior.ctypes.data,
            out.ctypes.data)
     return out
