@@ -147,7 +147,7 @@ def main():
             print(json.dumps(r), flush=True)
         return
     if "--prior" in sys.argv:
-        orders = (1,) if "--order1" in sys.argv else (0, 1)
+        orders = (1,) if "--order1" in sys.argv else (0,) if "--order0" in sys.argv else (0, 1)
         for order in orders:
             for H, W in ((1080, 1920), (2160, 3840)):
                 for seg in (1 << 12, 1 << 13, 1 << 14, 1 << 15, 1 << 17):
