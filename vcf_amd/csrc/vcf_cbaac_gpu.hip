@@ -36,6 +36,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 
 #include "vcf_amd.h"
 #include "vcf_internal.h"
@@ -690,6 +691,7 @@ int vcf_cbaac_tiled_prior(const uint8_t *sym_dev, int64_t n, uint16_t *prior_dev
 {
     if (n < 0) return set_error(VCF_ERR_INVALID, "negative symbol count");
     if (!prior_dev || !hist_dev || (n > 0 && !sym_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
+    if (reinterpret_cast<uintptr_t>(prior_dev) & 7) return set_error(VCF_ERR_INVALID, "prior_dev not 8-byte aligned");
     hipStream_t st = (hipStream_t)stream;
     if (int s = hip_check(hipMemsetAsync(hist_dev, 0, 256 * sizeof(uint32_t), st), "hipMemsetAsync")) return s;
     if (n > 0) {
@@ -707,6 +709,7 @@ int vcf_cbaac_tiled_encode_prior(const uint8_t *sym_dev, int64_t n, int32_t orde
 {
     if (out_capacity < 0) return set_error(VCF_ERR_INVALID, "negative capacity");
     if (n > 0 && (!out_dev || !prior_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
+    if (reinterpret_cast<uintptr_t>(prior_dev) & 7) return set_error(VCF_ERR_INVALID, "prior_dev not 8-byte aligned");
     return tiled_encode(sym_dev, n, order, seg_len, out_dev, out_capacity, seg_bytes_dev, nullptr, ws_dev, stream,
                         prior_dev);
 }
@@ -715,6 +718,7 @@ int vcf_cbaac_tiled_decode_prior(const uint8_t *in_dev, const int64_t *seg_offse
                                  const uint16_t *prior_dev, int64_t seg_len, uint8_t *sym_dev, void *stream)
 {
     if (n > 0 && !prior_dev) return set_error(VCF_ERR_INVALID, "null prior");
+    if (reinterpret_cast<uintptr_t>(prior_dev) & 7) return set_error(VCF_ERR_INVALID, "prior_dev not 8-byte aligned");
     return tiled_decode(in_dev, seg_offsets_dev, n, order, seg_len, sym_dev, stream, prior_dev);
 }
 
