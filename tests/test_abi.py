@@ -127,3 +127,17 @@ def test_perceptual_tables_match_the_oracle():
     y4, _ = O.perceptual_tables(4)
     assert y4[0, 0] == 13   # (16 + 11 + 12 + 12) / 4 = 12.75, rounded
     assert lib.vcf_dct_perceptual_tables(0, y.ctypes.data, c.ctypes.data) == L.VCF_ERR_INVALID
+
+
+def test_product_path_fails_loudly_without_the_library(tmp_path):
+    """No CPU fallback: with the HIP library absent, the codec raises instead of computing."""
+    import subprocess
+    import sys
+    code = ("import numpy as np, vcf_amd.dct as D\n"
+            "try:\n    D.encode(np.zeros((8, 8, 3), np.uint8), 32)\n"
+            "except ImportError as e:\n    print('raised', e)\n")
+    env = dict(os.environ, VCF_AMD_LIB=str(tmp_path / "absent.so"))
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert p.returncode == 0, p.stderr[-1500:]
+    assert p.stdout.startswith("raised") and "no CPU fallback" in p.stdout
