@@ -117,6 +117,24 @@ def case_prior(H, W, seg_len, order=0, reps=5):
                 round_trip=bool(np.array_equal(back, k.ravel())))
 
 
+def frames_throughput(H, W, n_frames=16, seg_len=1 << 15, streams=8, reps=3):
+    """n_frames frames' indices resident in HBM, each its own prior-seeded
+    tiled stream, coded concurrently on `streams` library streams."""
+    from vcf_amd import tcbaac
+    from vcf_amd.device import DeviceBuffer
+    k = frame_indices(H, W).ravel()
+    n = k.size
+    buf = DeviceBuffer.from_array(np.tile(k, n_frames))
+    tcbaac.encode_frames_device(buf, n_frames, n, 0, seg_len, prior=True, streams=streams)   # warm
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = tcbaac.encode_frames_device(buf, n_frames, n, 0, seg_len, prior=True, streams=streams)
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    return dict(case="tcbaac_prior_frames", frame=[H, W, 3], frames=n_frames, seg_len=seg_len, streams=streams,
+                ms_per_batch=round(ms, 2), ms_per_frame=round(ms / n_frames, 3),
+                Mpix_s=round(n_frames * H * W / ms / 1e3, 1), bytes_per_frame=len(res[0][1]) + 512)
+
+
 def c2_end_to_end(reps=5):
     from PIL import Image
 
@@ -142,6 +160,11 @@ def c2_end_to_end(reps=5):
 def main():
     from vcf_amd.device import set_device
     set_device(0)
+    if "--frames" in sys.argv:
+        for H, W in ((1080, 1920), (2160, 3840)):
+            for seg, st in ((1 << 15, 1), (1 << 15, 8), (1 << 14, 8)):
+                print(json.dumps(frames_throughput(H, W, 16, seg, st)), flush=True)
+        return
     if "--c2" in sys.argv:
         for r in c2_end_to_end():
             print(json.dumps(r), flush=True)

@@ -165,3 +165,23 @@ def test_dct_codec_with_tcbaacp_frame(tmp_path):
                                                                          str(tmp_path / "out.png"))
     out = np.asarray(Image.open(str(tmp_path / "out.png")))
     assert np.array_equal(out, O.decode_frame(k, 1080, 1920, 32, 0))
+
+
+@pytest.mark.parametrize("prior", [False, True])
+def test_frames_on_several_streams_equal_one_by_one(prior):
+    """encode_frames_device: frames coded concurrently on library streams give
+    each frame's stream exactly as coding it alone."""
+    from vcf_amd.device import DeviceBuffer
+    rng = np.random.Generator(np.random.PCG64(9))
+    n, F = 70_000, 5
+    frames = [np.where(rng.random(n) < 0.95 - 0.1 * f, 128, rng.integers(0, 256, n)).astype(np.uint8)
+              for f in range(F)]
+    buf = DeviceBuffer.from_array(np.concatenate(frames))
+    got = T.encode_frames_device(buf, F, n, 0, 8192, prior=prior, streams=3)
+    for f in range(F):
+        c = T.TiledCoder(0, 8192, prior=prior)
+        sizes, payload = c.encode(frames[f])
+        assert list(got[f][0]) == list(sizes) and got[f][1] == payload, f
+        if prior:
+            assert np.array_equal(got[f][2], T.prior_of(frames[f]))
+            assert np.array_equal(c.decode(payload, sizes, n, got[f][2]), frames[f])

@@ -169,6 +169,56 @@ def check_prior(prior) -> np.ndarray:
     return prior
 
 
+def encode_frames_device(sym: DeviceBuffer, n_frames: int, frame_symbols: int, order: int = 0,
+                         seg_len: int = DEFAULT_SEG, prior: bool = False, streams: int = 4):
+    """Several frames' symbols, back to back in HBM, each coded as its own
+    tiled stream (its own prior with prior=True).  One frame's segments fill
+    only a few hundred waves, so the frames go out round robin on `streams`
+    library streams and run concurrently; every launch is issued before the
+    first download.  -> [(segment byte counts, payload, prior or None)]."""
+    lib = L.lib()
+    n = int(frame_symbols)
+    ns = n_segments(n, seg_len)
+    ss = [Stream() for _ in range(max(1, min(int(streams), n_frames)))]
+    cap = int(lib.vcf_cbaac_tiled_bound(n, seg_len))
+    wsb = int(lib.vcf_cbaac_tiled_workspace(n, seg_len))
+    # every buffer first: an allocation can wait for the device, which would
+    # serialise the launches below
+    bufs = [(DeviceBuffer(max(cap, 1)), DeviceBuffer(8 * (ns + 1)), DeviceBuffer(max(wsb, 1)),
+             DeviceBuffer(512) if prior else None, DeviceBuffer(1024) if prior else None) for _ in range(n_frames)]
+    jobs = []
+    for f in range(n_frames):
+        st = ss[f % len(ss)]
+        out, sb, ws, pr, hist = bufs[f]
+        addr = sym.address(f * n)
+        if prior:
+            L.call("vcf_cbaac_tiled_prior", addr, n, pr.ptr, hist.ptr, st.handle)
+            L.call("vcf_cbaac_tiled_encode_prior", addr, n, int(order), pr.ptr, int(seg_len), out.ptr, cap, sb.ptr,
+                   ws.ptr, st.handle)
+            jobs.append((st, out, sb, ws, pr, hist))
+        else:
+            L.call("vcf_cbaac_tiled_encode", addr, n, int(order), int(seg_len), out.ptr, cap, sb.ptr, ws.ptr,
+                   st.handle)
+            jobs.append((st, out, sb, ws, None, None))
+    res = []
+    for st, out, sb, ws, pr, hist in jobs:
+        sizes = np.empty(ns + 1, np.int64)
+        sb.download(sizes, st)
+        p = None
+        if pr is not None:
+            p = np.empty(256, np.uint16)
+            pr.download(p, st)
+        st.synchronize()
+        payload = np.empty(int(sizes[-1]), np.uint8)
+        if payload.size:
+            out.download(payload, st)
+            st.synchronize()
+        res.append((sizes[:-1].copy(), payload.tobytes(), p))
+    for st in ss:
+        st.synchronize()
+    return res
+
+
 def pack(shape, order: int, seg_len: int, seg_bytes, payload: bytes, prior=None) -> bytes:
     seg_bytes = np.asarray(seg_bytes, np.int64)
     head = np.array([len(shape), *shape], np.uint32).tobytes()
