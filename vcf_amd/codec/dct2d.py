@@ -76,7 +76,7 @@ def make_entropy(args):
     if ec_name not in ENTROPY_CODECS:
         raise NotImplementedError(f"entropy codec {ec_name!r} (have: {sorted(ENTROPY_CODECS)})")
     maker = ENTROPY_CODECS[ec_name]
-    return maker(args) if maker in (_cbaac, _cbahc, _tcbaac) else maker()
+    return maker(args) if maker in (_cbaac, _cbahc, _tcbaac, _tcbaac_prior) else maker()
 
 
 def make_quantizer(args):
