@@ -213,6 +213,106 @@ def cpu_baseline(frame: np.ndarray, Q: int, budget_s: float):
     return out, k_c
 
 
+def c4_frame(bases, i: int) -> np.ndarray:
+    """Frame i of the C4 sequence: one of four S-smooth 1080p frames, shifted
+    by a frame-dependent constant (u8 wrap), so every frame's code-stream
+    differs and any rank can regenerate any frame cheaply."""
+    return bases[i % len(bases)] + np.uint8((i // len(bases)) * 7 % 256)
+
+
+def c4_block(args, world: int, rank: int, group):
+    """Config C4 of BASELINE.json: III over a 256-frame 1080p sequence,
+    frame-sharded across the ranks, end to end on the GPU with the exchange
+    (vcf_amd/codec/iii_device.py): DCT+deadzone, the GPU entropy stage
+    (-c TCBAACP), per-frame sizes all-gathered and the code-streams gathered
+    to rank 0 over RCCL (device to device).  Timed like the headline:
+    barrier + device sync on both sides, max over ranks.  Rank 0 checks what
+    it gathered: every frame's container equals that frame coded on its own
+    (TiledCBAACCodec.compress_device of the DCT indices) -- all frames when
+    P > 1 (rank 0 re-codes the other ranks' frames), and at P = 1 the
+    gathered bytes equal the coder's own output, and two frames decode back
+    to their indices.  Returns (block dict, error or None); never raises."""
+    from vcf_amd import tcbaac as T
+    from vcf_amd.codec.iii_device import DeviceIII
+    from vcf_amd.codec.shard import frame_range
+    from vcf_amd.comm import HostGroup
+    from vcf_amd.device import DeviceBuffer, synchronize
+    from vcf_amd.rccl import Communicator
+    N, H, W, Q = args.c4_frames, 1080, 1920, args.QSS
+    lo, hi = frame_range(N, rank, world)
+    info = {"workload": (f"III C4: {N} x 1080p frames, DCT+deadzone Q={Q} + GPU entropy (-c TCBAACP, "
+                         f"{T.PRIOR_SEG}-symbol segments), frame i on rank floor(i*P/N), sizes all-gather + "
+                         f"code-stream gatherv to rank 0 over RCCL (device to device), rank 0 copies them to host"),
+            "frames": N, "frame": [H, W, 3], "n_ranks": world, "frames_this_rank0": hi - lo if rank == 0 else None}
+    err, comm, t_rank = None, None, float("nan")
+    try:
+        bases = [synth_frame(H, W, seed=100 + s) for s in range(4)]
+        rgb = DeviceBuffer(max((hi - lo) * H * W * 3, 1))
+        for j, i in enumerate(range(lo, hi)):
+            rgb.upload(c4_frame(bases, i), offset=j * H * W * 3)
+        comm = Communicator(group if world > 1 else HostGroup(0, 1), timeout_s=args.c4_timeout)
+        info["backend"] = "rccl" if world > 1 else "rccl (single rank: the root's device copy)"
+        job = DeviceIII(comm, rank, world, N, H, W, Q)
+        for _ in range(args.c4_warmup):
+            job.run(rgb)
+        group.barrier()
+        synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.c4_steps):
+            sizes, got = job.run(rgb)
+        synchronize()
+        t_rank = (time.perf_counter() - t0) / args.c4_steps
+        stages = {}
+        job.run(rgb, stages)
+        info["stages_ms_rank0"] = {k: round(v * 1e3, 3) for k, v in stages.items()} if rank == 0 else None
+        if rank == 0:
+            info["code_bytes"] = int(sizes.sum())
+            info["bits_per_symbol"] = round(8 * int(sizes.sum()) / (N * job.n_sym), 5)
+            info["verified"] = c4_verify(got, bases, job, N, H, W, Q, world)
+    except Exception as e:   # reported in the block; the headline line still prints
+        err = f"{type(e).__name__}: {e}"
+    finally:
+        if comm is not None:
+            try:
+                comm.close()
+            except Exception:
+                pass
+    times = group.all_gather_f64(t_rank) if world > 1 else [t_rank]
+    if err is None and all(np.isfinite(times)):
+        tmax = max(times)
+        info.update(ms=round(tmax * 1e3, 3), steps=args.c4_steps, warmup=args.c4_warmup,
+                    value=round(N * H * W / tmax / 1e6, 1), unit="Mpixels/s",
+                    frames_per_s=round(N / tmax, 1))
+    else:
+        info["error"] = err or "another rank failed"
+    return info
+
+
+def c4_verify(got, bases, job, N, H, W, Q, world) -> str:
+    """Rank 0: the gathered containers against per-frame coding on this GPU."""
+    from vcf_amd import dct as D
+    from vcf_amd import tcbaac as T
+    from vcf_amd.device import DeviceBuffer
+    codec = T.TiledCBAACCodec(order=0, seg_len=T.PRIOR_SEG, prior=True)
+    frames = range(N) if world > 1 else sorted({0, N // 2, N - 1})
+    Hp, Wp = D.padded_shape(H, W)
+    for i in frames:
+        rgb = c4_frame(bases, i)
+        din = DeviceBuffer.from_array(rgb)
+        k = DeviceBuffer(Hp * Wp * 3)
+        D.encode_device(din, 1, H, W, Q, 0, out=k, stream=codec.coder.stream)
+        want = codec.compress_device(k, (Hp, Wp, 3)).getvalue()
+        if got[i] != want:
+            return f"MISMATCH at frame {i}"
+        if i in (0, N - 1):
+            kh = np.empty((Hp, Wp, 3), np.uint8)
+            k.download(kh)
+            if not np.array_equal(codec.decompress(got[i]), kh):
+                return f"decode MISMATCH at frame {i}"
+    what = "every frame" if world > 1 else f"frames {list(frames)}"
+    return f"ok: {what} equal to the frame coded alone; frames 0 and {N - 1} decode to their indices"
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc pass (if it matches)."""
     p = os.path.join(ROOT, "profiles", "pmc_encode_4k.json")
@@ -242,6 +342,10 @@ def main():
                     help="seconds of CPU time for cpu_baseline (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0, help="encode kernel (0 = automatic)")
+    ap.add_argument("--c4-frames", type=int, default=256, help="frames of the C4 block (0 disables it)")
+    ap.add_argument("--c4-steps", type=int, default=2)
+    ap.add_argument("--c4-warmup", type=int, default=1)
+    ap.add_argument("--c4-timeout", type=float, default=90.0, help="seconds before an RCCL call is aborted")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -295,6 +399,10 @@ def main():
     pixels = group.allreduce_sum(float(args.steps * F * H * W))
     value = pixels / wall_max / 1e6
 
+    # C4 (III, 256 x 1080p, frame-sharded, with the RCCL exchange): after the
+    # headline's timed region, reported in its own block
+    c4 = c4_block(args, world, rank, group) if args.c4_frames > 0 else None
+
     # after the timed region (an idle GPU during seconds of CPU work would start
     # the timed steps at low clocks): parity spot check of the timed kernel's
     # output, frame 0 vs the C oracle, and the CPU baseline
@@ -342,6 +450,7 @@ def main():
                          "read_frac_of_peak": round(F * H * W * 3 / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "cpu_baseline": cpu,
             "parity": parity,
+            "c4_e2e_with_gather": c4,
         }
         print(json.dumps(out), flush=True)
     group.close()

@@ -47,6 +47,8 @@ extern "C" {
 #define VCF_ERR_INVALID (-1)     /* bad argument (reference: ValueError)   */
 #define VCF_ERR_HIP (-2)         /* HIP runtime failure                    */
 #define VCF_ERR_UNSUPPORTED (-3) /* option not implemented on this path    */
+#define VCF_ERR_TIMEOUT (-4)     /* a cross-rank exchange did not finish in time
+                                    (the communicator is aborted)          */
 
 /* element types of the stand-alone quantizer */
 #define VCF_DTYPE_F32 0
@@ -82,6 +84,8 @@ int vcf_event_create(void **event);
 int vcf_event_destroy(void *event);
 int vcf_event_record(void *event, void *stream);
 int vcf_event_sync(void *event);
+/* later work on `stream` waits for `event` (hipStreamWaitEvent) */
+int vcf_stream_wait_event(void *stream, void *event);
 int vcf_event_elapsed_ms(void *start, void *stop, float *ms);
 
 /* ---- DCT + deadzone path (2D-DCT.py, deadzone.py, YCoCg.py) ---------------- */
@@ -507,8 +511,18 @@ typedef struct vcf_comm *vcf_comm_t;
  * out of band (vcf_amd/comm.py: a TCP host group). */
 int vcf_comm_unique_id(uint8_t *id, size_t capacity);
 /* Collective over `world` processes, each with its device already set
- * (vcf_set_device). */
+ * (vcf_set_device).  The communicator is non-blocking (ncclConfig_t
+ * blocking = 0): initialisation and every enqueue below are polled against
+ * a deadline of timeout_ms (<= 0: VCF_COMM_TIMEOUT_MS from the environment,
+ * else 120000); past it the communicator is aborted (ncclCommAbort) and the
+ * call returns VCF_ERR_TIMEOUT instead of hanging.  vcf_comm_init =
+ * vcf_comm_init_timeout(..., 0). */
 int vcf_comm_init(vcf_comm_t *comm, const uint8_t *id, int rank, int world);
+int vcf_comm_init_timeout(vcf_comm_t *comm, const uint8_t *id, int rank, int world, int64_t timeout_ms);
+/* Wait until everything enqueued on `stream` has finished, within the
+ * communicator's timeout; past it (or on an asynchronous RCCL error) the
+ * communicator is aborted and VCF_ERR_TIMEOUT (VCF_ERR_HIP) returned. */
+int vcf_comm_wait(vcf_comm_t comm, void *stream);
 int vcf_comm_destroy(vcf_comm_t comm);
 int vcf_comm_rank(vcf_comm_t comm, int *rank, int *world);
 /* recv_dev[r * count + i] = rank r's send_dev[i] (ncclAllGather, int64). */

@@ -154,3 +154,48 @@ def test_bench_two_ranks_under_torchrun():
     assert len(lines) == 1, p.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 8 and line["value"] > 0
+
+
+def test_device_iii_single_rank_rccl():
+    """The C4 data path (vcf_amd/codec/iii_device.py) on one rank with a real
+    single-rank RCCL communicator: every gathered container equals the frame
+    coded on its own by the TCBAACP codec, and decodes to its indices."""
+    from oracle import oracle as O
+    from vcf_amd import tcbaac as T
+    from vcf_amd.codec.iii_device import DeviceIII
+    from vcf_amd.comm import HostGroup
+    from vcf_amd.device import DeviceBuffer, set_device
+    from vcf_amd.rccl import Communicator
+    set_device(0)
+    n, H, W = 7, 61, 77                      # n_sym % 4 != 0: unaligned frame starts too
+    frames = _frames(n, H, W, 31)
+    rgb = DeviceBuffer.from_array(np.stack(frames))
+    comm = Communicator(HostGroup(0, 1), timeout_s=60)
+    job = DeviceIII(comm, 0, 1, n, H, W, 32, seg_len=1024, streams=3)
+    stages = {}
+    sizes, got = job.run(rgb, stages)
+    assert set(stages) == {"dct_dz", "entropy", "pack", "sizes_allgather", "gatherv", "d2h_rank0"}
+    codec = T.TiledCBAACCodec(order=0, seg_len=1024, prior=True)
+    for i, f in enumerate(frames):
+        k = O.encode_frame(f, 32, 0)
+        want = codec.compress(k).getvalue()
+        assert got[i] == want and sizes[i] == len(want), i
+        assert np.array_equal(codec.decompress(got[i]), k), i
+    sizes2, got2 = job.run(rgb)                  # reusable: same bytes again
+    assert got2 == got and list(sizes2) == list(sizes)
+    comm.close()
+
+
+def test_bench_c4_block_small():
+    """bench.py's C4 block at a small frame count: it runs, times, and rank 0's
+    self-check passes."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--frames", "2", "--steps", "2",
+                        "--warmup", "1", "--settle-max-s", "0", "--no-cpu-baseline", "--c4-frames", "6"],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    c4 = json.loads(p.stdout.strip().splitlines()[-1])["c4_e2e_with_gather"]
+    assert "error" not in c4, c4
+    assert c4["value"] > 0 and c4["verified"].startswith("ok"), c4

@@ -21,7 +21,12 @@ def test_container_round_trip_and_layout():
 
 
 @pytest.mark.parametrize("bad", [b"\x01", b"", T.pack((4, 4), 0, 256, [3], b"abc")[:-1],
-                                 T.pack((4, 4), 0, 256, [3], b"abc").replace(b"VCFT", b"XXXX")])
+                                 T.pack((4, 4), 0, 256, [3], b"abc").replace(b"VCFT", b"XXXX"),
+                                 # version-1 headers the GPU coder cannot take: order > 1,
+                                 # a segment length that is not a positive multiple of 256
+                                 T.pack((4, 4), 2, 256, [3], b"abc"),
+                                 T.pack((4, 4), 0, 300, [3], b"abc"),
+                                 T.pack((4, 4), 0, 0, [3], b"abc")])
 def test_malformed_streams_decode_to_reference_zeros(bad):
     assert np.array_equal(T.TiledCBAACCodec().decompress(bad), np.zeros((10, 10), np.uint8))
 

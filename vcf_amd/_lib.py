@@ -16,6 +16,7 @@ VCF_OK = 0
 VCF_ERR_INVALID = -1
 VCF_ERR_HIP = -2
 VCF_ERR_UNSUPPORTED = -3
+VCF_ERR_TIMEOUT = -4
 
 VCF_DTYPE_F32 = 0
 VCF_DTYPE_F64 = 1
@@ -42,6 +43,11 @@ class VCFInvalidArgument(VCFError, ValueError):
 
 class VCFUnsupported(VCFError, NotImplementedError):
     pass
+
+
+class VCFTimeout(VCFError, TimeoutError):
+    """VCF_ERR_TIMEOUT: a cross-rank exchange did not finish in time (the
+    RCCL communicator has been aborted)."""
 
 
 _P = ctypes.c_void_p
@@ -74,6 +80,7 @@ SIGNATURES = {
     "vcf_event_destroy": [_P],
     "vcf_event_record": [_P, _P],
     "vcf_event_sync": [_P],
+    "vcf_stream_wait_event": [_P, _P],
     "vcf_event_elapsed_ms": [_P, _P, ctypes.POINTER(ctypes.c_float)],
     "vcf_dct_padded_shape": [_I32, _I32, _I32, _PI32, _PI32],
     "vcf_dct_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
@@ -137,6 +144,8 @@ SIGNATURES = {
     "vcf_cbaac_decode_prior": [_P, _I64, _I64, _I32, _P, _P],
     "vcf_comm_unique_id": [_P, _SZ],
     "vcf_comm_init": [ctypes.POINTER(_P), _P, ctypes.c_int, ctypes.c_int],
+    "vcf_comm_init_timeout": [ctypes.POINTER(_P), _P, ctypes.c_int, ctypes.c_int, _I64],
+    "vcf_comm_wait": [_P, _P],
     "vcf_comm_destroy": [_P],
     "vcf_comm_rank": [_P, _PI, _PI],
     "vcf_comm_allgather_i64": [_P, _P, _I64, _P, _P],
@@ -190,6 +199,8 @@ def check(status: int) -> int:
         raise VCFInvalidArgument(status, msg)
     if status == VCF_ERR_UNSUPPORTED:
         raise VCFUnsupported(status, msg)
+    if status == VCF_ERR_TIMEOUT:
+        raise VCFTimeout(status, msg)
     raise VCFError(status, msg)
 
 

@@ -287,11 +287,12 @@ class CoDec(EICCoDec):
         H, W = img.shape[:2]
         Hp, Wp = D.padded_shape(H, W, self.block_size)
         coder = self.entropy.coder
-        src = DeviceBuffer.from_array(img, coder.stream)
-        k = DeviceBuffer(Hp * Wp * 3)
-        D.encode_device(src, 1, H, W, self.QSS, self.flags, out=k, stream=coder.stream,
-                        block_size=self.block_size)
-        return self.entropy.compress_device(k, (Hp, Wp, 3))
+        with coder.lock:     # the coder's stream is shared with other threads' calls
+            src = DeviceBuffer.from_array(img, coder.stream)
+            k = DeviceBuffer(Hp * Wp * 3)
+            D.encode_device(src, 1, H, W, self.QSS, self.flags, out=k, stream=coder.stream,
+                            block_size=self.block_size)
+            return self.entropy.compress_device(k, (Hp, Wp, 3))
 
     def encode(self, in_fn="/tmp/original.png", out_fn="/tmp/encoded"):
         # 2D-DCT.py:374-375: the reference's encode() ignores -o/-e

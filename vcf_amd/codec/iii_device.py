@@ -1,0 +1,140 @@
+"""III encode with every frame resident in HBM: config C4's data path.
+
+The reference's III loop (src/III.py:77-115) runs encode_fn frame after frame
+in one process: read PNG, 2D-DCT + deadzone (2D-DCT.py:276-361), entropy
+code, write /tmp/encoded_%04d.  Here a sequence of N frames is sharded over
+P ranks (frame i on rank floor(i*P/N), shard.frame_range) and each rank's
+chunk never leaves the GPU until its code-streams are final:
+
+  1. one launch of the fused DCT + deadzone kernel over the rank's chunk
+     (vcf_dct_dz_encode), indices stay in HBM;
+  2. the GPU entropy stage: every frame's indices coded as a prior-seeded
+     tiled CBAAC stream (`-c TCBAACP`, vcf_amd/tcbaac.py), frames
+     concurrent on library streams; only the small segment index comes to
+     the host;
+  3. every frame's container (header + segments, exactly the bytes
+     `TiledCBAACCodec.compress_device` returns for it) is assembled in a
+     device send buffer;
+  4. the exchange: per-frame container sizes all-gathered
+     (ncclAllGather), the containers gathered to rank 0 device to device
+     (vcf_comm_gatherv: one ncclSend per peer, P-1 receives on rank 0, each
+     over its own xGMI link), then one copy to rank 0's host.
+
+No PyTorch; RCCL through libvcf_amd.so (vcf_amd/rccl.py), bounded by its
+timeouts.  bench.py reports this as its C4 block next to the kernel
+headline.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from .. import dct as D
+from .. import tcbaac as T
+from ..device import DeviceBuffer, Stream, copy_dtod
+from .shard import frame_range
+
+
+class DeviceIII:
+    """One rank's part of a frame-sharded, HBM-resident III encode."""
+
+    def __init__(self, comm, rank: int, world: int, n_frames: int, H: int, W: int, Q: int = 32,
+                 seg_len: int = T.PRIOR_SEG, streams: int = 4):
+        self.comm, self.rank, self.world = comm, int(rank), int(world)
+        self.N, self.H, self.W, self.Q = int(n_frames), int(H), int(W), int(Q)
+        self.lo, self.hi = frame_range(self.N, self.rank, self.world)
+        self.n_local = self.hi - self.lo
+        self.Hp, self.Wp = D.padded_shape(self.H, self.W)
+        self.shape = (self.Hp, self.Wp, 3)
+        self.n_sym = self.Hp * self.Wp * 3
+        self.stream = Stream()
+        self.k = DeviceBuffer(max(self.n_local * self.n_sym, 1))
+        self.batch = T.FrameBatch(self.n_local, self.n_sym, 0, seg_len, prior=True, streams=streams)
+        self.send = None
+        self.recv = None
+        self.hstage = None
+
+    def _buf(self, name: str, nbytes: int) -> DeviceBuffer:
+        b = getattr(self, name)
+        if b is None or b.nbytes < nbytes:
+            b = DeviceBuffer(max(nbytes, 1))
+            setattr(self, name, b)
+        return b
+
+    def run(self, rgb: DeviceBuffer, stages: dict | None = None):
+        """Encode this rank's frames (rgb: n_local frames, H x W x 3 u8, back
+        to back) and gather every frame's container on rank 0.
+        -> (per-frame container sizes of all N frames, list of N container
+        bytes on rank 0 / None elsewhere).  With `stages`, each stage is
+        synchronised and its seconds are added under its name (diagnostic:
+        the syncs cost a little)."""
+        def mark(name, t0):
+            if stages is None:
+                return t0
+            self.stream.synchronize()
+            t1 = time.perf_counter()
+            stages[name] = stages.get(name, 0.0) + (t1 - t0)
+            return t1
+
+        t = time.perf_counter()
+        if self.n_local:
+            D.encode_device(rgb, self.n_local, self.H, self.W, self.Q, 0, out=self.k, stream=self.stream)
+        t = mark("dct_dz", t)
+        if self.n_local:
+            self.batch.launch(self.k, after=self.stream)
+        seg, totals, priors = self.batch.sizes()          # waits for the coder
+        t = mark("entropy", t)
+        headers = [self.batch.header(f, self.shape) for f in range(self.n_local)]
+        local_sizes = np.array([len(h) + int(totals[f]) for f, h in enumerate(headers)], np.int64)
+        nbytes = int(local_sizes.sum())
+        send = self._buf("send", nbytes)
+        if self.n_local:
+            hb = np.frombuffer(b"".join(headers), np.uint8)
+            hst = self._buf("hstage", hb.size)
+            hst.upload(hb, self.stream)
+            off = hoff = 0
+            for f, h in enumerate(headers):
+                copy_dtod(send, off, hst, hoff, len(h), self.stream)
+                copy_dtod(send, off + len(h), self.batch.out[f], 0, int(totals[f]), self.stream)
+                off += len(h) + int(totals[f])
+                hoff += len(h)
+        t = mark("pack", t)
+        sizes = self._all_gather_sizes(local_sizes)
+        t = mark("sizes_allgather", t)
+        counts = np.array([sizes[slice(*frame_range(self.N, r, self.world))].sum() for r in range(self.world)],
+                          np.int64)
+        total = int(counts.sum())
+        recv = self._buf("recv", total) if self.rank == 0 else None
+        if self.comm is not None:
+            self.comm.gatherv_device(send, nbytes, counts, recv, root=0, stream=self.stream)
+            self.comm.wait(self.stream)
+        elif nbytes:
+            copy_dtod(recv, 0, send, 0, nbytes, self.stream)
+        t = mark("gatherv", t)
+        out = None
+        if self.rank == 0:
+            blob = np.empty(total, np.uint8)
+            if total:
+                recv.download(blob, self.stream)
+            self.stream.synchronize()
+            out, off = [], 0
+            for s in sizes:
+                out.append(blob[off:off + int(s)].tobytes())
+                off += int(s)
+        else:
+            self.stream.synchronize()
+        mark("d2h_rank0", t)
+        return sizes, out
+
+    def _all_gather_sizes(self, local_sizes: np.ndarray) -> np.ndarray:
+        full = np.zeros(self.N, np.int64)
+        full[self.lo:self.hi] = local_sizes
+        if self.comm is None or self.world == 1:
+            return full
+        rows = self.comm.all_gather_i64(full)
+        out = np.zeros(self.N, np.int64)
+        for r in range(self.world):
+            rlo, rhi = frame_range(self.N, r, self.world)
+            out[rlo:rhi] = rows[r, rlo:rhi]
+        return out

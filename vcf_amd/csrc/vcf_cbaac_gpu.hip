@@ -306,10 +306,14 @@ struct Encoder {
     }
 };
 
-__device__ __forceinline__ uint32_t load_sym4(const uint8_t *p, int64_t off, int64_t len, uint32_t lane)
+// Four symbols per lane.  Segment starts are multiples of 256 symbols from
+// `sym`, so a dword load is aligned exactly when `sym` is (`aligned`,
+// wave-uniform); a caller's pointer into the middle of a buffer (a frame of
+// n % 4 != 0 symbols after the first) takes the byte loads.
+__device__ __forceinline__ uint32_t load_sym4(const uint8_t *p, int64_t off, int64_t len, uint32_t lane, bool aligned)
 {
     const int64_t i = off + 4 * (int64_t)lane;
-    if (i + 3 < len) return *reinterpret_cast<const uint32_t *>(p + i);   // segment starts are 256-aligned
+    if (aligned && i + 3 < len) return *reinterpret_cast<const uint32_t *>(p + i);
     uint32_t v = 0;
     for (int j = 0; j < 4; ++j)
         if (i + j < len) v |= (uint32_t)p[i + j] << (8 * j);
@@ -345,9 +349,10 @@ __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *_
     w.out = slots + seg * slot_words;
     Encoder e;
 
-    uint32_t cur = load_sym4(src, 0, len, lane);
+    const bool aligned = (reinterpret_cast<uintptr_t>(sym) & 3) == 0;
+    uint32_t cur = load_sym4(src, 0, len, lane, aligned);
     for (int64_t off = 0; off < len; off += kChunk) {
-        const uint32_t nxt = off + kChunk < len ? load_sym4(src, off + kChunk, len, lane) : 0u;
+        const uint32_t nxt = off + kChunk < len ? load_sym4(src, off + kChunk, len, lane, aligned) : 0u;
         const int cnt = len - off < kChunk ? (int)(len - off) : kChunk;
         for (int k = 0; k < cnt; ++k) {
             const uint32_t s = (rl(cur, k >> 2) >> (8 * (k & 3))) & 255u;
@@ -439,6 +444,7 @@ __global__ __launch_bounds__(64) void cbaac_tiled_decode_kernel(const uint8_t *_
     const int64_t start = seg * seg_len;
     const int64_t len = n - start < seg_len ? n - start : seg_len;
     uint8_t *dst = out + start;
+    const bool out_aligned = (reinterpret_cast<uintptr_t>(out) & 3) == 0;   // start is a multiple of 256
 
     Model m;
     if (prior) model_reset_prior(m, prior, lane);
@@ -504,8 +510,14 @@ __global__ __launch_bounds__(64) void cbaac_tiled_decode_kernel(const uint8_t *_
             obuf = lane == (uint32_t)((i >> 2) & 63) ? acc : obuf;
             acc = 0;
         }
-        if ((i & (kChunk - 1)) == kChunk - 1)   // a full chunk: one dword per lane
-            *reinterpret_cast<uint32_t *>(dst + (i - (kChunk - 1)) + 4 * lane) = obuf;
+        if ((i & (kChunk - 1)) == kChunk - 1) {   // a full chunk: one dword per lane
+            uint8_t *q = dst + (i - (kChunk - 1)) + 4 * lane;
+            if (out_aligned) {
+                *reinterpret_cast<uint32_t *>(q) = obuf;
+            } else {
+                for (int j = 0; j < 4; ++j) q[j] = (uint8_t)(obuf >> (8 * j));
+            }
+        }
     }
     const int64_t done = len & ~(int64_t)(kChunk - 1);
     if (done < len) {   // the partial last chunk, byte by byte

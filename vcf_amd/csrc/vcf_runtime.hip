@@ -141,6 +141,11 @@ int vcf_event_sync(void *event)
     return hip_check(hipEventSynchronize((hipEvent_t)event), "hipEventSynchronize");
 }
 
+int vcf_stream_wait_event(void *stream, void *event)
+{
+    return hip_check(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0), "hipStreamWaitEvent");
+}
+
 int vcf_event_elapsed_ms(void *start, void *stop, float *ms)
 {
     if (!ms) return vcf::set_error(VCF_ERR_INVALID, "null pointer");

@@ -31,6 +31,10 @@ class Stream:
     def synchronize(self) -> None:
         call("vcf_stream_sync", self.handle)
 
+    def wait_event(self, event: "Event") -> None:
+        """Later work on this stream waits for `event`."""
+        call("vcf_stream_wait_event", self.handle, event.handle)
+
     def close(self) -> None:
         if self.handle is not None and self.handle.value:
             lib().vcf_stream_destroy(self.handle)
@@ -124,3 +128,12 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def copy_dtod(dst: DeviceBuffer, dst_off: int, src: DeviceBuffer, src_off: int, nbytes: int, stream=None) -> None:
+    """nbytes from src[src_off:] to dst[dst_off:], enqueued on `stream`."""
+    if nbytes <= 0:
+        return
+    if dst_off + nbytes > dst.nbytes or src_off + nbytes > src.nbytes:
+        raise ValueError("device copy out of bounds")
+    call("vcf_memcpy_dtod", dst.address(dst_off), src.address(src_off), int(nbytes), _h(stream))

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import io
 import struct
+import threading
 
 import numpy as np
 
@@ -62,7 +63,12 @@ class _Scratch:
 
 
 class TiledCoder:
-    """The GPU calls, with reusable scratch and a stream."""
+    """The GPU calls, with reusable scratch and a stream.
+
+    One coder owns one set of scratch buffers and one stream, so its calls
+    are serialised by `lock` (the DCT CoDec's encode_fns/decode_fns call the
+    entropy codec from a thread pool): a call's upload, kernels and download
+    never interleave with another thread's on the same buffers."""
 
     def __init__(self, order: int = 0, seg_len: int = DEFAULT_SEG, stream: Stream | None = None,
                  prior: bool = False):
@@ -72,10 +78,16 @@ class TiledCoder:
         self.stream = stream if stream is not None else Stream()
         self.scratch = _Scratch()
         self.last_prior = None     # the prior table of the last encode (prior=True)
+        self.lock = threading.RLock()
 
     def encode_device(self, sym: DeviceBuffer, n: int, offset: int = 0):
         """Symbols already in HBM -> (segment byte counts, payload bytes);
-        with prior=True the frame's prior table is left in self.last_prior."""
+        with prior=True the frame's prior table is left in self.last_prior
+        (read it under self.lock when other threads share the coder)."""
+        with self.lock:
+            return self._encode_device(sym, n, offset)
+
+    def _encode_device(self, sym: DeviceBuffer, n: int, offset: int = 0):
         lib = L.lib()
         ns = n_segments(n, self.seg_len)
         ws = self.scratch.get("ws", int(lib.vcf_cbaac_tiled_workspace(n, self.seg_len)))
@@ -104,13 +116,18 @@ class TiledCoder:
 
     def encode(self, sym: np.ndarray):
         sym = np.ascontiguousarray(sym, np.uint8).ravel()
-        buf = self.scratch.get("sym", sym.size)
-        if sym.size:
-            buf.upload(sym, self.stream)
-        return self.encode_device(buf, sym.size)
+        with self.lock:
+            buf = self.scratch.get("sym", sym.size)
+            if sym.size:
+                buf.upload(sym, self.stream)
+            return self._encode_device(buf, sym.size)
 
     def trace(self, sym: np.ndarray) -> np.ndarray:
         """(n, 3) int32: the (low, high, total) handed to the coder per symbol."""
+        with self.lock:
+            return self._trace(sym)
+
+    def _trace(self, sym: np.ndarray) -> np.ndarray:
         lib = L.lib()
         sym = np.ascontiguousarray(sym, np.uint8).ravel()
         n = sym.size
@@ -130,6 +147,13 @@ class TiledCoder:
         return out
 
     def decode_to_device(self, payload: bytes, seg_bytes, n: int, out: DeviceBuffer, prior=None):
+        """Enqueue the decode of n symbols into `out` on self.stream (the
+        caller synchronises; hold self.lock across this and that wait when
+        other threads share the coder)."""
+        with self.lock:
+            self._decode_to_device(payload, seg_bytes, n, out, prior)
+
+    def _decode_to_device(self, payload: bytes, seg_bytes, n: int, out: DeviceBuffer, prior=None):
         seg_bytes = np.asarray(seg_bytes, np.int64)
         offs = np.zeros(seg_bytes.size + 1, np.int64)
         np.cumsum(seg_bytes, out=offs[1:])
@@ -151,13 +175,14 @@ class TiledCoder:
                    self.stream.handle)
 
     def decode(self, payload: bytes, seg_bytes, n: int, prior=None) -> np.ndarray:
-        out = self.scratch.get("dec", n)
-        self.decode_to_device(payload, seg_bytes, n, out, prior)
-        res = np.empty(n, np.uint8)
-        if n:
-            out.download(res, self.stream)
-        self.stream.synchronize()
-        return res
+        with self.lock:
+            out = self.scratch.get("dec", n)
+            self.decode_to_device(payload, seg_bytes, n, out, prior)
+            res = np.empty(n, np.uint8)
+            if n:
+                out.download(res, self.stream)
+            self.stream.synchronize()
+            return res
 
 
 def check_prior(prior) -> np.ndarray:
@@ -169,54 +194,121 @@ def check_prior(prior) -> np.ndarray:
     return prior
 
 
+class FrameBatch:
+    """Reusable device state for coding `n_frames` frames of `frame_symbols`
+    symbols each (the III driver's per-rank chunk), keeping every frame's
+    code-stream in HBM: per frame an output slot, its segment sizes and prior
+    (one contiguous device array each, so one download returns them all);
+    per library stream a workspace (frames on one stream run one after the
+    other).  launch() enqueues every frame, sizes() waits and downloads the
+    small index, device_payload(f) / download() hand out the code-streams."""
+
+    def __init__(self, n_frames: int, frame_symbols: int, order: int = 0, seg_len: int = PRIOR_SEG,
+                 prior: bool = True, streams: int = 4):
+        lib = L.lib()
+        self.n_frames, self.n = int(n_frames), int(frame_symbols)
+        self.order, self.seg_len, self.prior = int(order), int(seg_len), bool(prior)
+        if self.prior and self.order > 1:
+            raise NotImplementedError("prior-seeded tiled CBAAC: orders 0 and 1")
+        self.ns = n_segments(self.n, self.seg_len)
+        self.cap = int(lib.vcf_cbaac_tiled_bound(self.n, self.seg_len))
+        wsb = int(lib.vcf_cbaac_tiled_workspace(self.n, self.seg_len))
+        self.streams = [Stream() for _ in range(max(1, min(int(streams), max(self.n_frames, 1))))]
+        self.ws = [DeviceBuffer(max(wsb, 1)) for _ in self.streams]
+        self.hist = [DeviceBuffer(1024) for _ in self.streams]
+        self.out = [DeviceBuffer(max(self.cap, 1)) for _ in range(self.n_frames)]
+        self.sizes_dev = DeviceBuffer(max(8 * (self.ns + 1) * self.n_frames, 8))
+        self.prior_dev = DeviceBuffer(max(512 * self.n_frames, 8))
+        self._sizes = None
+        self._priors = None
+
+    def launch(self, sym: DeviceBuffer, offset: int = 0, after: Stream | None = None) -> None:
+        """Enqueue frame f = symbols [offset + f*n, offset + (f+1)*n) of `sym`
+        on library stream f % streams; `after` (the producer's stream) is
+        waited for through an event."""
+        from .device import Event
+        if after is not None:
+            ev = Event()
+            ev.record(after)
+            for st in self.streams:
+                st.wait_event(ev)
+        n, ns = self.n, self.ns
+        for f in range(self.n_frames):
+            k = f % len(self.streams)
+            st, ws, hist = self.streams[k], self.ws[k], self.hist[k]
+            addr = sym.address(offset + f * n)
+            sb = self.sizes_dev.address(8 * (ns + 1) * f)
+            if self.prior:
+                pr = self.prior_dev.address(512 * f)
+                L.call("vcf_cbaac_tiled_prior", addr, n, pr, hist.ptr, st.handle)
+                L.call("vcf_cbaac_tiled_encode_prior", addr, n, self.order, pr, self.seg_len, self.out[f].ptr,
+                       self.cap, sb, ws.ptr, st.handle)
+            else:
+                L.call("vcf_cbaac_tiled_encode", addr, n, self.order, self.seg_len, self.out[f].ptr, self.cap, sb,
+                       ws.ptr, st.handle)
+        self._sizes = None
+
+    def join(self, stream: Stream) -> None:
+        """`stream` waits for every frame's coding (no host synchronisation)."""
+        from .device import Event
+        for st in self.streams:
+            ev = Event()
+            ev.record(st)
+            stream.wait_event(ev)
+
+    def sizes(self):
+        """Wait for the coding; -> (per-frame segment byte counts (n_frames x
+        ns int64), per-frame payload bytes, priors (n_frames x 256) or None)."""
+        if self._sizes is None:
+            for st in self.streams:
+                st.synchronize()
+            allz = np.empty((self.n_frames, self.ns + 1), np.int64)
+            if self.n_frames:
+                self.sizes_dev.download(allz)
+            self._sizes = allz
+            self._priors = None
+            if self.prior:
+                self._priors = np.empty((self.n_frames, 256), np.uint16)
+                if self.n_frames:
+                    self.prior_dev.download(self._priors)
+        return self._sizes[:, :-1], self._sizes[:, -1].copy(), self._priors
+
+    def device_payload(self, f: int):
+        """(device buffer, byte count) of frame f's packed segments."""
+        _, totals, _ = self.sizes()
+        return self.out[f], int(totals[f])
+
+    def header(self, f: int, shape) -> bytes:
+        """Frame f's container bytes in front of its payload (pack() minus the payload)."""
+        seg, _, pri = self.sizes()
+        return pack(tuple(shape), self.order, self.seg_len, seg[f], b"", None if pri is None else pri[f])
+
+    def download(self):
+        """-> [(segment byte counts, payload bytes, prior or None)] per frame."""
+        seg, totals, pri = self.sizes()
+        res = []
+        for f in range(self.n_frames):
+            payload = np.empty(int(totals[f]), np.uint8)
+            if payload.size:
+                self.out[f].download(payload)
+            res.append((seg[f].copy(), payload.tobytes(), None if pri is None else pri[f].copy()))
+        return res
+
+
 def encode_frames_device(sym: DeviceBuffer, n_frames: int, frame_symbols: int, order: int = 0,
-                         seg_len: int = DEFAULT_SEG, prior: bool = False, streams: int = 4):
-    """Several frames' symbols, back to back in HBM, each coded as its own
-    tiled stream (its own prior with prior=True).  One frame's segments fill
-    only a few hundred waves, so the frames go out round robin on `streams`
-    library streams and run concurrently; every launch is issued before the
-    first download.  -> [(segment byte counts, payload, prior or None)]."""
-    lib = L.lib()
-    n = int(frame_symbols)
-    ns = n_segments(n, seg_len)
-    ss = [Stream() for _ in range(max(1, min(int(streams), n_frames)))]
-    cap = int(lib.vcf_cbaac_tiled_bound(n, seg_len))
-    wsb = int(lib.vcf_cbaac_tiled_workspace(n, seg_len))
-    # every buffer first: an allocation can wait for the device, which would
-    # serialise the launches below
-    bufs = [(DeviceBuffer(max(cap, 1)), DeviceBuffer(8 * (ns + 1)), DeviceBuffer(max(wsb, 1)),
-             DeviceBuffer(512) if prior else None, DeviceBuffer(1024) if prior else None) for _ in range(n_frames)]
-    jobs = []
-    for f in range(n_frames):
-        st = ss[f % len(ss)]
-        out, sb, ws, pr, hist = bufs[f]
-        addr = sym.address(f * n)
-        if prior:
-            L.call("vcf_cbaac_tiled_prior", addr, n, pr.ptr, hist.ptr, st.handle)
-            L.call("vcf_cbaac_tiled_encode_prior", addr, n, int(order), pr.ptr, int(seg_len), out.ptr, cap, sb.ptr,
-                   ws.ptr, st.handle)
-            jobs.append((st, out, sb, ws, pr, hist))
-        else:
-            L.call("vcf_cbaac_tiled_encode", addr, n, int(order), int(seg_len), out.ptr, cap, sb.ptr, ws.ptr,
-                   st.handle)
-            jobs.append((st, out, sb, ws, None, None))
-    res = []
-    for st, out, sb, ws, pr, hist in jobs:
-        sizes = np.empty(ns + 1, np.int64)
-        sb.download(sizes, st)
-        p = None
-        if pr is not None:
-            p = np.empty(256, np.uint16)
-            pr.download(p, st)
-        st.synchronize()
-        payload = np.empty(int(sizes[-1]), np.uint8)
-        if payload.size:
-            out.download(payload, st)
-            st.synchronize()
-        res.append((sizes[:-1].copy(), payload.tobytes(), p))
-    for st in ss:
-        st.synchronize()
-    return res
+                         seg_len: int = DEFAULT_SEG, prior: bool = False, streams: int = 4,
+                         after: Stream | None = None, offset: int = 0):
+    """Several frames' symbols, back to back in HBM from `offset`, each coded
+    as its own tiled stream (its own prior with prior=True).  One frame's
+    segments fill only a few hundred waves, so the frames go out round robin
+    on `streams` library streams and run concurrently; every launch is issued
+    before the first download.  `after`: the stream that produced the symbols
+    (e.g. the DCT encode's); the library streams wait for its work so far
+    (an event), so the caller need not synchronise it first.
+    -> [(segment byte counts, payload, prior or None)]."""
+    fb = FrameBatch(n_frames, frame_symbols, order, seg_len, prior, streams)
+    fb.launch(sym, offset, after)
+    return fb.download()
 
 
 def pack(shape, order: int, seg_len: int, seg_bytes, payload: bytes, prior=None) -> bytes:
@@ -245,8 +337,12 @@ def _parse(data: bytes):
     if data[p:p + 4] != MAGIC:
         raise ValueError("not a tiled CBAAC stream")
     version, order, seg_len, ns = struct.unpack_from("<IIII", data, p + 4)
-    if version not in (VERSION, VERSION_PRIOR) or (version == VERSION_PRIOR and order > 1):
+    if version not in (VERSION, VERSION_PRIOR):
         raise ValueError(f"version {version}")
+    if order > 1:                       # the GPU coder's orders (both versions)
+        raise ValueError(f"order {order}")
+    if seg_len <= 0 or seg_len % 256:   # vcf_cbaac_tiled_*: a positive multiple of 256
+        raise ValueError(f"segment length {seg_len}")
     p += 20
     prior = None
     if version == VERSION_PRIOR:
@@ -272,21 +368,25 @@ class TiledCBAACCodec:
         self.seg_len = int(seg_len)
         self.prior = bool(prior)
         self._coder = None
+        self._make = threading.Lock()
 
     @property
     def coder(self) -> TiledCoder:
-        if self._coder is None:
-            self._coder = TiledCoder(self.ORDER, self.seg_len, prior=self.prior)
-        return self._coder
+        with self._make:
+            if self._coder is None:
+                self._coder = TiledCoder(self.ORDER, self.seg_len, prior=self.prior)
+            return self._coder
 
     def compress(self, img: np.ndarray, fn=None) -> io.BytesIO:
         img = np.asarray(img)
         flat = img.ravel()
         if flat.size and (flat.min() < 0 or flat.max() > 255):
             raise ValueError("CBAAC codes byte symbols (0..255)")
-        sizes, payload = self.coder.encode(flat.astype(np.uint8))
-        b = io.BytesIO(pack(img.shape, self.ORDER, self.seg_len, sizes, payload,
-                            self.coder.last_prior if self.prior else None))
+        coder = self.coder
+        with coder.lock:    # last_prior belongs to this call's encode
+            sizes, payload = coder.encode(flat.astype(np.uint8))
+            prior = coder.last_prior if self.prior else None
+        b = io.BytesIO(pack(img.shape, self.ORDER, self.seg_len, sizes, payload, prior))
         b.seek(0)
         return b
 
@@ -294,9 +394,11 @@ class TiledCBAACCodec:
         """Indices already in HBM (e.g. the DCT encode's output): only the
         compressed bytes cross PCIe."""
         n = int(np.prod(shape))
-        sizes, payload = self.coder.encode_device(k, n, offset)
-        b = io.BytesIO(pack(tuple(shape), self.ORDER, self.seg_len, sizes, payload,
-                            self.coder.last_prior if self.prior else None))
+        coder = self.coder
+        with coder.lock:
+            sizes, payload = coder.encode_device(k, n, offset)
+            prior = coder.last_prior if self.prior else None
+        b = io.BytesIO(pack(tuple(shape), self.ORDER, self.seg_len, sizes, payload, prior))
         b.seek(0)
         return b
 
