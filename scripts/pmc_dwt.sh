@@ -1,20 +1,26 @@
 #!/bin/bash
-# PMC passes over the DWT bench (fused level kernels): scripts/pmc_dwt.sh
+# PMC passes + a kernel trace over the C3 DWT encode (scripts/dwt_once.py VARIANT):
+#   VARIANT=17 scripts/pmc_dwt.sh   -> gpurun_out/pmc_dwt_v$VARIANT/{summary.txt,trace}
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-ROOT=$(pwd); OUT=/tmp/pmc_dwt; rm -rf "$OUT"; mkdir -p "$OUT"; export TMPDIR=/tmp; cd /tmp   # raw counters stay on the box
+ROOT=$(pwd); V=${VARIANT:-0}; OUT=$ROOT/gpurun_out/pmc_dwt_v$V; RAW=/tmp/pmc_dwt_v$V
+rm -rf "$OUT" "$RAW"; mkdir -p "$OUT" "$RAW"; export TMPDIR=/tmp; cd /tmp   # raw counters stay on the box
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$RAW/trace" -o run \
+    -- python3 "$ROOT/scripts/dwt_once.py" "$V" 20 > "$OUT/trace.log" 2>&1
+rc=$?; echo "trace rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac
+find "$RAW/trace" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 i=0
 for grp in "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS" \
            "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES" \
            "SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVES SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_FMA_F64 GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o pmc \
-      -- python3 "$ROOT/scripts/bench_paths.py" --only dwt --dwt-variants 0 --steps 1 > "$OUT/p$i.log" 2>&1
+  timeout -k 10 -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d "$RAW/p$i" -o pmc \
+      -- python3 "$ROOT/scripts/dwt_once.py" "$V" 2 > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"
-  case $rc in 0) ;; 124|134|137|139) exit $rc;; *) tail -3 "$OUT/p$i.log";; esac
+  case $rc in 0) ;; *) exit $rc;; esac
 done
-python3 - "$OUT" << 'PY'
+python3 - "$RAW" > "$OUT/summary.txt" << 'PY'
 import csv, glob, sys, collections, re
 out = sys.argv[1]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -23,8 +29,9 @@ for f in glob.glob(f"{out}/p*/**/*counter_collection.csv", recursive=True):
         n = r.get("Kernel_Name", "")
         m = re.search(r"(\w+_kernel)<([^>]*)>", n) or re.search(r"(\w+_kernel)\(", n)
         if not m: continue
-        key = m.group(0)[:60] + " grid=" + r.get("Grid_Size", r.get("Grid_Size_X", "?"))
+        key = m.group(0)[:70] + " grid=" + r.get("Grid_Size", r.get("Grid_Size_X", "?"))
         acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in sorted(acc.items()):
     print(k, {c: round(sum(v) / len(v)) for c, v in sorted(d.items())})
 PY
+cat "$OUT/summary.txt"

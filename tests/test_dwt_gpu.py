@@ -174,7 +174,7 @@ def test_dwt_frame_pipeline_small(H, W, L, Q):
 def test_dwt_unknown_variant():
     import vcf_amd.dwt as DW
     with pytest.raises(ValueError):
-        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=27)
+        DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=28)
     with pytest.raises(ValueError):
         DW.decode(DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32), 16, 16, "db5", 2, 32, variant=17)
 
@@ -230,3 +230,40 @@ def test_cli_2d_dwt(tmp_path):
         assert r.returncode == 0, r.stderr[-2000:]
     sb = O.dwt_encode_frame(rgb, "bior4.4", 2, 32)
     assert np.array_equal(np.asarray(Image.open(dec)), O.dwt_decode_frame(sb, 48, 64, "bior4.4", 2, 32))
+
+
+@pytest.mark.parametrize("wavelet", ["bior4.4", "db5"])
+@pytest.mark.parametrize("H,W,L,Q", [(64, 512, 2, 32), (128, 1024, 3, 7), (200, 600, 4, 16), (68, 516, 5, 1),
+                                     (96, 1000, 2, 3), (264, 728, 5, 64)])
+def test_dwt_band12_vs_oracle(wavelet, H, W, L, Q):
+    """The fused level-1+2 band kernel (the default for bior4.4 / db5 on planes
+    with h % 4 == 0, w % 4 == 0, at least 64 x 512): every subband equals the
+    oracle and the level-by-level kernels (variant 27), whatever the band and
+    tile cuts (partial last tile, one-row bands, wrapped halos)."""
+    import vcf_amd.dwt as DW
+    rng = np.random.Generator(np.random.PCG64(H * 7 + W + L))
+    frames = rng.integers(0, 256, (2, H, W, 3), dtype=np.uint8)
+    frames[1] = np.clip(frames[1] // 8 + 100 + (np.arange(W)[None, :, None] // 3), 0, 255)   # smooth-ish
+    got = DW.encode(frames, wavelet, L, Q)
+    ref_chain = DW.encode(frames, wavelet, L, Q, variant=27)
+    for f in range(2):
+        ref = O.dwt_encode_frame(frames[f], wavelet, L, Q)
+        for name, arr in ref.items():
+            assert np.array_equal(got[f][name], arr), (f, name)
+            assert np.array_equal(ref_chain[f][name], arr), (f, name)
+
+
+@pytest.mark.parametrize("n", [1, 3, 8])
+def test_dwt_band12_batches(n):
+    """Batches of 1080p frames (the band count follows the batch) equal the level-by-level chain."""
+    import vcf_amd.dwt as DW
+    rng = np.random.Generator(np.random.PCG64(n))
+    frames = rng.integers(0, 256, (n, 1080, 1920, 3), dtype=np.uint8)
+    a = DW.encode(frames, "bior4.4", 5, 32)
+    b = DW.encode(frames, "bior4.4", 5, 32, variant=27)
+    for f in range(n):
+        for name in a[f]:
+            assert np.array_equal(a[f][name], b[f][name]), (f, name)
+    ref = O.dwt_encode_frame(frames[-1], "bior4.4", 5, 32)
+    for name, arr in ref.items():
+        assert np.array_equal(a[-1][name], arr), name

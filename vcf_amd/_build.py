@@ -17,7 +17,7 @@ SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_dct_any.hip", "vcf_quant.hi
            "vcf_cbahc.cpp", "vcf_ipp.hip", "vcf_ipp_rdo.hip",
            "vcf_png.cpp", "vcf_comm.cpp", "vcf_cbaac_gpu.hip", "vcf_plugins.hip"]
 HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h", "vcf_wavelets.h", "vcf_pocketfft.h", "vcf_pocketfft_tables.h",
-           "vcf_pocketfft_rt.h", "vcf_pipeline.h"]
+           "vcf_pocketfft_rt.h", "vcf_pipeline.h", "vcf_dwt_band.h"]
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("VCF_OFFLOAD_ARCH", "gfx950")
 
@@ -52,13 +52,30 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     from concurrent.futures import ThreadPoolExecutor
     os.makedirs(OBJDIR, exist_ok=True)
-    hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
-    hdr_t = max(hdr_t, os.path.getmtime(os.path.join(ROOT, "include", "vcf_amd.h")))
+
+    def deps_mtime(src):
+        """Newest mtime of a source and the local headers it includes (transitively)."""
+        seen, todo, newest = set(), [os.path.join(CSRC, src)], 0.0
+        while todo:
+            f = todo.pop()
+            if f in seen or not os.path.exists(f):
+                continue
+            seen.add(f)
+            newest = max(newest, os.path.getmtime(f))
+            for line in open(f, errors="replace"):
+                line = line.strip()
+                if line.startswith("#include \""):
+                    name = line.split('"')[1]
+                    for d in (CSRC, os.path.join(ROOT, "include")):
+                        if os.path.exists(os.path.join(d, name)):
+                            todo.append(os.path.join(d, name))
+                            break
+        return newest
 
     def compile_one(src):
         obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
         path = os.path.join(CSRC, src)
-        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(path)):
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > deps_mtime(src):
             return obj
         cmd = [hipcc(), *_flags(), "-c", path, "-o", obj + ".tmp"]
         if verbose:

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <type_traits>
@@ -1057,6 +1058,10 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
     direct_rows(o, std::false_type());   // fewer than P rows, and the bottom rows' wrapped taps
 }
 
+// fused forward levels 1 + 2 (the default for 10-tap filters on planes of even
+// sizes at both levels)
+#include "vcf_dwt_band.h"
+
 // Four consecutive outputs of the inverse from the register windows of the
 // approximation (xa) and detail (xd) inputs: pywt's order for a pair index
 // i >= F/4 (approximation taps j = 0.., then detail taps), tap loop outermost.
@@ -1558,6 +1563,74 @@ void launch_inv_level(const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t
         launch_inv_kernel<F, 0u, 0u>(a, tp, grid, from_packed, to_rgb, rgb_out);
 }
 
+// Levels 1 and 2 in one launch (dwt_band12_kernel): 10-tap filters with
+// compile-time taps (bior4.4, db5), planes with h % 4 == 0 and w % 4 == 0 and
+// at least 64 x 512 (the windows wrap at most once), levels >= 2.
+bool band12_ok(const DwtGeom &g, const WaveletDef &wd, int &id)
+{
+    if (g.F != 10 || g.levels < 2 || g.H % 4 || g.W % 4 || g.H < 64 || g.W < 512) return false;
+    const bool b44 = zero_mask(wd.dec_lo, 10) == kB44DecLo && zero_mask(wd.dec_hi, 10) == kB44DecHi;
+    id = b44 ? 1 : 2;
+    for (int m = 0; m < 10; ++m) {
+        const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
+        if (std::memcmp(&l, &wd.dec_lo[m], 8) || std::memcmp(&h, &wd.dec_hi[m], 8)) return false;
+    }
+    return true;
+}
+
+template <unsigned ZL, unsigned ZH, int CT>
+void launch_band12_t(const DwtGeom &g, const uint8_t *rgb, long long n_frames, double *LL2, long long plane_stride,
+                     uint8_t *packed, int Q, hipStream_t s)
+{
+    const int h2 = g.hs[2], w2 = g.ws[2];
+    const int n_tiles = (w2 + kBT2 - 1) / kBT2;
+    // bands: the time is about (rounds of resident workgroups) x (steps per band,
+    // 2 rows + the F - 2 halo rows + 3 of pipeline per level-2 row pair); two
+    // 512-thread workgroups fit a CU (VGPRs)
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0, v = 0;
+        n_cu = hipGetDevice(&dev) == hipSuccess &&
+                       hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0
+                   ? v
+                   : 256;
+    }
+    const long long slots = 2LL * n_cu, per_band = 3LL * n_frames * n_tiles;
+    int n_bands = 1;
+    long long best = -1;
+    for (int nb = 1; nb <= std::max(1, h2 / 2); ++nb) {
+        const int br = (h2 + nb - 1) / nb;
+        if (nb > 1 && (h2 + br - 1) / br != nb) continue;
+        const long long rounds = (per_band * nb + slots - 1) / slots;
+        const long long cost = rounds * (2LL * br + 10 + 3);
+        if (best < 0 || cost < best) {
+            best = cost;
+            n_bands = nb;
+        }
+    }
+    if (const char *e = getenv("VCF_DWT_BANDS"))   // tuning knob (A/B of the band cut)
+        n_bands = std::max(1, std::min(atoi(e), std::max(1, h2 / 2)));
+    const int brows = (h2 + n_bands - 1) / n_bands;
+    n_bands = (h2 + brows - 1) / brows;
+    const long long units = n_frames * n_tiles * n_bands;
+    const unsigned grid = (unsigned)(24 * ((units + 7) / 8));
+    const bool last2 = g.levels == 2, qp2 = (Q & (Q - 1)) == 0;
+    auto kern = last2 ? (qp2 ? dwt_band12_kernel<10, ZL, ZH, CT, true, true> : dwt_band12_kernel<10, ZL, ZH, CT, true, false>)
+                      : (qp2 ? dwt_band12_kernel<10, ZL, ZH, CT, false, true>
+                             : dwt_band12_kernel<10, ZL, ZH, CT, false, false>);
+    const Taps<10> tp{};
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBNT), 0, s, rgb, (long long)g.H * g.W * 3, LL2, plane_stride, packed,
+                       g.packed_bytes, g.ll_off, g.sb_off[1][0], g.sb_off[1][1], g.sb_off[1][2], g.sb_off[2][0],
+                       g.sb_off[2][1], g.sb_off[2][2], g.H, g.W, Q, n_tiles, n_bands, brows, (int)units, tp);
+}
+
+void launch_band12(int id, const DwtGeom &g, const uint8_t *rgb, long long n_frames, double *LL2,
+                   long long plane_stride, uint8_t *packed, int Q, hipStream_t s)
+{
+    if (id == 1) launch_band12_t<kB44DecLo, kB44DecHi, 1>(g, rgb, n_frames, LL2, plane_stride, packed, Q, s);
+    else launch_band12_t<0u, 0u, 2>(g, rgb, n_frames, LL2, plane_stride, packed, Q, s);
+}
+
 #define VCF_DWT_FOR_EACH_F(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18)
 
 void fwd_level(int F, const LevelArgs &a, bool first, bool last)
@@ -1667,7 +1740,7 @@ int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
 // call it per chunk of frames with their hook)
 static int encode_chain(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                         int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, hipStream_t s,
-                        const PipeHook *hook, long long sep_area = 0)
+                        const PipeHook *hook, long long sep_area = 0, bool no_band = false)
 {
     int rc = VCF_OK;
     // 10: variant 0 with the byte-wise copy-out, 11: with the earlier row-pass mapping,
@@ -1710,7 +1783,18 @@ static int encode_chain(int variant, const uint8_t *rgb_dev, int64_t n_frames, i
                                LLout, ws_stride, packed_dev, g.packed_bytes, g.ll_off, g.sb_off[l][0],
                                g.sb_off[l][1], g.sb_off[l][2], hh, w, hw, F, Q, flt);
     };
-    for (int l = 1; fused && l <= levels; ++l) {
+    int l_start = 1;
+    int band_id = 0;
+    if (fused && (variant == 0 || variant == 9) && !no_band && band12_ok(g, kWavelets[wavelet], band_id)) {
+        // levels 1 and 2 in one launch: LL1 never leaves the chip; LL2 lands where level 2's would
+        if ((rc = hook_wait(hook, s)) != VCF_OK) return rc;
+        launch_band12(band_id, g, rgb_dev, n_frames, LL1, ws_stride, packed_dev, Q, s);
+        if ((rc = hip_check(hipGetLastError(), "dwt_band12_kernel launch")) != VCF_OK) return rc;
+        if ((rc = hook_rec(hook, s)) != VCF_OK) return rc;
+        in = LL1;
+        l_start = 3;
+    }
+    for (int l = l_start; fused && l <= levels; ++l) {
         double *LLout = (l & 1) ? LL0 : LL1;
         const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
                           g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
@@ -1744,7 +1828,10 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant > 26) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant > 27) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    // 27: variant 0 without the fused level-1+2 band kernel (levels 1 and 2 as separate launches; A/B)
+    const bool no_band = variant == 27;
+    if (variant == 27) variant = 0;
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -1755,7 +1842,17 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
     // 19 = four streams, four chunks; 17 = variant 0 on the caller's stream alone)
     hipStream_t s = (hipStream_t)stream;
     PipeShape ps;
-    if (variant == 0 && pipeline_default(n_frames, H, W)) ps = kEncodePipe;
+    // the frame pipeline pays only for the level-by-level chain: with the fused
+    // level-1+2 band kernel one launch fills the chip (C3: 0.594 ms on one
+    // stream vs 0.635 ms pipelined, ABBA)
+    bool band = false;
+    {
+        DwtGeom g;
+        dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
+        int id = 0;
+        band = !no_band && band12_ok(g, kWavelets[wavelet], id);
+    }
+    if (variant == 0 && pipeline_default(n_frames, H, W) && !band) ps = kEncodePipe;
     if (variant == 13) ps = {2, 2, false};
     if (variant == 14) ps = {2, 2, true};
     if (variant == 15) ps = {2, 4, true};
@@ -1771,7 +1868,7 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
                                : variant == 21                                    ? 140000
                                : variant == 22                                    ? 600000
                                                                                   : 40000;
-    if (variant >= 20 && pipeline_default(n_frames, H, W)) ps = kEncodePipe;
+    if (variant >= 20 && pipeline_default(n_frames, H, W) && !band) ps = kEncodePipe;
     // 23: variant 0 with the fused levels' sums started at 0.0 (no Z0, A/B)
     // 24: variant 0 with level 1 in 512-thread tiles of 16 output rows (int16 staging)
     // 25: variant 0 with the earlier tail strip (every row through the generic sums)
@@ -1783,11 +1880,11 @@ int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_fra
         const long long fpx = (long long)H * W * 3, wsf = 3 * plane_doubles(g);
         return run_pipelined(n_frames, ps, s, [&](long long f0, long long n, hipStream_t cs, const PipeHook *hook) {
             return encode_chain(cv, rgb_dev + f0 * fpx, n, H, W, wavelet, levels, Q, packed_dev + f0 * g.packed_bytes,
-                                (double *)workspace_dev + f0 * wsf, cs, hook, sep_area);
+                                (double *)workspace_dev + f0 * wsf, cs, hook, sep_area, no_band);
         });
     }
     return encode_chain(variant, rgb_dev, n_frames, H, W, wavelet, levels, Q, packed_dev, workspace_dev, s, nullptr,
-                        sep_area);
+                        sep_area, no_band);
 }
 
 int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
