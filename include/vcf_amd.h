@@ -84,6 +84,11 @@ int vcf_event_create(void **event);
 int vcf_event_destroy(void *event);
 int vcf_event_record(void *event, void *stream);
 int vcf_event_sync(void *event);
+/* n_pieces device copies in one launch: piece p moves table_dev[3p + 2] bytes
+ * from src_dev + table_dev[3p] to dst_dev + table_dev[3p + 1] (int64 table in
+ * device memory); e.g. per-frame code-streams packed for the gather */
+int vcf_copy_pieces(const uint8_t *src_dev, const int64_t *table_dev, int64_t n_pieces, uint8_t *dst_dev,
+                    void *stream);
 /* later work on `stream` waits for `event` (hipStreamWaitEvent) */
 int vcf_stream_wait_event(void *stream, void *event);
 int vcf_event_elapsed_ms(void *start, void *stop, float *ms);
@@ -376,6 +381,12 @@ int64_t vcf_cbaac_tiled_bound(int64_t n, int64_t seg_len);
  * means the output was cut: retry with vcf_cbaac_tiled_bound bytes). */
 int vcf_cbaac_tiled_encode(const uint8_t *sym_dev, int64_t n, int32_t order, int64_t seg_len, uint8_t *out_dev,
                            int64_t out_capacity, int64_t *seg_bytes_dev, void *ws_dev, void *stream);
+/* Kernel choice (process-wide; A/B and tests): 0 = automatic -- order 0 codes
+ * one segment per LANE (64 segments per wave, each with its own model in
+ * LDS) once a call has at least 2048 segments, else one segment per wave
+ * (64 lanes share one model: a shorter time per segment); 1 = one segment per
+ * wave always; 2 = one segment per lane for order 0 always.  Same bytes. */
+int vcf_cbaac_tiled_set_variant(int32_t variant);
 /* The model alone: the (low, high, total) triple handed to the coder for
  * every symbol (3*n int32), segment by segment (parity checks). */
 int vcf_cbaac_tiled_trace(const uint8_t *sym_dev, int64_t n, int32_t order, int64_t seg_len, int32_t *triples_dev,
@@ -397,6 +408,26 @@ int vcf_cbaac_tiled_encode_prior(const uint8_t *sym_dev, int64_t n, int32_t orde
                                  void *ws_dev, void *stream);
 int vcf_cbaac_tiled_decode_prior(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
                                  const uint16_t *prior_dev, int64_t seg_len, uint8_t *sym_dev, void *stream);
+/* Batches of frames, each coded exactly as the single-frame calls code it,
+ * in one launch per stage (a frame's segments alone fill few waves): n_frames
+ * (<= 65535) frames of frame_symbols symbols, frame f's symbols at sym_dev +
+ * f * frame_stride (any alignment); priors_dev = n_frames x 256 uint16 (frame
+ * f's prior at priors_dev + 256 f; NULL = fresh models, container version 1),
+ * hist_dev = n_frames x 256 uint32 of scratch; frame f's packed segments at
+ * out_dev + f * out_frame_capacity, its segment byte counts and total at
+ * seg_bytes_dev + f * (segments + 1); ws_dev = vcf_cbaac_tiled_frames_workspace
+ * bytes.  Decode: frame f's segment offsets at seg_offsets_dev + f * (segments
+ * + 1), offsets into in_dev; its symbols to sym_dev + f * out_frame_stride. */
+int64_t vcf_cbaac_tiled_frames_workspace(int64_t n_frames, int64_t frame_symbols, int64_t seg_len);
+int vcf_cbaac_tiled_prior_frames(const uint8_t *sym_dev, int64_t n_frames, int64_t frame_symbols,
+                                 int64_t frame_stride, uint16_t *priors_dev, uint32_t *hist_dev, void *stream);
+int vcf_cbaac_tiled_encode_frames(const uint8_t *sym_dev, int64_t n_frames, int64_t frame_symbols,
+                                  int64_t frame_stride, int32_t order, const uint16_t *priors_dev, int64_t seg_len,
+                                  uint8_t *out_dev, int64_t out_frame_capacity, int64_t *seg_bytes_dev, void *ws_dev,
+                                  void *stream);
+int vcf_cbaac_tiled_decode_frames(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n_frames,
+                                  int64_t frame_symbols, int32_t order, const uint16_t *priors_dev, int64_t seg_len,
+                                  uint8_t *sym_dev, int64_t out_frame_stride, void *stream);
 /* host, orders 0 / 1: vcf_cbaac_encode / _decode with every model seeded by prior (256 uint16, each >= 1) */
 int vcf_cbaac_encode_prior(const uint8_t *symbols, int64_t n, int32_t order, const uint16_t *prior, uint8_t *out,
                            int64_t out_capacity, int64_t *out_bytes, int64_t *out_bits);

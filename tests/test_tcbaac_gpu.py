@@ -257,3 +257,83 @@ def test_threaded_encode_fns_decode_fns(tmp_path, codec):
     for i in range(n):
         got = np.asarray(Image.open(str(tmp_path / f"dec_{i}.png")))
         assert np.array_equal(got, O.decode_frame(O.encode_frame(frames[i], 32, 0), H, W, 32, 0)), i
+
+
+@pytest.mark.parametrize("prior", [False, True])
+@pytest.mark.parametrize("seg_len", [256, 4096, 32768])
+def test_lane_kernels_equal_wave_kernels(prior, seg_len):
+    """Order 0 codes one segment per lane (vcf_cbaac_tiled_set_variant(2); the
+    default from 2048 segments on) or one per wave (1): identical streams, and
+    each decoder inverts the other's output; long segments cross several
+    model rescales."""
+    from vcf_amd import _lib as L
+    rng = np.random.Generator(np.random.PCG64(seg_len + prior))
+    n = 200_003
+    base = np.where(rng.random(n) < 0.97, 128, rng.integers(0, 256, n))
+    sym = np.clip(base + (rng.random(n) < 0.3) * rng.integers(-2, 3, n), 0, 255).astype(np.uint8)
+    sym[:5000] = rng.integers(0, 256, 5000)           # a noisy stretch: wide ranges, frequent rescales
+    sym[-70:] = 255
+    try:
+        L.call("vcf_cbaac_tiled_set_variant", 1)
+        c1 = T.TiledCoder(0, seg_len, prior=prior)
+        s1, p1 = c1.encode(sym)
+        L.call("vcf_cbaac_tiled_set_variant", 2)
+        c0 = T.TiledCoder(0, seg_len, prior=prior)
+        s0, p0 = c0.encode(sym)
+        assert list(s0) == list(s1) and p0 == p1
+        pr = c0.last_prior if prior else None
+        assert np.array_equal(c0.decode(p0, s0, n, pr), sym)     # lane decoder
+        L.call("vcf_cbaac_tiled_set_variant", 1)
+        assert np.array_equal(c1.decode(p0, s0, n, pr), sym)     # wave decoder, same stream
+    finally:
+        L.call("vcf_cbaac_tiled_set_variant", 0)
+
+
+def test_lane_kernels_on_dct_indices_many_segments():
+    """A 1080p frame's indices in 256-symbol segments (24 300 segments: the
+    automatic choice codes one per lane, 380 waves): every segment equals the
+    host coder seeded with the frame's prior."""
+    from bench import synth_frame
+    from oracle import oracle as O
+    k = O.encode_frame(synth_frame(1080, 1920, 5), 32, 0).ravel()
+    c = T.TiledCoder(0, 256, prior=True)
+    sizes, payload = c.encode(k)
+    host = T.host_segments_prior(k, T.prior_of(k), 256)
+    assert list(sizes) == [len(h) for h in host]
+    assert payload == b"".join(host)
+    assert np.array_equal(c.decode(payload, sizes, k.size, c.last_prior), k)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_batch_decode_frames(variant):
+    """vcf_cbaac_tiled_decode_frames: a batch of prior-seeded frames decoded in
+    one launch (segment offsets into one payload buffer, outputs at a stride)
+    gives every frame back, with either kernel."""
+    from vcf_amd import _lib as L
+    from vcf_amd.device import DeviceBuffer
+    rng = np.random.Generator(np.random.PCG64(21))
+    n, F, seg = 10_001, 6, 1024
+    frames = [np.clip(np.rint(rng.laplace(128, 0.7 + f, n)), 0, 255).astype(np.uint8) for f in range(F)]
+    enc = T.encode_frames_device(DeviceBuffer.from_array(np.concatenate(frames)), F, n, 0, seg, prior=True)
+    ns = T.n_segments(n, seg)
+    payload = b"".join(e[1] for e in enc)
+    offs, base = [], 0
+    for e in enc:
+        o = np.concatenate([[0], np.cumsum(e[0])]) + base
+        offs.append(o)
+        base += len(e[1])
+    offs = np.concatenate(offs).astype(np.int64)
+    assert offs.size == F * (ns + 1)
+    priors = np.stack([e[2] for e in enc]).astype(np.uint16)
+    src, doffs, dpr = (DeviceBuffer.from_array(np.frombuffer(payload, np.uint8)), DeviceBuffer.from_array(offs),
+                       DeviceBuffer.from_array(priors))
+    stride = n + 3                                   # unaligned output frames
+    out = DeviceBuffer(F * stride)
+    try:
+        L.call("vcf_cbaac_tiled_set_variant", variant)
+        L.call("vcf_cbaac_tiled_decode_frames", src.ptr, doffs.ptr, F, n, 0, dpr.ptr, seg, out.ptr, stride, None)
+        got = out.download(np.empty(F * stride, np.uint8))
+    finally:
+        L.call("vcf_cbaac_tiled_set_variant", 0)
+    for f in range(F):
+        assert np.array_equal(got[f * stride:f * stride + n], frames[f]), f

@@ -81,6 +81,7 @@ SIGNATURES = {
     "vcf_event_record": [_P, _P],
     "vcf_event_sync": [_P],
     "vcf_stream_wait_event": [_P, _P],
+    "vcf_copy_pieces": [_P, _P, _I64, _P, _P],
     "vcf_event_elapsed_ms": [_P, _P, ctypes.POINTER(ctypes.c_float)],
     "vcf_dct_padded_shape": [_I32, _I32, _I32, _PI32, _PI32],
     "vcf_dct_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
@@ -131,7 +132,12 @@ SIGNATURES = {
     "vcf_png_encode_bound": [_I32, _I32],
     "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],
     "vcf_deadzone_dequantize": [_P, _I32, _I64, _I32, _P, _P],
+    "vcf_cbaac_tiled_set_variant": [_I32],
     "vcf_cbaac_tiled_segments": [_I64, _I64],
+    "vcf_cbaac_tiled_frames_workspace": [_I64, _I64, _I64],
+    "vcf_cbaac_tiled_prior_frames": [_P, _I64, _I64, _I64, _P, _P, _P],
+    "vcf_cbaac_tiled_encode_frames": [_P, _I64, _I64, _I64, _I32, _P, _I64, _P, _I64, _P, _P, _P],
+    "vcf_cbaac_tiled_decode_frames": [_P, _P, _I64, _I64, _I32, _P, _I64, _P, _I64, _P],
     "vcf_cbaac_tiled_workspace": [_I64, _I64],
     "vcf_cbaac_tiled_bound": [_I64, _I64],
     "vcf_cbaac_tiled_encode": [_P, _I64, _I32, _I64, _P, _I64, _P, _P, _P],
@@ -183,7 +189,8 @@ def lib():
             L.vcf_cbaac_bound.restype = ctypes.c_int64
             L.vcf_cbahc_bound.restype = ctypes.c_int64
             L.vcf_png_encode_bound.restype = ctypes.c_int64
-            for name in ("vcf_cbaac_tiled_segments", "vcf_cbaac_tiled_workspace", "vcf_cbaac_tiled_bound"):
+            for name in ("vcf_cbaac_tiled_segments", "vcf_cbaac_tiled_workspace", "vcf_cbaac_tiled_bound",
+                         "vcf_cbaac_tiled_frames_workspace"):
                 getattr(L, name).restype = ctypes.c_int64
             _lib = L
     return _lib

@@ -9,9 +9,8 @@ chunk never leaves the GPU until its code-streams are final:
   1. one launch of the fused DCT + deadzone kernel over the rank's chunk
      (vcf_dct_dz_encode), indices stay in HBM;
   2. the GPU entropy stage: every frame's indices coded as a prior-seeded
-     tiled CBAAC stream (`-c TCBAACP`, vcf_amd/tcbaac.py), frames
-     concurrent on library streams; only the small segment index comes to
-     the host;
+     tiled CBAAC stream (`-c TCBAACP`, vcf_amd/tcbaac.py), all frames in
+     one launch per stage; only the small segment index comes to the host;
   3. every frame's container (header + segments, exactly the bytes
      `TiledCBAACCodec.compress_device` returns for it) is assembled in a
      device send buffer;
@@ -32,7 +31,7 @@ import numpy as np
 
 from .. import dct as D
 from .. import tcbaac as T
-from ..device import DeviceBuffer, Stream, copy_dtod
+from ..device import DeviceBuffer, HostBuffer, Stream, copy_dtod, copy_pieces
 from .shard import frame_range
 
 
@@ -50,10 +49,12 @@ class DeviceIII:
         self.n_sym = self.Hp * self.Wp * 3
         self.stream = Stream()
         self.k = DeviceBuffer(max(self.n_local * self.n_sym, 1))
-        self.batch = T.FrameBatch(self.n_local, self.n_sym, 0, seg_len, prior=True, streams=streams)
+        self.batch = T.FrameBatch(self.n_local, self.n_sym, 0, seg_len, prior=True)
         self.send = None
         self.recv = None
         self.hstage = None
+        self.table = None
+        self.host = None
 
     def _buf(self, name: str, nbytes: int) -> DeviceBuffer:
         b = getattr(self, name)
@@ -90,15 +91,25 @@ class DeviceIII:
         nbytes = int(local_sizes.sum())
         send = self._buf("send", nbytes)
         if self.n_local:
+            # headers (staged from the host) and payloads (in the coder's output)
+            # land back to back in the send buffer: two gather-copy launches
             hb = np.frombuffer(b"".join(headers), np.uint8)
             hst = self._buf("hstage", hb.size)
             hst.upload(hb, self.stream)
+            hdr_tab = np.empty((self.n_local, 3), np.int64)
+            pay_tab = np.empty((self.n_local, 3), np.int64)
             off = hoff = 0
             for f, h in enumerate(headers):
-                copy_dtod(send, off, hst, hoff, len(h), self.stream)
-                copy_dtod(send, off + len(h), self.batch.out[f], 0, int(totals[f]), self.stream)
-                off += len(h) + int(totals[f])
+                pbuf, poff, pn = self.batch.payload(f)
+                hdr_tab[f] = (hoff, off, len(h))
+                pay_tab[f] = (poff, off + len(h), pn)
+                off += len(h) + pn
                 hoff += len(h)
+            tab = np.concatenate([hdr_tab, pay_tab]).ravel()
+            tb = self._buf("table", tab.nbytes)
+            tb.upload(tab, self.stream)
+            copy_pieces(hst, tb, self.n_local, send, self.stream)
+            copy_pieces(self.batch.out, _View(tb, hdr_tab.nbytes), self.n_local, send, self.stream)
         t = mark("pack", t)
         sizes = self._all_gather_sizes(local_sizes)
         t = mark("sizes_allgather", t)
@@ -114,7 +125,9 @@ class DeviceIII:
         t = mark("gatherv", t)
         out = None
         if self.rank == 0:
-            blob = np.empty(total, np.uint8)
+            if self.host is None or self.host.nbytes < total:
+                self.host = HostBuffer(total)   # page-locked: the gathered bytes come back at full PCIe speed
+            blob = self.host.array[:total]
             if total:
                 recv.download(blob, self.stream)
             self.stream.synchronize()
@@ -138,3 +151,10 @@ class DeviceIII:
             rlo, rhi = frame_range(self.N, r, self.world)
             out[rlo:rhi] = rows[r, rlo:rhi]
         return out
+
+
+class _View:
+    """A DeviceBuffer-like view `off` bytes into another (what vcf_copy_pieces takes)."""
+
+    def __init__(self, buf: DeviceBuffer, off: int):
+        self.ptr = buf.address(off)

@@ -322,14 +322,29 @@ __device__ __forceinline__ uint32_t load_sym4(const uint8_t *p, int64_t off, int
 
 __device__ __forceinline__ double rcp_exact(uint32_t t) { return rcp_nr((double)t); }
 
+// Frames of a batch (blockIdx.y = frame): frame f's symbols at sym + f *
+// sym_stride, its prior at prior + f * prior_stride (0: one prior for all),
+// its decoded symbols at out + f * out_stride, its packed segments at
+// out + f * cap (encode)
+struct Frames {
+    int64_t sym_stride = 0, prior_stride = 0, out_stride = 0, cap = 0;
+};
+
 template <int ORDER, bool TRACE>
 __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *__restrict__ sym, int64_t n,
                                                                 int64_t seg_len, uint32_t *__restrict__ slots,
                                                                 int64_t slot_words, int64_t *__restrict__ seg_bits,
                                                                 int32_t *__restrict__ trace,
-                                                                const uint16_t *__restrict__ prior)
+                                                                const uint16_t *__restrict__ prior, Frames fr)
 {
     Tables *tabs = Lds<ORDER>::get();
+    {   // frame blockIdx.y of a batch
+        const int64_t f = blockIdx.y, nsf = (n + seg_len - 1) / seg_len;
+        sym += f * fr.sym_stride;
+        slots += f * nsf * slot_words;
+        seg_bits += f * nsf;
+        if (prior) prior += f * fr.prior_stride;
+    }
     const int64_t seg = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     const int64_t start = seg * seg_len;
@@ -436,9 +451,15 @@ template <int ORDER>
 __global__ __launch_bounds__(64) void cbaac_tiled_decode_kernel(const uint8_t *__restrict__ in,
                                                                 const int64_t *__restrict__ offs, int64_t n,
                                                                 int64_t seg_len, uint8_t *__restrict__ out,
-                                                                const uint16_t *__restrict__ prior)
+                                                                const uint16_t *__restrict__ prior, Frames fr)
 {
     Tables *tabs = Lds<ORDER>::get();
+    {
+        const int64_t f = blockIdx.y, nsf = (n + seg_len - 1) / seg_len;
+        offs += f * (nsf + 1);
+        out += f * fr.out_stride;
+        if (prior) prior += f * fr.prior_stride;
+    }
     const int64_t seg = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     const int64_t start = seg * seg_len;
@@ -534,6 +555,9 @@ __global__ __launch_bounds__(1024) void cbaac_tiled_scan_kernel(const int64_t *_
                                                                 int64_t *__restrict__ offs,
                                                                 int64_t *__restrict__ seg_bytes)
 {
+    seg_bits += (int64_t)blockIdx.x * nseg;   // frame blockIdx.x
+    offs += (int64_t)blockIdx.x * (nseg + 1);
+    seg_bytes += (int64_t)blockIdx.x * (nseg + 1);
     __shared__ int64_t part[1024];
     const int t = threadIdx.x;
     const int64_t per = (nseg + 1023) / 1024;
@@ -566,6 +590,10 @@ __global__ __launch_bounds__(256) void cbaac_tiled_pack_kernel(const uint32_t *_
                                                                const int64_t *__restrict__ offs, uint8_t *__restrict__ out,
                                                                int64_t capacity)
 {
+    const int64_t f = blockIdx.y;   // frame of a batch: gridDim.x segments each, out regions `capacity` apart
+    slots += f * (int64_t)gridDim.x * slot_words;
+    offs += f * ((int64_t)gridDim.x + 1);
+    out += f * capacity;
     const int64_t seg = blockIdx.x;
     const uint8_t *src = reinterpret_cast<const uint8_t *>(slots + seg * slot_words);
     const int64_t o = offs[seg], nb = offs[seg + 1] - o;
@@ -575,8 +603,10 @@ __global__ __launch_bounds__(256) void cbaac_tiled_pack_kernel(const uint32_t *_
 
 // order-0 histogram of the frame's symbols (LDS bins, one global atomic per bin and workgroup)
 __global__ __launch_bounds__(256) void cbaac_hist_kernel(const uint8_t *__restrict__ sym, int64_t n,
-                                                         uint32_t *__restrict__ hist)
+                                                         uint32_t *__restrict__ hist, int64_t sym_stride)
 {
+    sym += (int64_t)blockIdx.y * sym_stride;   // frame blockIdx.y
+    hist += 256 * blockIdx.y;
     __shared__ uint32_t bins[256];
     bins[threadIdx.x] = 0;
     __syncthreads();
@@ -589,11 +619,448 @@ __global__ __launch_bounds__(256) void cbaac_hist_kernel(const uint8_t *__restri
 __global__ __launch_bounds__(256) void cbaac_prior_kernel(const uint32_t *__restrict__ hist, int64_t n,
                                                           uint16_t *__restrict__ prior)
 {
+    hist += 256 * blockIdx.x;   // frame blockIdx.x
+    prior += 256 * blockIdx.x;
     const uint32_t t = threadIdx.x;
     prior[t] = (uint16_t)(1u + (n > 0 ? (uint32_t)((uint64_t)hist[t] * kPriorScale / (uint64_t)n) : 0u));
 }
 
+// ---- lane-per-segment coder (order 0) ----------------------------------------------
+// One LANE per segment: a wave codes 64 segments at once, each with its own
+// model and coder state, where the kernels above spend a whole wave on one
+// segment's model.  Same algorithm, same bytes (the A8 coder and
+// AdaptiveModel of CBAAC.py:17-47, 114-131 per segment).
+// The model is two-level, u16 in LDS: C[b] (b = 0..15) = the frequencies of
+// the symbols below 16 b summed (block starts), E[b][j] = those of 16 b ..
+// 16 b + j - 1 (exclusive prefixes inside block b).  get_range(s) = (C[b] +
+// E[b][j], C[b] + E[b][j + 1]) -- at j = 15 the upper end is C[b + 1], or the
+// total at b = 15.  update(s) adds 1 to E[b][t > j] and to C[t > b]: an add
+// of a mask to four 16-byte chunks (u16 entries never carry into the next:
+// every count is below 2^15), and every frequency becomes (f >> 1) + 1 when
+// the stale total reaches max_freq (CBAAC.py:32-36), rebuilt from the
+// prefixes.  LDS units of 16 bytes are laid out [block][half][lane]: the b128
+// accesses of a wave (one block and half per lane) are bank-conflict free.
+constexpr int kLW = 64;   // segments (lanes) per workgroup
+
+struct LaneLds {
+    uint4 E[16][2][kLW];   // [block][half][lane]: entries 8 half .. 8 half + 7 of block `block`
+    uint4 C[2][kLW];       // [half][lane]: block starts 8 half .. 8 half + 7
+    uint4 M[16][2];        // M[i]: 1 in the u16 entries t > i
+    uint4 E0[16][2];       // the initial model, shared
+    uint4 C0[2];
+    uint32_t bsum[16];
+};
+
+__device__ __forceinline__ uint32_t u16_of(const uint4 &v, int k)   // k compile-time
+{
+    const uint32_t d = k < 2 ? v.x : k < 4 ? v.y : k < 6 ? v.z : v.w;
+    return (k & 1) ? d >> 16 : d & 0xFFFFu;
+}
+__device__ __forceinline__ uint4 add4(const uint4 &a, const uint4 &b)
+{
+    return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// the initial model (prior frequencies, or 256 ones) into every lane's copy, the mask table
+__device__ __forceinline__ void lane_model_init(LaneLds &L, const uint16_t *__restrict__ prior, uint32_t lane,
+                                                uint32_t &total)
+{
+    if (lane < 16) {
+        uint32_t acc = 0, e[16];
+        for (int k = 0; k < 16; ++k) {
+            e[k] = acc;
+            acc += prior ? prior[16 * lane + k] : 1u;
+        }
+        L.E0[lane][0] = make_uint4(e[0] | e[1] << 16, e[2] | e[3] << 16, e[4] | e[5] << 16, e[6] | e[7] << 16);
+        L.E0[lane][1] = make_uint4(e[8] | e[9] << 16, e[10] | e[11] << 16, e[12] | e[13] << 16, e[14] | e[15] << 16);
+        L.bsum[lane] = acc;
+    } else if (lane < 48) {   // mask table
+        const int i = (lane - 16) >> 1, h = (lane - 16) & 1;
+        uint32_t d[4];
+        for (int k = 0; k < 4; ++k) {
+            const int t = 8 * h + 2 * k;
+            d[k] = (t > i ? 1u : 0u) | (t + 1 > i ? 0x10000u : 0u);
+        }
+        L.M[i][h] = make_uint4(d[0], d[1], d[2], d[3]);
+    }
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t acc = 0, c[16];
+        for (int b = 0; b < 16; ++b) {
+            c[b] = acc;
+            acc += L.bsum[b];
+        }
+        L.C0[0] = make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
+        L.C0[1] = make_uint4(c[8] | c[9] << 16, c[10] | c[11] << 16, c[12] | c[13] << 16, c[14] | c[15] << 16);
+        L.bsum[0] = acc;   // total (read after the barrier)
+    }
+    __syncthreads();
+    total = L.bsum[0];
+    for (int b = 0; b < 16; ++b) {
+        L.E[b][0][lane] = L.E0[b][0];
+        L.E[b][1][lane] = L.E0[b][1];
+    }
+    L.C[0][lane] = L.C0[0];
+    L.C[1][lane] = L.C0[1];
+}
+
+// every frequency -> (f >> 1) + 1 (CBAAC.py:34-36), from the prefixes; returns the new total
+__device__ __attribute__((noinline)) uint32_t lane_model_rescale(LaneLds &L, uint32_t lane, uint32_t total)
+{
+    uint32_t cs[17];
+    {
+        const uint4 c0 = L.C[0][lane], c1 = L.C[1][lane];
+        const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        for (int k = 0; k < 8; ++k) {
+            cs[2 * k] = w[k] & 0xFFFFu;
+            cs[2 * k + 1] = w[k] >> 16;
+        }
+        cs[16] = total;
+    }
+    uint32_t run = 0, cn[16];
+    for (int b = 0; b < 16; ++b) {
+        const uint4 e0 = L.E[b][0][lane], e1 = L.E[b][1][lane];
+        const uint32_t w[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+        uint32_t e[17];
+        for (int k = 0; k < 8; ++k) {
+            e[2 * k] = w[k] & 0xFFFFu;
+            e[2 * k + 1] = w[k] >> 16;
+        }
+        e[16] = cs[b + 1] - cs[b];
+        cn[b] = run;
+        uint32_t acc = 0, ne[16];
+        for (int t = 0; t < 16; ++t) {
+            ne[t] = acc;
+            acc += ((e[t + 1] - e[t]) >> 1) + 1;
+        }
+        run += acc;
+        L.E[b][0][lane] = make_uint4(ne[0] | ne[1] << 16, ne[2] | ne[3] << 16, ne[4] | ne[5] << 16, ne[6] | ne[7] << 16);
+        L.E[b][1][lane] =
+            make_uint4(ne[8] | ne[9] << 16, ne[10] | ne[11] << 16, ne[12] | ne[13] << 16, ne[14] | ne[15] << 16);
+    }
+    L.C[0][lane] = make_uint4(cn[0] | cn[1] << 16, cn[2] | cn[3] << 16, cn[4] | cn[5] << 16, cn[6] | cn[7] << 16);
+    L.C[1][lane] =
+        make_uint4(cn[8] | cn[9] << 16, cn[10] | cn[11] << 16, cn[12] | cn[13] << 16, cn[14] | cn[15] << 16);
+    return run;
+}
+
+// per-lane MSB-first bit writer: acc holds nb < 32 pending bits at its top, whole
+// words go to the lane's own slot (bitarray endian='big')
+struct LaneBits {
+    uint32_t *out;
+    uint64_t acc = 0;
+    uint32_t nb = 0, words = 0;
+    __device__ __forceinline__ void bits(uint32_t v, uint32_t k)   // the top k bits of v, 1 <= k <= 32
+    {
+        if (k < 32) v &= ~(0xFFFFFFFFu >> k);
+        acc |= (uint64_t)v << (32 - nb);
+        nb += k;
+        if (nb >= 32) {
+            out[words++] = __builtin_bswap32((uint32_t)(acc >> 32));
+            acc <<= 32;
+            nb -= 32;
+        }
+    }
+    __device__ __forceinline__ void run(uint32_t bit, uint32_t count)
+    {
+        const uint32_t v = bit ? 0xFFFFFFFFu : 0u;
+        for (; count >= 32; count -= 32) bits(v, 32);
+        if (count) bits(v, count);
+    }
+};
+
+template <bool PRIOR>
+__global__ __launch_bounds__(kLW) void cbaac_lane_encode_kernel(const uint8_t *__restrict__ sym, int64_t n,
+                                                                int64_t seg_len, int64_t nseg,
+                                                                uint32_t *__restrict__ slots, int64_t slot_words,
+                                                                int64_t *__restrict__ seg_bits,
+                                                                const uint16_t *__restrict__ prior, Frames fr)
+{
+    __shared__ LaneLds L;
+    {   // frame blockIdx.y of a batch (nseg segments each)
+        const int64_t f = blockIdx.y;
+        sym += f * fr.sym_stride;
+        slots += f * nseg * slot_words;
+        seg_bits += f * nseg;
+        if (prior) prior += f * fr.prior_stride;
+    }
+    const uint32_t lane = threadIdx.x;
+    const int64_t seg = (int64_t)blockIdx.x * kLW + lane;
+    const bool act = seg < nseg;
+    const int64_t start = act ? seg * seg_len : 0;
+    const int64_t len = act ? (n - start < seg_len ? n - start : seg_len) : 0;
+    uint32_t total;
+    lane_model_init(L, PRIOR ? prior : nullptr, lane, total);
+    double inv = rcp_nr((double)total);
+    LaneBits w;
+    w.out = slots + (act ? seg : 0) * slot_words;
+    uint32_t low = 0, high = 0xFFFFFFFFu, pending = 0;
+    const uint8_t *src = sym + start;
+    const bool aligned = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+    auto load16 = [&](int64_t off) -> uint4 {   // symbols off .. off + 15 (zeros past the segment)
+        if (aligned && off + 16 <= len) return *reinterpret_cast<const uint4 *>(src + off);
+        uint32_t d[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 16; ++k)
+            if (off + k < len) d[k >> 2] |= (uint32_t)src[off + k] << (8 * (k & 3));
+        return make_uint4(d[0], d[1], d[2], d[3]);
+    };
+    const int64_t seg0 = (int64_t)blockIdx.x * kLW;
+    const int64_t wave_len = n - seg0 * seg_len < seg_len ? n - seg0 * seg_len : seg_len;   // the longest lane's
+    uint4 cur = load16(0);
+    char *const Eb = reinterpret_cast<char *>(&L.E[0][0][lane]);
+    char *const Cb = reinterpret_cast<char *>(&L.C[0][lane]);
+    constexpr uint32_t kHalfStride = kLW * 16;   // bytes from (b, half) to (b, half + 1) of a lane
+    // get_range(s) of the model as it stands (u16 reads of the lane's tables)
+    auto query = [&](uint32_t s, uint32_t tot, uint32_t &lo, uint32_t &hi) {
+        const uint32_t b = s >> 4, j = s & 15u, j1 = j < 15 ? j + 1 : 15, b1 = b < 15 ? b + 1 : 15;
+        const uint32_t eb = b * (2 * kHalfStride);
+        const uint32_t e_lo = *reinterpret_cast<const uint16_t *>(Eb + eb + (j >> 3) * kHalfStride + (j & 7) * 2);
+        const uint32_t e_hi = *reinterpret_cast<const uint16_t *>(Eb + eb + (j1 >> 3) * kHalfStride + (j1 & 7) * 2);
+        const uint32_t c_lo = *reinterpret_cast<const uint16_t *>(Cb + (b >> 3) * kHalfStride + (b & 7) * 2);
+        const uint32_t c_hi = *reinterpret_cast<const uint16_t *>(Cb + (b1 >> 3) * kHalfStride + (b1 & 7) * 2);
+        lo = c_lo + e_lo;
+        hi = j < 15 ? c_lo + e_hi : (b < 15 ? c_hi : tot);
+    };
+    // Software pipeline: symbol i+1's range is read from the model BEFORE
+    // symbol i's update and corrected afterwards (the update adds one to every
+    // cumulative count above s_i and to the total): get_range(s') after
+    // update(s) = (cum[s'] + [s' > s], cum[s' + 1] + [s' >= s]), total + 1.
+    // So the model's LDS round trips run beside the coder's arithmetic chain,
+    // not in front of it.  A rescale (the stale total at max_freq) reads again.
+    uint32_t s_cur = cur.x & 0xFFu, lo_cur = 0, hi_cur = 0;
+    if (len > 0) query(s_cur, total, lo_cur, hi_cur);
+    for (int64_t off = 0; off < wave_len; off += 16) {
+        const uint4 nxt = off + 16 < wave_len ? load16(off + 16) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (off + k < len) {
+                const uint32_t s = s_cur;
+                const uint32_t s_n = k < 15 ? ((k + 1 < 4 ? cur.x : k + 1 < 8 ? cur.y : k + 1 < 12 ? cur.z : cur.w) >>
+                                               (8 * ((k + 1) & 3))) & 0xFFu
+                                            : nxt.x & 0xFFu;
+                const bool more = off + k + 1 < len;
+                const uint32_t b = s >> 4, j = s & 15u;
+                const uint32_t tot_i = total;
+                const bool resc = tot_i >= kMaxFreq;            // the stale total (CBAAC.py:34)
+                const double inv_n = rcp_nr((double)(tot_i + 1));   // the next symbol's, off the chain
+                uint32_t lo_n = 0, hi_n = 0;
+                if (more) query(s_n, tot_i, lo_n, hi_n);         // before this symbol's update
+                // update(s): the four chunks plus the mask rows
+                const uint4 e0 = L.E[b][0][lane], e1 = L.E[b][1][lane];
+                const uint4 c0 = L.C[0][lane], c1 = L.C[1][lane];
+                const uint4 mj0 = L.M[j][0], mj1 = L.M[j][1], mb0 = L.M[b][0], mb1 = L.M[b][1];
+                L.E[b][0][lane] = add4(e0, mj0);
+                L.E[b][1][lane] = add4(e1, mj1);
+                L.C[0][lane] = add4(c0, mb0);
+                L.C[1][lane] = add4(c1, mb1);
+                // the A8 interval update (the wave kernel's Encoder::code, per lane)
+                const double rng = (double)(high - low) + 1.0, tot = (double)tot_i;
+                const double qh = floordiv(rng * (double)hi_cur, tot, inv);
+                const double ql = floordiv(rng * (double)lo_cur, tot, inv);
+                high = low + (uint32_t)(qh - 1.0);
+                low = low + (uint32_t)ql;
+                const uint32_t d = __builtin_clz(low ^ high);
+                if (d) {
+                    const uint32_t bit = low >> 31;
+                    w.bits(low, 1);
+                    w.run(bit ^ 1u, pending);
+                    pending = 0;
+                    if (d > 1) w.bits(low << 1, d - 1);
+                    low <<= d;
+                    high = (high << d) | ((1u << d) - 1u);
+                }
+                const uint32_t x = (low << 1) & ~(high << 1);
+                const uint32_t p = __builtin_clz(~x);
+                if (p) {
+                    pending += p;
+                    low = (low << p) & 0x7FFFFFFFu;
+                    high = (high << p) | ((1u << p) - 1u) | 0x80000000u;
+                }
+                total = tot_i + 1;
+                lo_n += s_n > s ? 1u : 0u;
+                hi_n += s_n >= s ? 1u : 0u;
+                inv = inv_n;
+                if (resc) {   // rare: every frequency halved, read the next range again
+                    total = lane_model_rescale(L, lane, total);
+                    inv = rcp_nr((double)total);
+                    if (more) query(s_n, total, lo_n, hi_n);
+                }
+                s_cur = s_n;
+                lo_cur = lo_n;
+                hi_cur = hi_n;
+            }
+        }
+        cur = nxt;
+    }
+    if (act) {
+        const uint32_t bit = low < kQ1 ? 0u : 1u;   // flush (CBAAC.py:130 -> A8)
+        w.bits(bit << 31, 1);
+        w.run(bit ^ 1u, pending + 1);
+        if (w.nb) w.out[w.words] = __builtin_bswap32((uint32_t)(w.acc >> 32));
+        seg_bits[seg] = (int64_t)w.words * 32 + w.nb;
+    }
+}
+
+// floor(a / t) for integers a < 2^47, 1 <= t <= 2^32 held exactly in doubles,
+// inv ~= 1/t: the quotient estimate is within one of the floor, the remainder
+// (an exact fma) says which way
+__device__ __forceinline__ double floordiv_big(double a, double t, double inv)
+{
+    double q = __builtin_trunc(a * inv);
+    const double r = __builtin_fma(-q, t, a);
+    q = r < 0.0 ? q - 1.0 : (r >= t ? q + 1.0 : q);
+    return q;
+}
+
+// the 16 u16 entries of (a, b): how many are <= v (entries start at 0 and
+// increase strictly), the last of those and the first above v (`none` if none)
+__device__ __forceinline__ void scan16(const uint4 &a, const uint4 &b, uint32_t v, uint32_t none, uint32_t &cnt,
+                                       uint32_t &le, uint32_t &gt)
+{
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    cnt = 0;
+    le = 0;
+    gt = none;
+#pragma unroll
+    for (int t = 15; t >= 0; --t) {
+        const uint32_t x = (t & 1) ? w[t >> 1] >> 16 : w[t >> 1] & 0xFFFFu;
+        const bool in = x <= v;
+        cnt += in ? 1u : 0u;
+        gt = in ? gt : x;
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const uint32_t x = (t & 1) ? w[t >> 1] >> 16 : w[t >> 1] & 0xFFFFu;
+        le = x <= v ? x : le;
+    }
+}
+
+// per-lane MSB-first bit reader over a segment's bytes, zeros past its end (A8)
+struct LaneReader {
+    const uint8_t *p;
+    int64_t nbytes, pos = 0;
+    uint64_t buf = 0;
+    uint32_t avail = 0;
+    __device__ __forceinline__ void refill()
+    {
+        while (avail <= 56) {
+            const uint32_t byte = pos < nbytes ? p[pos] : 0u;
+            buf |= (uint64_t)byte << (56 - avail);
+            ++pos;
+            avail += 8;
+        }
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t k)   // 1 <= k <= 32, right-aligned
+    {
+        if (avail < k) refill();
+        const uint32_t v = (uint32_t)(buf >> (64 - k));
+        buf <<= k;
+        avail -= k;
+        return v;
+    }
+};
+
+template <bool PRIOR>
+__global__ __launch_bounds__(kLW) void cbaac_lane_decode_kernel(const uint8_t *__restrict__ in,
+                                                                const int64_t *__restrict__ offs, int64_t n,
+                                                                int64_t seg_len, int64_t nseg,
+                                                                uint8_t *__restrict__ out,
+                                                                const uint16_t *__restrict__ prior, Frames fr)
+{
+    __shared__ LaneLds L;
+    {
+        const int64_t f = blockIdx.y;
+        offs += f * (nseg + 1);
+        out += f * fr.out_stride;
+        if (prior) prior += f * fr.prior_stride;
+    }
+    const uint32_t lane = threadIdx.x;
+    const int64_t seg = (int64_t)blockIdx.x * kLW + lane;
+    const bool act = seg < nseg;
+    const int64_t start = act ? seg * seg_len : 0;
+    const int64_t len = act ? (n - start < seg_len ? n - start : seg_len) : 0;
+    uint32_t total;
+    lane_model_init(L, PRIOR ? prior : nullptr, lane, total);
+    double tinv = 1.0 / (double)total;   // (unused until the first symbol; recomputed per symbol)
+    (void)tinv;
+    LaneReader br;
+    br.p = in + (act ? offs[seg] : 0);
+    br.nbytes = act ? offs[seg + 1] - offs[seg] : 0;
+    uint32_t low = 0, high = 0xFFFFFFFFu, value = br.get(32);
+    uint8_t *dst = out + start;
+    const bool aligned = (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
+    uint4 c0 = L.C[0][lane], c1 = L.C[1][lane];
+    const int64_t seg0 = (int64_t)blockIdx.x * kLW;
+    const int64_t wave_len = n - seg0 * seg_len < seg_len ? n - seg0 * seg_len : seg_len;
+    for (int64_t off = 0; off < wave_len; off += 16) {
+        uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (off + k < len) {
+                const double rng = (double)(high - low) + 1.0, tot = (double)total;
+                const uint32_t T = value - low;
+                const double scaled = floordiv_big(((double)T + 1.0) * tot - 1.0, rng, rcp_nr(rng));
+                const uint32_t sv = (uint32_t)scaled;
+                uint32_t nb, cb, cb1;
+                scan16(c0, c1, sv, total, nb, cb, cb1);   // C lives in registers: no LDS round trip
+                const uint32_t b = nb - 1;
+                const uint4 e0 = L.E[b][0][lane], e1 = L.E[b][1][lane];
+                const uint4 mb0 = L.M[b][0], mb1 = L.M[b][1];
+                uint32_t nj, elo, ehi;
+                scan16(e0, e1, sv - cb, cb1 - cb, nj, elo, ehi);
+                const uint32_t j = nj - 1;
+                const uint32_t lo = cb + elo, hi = cb + ehi;
+                const uint4 mj0 = L.M[j][0], mj1 = L.M[j][1];
+                const double inv = rcp_nr(tot);
+                const double qh = floordiv(rng * (double)hi, tot, inv);
+                const double ql = floordiv(rng * (double)lo, tot, inv);
+                high = low + (uint32_t)(qh - 1.0);
+                low = low + (uint32_t)ql;
+                const uint32_t d = __builtin_clz(low ^ high);
+                if (d) {
+                    low <<= d;
+                    high = (high << d) | ((1u << d) - 1u);
+                    value = (value << d) | br.get(d);
+                }
+                const uint32_t x = (low << 1) & ~(high << 1);
+                const uint32_t p = __builtin_clz(~x);
+                if (p) {
+                    low = (low << p) & 0x7FFFFFFFu;
+                    high = (high << p) | ((1u << p) - 1u) | 0x80000000u;
+                    value = ((value << p) ^ 0x80000000u) | br.get(p);
+                }
+                L.E[b][0][lane] = add4(e0, mj0);
+                L.E[b][1][lane] = add4(e1, mj1);
+                c0 = add4(c0, mb0);
+                c1 = add4(c1, mb1);
+                const uint32_t stale = total++;
+                if (stale >= kMaxFreq) {   // rare: the rebuild reads and writes C through LDS
+                    L.C[0][lane] = c0;
+                    L.C[1][lane] = c1;
+                    total = lane_model_rescale(L, lane, total);
+                    c0 = L.C[0][lane];
+                    c1 = L.C[1][lane];
+                }
+                o[k >> 2] |= (16 * b + j) << (8 * (k & 3));
+            }
+        }
+        if (off < len) {
+            if (aligned && off + 16 <= len) {
+                *reinterpret_cast<uint4 *>(dst + off) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
+                for (int k = 0; k < 16; ++k)
+                    if (off + k < len) dst[off + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+            }
+        }
+    }
+}
+
 int64_t slot_words_for(int64_t seg_len) { return (vcf_cbaac_bound(seg_len) + 3) / 4; }
+
+// 0 = automatic (order 0: one lane per segment from kLaneMinSegments segments
+// on), 1 = one wave per segment, 2 = one lane per segment (order 0; A/B)
+int g_tiled_variant = 0;
+constexpr int64_t kLaneMinSegments = 2048;
 
 int check_args(int64_t n, int32_t order, int64_t seg_len)
 {
@@ -610,6 +1077,13 @@ int check_args(int64_t n, int32_t order, int64_t seg_len)
 using namespace vcf;
 
 extern "C" {
+
+int vcf_cbaac_tiled_set_variant(int32_t variant)
+{
+    if (variant < 0 || variant > 2) return set_error(VCF_ERR_INVALID, "tiled CBAAC variant %d (0, 1, 2)", variant);
+    g_tiled_variant = variant;
+    return VCF_OK;
+}
 
 int64_t vcf_cbaac_tiled_segments(int64_t n, int64_t seg_len)
 {
@@ -630,31 +1104,54 @@ int64_t vcf_cbaac_tiled_bound(int64_t n, int64_t seg_len)
     return vcf_cbaac_tiled_segments(n, seg_len) * slot_words_for(seg_len > 0 ? seg_len : 1) * 4;
 }
 
-static int tiled_encode(const uint8_t *sym_dev, int64_t n, int32_t order, int64_t seg_len, uint8_t *out_dev,
-                        int64_t out_capacity, int64_t *seg_bytes_dev, int32_t *trace_dev, void *ws_dev,
-                        void *stream, const uint16_t *prior_dev = nullptr)
+int64_t vcf_cbaac_tiled_frames_workspace(int64_t n_frames, int64_t frame_symbols, int64_t seg_len)
+{
+    return n_frames <= 0 ? 0 : n_frames * vcf_cbaac_tiled_workspace(frame_symbols, seg_len);
+}
+
+// one lane per segment when there are enough segments to fill waves with them
+// (a lane codes a symbol in about twice a wave's time, but 64 segments at once)
+static bool use_lanes(int32_t order, int64_t total_segments)
+{
+    if (order != 0 || g_tiled_variant == 1) return false;
+    return g_tiled_variant == 2 || total_segments >= kLaneMinSegments;
+}
+
+static int tiled_encode(const uint8_t *sym_dev, int64_t n_frames, int64_t n, int64_t sym_stride, int32_t order,
+                        int64_t seg_len, uint8_t *out_dev, int64_t out_capacity, int64_t *seg_bytes_dev,
+                        int32_t *trace_dev, void *ws_dev, void *stream, const uint16_t *prior_dev = nullptr,
+                        int64_t prior_stride = 0)
 {
     if (int s = check_args(n, order, seg_len)) return s;
+    if (n_frames < 1 || n_frames > 65535) return set_error(VCF_ERR_INVALID, "n_frames %lld (1 .. 65535)", (long long)n_frames);
     const int64_t ns = vcf_cbaac_tiled_segments(n, seg_len);
     if (!seg_bytes_dev) return set_error(VCF_ERR_INVALID, "null seg_bytes");
     hipStream_t st = (hipStream_t)stream;
-    if (ns == 0) return hip_check(hipMemsetAsync(seg_bytes_dev, 0, 8, st), "hipMemsetAsync");
+    if (ns == 0) return hip_check(hipMemsetAsync(seg_bytes_dev, 0, 8 * n_frames, st), "hipMemsetAsync");
     if (!sym_dev || !ws_dev || (!trace_dev && !out_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
     if (ns > 0x7FFFFFFF) return set_error(VCF_ERR_INVALID, "too many segments");
     const int64_t sw = slot_words_for(seg_len);
     uint32_t *slots = (uint32_t *)ws_dev;
-    int64_t *bits = (int64_t *)(slots + ns * sw);
-    int64_t *offs = bits + ns;
-    const dim3 grid((unsigned)ns);
-    if (trace_dev) {
-        if (order == 0) cbaac_tiled_encode_kernel<0, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev, prior_dev);
-        else cbaac_tiled_encode_kernel<1, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev, prior_dev);
+    int64_t *bits = (int64_t *)(slots + n_frames * ns * sw);
+    int64_t *offs = bits + n_frames * ns;
+    Frames fr;
+    fr.sym_stride = sym_stride;
+    fr.prior_stride = prior_stride;
+    const dim3 grid((unsigned)ns, (unsigned)n_frames);
+    if (!trace_dev && use_lanes(order, ns * n_frames)) {   // one lane per segment
+        const dim3 lg((unsigned)((ns + kLW - 1) / kLW), (unsigned)n_frames);
+        if (prior_dev) cbaac_lane_encode_kernel<true><<<lg, kLW, 0, st>>>(sym_dev, n, seg_len, ns, slots, sw, bits, prior_dev, fr);
+        else cbaac_lane_encode_kernel<false><<<lg, kLW, 0, st>>>(sym_dev, n, seg_len, ns, slots, sw, bits, nullptr, fr);
+    } else if (trace_dev) {
+        if (n_frames != 1) return set_error(VCF_ERR_INVALID, "traces take one frame");
+        if (order == 0) cbaac_tiled_encode_kernel<0, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev, prior_dev, fr);
+        else cbaac_tiled_encode_kernel<1, true><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, trace_dev, prior_dev, fr);
     } else {
-        if (order == 0) cbaac_tiled_encode_kernel<0, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr, prior_dev);
-        else cbaac_tiled_encode_kernel<1, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr, prior_dev);
+        if (order == 0) cbaac_tiled_encode_kernel<0, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr, prior_dev, fr);
+        else cbaac_tiled_encode_kernel<1, false><<<grid, 64, 0, st>>>(sym_dev, n, seg_len, slots, sw, bits, nullptr, prior_dev, fr);
     }
     if (int s = hip_check(hipGetLastError(), "cbaac_tiled_encode_kernel")) return s;
-    cbaac_tiled_scan_kernel<<<1, 1024, 0, st>>>(bits, ns, offs, seg_bytes_dev);
+    cbaac_tiled_scan_kernel<<<(unsigned)n_frames, 1024, 0, st>>>(bits, ns, offs, seg_bytes_dev);
     if (int s = hip_check(hipGetLastError(), "cbaac_tiled_scan_kernel")) return s;
     if (out_dev) {
         cbaac_tiled_pack_kernel<<<grid, 256, 0, st>>>(slots, sw, offs, out_dev, out_capacity);
@@ -668,51 +1165,73 @@ int vcf_cbaac_tiled_encode(const uint8_t *sym_dev, int64_t n, int32_t order, int
 {
     if (out_capacity < 0) return set_error(VCF_ERR_INVALID, "negative capacity");
     if (n > 0 && !out_dev) return set_error(VCF_ERR_INVALID, "null output buffer");
-    return tiled_encode(sym_dev, n, order, seg_len, out_dev, out_capacity, seg_bytes_dev, nullptr, ws_dev, stream);
+    return tiled_encode(sym_dev, 1, n, 0, order, seg_len, out_dev, out_capacity, seg_bytes_dev, nullptr, ws_dev,
+                        stream);
 }
 
 int vcf_cbaac_tiled_trace(const uint8_t *sym_dev, int64_t n, int32_t order, int64_t seg_len, int32_t *triples_dev,
                           int64_t *seg_bytes_dev, void *ws_dev, void *stream)
 {
     if (n > 0 && !triples_dev) return set_error(VCF_ERR_INVALID, "null trace buffer");
-    return tiled_encode(sym_dev, n, order, seg_len, nullptr, 0, seg_bytes_dev, triples_dev, ws_dev, stream);
+    return tiled_encode(sym_dev, 1, n, 0, order, seg_len, nullptr, 0, seg_bytes_dev, triples_dev, ws_dev, stream);
 }
 
-static int tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
-                        int64_t seg_len, uint8_t *sym_dev, void *stream, const uint16_t *prior_dev)
+static int tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n_frames, int64_t n,
+                        int32_t order, int64_t seg_len, uint8_t *sym_dev, int64_t out_stride, void *stream,
+                        const uint16_t *prior_dev, int64_t prior_stride)
 {
     if (int s = check_args(n, order, seg_len)) return s;
+    if (n_frames < 1 || n_frames > 65535) return set_error(VCF_ERR_INVALID, "n_frames %lld (1 .. 65535)", (long long)n_frames);
     const int64_t ns = vcf_cbaac_tiled_segments(n, seg_len);
     if (ns == 0) return VCF_OK;
     if (!in_dev || !seg_offsets_dev || !sym_dev) return set_error(VCF_ERR_INVALID, "null buffer");
     if (ns > 0x7FFFFFFF) return set_error(VCF_ERR_INVALID, "too many segments");
     hipStream_t st = (hipStream_t)stream;
-    const dim3 grid((unsigned)ns);
-    if (order == 0) cbaac_tiled_decode_kernel<0><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev, prior_dev);
-    else cbaac_tiled_decode_kernel<1><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev, prior_dev);
+    Frames fr;
+    fr.out_stride = out_stride;
+    fr.prior_stride = prior_stride;
+    const dim3 grid((unsigned)ns, (unsigned)n_frames);
+    if (use_lanes(order, ns * n_frames)) {   // one lane per segment
+        const dim3 lg((unsigned)((ns + kLW - 1) / kLW), (unsigned)n_frames);
+        if (prior_dev)
+            cbaac_lane_decode_kernel<true><<<lg, kLW, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, ns, sym_dev, prior_dev, fr);
+        else
+            cbaac_lane_decode_kernel<false><<<lg, kLW, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, ns, sym_dev, nullptr, fr);
+        return hip_check(hipGetLastError(), "cbaac_lane_decode_kernel");
+    }
+    if (order == 0) cbaac_tiled_decode_kernel<0><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev, prior_dev, fr);
+    else cbaac_tiled_decode_kernel<1><<<grid, 64, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, sym_dev, prior_dev, fr);
     return hip_check(hipGetLastError(), "cbaac_tiled_decode_kernel");
 }
 
 int vcf_cbaac_tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n, int32_t order,
                            int64_t seg_len, uint8_t *sym_dev, void *stream)
 {
-    return tiled_decode(in_dev, seg_offsets_dev, n, order, seg_len, sym_dev, stream, nullptr);
+    return tiled_decode(in_dev, seg_offsets_dev, 1, n, order, seg_len, sym_dev, 0, stream, nullptr, 0);
+}
+
+static int tiled_prior(const uint8_t *sym_dev, int64_t n_frames, int64_t n, int64_t sym_stride, uint16_t *prior_dev,
+                       uint32_t *hist_dev, void *stream)
+{
+    if (n < 0) return set_error(VCF_ERR_INVALID, "negative symbol count");
+    if (n_frames < 1 || n_frames > 65535) return set_error(VCF_ERR_INVALID, "n_frames %lld (1 .. 65535)", (long long)n_frames);
+    if (!prior_dev || !hist_dev || (n > 0 && !sym_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
+    if (reinterpret_cast<uintptr_t>(prior_dev) & 7) return set_error(VCF_ERR_INVALID, "prior_dev not 8-byte aligned");
+    hipStream_t st = (hipStream_t)stream;
+    if (int s = hip_check(hipMemsetAsync(hist_dev, 0, 256 * sizeof(uint32_t) * n_frames, st), "hipMemsetAsync"))
+        return s;
+    if (n > 0) {
+        const int64_t blocks = std::min<int64_t>((n + 4095) / 4096, 2048);
+        cbaac_hist_kernel<<<dim3((unsigned)blocks, (unsigned)n_frames), 256, 0, st>>>(sym_dev, n, hist_dev, sym_stride);
+        if (int s = hip_check(hipGetLastError(), "cbaac_hist_kernel")) return s;
+    }
+    cbaac_prior_kernel<<<(unsigned)n_frames, 256, 0, st>>>(hist_dev, n, prior_dev);
+    return hip_check(hipGetLastError(), "cbaac_prior_kernel");
 }
 
 int vcf_cbaac_tiled_prior(const uint8_t *sym_dev, int64_t n, uint16_t *prior_dev, uint32_t *hist_dev, void *stream)
 {
-    if (n < 0) return set_error(VCF_ERR_INVALID, "negative symbol count");
-    if (!prior_dev || !hist_dev || (n > 0 && !sym_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
-    if (reinterpret_cast<uintptr_t>(prior_dev) & 7) return set_error(VCF_ERR_INVALID, "prior_dev not 8-byte aligned");
-    hipStream_t st = (hipStream_t)stream;
-    if (int s = hip_check(hipMemsetAsync(hist_dev, 0, 256 * sizeof(uint32_t), st), "hipMemsetAsync")) return s;
-    if (n > 0) {
-        const int64_t blocks = std::min<int64_t>((n + 4095) / 4096, 2048);
-        cbaac_hist_kernel<<<(unsigned)blocks, 256, 0, st>>>(sym_dev, n, hist_dev);
-        if (int s = hip_check(hipGetLastError(), "cbaac_hist_kernel")) return s;
-    }
-    cbaac_prior_kernel<<<1, 256, 0, st>>>(hist_dev, n, prior_dev);
-    return hip_check(hipGetLastError(), "cbaac_prior_kernel");
+    return tiled_prior(sym_dev, 1, n, 0, prior_dev, hist_dev, stream);
 }
 
 int vcf_cbaac_tiled_encode_prior(const uint8_t *sym_dev, int64_t n, int32_t order, const uint16_t *prior_dev,
@@ -722,7 +1241,7 @@ int vcf_cbaac_tiled_encode_prior(const uint8_t *sym_dev, int64_t n, int32_t orde
     if (out_capacity < 0) return set_error(VCF_ERR_INVALID, "negative capacity");
     if (n > 0 && (!out_dev || !prior_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
     if (reinterpret_cast<uintptr_t>(prior_dev) & 7) return set_error(VCF_ERR_INVALID, "prior_dev not 8-byte aligned");
-    return tiled_encode(sym_dev, n, order, seg_len, out_dev, out_capacity, seg_bytes_dev, nullptr, ws_dev, stream,
+    return tiled_encode(sym_dev, 1, n, 0, order, seg_len, out_dev, out_capacity, seg_bytes_dev, nullptr, ws_dev, stream,
                         prior_dev);
 }
 
@@ -731,7 +1250,37 @@ int vcf_cbaac_tiled_decode_prior(const uint8_t *in_dev, const int64_t *seg_offse
 {
     if (n > 0 && !prior_dev) return set_error(VCF_ERR_INVALID, "null prior");
     if (reinterpret_cast<uintptr_t>(prior_dev) & 7) return set_error(VCF_ERR_INVALID, "prior_dev not 8-byte aligned");
-    return tiled_decode(in_dev, seg_offsets_dev, n, order, seg_len, sym_dev, stream, prior_dev);
+    return tiled_decode(in_dev, seg_offsets_dev, 1, n, order, seg_len, sym_dev, 0, stream, prior_dev, 0);
+}
+
+// ---- batches of frames: one launch per stage for all of them -------------------------
+int vcf_cbaac_tiled_prior_frames(const uint8_t *sym_dev, int64_t n_frames, int64_t frame_symbols,
+                                 int64_t frame_stride, uint16_t *priors_dev, uint32_t *hist_dev, void *stream)
+{
+    return tiled_prior(sym_dev, n_frames, frame_symbols, frame_stride, priors_dev, hist_dev, stream);
+}
+
+int vcf_cbaac_tiled_encode_frames(const uint8_t *sym_dev, int64_t n_frames, int64_t frame_symbols,
+                                  int64_t frame_stride, int32_t order, const uint16_t *priors_dev, int64_t seg_len,
+                                  uint8_t *out_dev, int64_t out_frame_capacity, int64_t *seg_bytes_dev, void *ws_dev,
+                                  void *stream)
+{
+    if (out_frame_capacity < 0) return set_error(VCF_ERR_INVALID, "negative capacity");
+    if (frame_symbols > 0 && !out_dev) return set_error(VCF_ERR_INVALID, "null output buffer");
+    if (priors_dev && (reinterpret_cast<uintptr_t>(priors_dev) & 7))
+        return set_error(VCF_ERR_INVALID, "priors_dev not 8-byte aligned");
+    return tiled_encode(sym_dev, n_frames, frame_symbols, frame_stride, order, seg_len, out_dev, out_frame_capacity,
+                        seg_bytes_dev, nullptr, ws_dev, stream, priors_dev, priors_dev ? 256 : 0);
+}
+
+int vcf_cbaac_tiled_decode_frames(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n_frames,
+                                  int64_t frame_symbols, int32_t order, const uint16_t *priors_dev, int64_t seg_len,
+                                  uint8_t *sym_dev, int64_t out_frame_stride, void *stream)
+{
+    if (priors_dev && (reinterpret_cast<uintptr_t>(priors_dev) & 7))
+        return set_error(VCF_ERR_INVALID, "priors_dev not 8-byte aligned");
+    return tiled_decode(in_dev, seg_offsets_dev, n_frames, frame_symbols, order, seg_len, sym_dev, out_frame_stride,
+                        stream, priors_dev, priors_dev ? 256 : 0);
 }
 
 }  // extern "C"

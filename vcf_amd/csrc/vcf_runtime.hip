@@ -141,6 +141,34 @@ int vcf_event_sync(void *event)
     return hip_check(hipEventSynchronize((hipEvent_t)event), "hipEventSynchronize");
 }
 
+// piece p: table[3p] = source offset, table[3p + 1] = destination offset,
+// table[3p + 2] = bytes; one workgroup per piece, dword copies when aligned
+__global__ __launch_bounds__(256) void copy_pieces_kernel(const uint8_t *__restrict__ src,
+                                                          const int64_t *__restrict__ table,
+                                                          uint8_t *__restrict__ dst)
+{
+    const int64_t so = table[3 * blockIdx.x], d = table[3 * blockIdx.x + 1], nb = table[3 * blockIdx.x + 2];
+    const uint8_t *s = src + so;
+    uint8_t *o = dst + d;
+    if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(o)) & 3) == 0) {
+        const int64_t nw = nb >> 2;
+        for (int64_t i = threadIdx.x; i < nw; i += 256)
+            reinterpret_cast<uint32_t *>(o)[i] = reinterpret_cast<const uint32_t *>(s)[i];
+        for (int64_t i = 4 * nw + threadIdx.x; i < nb; i += 256) o[i] = s[i];
+    } else {
+        for (int64_t i = threadIdx.x; i < nb; i += 256) o[i] = s[i];
+    }
+}
+
+int vcf_copy_pieces(const uint8_t *src_dev, const int64_t *table_dev, int64_t n_pieces, uint8_t *dst_dev, void *stream)
+{
+    if (n_pieces < 0 || n_pieces > 0x7FFFFFFF) return vcf::set_error(VCF_ERR_INVALID, "piece count");
+    if (n_pieces == 0) return VCF_OK;
+    if (!src_dev || !table_dev || !dst_dev) return vcf::set_error(VCF_ERR_INVALID, "null buffer");
+    copy_pieces_kernel<<<(unsigned)n_pieces, 256, 0, (hipStream_t)stream>>>(src_dev, table_dev, dst_dev);
+    return hip_check(hipGetLastError(), "copy_pieces_kernel");
+}
+
 int vcf_stream_wait_event(void *stream, void *event)
 {
     return hip_check(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0), "hipStreamWaitEvent");

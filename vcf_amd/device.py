@@ -137,3 +137,32 @@ def copy_dtod(dst: DeviceBuffer, dst_off: int, src: DeviceBuffer, src_off: int, 
     if dst_off + nbytes > dst.nbytes or src_off + nbytes > src.nbytes:
         raise ValueError("device copy out of bounds")
     call("vcf_memcpy_dtod", dst.address(dst_off), src.address(src_off), int(nbytes), _h(stream))
+
+
+class HostBuffer:
+    """Page-locked host memory (hipHostMalloc): full-speed copies to and from
+    the device; `array` is a uint8 view."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        call("vcf_host_alloc", ctypes.byref(p), max(1, self.nbytes))
+        self.ptr = p
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, self.nbytes)).from_address(p.value))[:self.nbytes]
+
+    def free(self) -> None:
+        if self.ptr is not None and self.ptr.value:
+            lib().vcf_host_free(self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def copy_pieces(src: DeviceBuffer, table: DeviceBuffer, n_pieces: int, dst: DeviceBuffer, stream=None) -> None:
+    """n_pieces device copies in one launch (vcf_copy_pieces): table = int64
+    (src offset, dst offset, bytes) triples in device memory."""
+    call("vcf_copy_pieces", src.ptr, table.ptr, int(n_pieces), dst.ptr, _h(stream))

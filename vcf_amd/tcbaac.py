@@ -196,15 +196,18 @@ def check_prior(prior) -> np.ndarray:
 
 class FrameBatch:
     """Reusable device state for coding `n_frames` frames of `frame_symbols`
-    symbols each (the III driver's per-rank chunk), keeping every frame's
-    code-stream in HBM: per frame an output slot, its segment sizes and prior
-    (one contiguous device array each, so one download returns them all);
-    per library stream a workspace (frames on one stream run one after the
-    other).  launch() enqueues every frame, sizes() waits and downloads the
-    small index, device_payload(f) / download() hand out the code-streams."""
+    symbols each (the III driver's per-rank chunk), every frame's code-stream
+    kept in HBM.  One launch per stage codes all the frames
+    (vcf_cbaac_tiled_*_frames): a frame's few hundred segments alone leave most
+    of the chip idle, a batch's segments fill it (and with 2048 or more, order
+    0 codes one segment per lane).  Frame f's packed segments sit at byte
+    f * cap of `out`, its segment sizes and prior in one contiguous device
+    array each, so one download returns the index.  launch() enqueues,
+    sizes() waits and downloads the index, payload(f) / download() hand out
+    the code-streams."""
 
     def __init__(self, n_frames: int, frame_symbols: int, order: int = 0, seg_len: int = PRIOR_SEG,
-                 prior: bool = True, streams: int = 4):
+                 prior: bool = True, streams: int | None = None):
         lib = L.lib()
         self.n_frames, self.n = int(n_frames), int(frame_symbols)
         self.order, self.seg_len, self.prior = int(order), int(seg_len), bool(prior)
@@ -212,71 +215,65 @@ class FrameBatch:
             raise NotImplementedError("prior-seeded tiled CBAAC: orders 0 and 1")
         self.ns = n_segments(self.n, self.seg_len)
         self.cap = int(lib.vcf_cbaac_tiled_bound(self.n, self.seg_len))
-        wsb = int(lib.vcf_cbaac_tiled_workspace(self.n, self.seg_len))
-        self.streams = [Stream() for _ in range(max(1, min(int(streams), max(self.n_frames, 1))))]
-        self.ws = [DeviceBuffer(max(wsb, 1)) for _ in self.streams]
-        self.hist = [DeviceBuffer(1024) for _ in self.streams]
-        self.out = [DeviceBuffer(max(self.cap, 1)) for _ in range(self.n_frames)]
-        self.sizes_dev = DeviceBuffer(max(8 * (self.ns + 1) * self.n_frames, 8))
-        self.prior_dev = DeviceBuffer(max(512 * self.n_frames, 8))
+        self.stream = Stream()
+        nf = max(self.n_frames, 1)
+        self.ws = DeviceBuffer(max(int(lib.vcf_cbaac_tiled_frames_workspace(nf, self.n, self.seg_len)), 1))
+        self.out = DeviceBuffer(max(self.cap * nf, 1))
+        self.sizes_dev = DeviceBuffer(8 * (self.ns + 1) * nf)
+        self.prior_dev = DeviceBuffer(512 * nf)
+        self.hist = DeviceBuffer(1024 * nf)
         self._sizes = None
         self._priors = None
 
-    def launch(self, sym: DeviceBuffer, offset: int = 0, after: Stream | None = None) -> None:
-        """Enqueue frame f = symbols [offset + f*n, offset + (f+1)*n) of `sym`
-        on library stream f % streams; `after` (the producer's stream) is
+    def launch(self, sym: DeviceBuffer, offset: int = 0, after: Stream | None = None,
+               frame_stride: int | None = None) -> None:
+        """Enqueue frame f = symbols [offset + f * frame_stride, + n) of `sym`
+        (frame_stride defaults to n); `after` (the producer's stream) is
         waited for through an event."""
         from .device import Event
         if after is not None:
             ev = Event()
             ev.record(after)
-            for st in self.streams:
-                st.wait_event(ev)
-        n, ns = self.n, self.ns
-        for f in range(self.n_frames):
-            k = f % len(self.streams)
-            st, ws, hist = self.streams[k], self.ws[k], self.hist[k]
-            addr = sym.address(offset + f * n)
-            sb = self.sizes_dev.address(8 * (ns + 1) * f)
-            if self.prior:
-                pr = self.prior_dev.address(512 * f)
-                L.call("vcf_cbaac_tiled_prior", addr, n, pr, hist.ptr, st.handle)
-                L.call("vcf_cbaac_tiled_encode_prior", addr, n, self.order, pr, self.seg_len, self.out[f].ptr,
-                       self.cap, sb, ws.ptr, st.handle)
-            else:
-                L.call("vcf_cbaac_tiled_encode", addr, n, self.order, self.seg_len, self.out[f].ptr, self.cap, sb,
-                       ws.ptr, st.handle)
+            self.stream.wait_event(ev)
         self._sizes = None
+        if not self.n_frames:
+            return
+        stride = self.n if frame_stride is None else int(frame_stride)
+        base = sym.address(offset)
+        h = self.stream.handle
+        if self.prior:
+            L.call("vcf_cbaac_tiled_prior_frames", base, self.n_frames, self.n, stride, self.prior_dev.ptr,
+                   self.hist.ptr, h)
+        L.call("vcf_cbaac_tiled_encode_frames", base, self.n_frames, self.n, stride, self.order,
+               self.prior_dev.ptr if self.prior else None, self.seg_len, self.out.ptr, self.cap, self.sizes_dev.ptr,
+               self.ws.ptr, h)
 
     def join(self, stream: Stream) -> None:
-        """`stream` waits for every frame's coding (no host synchronisation)."""
+        """`stream` waits for the coding (no host synchronisation)."""
         from .device import Event
-        for st in self.streams:
-            ev = Event()
-            ev.record(st)
-            stream.wait_event(ev)
+        ev = Event()
+        ev.record(self.stream)
+        stream.wait_event(ev)
 
     def sizes(self):
         """Wait for the coding; -> (per-frame segment byte counts (n_frames x
         ns int64), per-frame payload bytes, priors (n_frames x 256) or None)."""
         if self._sizes is None:
-            for st in self.streams:
-                st.synchronize()
             allz = np.empty((self.n_frames, self.ns + 1), np.int64)
-            if self.n_frames:
-                self.sizes_dev.download(allz)
-            self._sizes = allz
             self._priors = None
-            if self.prior:
-                self._priors = np.empty((self.n_frames, 256), np.uint16)
-                if self.n_frames:
-                    self.prior_dev.download(self._priors)
+            if self.n_frames:
+                self.sizes_dev.download(allz, self.stream)
+                if self.prior:
+                    self._priors = np.empty((self.n_frames, 256), np.uint16)
+                    self.prior_dev.download(self._priors, self.stream)
+            self.stream.synchronize()
+            self._sizes = allz
         return self._sizes[:, :-1], self._sizes[:, -1].copy(), self._priors
 
-    def device_payload(self, f: int):
-        """(device buffer, byte count) of frame f's packed segments."""
+    def payload(self, f: int):
+        """(device buffer, byte offset, byte count) of frame f's packed segments."""
         _, totals, _ = self.sizes()
-        return self.out[f], int(totals[f])
+        return self.out, f * self.cap, int(totals[f])
 
     def header(self, f: int, shape) -> bytes:
         """Frame f's container bytes in front of its payload (pack() minus the payload)."""
@@ -290,7 +287,7 @@ class FrameBatch:
         for f in range(self.n_frames):
             payload = np.empty(int(totals[f]), np.uint8)
             if payload.size:
-                self.out[f].download(payload)
+                self.out.download(payload, offset=f * self.cap)
             res.append((seg[f].copy(), payload.tobytes(), None if pri is None else pri[f].copy()))
         return res
 
@@ -299,14 +296,13 @@ def encode_frames_device(sym: DeviceBuffer, n_frames: int, frame_symbols: int, o
                          seg_len: int = DEFAULT_SEG, prior: bool = False, streams: int = 4,
                          after: Stream | None = None, offset: int = 0):
     """Several frames' symbols, back to back in HBM from `offset`, each coded
-    as its own tiled stream (its own prior with prior=True).  One frame's
-    segments fill only a few hundred waves, so the frames go out round robin
-    on `streams` library streams and run concurrently; every launch is issued
-    before the first download.  `after`: the stream that produced the symbols
-    (e.g. the DCT encode's); the library streams wait for its work so far
-    (an event), so the caller need not synchronise it first.
+    as its own tiled stream (its own prior with prior=True), all of them in
+    one launch per stage (FrameBatch; `streams` is accepted for the earlier
+    interface and unused).  `after`: the stream that produced the symbols
+    (e.g. the DCT encode's); the coder waits for its work so far (an event),
+    so the caller need not synchronise it first.
     -> [(segment byte counts, payload, prior or None)]."""
-    fb = FrameBatch(n_frames, frame_symbols, order, seg_len, prior, streams)
+    fb = FrameBatch(n_frames, frame_symbols, order, seg_len, prior)
     fb.launch(sym, offset, after)
     return fb.download()
 
