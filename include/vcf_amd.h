@@ -383,7 +383,8 @@ int vcf_cbaac_tiled_encode(const uint8_t *sym_dev, int64_t n, int32_t order, int
                            int64_t out_capacity, int64_t *seg_bytes_dev, void *ws_dev, void *stream);
 /* Kernel choice (process-wide; A/B and tests): 0 = automatic -- order 0 codes
  * one segment per LANE (64 segments per wave, each with its own model in
- * LDS) once a call has at least 2048 segments, else one segment per wave
+ * LDS) once a call has at least 4608 segments to encode / 6144 to decode
+ * (all frames of the call), else one segment per wave
  * (64 lanes share one model: a shorter time per segment); 1 = one segment per
  * wave always; 2 = one segment per lane for order 0 always.  Same bytes. */
 int vcf_cbaac_tiled_set_variant(int32_t variant);

@@ -1,5 +1,5 @@
 """Run the 2D-DWT encode (8 4K frames, l=5, bior4.4) N times with one variant: for rocprofv3 --pmc passes.
-python scripts/dwt_once.py VARIANT [N]"""
+python scripts/dwt_once.py VARIANT [N]   (DECODE=1: the decode of those frames' subbands)"""
 import os
 import sys
 
@@ -20,7 +20,12 @@ _, pb, wb = DW.layout(H, W, LV)
 frames = np.stack([bench.synth_frame(H, W, s) for s in range(F)])
 din, dws, dout = DeviceBuffer.from_array(frames), DeviceBuffer(F * wb), DeviceBuffer(F * pb)
 s = Stream()
-for _ in range(n):
-    L.call("vcf_dwt_dz_encode_variant", v, din.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
+if os.environ.get("DECODE", "0") == "1":
+    L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
+    for _ in range(n):
+        L.call("vcf_dwt_dz_decode_variant", v, dout.ptr, F, H, W, w, LV, Q, din.ptr, dws.ptr, s.handle)
+else:
+    for _ in range(n):
+        L.call("vcf_dwt_dz_encode_variant", v, din.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
 s.synchronize()
 print("ok", v, n)

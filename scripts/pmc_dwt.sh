@@ -1,9 +1,11 @@
 #!/bin/bash
 # PMC passes + a kernel trace over the C3 DWT encode (scripts/dwt_once.py VARIANT):
 #   VARIANT=17 scripts/pmc_dwt.sh   -> gpurun_out/pmc_dwt_v$VARIANT/{summary.txt,trace}
+#   DECODE=1 VARIANT=0 scripts/pmc_dwt.sh -> the decode, gpurun_out/pmc_dwt_v0_dec/
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-ROOT=$(pwd); V=${VARIANT:-0}; OUT=$ROOT/gpurun_out/pmc_dwt_v$V; RAW=/tmp/pmc_dwt_v$V
+ROOT=$(pwd); V=${VARIANT:-0}; SUF=""; if [ "${DECODE:-0}" = 1 ]; then SUF=_dec; fi
+OUT=$ROOT/gpurun_out/pmc_dwt_v$V$SUF; RAW=/tmp/pmc_dwt_v$V$SUF
 rm -rf "$OUT" "$RAW"; mkdir -p "$OUT" "$RAW"; export TMPDIR=/tmp; cd /tmp   # raw counters stay on the box
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$RAW/trace" -o run \
     -- python3 "$ROOT/scripts/dwt_once.py" "$V" 20 > "$OUT/trace.log" 2>&1

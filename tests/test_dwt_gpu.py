@@ -176,7 +176,7 @@ def test_dwt_unknown_variant():
     with pytest.raises(ValueError):
         DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32, variant=28)
     with pytest.raises(ValueError):
-        DW.decode(DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32), 16, 16, "db5", 2, 32, variant=17)
+        DW.decode(DW.encode(np.zeros((16, 16, 3), np.uint8), "db5", 2, 32), 16, 16, "db5", 2, 32, variant=19)
 
 
 def test_dwt_errors():
@@ -267,3 +267,33 @@ def test_dwt_band12_batches(n):
     ref = O.dwt_encode_frame(frames[-1], "bior4.4", 5, 32)
     for name, arr in ref.items():
         assert np.array_equal(a[-1][name], arr), name
+
+
+@pytest.mark.parametrize("wavelet", ["bior4.4", "db5"])
+@pytest.mark.parametrize("H,W,L,Q", [(96, 128, 3, 32), (67, 45, 2, 7), (141, 301, 4, 3), (300, 530, 3, 16),
+                                     (20, 1030, 2, 1), (44, 44, 3, 5)])
+def test_dwt_line_decode_vs_oracle(wavelet, H, W, L, Q):
+    """The line-based inverse levels (decode variant 0; 18 = level 1 only) against the tiled level kernels
+    (variant 17) and the oracle: partial column tiles, odd subband sizes, the packed-LL coarsest level."""
+    import vcf_amd.dwt as DW
+    rng = np.random.Generator(np.random.PCG64(H * 7 + W + L))
+    frames = rng.integers(0, 256, (3, H, W, 3), dtype=np.uint8)
+    got = DW.encode(frames, wavelet, L, Q)
+    out = DW.decode(got, H, W, wavelet, L, Q)
+    assert np.array_equal(out, DW.decode(got, H, W, wavelet, L, Q, variant=17))
+    assert np.array_equal(out, DW.decode(got, H, W, wavelet, L, Q, variant=18))
+    for f in (0, 2):
+        assert np.array_equal(out[f], O.dwt_decode_frame(got[f], H, W, wavelet, L, Q))
+
+
+@pytest.mark.parametrize("wavelet", ["bior4.4", "db5"])
+def test_dwt_line_decode_4k(wavelet):
+    """Config C3 frames: the line-based inverse equals the tiled level kernels and the oracle."""
+    import vcf_amd.dwt as DW
+    H, W, L, Q = 2160, 3840, 5, 32
+    rng = np.random.Generator(np.random.PCG64(12))
+    frames = rng.integers(0, 256, (2, H, W, 3), dtype=np.uint8)
+    got = DW.encode(frames, wavelet, L, Q)
+    out = DW.decode(got, H, W, wavelet, L, Q)
+    assert np.array_equal(out, DW.decode(got, H, W, wavelet, L, Q, variant=17))
+    assert np.array_equal(out[1], O.dwt_decode_frame(got[1], H, W, wavelet, L, Q))

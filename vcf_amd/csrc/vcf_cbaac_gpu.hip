@@ -1057,10 +1057,17 @@ __global__ __launch_bounds__(kLW) void cbaac_lane_decode_kernel(const uint8_t *_
 
 int64_t slot_words_for(int64_t seg_len) { return (vcf_cbaac_bound(seg_len) + 3) / 4; }
 
-// 0 = automatic (order 0: one lane per segment from kLaneMinSegments segments
-// on), 1 = one wave per segment, 2 = one lane per segment (order 0; A/B)
+// 0 = automatic (order 0: one lane per segment from kLaneMinEncode /
+// kLaneMinDecode segments on), 1 = one wave per segment, 2 = one lane per
+// segment (order 0; A/B)
 int g_tiled_variant = 0;
-constexpr int64_t kLaneMinSegments = 2048;
+// Crossovers measured on MI355X at 32768-symbol segments (scripts/
+// bench_tcbaac_lane.py, profiles/r03_tcbaac_lane.jsonl): a wave per segment
+// fills the 1024 SIMDs from ~1000 segments on and then grows linearly (encode
+// 16.3 ms at 3038 segments, 39.0 at 12150; decode 21.9 / 63.0), a lane per
+// segment stays at one segment's latency until 64k segments (encode ~20 ms,
+// decode ~35 ms)
+constexpr int64_t kLaneMinEncode = 4608, kLaneMinDecode = 6144;
 
 int check_args(int64_t n, int32_t order, int64_t seg_len)
 {
@@ -1111,10 +1118,10 @@ int64_t vcf_cbaac_tiled_frames_workspace(int64_t n_frames, int64_t frame_symbols
 
 // one lane per segment when there are enough segments to fill waves with them
 // (a lane codes a symbol in about twice a wave's time, but 64 segments at once)
-static bool use_lanes(int32_t order, int64_t total_segments)
+static bool use_lanes(int32_t order, int64_t total_segments, bool decode)
 {
     if (order != 0 || g_tiled_variant == 1) return false;
-    return g_tiled_variant == 2 || total_segments >= kLaneMinSegments;
+    return g_tiled_variant == 2 || total_segments >= (decode ? kLaneMinDecode : kLaneMinEncode);
 }
 
 static int tiled_encode(const uint8_t *sym_dev, int64_t n_frames, int64_t n, int64_t sym_stride, int32_t order,
@@ -1138,7 +1145,7 @@ static int tiled_encode(const uint8_t *sym_dev, int64_t n_frames, int64_t n, int
     fr.sym_stride = sym_stride;
     fr.prior_stride = prior_stride;
     const dim3 grid((unsigned)ns, (unsigned)n_frames);
-    if (!trace_dev && use_lanes(order, ns * n_frames)) {   // one lane per segment
+    if (!trace_dev && use_lanes(order, ns * n_frames, false)) {   // one lane per segment
         const dim3 lg((unsigned)((ns + kLW - 1) / kLW), (unsigned)n_frames);
         if (prior_dev) cbaac_lane_encode_kernel<true><<<lg, kLW, 0, st>>>(sym_dev, n, seg_len, ns, slots, sw, bits, prior_dev, fr);
         else cbaac_lane_encode_kernel<false><<<lg, kLW, 0, st>>>(sym_dev, n, seg_len, ns, slots, sw, bits, nullptr, fr);
@@ -1191,7 +1198,7 @@ static int tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, i
     fr.out_stride = out_stride;
     fr.prior_stride = prior_stride;
     const dim3 grid((unsigned)ns, (unsigned)n_frames);
-    if (use_lanes(order, ns * n_frames)) {   // one lane per segment
+    if (use_lanes(order, ns * n_frames, true)) {   // one lane per segment
         const dim3 lg((unsigned)((ns + kLW - 1) / kLW), (unsigned)n_frames);
         if (prior_dev)
             cbaac_lane_decode_kernel<true><<<lg, kLW, 0, st>>>(in_dev, seg_offsets_dev, n, seg_len, ns, sym_dev, prior_dev, fr);

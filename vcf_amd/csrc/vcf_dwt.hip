@@ -1272,6 +1272,9 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
     }
 }
 
+// line-based inverse level (the default for 10-tap filters)
+#include "vcf_idwt_line.h"
+
 #ifndef VCF_DWT_KERNELS_ONLY   // (micro-experiments compile the kernels alone)
 // ---------------------------------------------------------------------------
 // host side
@@ -1631,6 +1634,78 @@ void launch_band12(int id, const DwtGeom &g, const uint8_t *rgb, long long n_fra
     else launch_band12_t<0u, 0u, 2>(g, rgb, n_frames, LL2, plane_stride, packed, Q, s);
 }
 
+// Line-based inverse level (idwt_line_kernel): 10-tap reconstruction filters
+// with compile-time taps (bior4.4, db5) on subbands of at least 5 x 5.
+bool line_ok(const WaveletDef &wd, int h, int w, int &id)
+{
+    if (wd.len != 10 || h < 5 || w < 5) return false;
+    const bool b44 = zero_mask(wd.rec_lo, 10) == kB44RecLo && zero_mask(wd.rec_hi, 10) == kB44RecHi;
+    id = b44 ? 1 : 2;
+    for (int m = 0; m < 10; ++m) {
+        const double l = ct_rec(id, false, m), hv = ct_rec(id, true, m);
+        if (std::memcmp(&l, &wd.rec_lo[m], 8) || std::memcmp(&hv, &wd.rec_hi[m], 8)) return false;
+    }
+    return true;
+}
+
+template <bool FP, bool RGB, unsigned ZL, unsigned ZH, int CT>
+void launch_line_t(const LevelArgs &a, uint8_t *rgb_out)
+{
+    // Q <= 256: the detail dequant never wraps in int16 (the fma form)
+    auto kern = a.Q <= 256 ? idwt_line_kernel<FP, RGB, ZL, ZH, CT, true> : idwt_line_kernel<FP, RGB, ZL, ZH, CT, false>;
+    static int slots = 0;   // resident workgroups on the device (per instantiation)
+    if (!slots) {
+        int dev = 0, n_cu = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+            n_cu = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kINT, 0) != hipSuccess || per_cu <= 0)
+            per_cu = 2;
+        slots = n_cu * per_cu;
+    }
+    const int n_tiles = (a.w + kILC - 1) / kILC, ohp = (a.hh + 1) / 2;
+    // bands: time ~ (rounds of resident workgroups) x (steps per band: rows + 4 halo + 1)
+    const long long per_band = (long long)n_tiles * a.n_frames;
+    int n_bands = 1;
+    long long best = -1;
+    for (int nb = 1; nb <= ohp; ++nb) {
+        const int br = (ohp + nb - 1) / nb;
+        if (nb > 1 && (ohp + br - 1) / br != nb) continue;
+        const long long rounds = (per_band * nb + slots - 1) / slots;
+        const long long cost = rounds * (br + 5);
+        if (best < 0 || cost < best) {
+            best = cost;
+            n_bands = nb;
+        }
+    }
+    if (const char *e = getenv("VCF_IDWT_BANDS"))   // tuning knob (A/B of the band cut)
+        n_bands = std::max(1, std::min(atoi(e), ohp));
+    const int brows = (ohp + n_bands - 1) / n_bands;
+    n_bands = (ohp + brows - 1) / brows;
+    const long long grid = per_band * n_bands;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kINT), 0, a.s, a.packed, a.packed_stride, a.ll_off, a.off_lh,
+                       a.off_hl, a.off_hh, a.in, a.plane_stride, a.lda, a.LLout, rgb_out, a.h, a.w, a.hh, a.hw, a.Q,
+                       n_tiles, n_bands, brows);
+}
+
+template <unsigned ZL, unsigned ZH, int CT>
+void launch_line_id(const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t *rgb_out)
+{
+    if (from_packed) {
+        if (to_rgb) launch_line_t<true, true, ZL, ZH, CT>(a, rgb_out);
+        else launch_line_t<true, false, ZL, ZH, CT>(a, rgb_out);
+    } else {
+        if (to_rgb) launch_line_t<false, true, ZL, ZH, CT>(a, rgb_out);
+        else launch_line_t<false, false, ZL, ZH, CT>(a, rgb_out);
+    }
+}
+
+void launch_line(int id, const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t *rgb_out)
+{
+    if (id == 1) launch_line_id<kB44RecLo, kB44RecHi, 1>(a, from_packed, to_rgb, rgb_out);
+    else launch_line_id<0u, 0u, 2>(a, from_packed, to_rgb, rgb_out);
+}
+
 #define VCF_DWT_FOR_EACH_F(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18)
 
 void fwd_level(int F, const LevelArgs &a, bool first, bool last)
@@ -1897,7 +1972,7 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
 // one stream's level chain of the decode (variants 0-5)
 static int decode_chain(int variant, const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W,
                         int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
-                        hipStream_t s, const PipeHook *hook, long long sep_area = 0)
+                        hipStream_t s, const PipeHook *hook, long long sep_area = 0, int line_mode = 0)
 {
     int rc = VCF_OK;
     Filters flt;
@@ -1952,7 +2027,14 @@ static int decode_chain(int variant, const uint8_t *packed_dev, int64_t n_frames
                 continue;
             }
             if (r == 1 && (rc = hook_wait(hook, s)) != VCF_OK) return rc;
-            inv_level(F, a, r == levels, r == 1, rgb_dev);
+            // line_mode: 0 = line kernel on every eligible level, 1 = none (the
+            // tiled level kernels, decode variant 17), 2 = level 1 only (18)
+            int id = 0;
+            if ((variant == 0 || variant == 9) && (line_mode == 0 || (line_mode == 2 && r == 1)) &&
+                line_ok(kWavelets[wavelet], h, w, id))
+                launch_line(id, a, r == levels, r == 1, rgb_dev);
+            else
+                inv_level(F, a, r == levels, r == 1, rgb_dev);
             prev = out;
             lda = ow;
             rc = hip_check(hipGetLastError(), "idwt level launch");
@@ -1990,7 +2072,11 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
                               int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
                               void *stream)
 {
-    if (variant < 0 || variant == 3 || variant > 16) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    if (variant < 0 || variant == 3 || variant > 18) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    // 17 / 18: variant 0 with the tiled level kernels on every level / on every level but the first
+    // (the line kernel's A/B)
+    const int line_mode = variant == 17 ? 1 : variant == 18 ? 2 : 0;
+    if (variant >= 17) variant = 0;
     int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
@@ -2020,12 +2106,13 @@ int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_
                                  [&](long long f0, long long n, hipStream_t cs, const PipeHook *hook) {
                                      return decode_chain(0, packed_dev + f0 * g.packed_bytes, n, H, W, wavelet,
                                                          levels, Q, rgb_dev + f0 * fpx,
-                                                         (double *)workspace_dev + f0 * wsf, cs, hook);
+                                                         (double *)workspace_dev + f0 * wsf, cs, hook, 0,
+                                                         line_mode);
                                  });
         }
     }
     return decode_chain(variant, packed_dev, n_frames, H, W, wavelet, levels, Q, rgb_dev, workspace_dev,
-                        (hipStream_t)stream, nullptr, sep_area);
+                        (hipStream_t)stream, nullptr, sep_area, line_mode);
 }
 
 }  // extern "C"

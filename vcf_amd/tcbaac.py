@@ -199,8 +199,8 @@ class FrameBatch:
     symbols each (the III driver's per-rank chunk), every frame's code-stream
     kept in HBM.  One launch per stage codes all the frames
     (vcf_cbaac_tiled_*_frames): a frame's few hundred segments alone leave most
-    of the chip idle, a batch's segments fill it (and with 2048 or more, order
-    0 codes one segment per lane).  Frame f's packed segments sit at byte
+    of the chip idle, a batch's segments fill it (and from ~5000 on, order 0
+    codes one segment per lane).  Frame f's packed segments sit at byte
     f * cap of `out`, its segment sizes and prior in one contiguous device
     array each, so one download returns the index.  launch() enqueues,
     sizes() waits and downloads the index, payload(f) / download() hand out
