@@ -109,40 +109,7 @@ int vcf_dct_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *k_dev,
                       void *stream);
 
-/* Same as vcf_dct_dz_encode with an explicit kernel choice (benchmarking and
- * tests): 0 = automatic (5 for a power-of-two Q without -p, else 1),
- * 1 = lane-per-block tile kernel, scalar fp32 transforms,
- * 2 = diagnostic: variant 1's arithmetic with no memory traffic (writes one
- * word per block, not the coefficients; power-of-two Q only),
- * 3 = column-per-lane tile kernel (8 lanes per block, LDS transpose),
- * 4 = variant 1 with compiler-generated byte code for the colour conversion
- * instead of SDWA operands (A/B reference; power-of-two Q, default flags,
- * frames that need no padding),
- * 5 = variant 1 with packed-fp32 transforms (two 1-D transforms per
- * v_pk_add_f32 / v_pk_mul_f32; power-of-two Q, no -p; else as 1),
- * 6 = diagnostic 2 with variant 5's arithmetic,
- * 7 = variant 5 with its earlier store policy (non-temporal stores, tiles in
- *     dispatch order; A/B reference, aligned frames with subbands),
- * 8 = diagnostic: variant 1's loads, LDS image and copy-out without the
- * transforms (output bytes are not the coefficients; aligned frames, subbands),
- * 9, 10 = diagnostics: 8 with the image written as 64 aligned streams that
- * continue from tile to tile (9), or the same streams 32 bytes off line
- * boundaries (10) -- the cost of partial lines (output bytes wrong),
- * 11 = variant 5 with non-temporal input loads (the earlier load policy;
- *      A/B reference, aligned frames with subbands),
- * 12-16 = variant 5 with wave priority 3 for the load issue and copy-out
- *      (12, the default's setting), 1 for both (13), the copy-out only (14),
- *      the loads only (15), none (16) (A/B references, aligned frames with
- *      subbands),
- * 17 = variant 5 with the earlier address arithmetic (32-bit divisions and
- *      multiplies per copy-out chunk, a 64-bit multiply per input row; A/B).
- * 18, 19 = variant 0 with the frames cut into two / four chunks whose
- *      launches run on two library streams (forked from and joined to the
- *      caller's stream; A/B).
- * Variants 1, 3, 4, 5, 7 and 11-19 produce identical bytes. */
-int vcf_dct_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H,
-                              int32_t W, int32_t block_size, int32_t Q, uint32_t flags,
-                              uint8_t *k_dev, void *stream);
+
 
 /* Inverse: n_frames coefficient frames (Hp x Wp x 3) -> RGB frames (H x W x 3),
  * the padding removed.  1 <= Q <= 32767 (the dequantizer works in int16). */
@@ -198,21 +165,7 @@ int vcf_dct_raw_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int3
 int vcf_dct_raw_decode(const int16_t *coef_dev, int64_t n_frames, int32_t H, int32_t W, int32_t block_size,
                        uint32_t flags, uint8_t *rgb_dev, void *stream);
 
-/* Same as vcf_dct_dz_decode with an explicit kernel choice (A/B tests and
- * benchmarks): 0 = automatic (column-per-lane with the dequantization table
- * and, for aligned frames, the packed int16 epilogue; any flags), 1 = lane-per-block (one block's 64 float64 samples per lane),
- * 2 = column-per-lane (8 lanes per block, LDS transpose) dequantizing with a
- * 32-bit multiply and scaling each output by 1/16 (the round-1 default),
- * 3, 4, 5 = variant 2 with non-temporal index loads (3, the earlier policy),
- * plain pixel stores (4) or no raised wave priority for the load phase (5),
- * 6 = the LDS table of the 256 dequantized values / 16 alone, 7 = variant 2
- * with a 24-bit multiply, 8 = the automatic kernel: the table plus to_RGB,
- * += 128 and the clamp on pixel pairs in packed int16 arithmetic, bytes by
- * permutes, 24-bit staging offsets (3-8: A/B references; aligned frames,
- * subbands, no -p).
- * Outputs identical. */
-int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t W,
-                              int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev, void *stream);
+
 
 /* ---- 2D-DWT + deadzone path (2D-DWT.py, deadzone.py, YCoCg.py) ---------------- */
 
@@ -244,54 +197,7 @@ int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
 int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                       int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, void *stream);
 
-/* Same, with an explicit kernel choice (for A/B tests and benchmarks):
- * 0 = automatic (9 for filters up to 10 taps, else 1 when its LDS tile fits,
- * else 2), 1 = fused LDS-tiled level kernels on every level (one launch per
- * level; filters up to 18 taps), 2 = separable column/row kernels through
- * float64 workspace planes, 3 = 1 with the earlier three-barrier schedule
- * for bior4.4 (A/B reference; other filters as 1), 4 = 1 with bior4.4's taps
- * as kernel arguments instead of compile-time constants (A/B reference),
- * 5 = 1 with level 1 staging its samples as float at 4 waves/SIMD and no
- * raised wave priority for its loads and copy-out (A/B reference), 6 = strip
- * kernels (one wave per channel and 64-column strip sliding down a register
- * window, no workgroup barriers; filters up to 10 taps, planes of at least
- * 2F rows and columns) on every level, 7 = 6 with every tap sum started at
- * 0.0 (A/B), 8 = diagnostic: 6 without the detail-subband stores (outputs
- * incomplete), 9 = strips for the middle levels, fused kernels for the first
- * and last, 10 = 0 with the fused levels' subband copy-out byte by byte
- * instead of in dwords, 11 = 0 with the fused levels' earlier row-pass work
- * mapping (NG group slots per row instead of 16), 12 = 0 with no raised wave
- * priority on any fused level and the staging unchanged (A/B references;
- * 5 changes level 1's priority and, for db5, its staging together),
- * 13-19 = 0 with the batch cut into chunks of consecutive frames whose
- * level chains run on the library's streams, forked from and joined to the
- * caller's stream (13: two streams, two chunks; 14: 13 staggered -- chunk k's
- * level 1 waits for chunk k-1's -- ; 15 / 16: two streams, four / eight
- * chunks, staggered; 18: three streams, four chunks, staggered; 19: four
- * streams, four chunks), 17 = 0 on the caller's stream alone, 20 = 0 with
- * every level after the first on the fused/strip kernels (variant 0 runs the
- * levels whose input planes have at most 40 k samples -- at 4K level 5 -- on
- * the separable kernels), 21 / 22 = 0 with up to 140 k / 600 k samples on
- * them, 23 = 0 with the fused levels' tap sums
- * started at 0.0 instead of their first nonzero product (the earlier
- * arithmetic; variants 3-5 and 12 keep it too), 24 = 0 with level 1 in
- * 512-thread tiles of 16 output rows, 25 = 0 with the strip levels' last
- * strip (whose outputs' taps wrap past the line end) running every row
- * through the generic sums (the earlier form), 26 = 13 with chunk 0 on the
- * caller's stream.  Variant 0 pipelines (as 13) when the
- * batch has at least 2 frames of at least 2^20 pixels.  vcf_dwt_dz_decode_variant takes 0, 1, 2, 4 (bior4.4's
- * reconstruction taps at run time), 5 (no raised wave priority while the
- * subbands are staged), 6 / 7 / 8 / 10 / 11 (0 pipelined as the encode's
- * 13 / 14 / 15 / 16 / 18; staggering orders the chunks' last levels) and 9
- * (0 on the caller's stream alone; 0 does not pipeline), 12 / 13 / 14 (small
- * levels on the separable kernels) and 15 / 16 (bior4.4 / db5 inverse levels
- * in 32 x 32 / 128 x 8 output tiles instead of 64 x 16).  Outputs identical. */
-int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
-                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
-                              void *stream);
-int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W,
-                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
-                              void *stream);
+
 
 /* ---- IPP temporal tools (IPP_DCT.py) --------------------------------------------- */
 

@@ -27,11 +27,11 @@ if DECODE:   # decode the default encode's subbands; outputs are RGB frames
     Ho, Wo = 2 * shapes[0][0], 2 * shapes[0][1]
     nout = F * Ho * Wo * 3
     outs = {v: DeviceBuffer(nout) for v in variants}
-    run = lambda v: L.call("vcf_dwt_dz_decode_variant", v, dpk.ptr, F, H, W, w, LV, Q, outs[v].ptr, dws.ptr,
+    run = lambda v: L.dwt_decode_v(v, dpk.ptr, F, H, W, w, LV, Q, outs[v].ptr, dws.ptr,
                            s.handle)
 else:
     nout = F * pb
-    run = lambda v: L.call("vcf_dwt_dz_encode_variant", v, din.ptr, F, H, W, w, LV, Q, outs[v].ptr, dws.ptr,
+    run = lambda v: L.dwt_encode_v(v, din.ptr, F, H, W, w, LV, Q, outs[v].ptr, dws.ptr,
                            s.handle)
 for v in variants:
     run(v)

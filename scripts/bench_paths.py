@@ -83,9 +83,9 @@ def dwt(args):
              1: "fused level kernels", 2: "separable kernels"}
     for variant in [int(v) for v in args.dwt_variants.split(",")]:
         vname = names.get(variant, f"variant {variant}")
-        enc = lambda: L.call("vcf_dwt_dz_encode_variant", variant, din.ptr, F, H, W, w, L_, Q, dpk.ptr, dws.ptr,
+        enc = lambda: L.dwt_encode_v(variant, din.ptr, F, H, W, w, L_, Q, dpk.ptr, dws.ptr,
                              s.handle)
-        dec = lambda: L.call("vcf_dwt_dz_decode_variant", variant, dpk.ptr, F, H, W, w, L_, Q, dout.ptr, dws.ptr,
+        dec = lambda: L.dwt_decode_v(variant, dpk.ptr, F, H, W, w, L_, Q, dout.ptr, dws.ptr,
                              s.handle)
         te = timed(s, enc, args.steps, 2)
         td = timed(s, dec, args.steps, 2)

@@ -20,7 +20,7 @@ frames = np.stack([bench.synth_frame(H, W, s % 4) for s in range(FM)])
 din, dws, dout = DeviceBuffer.from_array(frames), DeviceBuffer(FM * wb), DeviceBuffer(FM * pb)
 s = Stream()
 e0, e1 = Event(), Event()
-run = lambda v, n: L.call("vcf_dwt_dz_encode_variant", v, din.ptr, n, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
+run = lambda v, n: L.dwt_encode_v(v, din.ptr, n, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
 for _ in range(200):
     run(0, 8)
 for n in (1, 2, 4, 8, 16):

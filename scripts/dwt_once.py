@@ -23,9 +23,9 @@ s = Stream()
 if os.environ.get("DECODE", "0") == "1":
     L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
     for _ in range(n):
-        L.call("vcf_dwt_dz_decode_variant", v, dout.ptr, F, H, W, w, LV, Q, din.ptr, dws.ptr, s.handle)
+        L.dwt_decode_v(v, dout.ptr, F, H, W, w, LV, Q, din.ptr, dws.ptr, s.handle)
 else:
     for _ in range(n):
-        L.call("vcf_dwt_dz_encode_variant", v, din.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
+        L.dwt_encode_v(v, din.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
 s.synchronize()
 print("ok", v, n)

@@ -28,7 +28,7 @@ din, dws, dpk = DeviceBuffer.from_array(frames), DeviceBuffer(F * wb), DeviceBuf
 s = Stream()
 L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, LV, Q, dpk.ptr, dws.ptr, s.handle)
 ref = DeviceBuffer(F * H * W * 3)
-L.call("vcf_dwt_dz_decode_variant", 17, dpk.ptr, F, H, W, w, LV, Q, ref.ptr, dws.ptr, s.handle)
+L.dwt_decode_v(17, dpk.ptr, F, H, W, w, LV, Q, ref.ptr, dws.ptr, s.handle)
 s.synchronize()
 want = ref.download(np.empty(F * H * W * 3, np.uint8))
 hs = [H] + [h for h, _ in shapes]

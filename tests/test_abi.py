@@ -15,9 +15,9 @@ from conftest import ROOT
 import vcf_amd._lib as L
 
 
-def _declared():
+def _declared(header="vcf_amd.h"):
     names = []
-    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+    for h in glob.glob(os.path.join(ROOT, "include", header)):
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names += re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s]*?[\s*](vcf_\w+)\s*\(", src, flags=re.M)
@@ -44,6 +44,17 @@ def test_python_binding_covers_the_header():
     """Every declared entry point has argtypes in vcf_amd/_lib.py, and no extra."""
     declared = set(_declared()) - {"vcf_last_error"}
     assert declared == set(L.SIGNATURES), (declared ^ set(L.SIGNATURES))
+
+
+def test_ab_library_is_separate():
+    """The A/B kernel variants (include/vcf_amd_ab.h) live in libvcf_amd_ab.so
+    only: the product library does not export them, the A/B library does."""
+    ab = _declared("vcf_amd_ab.h")
+    assert set(ab) == set(L.AB_SIGNATURES), set(ab) ^ set(L.AB_SIGNATURES)
+    assert not set(ab) & set(_declared())
+    lib, abl = L.lib(), L.ab()
+    assert not [n for n in ab if hasattr(lib, n)]
+    assert not [n for n in ab if not hasattr(abl, n)]
 
 
 def test_padded_shape_is_host_only():

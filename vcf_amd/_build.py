@@ -1,7 +1,10 @@
 """Build recipe for libvcf_amd.so (hipcc, gfx950) -- used by __graft_entry__.build().
 
 The library is built in-tree (vcf_amd/libvcf_amd.so) so it travels to the GPU
-box with the repository snapshot.
+box with the repository snapshot.  A second, experimental library
+(vcf_amd/libvcf_amd_ab.so, include/vcf_amd_ab.h) holds the A/B kernel
+variants the product defaults were measured against (csrc/ab/); the A/B
+scripts and the cross-check tests load it, the product path never does.
 """
 from __future__ import annotations
 
@@ -13,6 +16,10 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libvcf_amd.so")
+AB_LIB = os.path.join(PKG, "libvcf_amd_ab.so")
+# the A/B archive's own sources, linked with these product objects
+AB_SOURCES = ["ab/vcf_dct_dz_ab.hip", "ab/vcf_dwt_ab.hip"]
+AB_LINK = ["vcf_runtime.hip", "vcf_dct_any.hip"]
 SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_dct_any.hip", "vcf_quant.hip", "vcf_dwt.hip", "vcf_cbaac.cpp",
            "vcf_cbahc.cpp", "vcf_ipp.hip", "vcf_ipp_rdo.hip",
            "vcf_png.cpp", "vcf_comm.cpp", "vcf_cbaac_gpu.hip", "vcf_plugins.hip"]
@@ -30,11 +37,11 @@ def hipcc() -> str:
 
 
 def needs_rebuild() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(AB_LIB):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    deps.append(os.path.join(ROOT, "include", "vcf_amd.h"))
+    t = min(os.path.getmtime(LIB), os.path.getmtime(AB_LIB))
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS + AB_SOURCES]
+    deps += [os.path.join(ROOT, "include", h) for h in ("vcf_amd.h", "vcf_amd_ab.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
@@ -74,6 +81,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     def compile_one(src):
         obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+        os.makedirs(os.path.dirname(obj), exist_ok=True)
         path = os.path.join(CSRC, src)
         if not force and os.path.exists(obj) and os.path.getmtime(obj) > deps_mtime(src):
             return obj
@@ -84,14 +92,21 @@ def build(force: bool = False, verbose: bool = False) -> str:
         os.replace(obj + ".tmp", obj)
         return obj
 
-    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "8")), os.cpu_count() or 1))
+    everything = SOURCES + AB_SOURCES
+    jobs = max(1, min(len(everything), int(os.environ.get("MAX_JOBS", "8")), os.cpu_count() or 1))
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(compile_one, SOURCES))
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-lz", "-ldl", "-o", LIB + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
+        objs = dict(zip(everything, ex.map(compile_one, everything)))
+
+    def link(lib, srcs):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[objs[x] for x in srcs], "-lz", "-ldl",
+               "-o", lib + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(lib + ".tmp", lib)
+
+    link(LIB, SOURCES)
+    link(AB_LIB, AB_SOURCES + AB_LINK)
     return LIB
 
 

@@ -85,9 +85,7 @@ SIGNATURES = {
     "vcf_event_elapsed_ms": [_P, _P, ctypes.POINTER(ctypes.c_float)],
     "vcf_dct_padded_shape": [_I32, _I32, _I32, _PI32, _PI32],
     "vcf_dct_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
-    "vcf_dct_dz_encode_variant": [ctypes.c_int, _P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_dz_decode": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
-    "vcf_dct_dz_decode_variant": [ctypes.c_int, _P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dct_block_size_supported": [_I32],
     "vcf_dct_perceptual_tables": [_I32, ctypes.c_void_p, ctypes.c_void_p],
     "vcf_dct_dz_encode_any": [_P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
@@ -109,8 +107,6 @@ SIGNATURES = {
     "vcf_dwt_layout": [_I32, _I32, _I32, _PI32, _PI32, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     "vcf_dwt_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
     "vcf_dwt_dz_decode": [_P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
-    "vcf_dwt_dz_encode_variant": [_I32, _P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
-    "vcf_dwt_dz_decode_variant": [_I32, _P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
     "vcf_ipp_block_match": [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
     "vcf_ipp_set_full_search_variant": [_I32],
     "vcf_ipp_motion_compensate": [_P, _P, _I32, _I32, _I32, _P, _P],
@@ -159,7 +155,17 @@ SIGNATURES = {
     "vcf_comm_gatherv": [_P, _P, _I64, _P, _P, ctypes.c_int, _P],
 }
 
+# the experimental A/B library (include/vcf_amd_ab.h): kernel variants, loaded
+# only by the A/B scripts and the cross-check tests
+AB_SIGNATURES = {
+    "vcf_dct_dz_encode_variant": [ctypes.c_int, _P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dct_dz_decode_variant": [ctypes.c_int, _P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
+    "vcf_dwt_dz_encode_variant": [_I32, _P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
+    "vcf_dwt_dz_decode_variant": [_I32, _P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
+}
+
 _lib = None
+_ab = None
 _lock = threading.Lock()
 
 
@@ -196,12 +202,33 @@ def lib():
     return _lib
 
 
-def check(status: int) -> int:
+def ab():
+    """Load (once) and return the A/B library (libvcf_amd_ab.so)."""
+    global _ab
+    if _ab is not None:
+        return _ab
+    with _lock:
+        if _ab is None:
+            path = os.environ.get("VCF_AMD_AB_LIB", _build.AB_LIB)
+            if not os.path.exists(path):
+                raise ImportError(f"libvcf_amd_ab.so not found at {path}: `python -m vcf_amd._build` builds it")
+            L = ctypes.CDLL(path)
+            for name, argtypes in AB_SIGNATURES.items():
+                f = getattr(L, name)
+                f.argtypes = argtypes
+                f.restype = ctypes.c_int
+            L.vcf_last_error.argtypes = []
+            L.vcf_last_error.restype = ctypes.c_char_p
+            _ab = L
+    return _ab
+
+
+def check(status: int, handle=None) -> int:
     """Raise for a negative status; a non-negative one (VCF_OK, or a count such as
     vcf_lm_levels' N) is returned."""
     if status >= VCF_OK:
         return status
-    msg = lib().vcf_last_error().decode(errors="replace")
+    msg = (handle or lib()).vcf_last_error().decode(errors="replace")
     if status == VCF_ERR_INVALID:
         raise VCFInvalidArgument(status, msg)
     if status == VCF_ERR_UNSUPPORTED:
@@ -213,3 +240,26 @@ def check(status: int) -> int:
 
 def call(name: str, *args) -> int:
     return check(getattr(lib(), name)(*args))
+
+
+def call_ab(name: str, *args) -> int:
+    """An entry point of the A/B library (variants; not the product path)."""
+    L = ab()
+    return check(getattr(L, name)(*args), L)
+
+
+# A/B scripts: variant 0 = the product entry point, others = the A/B library's
+def dct_encode_v(variant, *args):
+    return call("vcf_dct_dz_encode", *args) if variant == 0 else call_ab("vcf_dct_dz_encode_variant", variant, *args)
+
+
+def dct_decode_v(variant, *args):
+    return call("vcf_dct_dz_decode", *args) if variant == 0 else call_ab("vcf_dct_dz_decode_variant", variant, *args)
+
+
+def dwt_encode_v(variant, *args):
+    return call("vcf_dwt_dz_encode", *args) if variant == 0 else call_ab("vcf_dwt_dz_encode_variant", variant, *args)
+
+
+def dwt_decode_v(variant, *args):
+    return call("vcf_dwt_dz_decode", *args) if variant == 0 else call_ab("vcf_dwt_dz_decode_variant", variant, *args)

@@ -1,3 +1,6 @@
+// vcf_dwt_ab.hip -- A/B archive (libvcf_amd_ab.so; not the product library): the
+// round-2/3 vcf_dwt.hip with every measured kernel variant, kept for the A/B
+// scripts and cross-check tests.  Original header:
 // vcf_dwt.hip -- 2D-DWT + deadzone encode and decode (src/2D-DWT.py) for
 // gfx950, and the vcf_dwt_* entry points of the C ABI.
 //
@@ -34,6 +37,7 @@
 #include <type_traits>
 
 #include "vcf_amd.h"
+#include "vcf_amd_ab.h"
 #include "vcf_internal.h"
 #include "vcf_pipeline.h"
 #include "vcf_wavelets.h"
@@ -326,7 +330,7 @@ __global__ __launch_bounds__(256) void dwt_to_rgb_kernel(const double *__restric
 }
 
 // ---------------------------------------------------------------------------
-// fused level kernels (filters of at most kMaxFastF taps)
+// fused level kernels (variant 1, the default when the tile fits in LDS)
 // ---------------------------------------------------------------------------
 // One launch per level.  A workgroup owns a tile of a level's outputs, stages
 // the input samples it needs (halo included, wrapped at load time) in LDS,
@@ -477,6 +481,12 @@ __device__ __forceinline__ void fwd_store(int src, double lo, double hi, int e, 
 // quantize into a byte image of the three detail subbands; one copy-out of
 // contiguous runs at the end.  Outputs whose taps wrap past the line end
 // (i >= N) take pywt's order through the generic LDS sum.
+// PIPE (default): two barriers per channel instead of three -- channel c+1's
+// samples are staged during channel c's row pass (the staging tile is free
+// once the column pass has read it) -- and the LL outputs of a non-final
+// level go straight from the row pass to HBM (4 consecutive doubles per work
+// item, contiguous across a wave) instead of through an LDS tile and a third
+// barrier.  PIPE = false is the earlier schedule (dwt encode variant 3).
 // Decomposition taps as compile-time constants, bit for bit the table's
 // (vcf_wavelets.h; the launcher checks): id 1 = bior4.4 (CDF 9/7, config
 // C3), id 2 = db5 (the reference's default -w).
@@ -505,23 +515,19 @@ __host__ __device__ constexpr double ct_dec(int id, bool hi, int m)
 // STG (level 1): 1 = the YCoCg samples staged as int16 (exact; 29 KB of LDS
 // instead of 35 KB) with the registers held to 5 waves, so five workgroups
 // fit a CU; 0 = staged as float, 4 waves.  Used for db5 (−7.5 %, ABBA); for
-// bior4.4 the register cap spills (+2 %), so it keeps 0.
-// Schedule: two barriers per channel -- channel c+1's samples are staged
-// during channel c's row pass (the staging tile is free once the column pass
-// has read it) -- and the LL outputs of a non-final level go straight from the
-// row pass to HBM (4 consecutive doubles per work item, contiguous across a
-// wave).  Wave priority 3 while a workgroup issues its loads and its
-// copy-out (as the DCT encode).
-template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0, int STG = 0, bool Z0 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIRST && STG ? 5 : 1)))
+// bior4.4 the register cap spills (+2 %), so it keeps 0 (dwt variant 5
+// flips db5 back to 0 for A/B).
+template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, bool PIPE = true, int CT = 0,
+          int STG = 0, int PRI = 3, bool Z0 = false, int NT = 256>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FIRST && STG && NT == 256 ? 5 : 1)))
 void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
                                                         long long packed_stride, long long ll_off, long long off_lh,
                                                         long long off_hl, long long off_hh, int h, int w, int hh,
-                                                        int hw, int Q, Taps<F> tp, Filters flt)
+                                                        int hw, int Q, Taps<F> tp, Filters flt, int cw)
 {
-    constexpr int NT = 256, FTH = kFTH;
+    constexpr int FTH = NT / kFIW * kG;   // output rows per tile (kFTH at 256 threads)
     constexpr int TW = fwd_tile_w(F), IH = 2 * (FTH - 1) + F, IW = kFIW;
     constexpr int NWIN = 2 * (kG - 1) + F;
     constexpr int NG = (TW + kG - 1) / kG;
@@ -535,6 +541,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
     __shared__ double tA[FTH * RS + 8], tD[FTH * RS + 8];   // +8: the last row group's window overhang
     __shared__ __attribute__((aligned(16))) uint8_t stage[3 * SB];
     __shared__ uint8_t stage16[LAST ? 2 * SB : 1];
+    __shared__ double stageLL[LAST || PIPE ? 1 : FTH * TW];
     const int o0 = blockIdx.y * FTH, c0 = blockIdx.x * TW;
     const long long frame = blockIdx.z;
     const int R0 = F / 2 + 2 * o0 - F + 1, C0 = F / 2 + 2 * c0 - F + 1;
@@ -592,12 +599,20 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
             }
         }
     };
-    __builtin_amdgcn_s_setprio(3);
+    // PRI: wave priority while a workgroup issues its loads and its copy-out
+    // (as the DCT encode); 0 = none (dwt variant 5, A/B)
+    if (PRI) __builtin_amdgcn_s_setprio(PRI);
     fetch(0);
-    __builtin_amdgcn_s_setprio(0);
-    stage_in(0);
-    if (!FIRST) fetch(1);
+    if (PRI) __builtin_amdgcn_s_setprio(0);
+    if (PIPE) {
+        stage_in(0);
+        if (!FIRST) fetch(1);
+    }
     for (int ch = 0; ch < 3; ++ch) {
+        if (!PIPE) {
+            stage_in(ch);
+            if (!FIRST && ch < 2) fetch(ch + 1);
+        }
         __syncthreads();
         {   // column pass (axis 0): 128 columns x 2 groups of 4 output rows
             const int c = tid % IW, g = tid / IW;
@@ -624,22 +639,37 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
             }
         }
         __syncthreads();
-        if (ch < 2) {   // tin is free: stage the next channel while this one's rows run
+        if (PIPE && ch < 2) {   // tin is free: stage the next channel while this one's rows run
             stage_in(ch + 1);
             if (!FIRST && ch == 0) fetch(2);
         }
-        // LL of a non-final level: straight to HBM
+        // LL of a non-final level: straight to HBM (PIPE) or through stageLL
         double *const llp = LLout + (frame * 3 + ch) * plane_stride + (long long)o0 * hw + c0;
-        auto ll_dst = [&](int o, int oc) -> double * { return llp + (long long)o * hw + oc; };
-        // row pass (axis 1): (A or D) x FTH rows x NG groups of 4 outputs, 16 group
-        // slots per row, so a lane's (src, o, gq) are bit fields and every half-wave
-        // reads two whole rows -- conflict-free LDS banks -- with the slots past NG idle
+        auto ll_dst = [&](int o, int oc) -> double * {
+            return PIPE ? llp + (long long)o * hw + oc : stageLL + (o * TW + oc);
+        };
+        // row pass (axis 1): (A or D) x FTH rows x NG groups of 4 outputs.  Mapping
+        // (cw & 8 == 0, default): 16 group slots per row, so a lane's (src, o, gq)
+        // are bit fields and every half-wave reads two whole rows -- conflict-free
+        // LDS banks -- with the slots past NG idle; cw & 8: NG slots per row (the
+        // earlier mapping, dwt variant 11)
         const int first_tail = row_tail ? max(0, (w - F / 2 + 1) / 2 - c0) : TW;   // first column with i >= w
         constexpr int NGP = 16;
         static_assert(NG <= NGP && 2 * FTH * NGP == NT, "row-pass slots");
-        for (int t = tid; t < NT; t += NT) {
-            const int src = t / (FTH * NGP), o = (t >> 4) & (FTH - 1), gq = t & (NGP - 1);
-            if (gq >= NG) continue;
+        const bool slots16 = (cw & 8) == 0;
+        for (int t = tid; t < (slots16 ? NT : 2 * FTH * NG); t += NT) {
+            int src, o, gq;
+            if (slots16) {
+                src = t / (FTH * NGP);
+                o = (t >> 4) & (FTH - 1);
+                gq = t & (NGP - 1);
+                if (gq >= NG) continue;
+            } else {
+                src = t / (FTH * NG);
+                const int rest = t % (FTH * NG);
+                o = rest / NG;
+                gq = rest % NG;
+            }
             const int oc0 = kG * gq;
             const double *row = (src ? tD : tA) + o * RS;
             double v[NWIN];
@@ -670,16 +700,27 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                 fwd_store<LAST>(src, lo, hi, (o * TW + oc) * 3 + ch, stage, stage16, SB, Q, ll_dst(o, oc));
             }
         }
+        if (!PIPE) {
+            __syncthreads();
+            if (!LAST) {   // LL rows leave as contiguous runs of doubles
+                const int rows = min(FTH, hh - o0), nw = min(TW, hw - c0);
+                for (int t = tid; t < rows * TW; t += NT) {
+                    const int o = t / TW, oc = t - o * TW;
+                    if (oc < nw) llp[(long long)o * hw + oc] = stageLL[t];
+                }
+            }
+        }
     }
-    __syncthreads();   // the byte image is complete
-    __builtin_amdgcn_s_setprio(3);
+    if (PIPE) __syncthreads();   // the byte image is complete
+    if (PRI) __builtin_amdgcn_s_setprio(PRI);
     // copy-out: each subband row of the tile is one contiguous byte run, moved
-    // as dwords when every run start is 4-byte aligned, else as bytes
+    // as dwords when every run start is 4-byte aligned (cw 4; cw 1 = bytes, the
+    // earlier copy kept for A/B as dwt variant 10)
     const int rows = min(FTH, hh - o0), nb = min(TW, hw - c0) * 3;
     uint8_t *pk = packed + frame * packed_stride;
     const long long offs[3] = {off_lh, off_hl, off_hh};
     constexpr int TWW = TW * 3 / 4;   // dwords per staged subband row
-    const bool dw = (TW * 3) % 4 == 0 &&
+    const bool dw = (TW * 3) % 4 == 0 && (cw & 7) == 4 &&
                     ((reinterpret_cast<uintptr_t>(pk) | (uintptr_t)(off_lh | off_hl | off_hh | (long long)hw * 3 |
                                                                     (long long)c0 * 3 | nb)) & 3u) == 0;
     if (dw) {
@@ -706,7 +747,7 @@ void dwt_level_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
 }
 
 // ---------------------------------------------------------------------------
-// strip kernels (forward): one wave per column strip, no barriers
+// strip kernels (forward, dwt variant 6): one wave per column strip, no barriers
 // ---------------------------------------------------------------------------
 // A wave owns 64 consecutive input columns (one per lane) of a vertical
 // segment of the level's output rows and slides down it: every step takes
@@ -797,12 +838,12 @@ __device__ __forceinline__ void strip_row_generic(const double *row, Filters flt
     hi = dwt_tap_sum_logical(flt.dec_hi, F, w, ic, load);
 }
 
-// The strip holding the outputs whose taps wrap past the line end slides like
-// the others (its wrapping lanes reorder their row-pass taps from the same
-// window, wrap_sum) instead of running every row through the generic sums with
-// per-tap global loads -- the slowest wave of a small level
+// TAILFAST: the strip holding the outputs whose taps wrap past the line end
+// slides like the others (its wrapping lanes reorder their row-pass taps from
+// the same window, wrap_sum) instead of running every row through the generic
+// sums with per-tap global loads -- the slowest wave of a small level
 template <int F, bool FIRST, bool LAST, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0, bool Z0 = true,
-          bool QP2 = true>
+          bool QP2 = true, int DIAG = 0, bool TAILFAST = true>
 __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                         const double *__restrict__ in, long long plane_stride,
                                                         double *__restrict__ LLout, uint8_t *__restrict__ packed,
@@ -924,7 +965,7 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
             }
             lo = nat_sum<F, ZLO, Z0>(flo, v);
             hi = nat_sum<F, ZHI, Z0>(fhi, v);
-            if (strip_tail && ic >= w) {   // this lane's taps wrap past the line end
+            if (TAILFAST && strip_tail && ic >= w) {   // this lane's taps wrap past the line end
                 lo = wrap_sum<F, ZLO>(flo, v, ic, w);
                 hi = wrap_sum<F, ZHI>(fhi, v, ic, w);
             }
@@ -934,8 +975,10 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
         }
         // A lanes: ad -> HL, aa -> LL; D lanes: da -> LH, dd -> HH
         const uint32_t e = rb + e_lane;
-        __builtin_amdgcn_raw_buffer_store_b8(q8(src ? lo : hi), rs_pk, ((uint32_t)off_r1 + e) | drop1, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b8(q8(hi), rs_pk, ((uint32_t)off_hh + e) | drop_d, 0, 0);
+        if (DIAG != 1) {
+            __builtin_amdgcn_raw_buffer_store_b8(q8(src ? lo : hi), rs_pk, ((uint32_t)off_r1 + e) | drop1, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8(q8(hi), rs_pk, ((uint32_t)off_hh + e) | drop_d, 0, 0);
+        }
         if (LAST)
             __builtin_amdgcn_raw_buffer_store_b16(q16(lo), rs_pk, ((uint32_t)ll_off + 2 * e) | drop_a, 0, 0);
         else
@@ -956,6 +999,11 @@ __global__ __launch_bounds__(192) void dwt_strip_kernel(const uint8_t *__restric
             row_pass(o, 0, generic);
         }
     };
+    if (strip_tail && !TAILFAST) {   // the earlier tail strip: every row through the generic sums
+        direct_rows(o0, std::true_type());
+        return;
+    }
+
     // sliding rows: groups of P steps; window slot (2u + k) % F of step u of a
     // group holds logical input row 2o - F/2 + 1 + k.  Rows are loaded P
     // steps ahead.  Level 1 runs one copy of the loop per channel (the YCoCg
@@ -1081,11 +1129,11 @@ __host__ __device__ constexpr double ct_rec(int id, bool hi, int m)
 }
 
 // CT: reconstruction taps of wavelet CT (ct_rec) as compile-time constants
-// (no tap registers: 40 fewer VGPRs than taps staged through LDS).  Output
-// tiles of 64 x 16 (32 x 32 / 128 x 8 measured +3 % / +21 % on C3,
-// profiles/r02_dwt_decode_ab_tiles.log); wave priority 3 while the subbands
-// are staged.
-template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0>
+// (no tap registers: 40 fewer VGPRs than taps staged through LDS)
+// ITW: output tile width (the tile is 1024 / ITW rows; 64 x 16 the default, 32 x 32 / 128 x 8 = dwt decode
+// variants 15 / 16, A/B: +3 % / +21 % on C3, profiles/r02_dwt_decode_ab_tiles.log)
+template <int F, bool FROM_PACKED_LL, bool TO_RGB, unsigned ZLO = 0, unsigned ZHI = 0, int CT = 0, int PRI = 3,
+          int ITW = kITW>
 __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
                                                          long long ll_off, long long off_lh, long long off_hl,
                                                          long long off_hh, const double *__restrict__ prev,
@@ -1093,7 +1141,7 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
                                                          int h, int w, int oh, int ow, int Q, Taps<F> tp,
                                                          Filters flt, uint8_t *__restrict__ rgb, long long rgb_stride)
 {
-    constexpr int ITW = kITW, ITH = 1024 / ITW;
+    constexpr int ITH = 1024 / ITW;
     constexpr int F2 = F / 2, T = F2 / 2;
     constexpr int KHm = ITH / 2 + F2, KWm = ITW / 2 + F2;
     constexpr int P0 = (F2 - 1) & 1;                 // parity of n + F2 - 1 for even n
@@ -1132,7 +1180,8 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
         fhi[m] = CT ? ct_rec(CT, true, m) : taps[F + m];
     }
     for (int ch = ch_lo; ch < ch_hi; ++ch) {
-        __builtin_amdgcn_s_setprio(3);
+        // PRI: wave priority while the subbands are staged (0: decode variant 5, A/B)
+        if (PRI) __builtin_amdgcn_s_setprio(PRI);
         for (int t = tid; t < KH * KW; t += 256) {
             const int r = t / KW, c = t - r * KW;
             const int y = rows_in ? K0r + r : mod_pos(K0r + r, h);
@@ -1151,7 +1200,7 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
             sDA[l] = dequant((int16_t)pk[off_lh + e], Q);   // 'da' = cH = LH
             sDD[l] = dequant((int16_t)pk[off_hh + e], Q);   // 'dd' = cD = HH
         }
-        __builtin_amdgcn_s_setprio(0);
+        if (PRI) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         // row pass (axis 1): 'a' = idwt(aa, ad), 'd' = idwt(da, dd)
         for (int t = tid; t < KH * NGC * 2; t += 256) {
@@ -1309,6 +1358,9 @@ struct LevelArgs {
     Filters flt;
     const WaveletDef *wd;
     hipStream_t s;
+    int pipe = 1;   // fused levels, bior4.4/db5: 0 = the three-barrier schedule (variant 3), 2 = run-time taps (4),
+                    // 3 = level 1 staged as float (5)
+    int copy_w = 4; // fused forward levels' copy-out: 4 = dwords when aligned, 1 = bytes (variant 10)
 };
 
 // bit m set = tap m is exactly 0.0
@@ -1329,22 +1381,59 @@ void launch_fwd_kernel(const LevelArgs &a, const Taps<F> &tp, const dim3 &grid, 
 {
     auto kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI> : dwt_level_kernel<F, true, false, ZLO, ZHI>)
                       : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI> : dwt_level_kernel<F, false, false, ZLO, ZHI>);
-    if constexpr (F == 10) {   // bior4.4 / db5: compile-time taps, sums started by their first product
+    if constexpr (F == 10) {   // bior4.4 / db5: constant taps (pipe 2: run-time taps, dwt variant 4)
         constexpr int id = ZLO != 0 ? 1 : 2;
-        constexpr int stg = id == 2 ? 1 : 0;
-        bool ct = true;
+        bool ct = a.pipe == 1 || a.pipe == 3 || a.pipe == 5 || a.pipe == 6 || a.pipe == 7 || a.pipe == 8;
         for (int m = 0; m < F; ++m) {
             const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
             ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
         }
-        if (ct)
-            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, id, stg, true>
-                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, id, stg, true>)
-                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, id, 0, true>
-                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, id, 0, true>);
+        constexpr int stg = id == 2 ? 1 : 0;
+        if (ct && a.pipe == 6)   // sums started at 0.0 (dwt variant 23, A/B)
+            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, stg>
+                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, stg>)
+                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, id>
+                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, true, id>);
+        else if (ct)
+            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, stg, 3, true>
+                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, stg, 3, true>)
+                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, id, 0, 3, true>
+                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, true, id, 0, 3, true>);
+        if (ct && a.pipe == 3 && first)   // level 1 staged as float, no wave priority (dwt variant 5, A/B)
+            kern = last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, 0, 0>
+                        : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, 0, 0>;
+        if (ct && a.pipe == 5)   // no raised wave priority on any fused level, staging unchanged (variant 12, A/B)
+            kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, true, id, stg, 0>
+                                 : dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, stg, 0>)
+                         : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, true, id, 0, 0>
+                                 : dwt_level_kernel<F, false, false, ZLO, ZHI, true, id, 0, 0>);
+        if constexpr (ZLO != 0) {   // bior4.4: the earlier three-barrier schedule for A/B (variant 3)
+            if (a.pipe == 0)
+                kern = first ? (last ? dwt_level_kernel<F, true, true, ZLO, ZHI, false>
+                                     : dwt_level_kernel<F, true, false, ZLO, ZHI, false>)
+                             : (last ? dwt_level_kernel<F, false, true, ZLO, ZHI, false>
+                                     : dwt_level_kernel<F, false, false, ZLO, ZHI, false>);
+        }
+    }
+    if constexpr (F == 10) {
+        constexpr int id = ZLO != 0 ? 1 : 2;
+        bool ct = a.pipe == 7;
+        for (int m = 0; m < F; ++m) {
+            const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
+            ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
+        }
+        if (ct && first && !last) {   // level 1 in 512-thread tiles of 16 output rows, int16 staging (variant 24)
+            constexpr int NT = 512, FTH = NT / kFIW * kG;
+            const dim3 g2(grid.x, (a.hh + FTH - 1) / FTH, grid.z);
+            hipLaunchKernelGGL((dwt_level_kernel<F, true, false, ZLO, ZHI, true, id, 1, 3, true, NT>), g2, dim3(NT),
+                               0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed, a.packed_stride,
+                               a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, a.copy_w);
+            return;
+        }
     }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.rgb, a.rgb_stride, a.in, a.plane_stride, a.LLout, a.packed,
-                       a.packed_stride, a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt);
+                       a.packed_stride, a.ll_off, a.off_lh, a.off_hl, a.off_hh, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt,
+                       a.copy_w);
 }
 
 template <int F>
@@ -1359,7 +1448,7 @@ void launch_fwd_level(const LevelArgs &a, bool first, bool last)
         launch_fwd_kernel<F, 0u, 0u>(a, tp, grid, first, last);
 }
 
-// strip kernels
+// strip kernels (dwt variant 6; 7 = the same with every sum started at 0.0)
 constexpr int kMaxStripF = 10;   // longest filter with a strip kernel (F samples of window in VGPRs)
 
 template <int F>
@@ -1367,18 +1456,19 @@ using StripKern = void (*)(const uint8_t *, long long, const double *, long long
                            long long, long long, long long, long long, int, int, int, int, int, int, int, Taps<F>,
                            Filters);
 
-template <int F, unsigned ZL, unsigned ZH, int CT, bool QP2>
+template <int F, unsigned ZL, unsigned ZH, int CT, bool Z0, bool QP2, int DIAG = 0, bool TF = true>
 StripKern<F> strip_kern(bool first, bool last)
 {
-    return first ? (last ? dwt_strip_kernel<F, true, true, ZL, ZH, CT, true, QP2>
-                         : dwt_strip_kernel<F, true, false, ZL, ZH, CT, true, QP2>)
-                 : (last ? dwt_strip_kernel<F, false, true, ZL, ZH, CT, true, QP2>
-                         : dwt_strip_kernel<F, false, false, ZL, ZH, CT, true, QP2>);
+    return first ? (last ? dwt_strip_kernel<F, true, true, ZL, ZH, CT, Z0, QP2, DIAG, TF>
+                         : dwt_strip_kernel<F, true, false, ZL, ZH, CT, Z0, QP2, DIAG, TF>)
+                 : (last ? dwt_strip_kernel<F, false, true, ZL, ZH, CT, Z0, QP2, DIAG, TF>
+                         : dwt_strip_kernel<F, false, false, ZL, ZH, CT, Z0, QP2, DIAG, TF>);
 }
 
 template <int F>
-void launch_strip_level(const LevelArgs &a, bool first, bool last)
+void launch_strip_level(const LevelArgs &a, bool first, bool last, int mode)
 {
+    const bool z0 = mode != 7;
     if constexpr (F > kMaxStripF) {
         return;
     } else {
@@ -1392,7 +1482,8 @@ void launch_strip_level(const LevelArgs &a, bool first, bool last)
         seg = std::min((seg + P - 1) / P * P, a.hh);
         const long long nblk = (long long)n_strips * ((a.hh + seg - 1) / seg) * a.n_frames;
         const bool qp2 = (a.Q & (a.Q - 1)) == 0;
-        StripKern<F> kern = qp2 ? strip_kern<F, 0u, 0u, 0, true>(first, last) : strip_kern<F, 0u, 0u, 0, false>(first, last);
+        StripKern<F> kern = qp2 ? strip_kern<F, 0u, 0u, 0, true, true>(first, last)
+                                : strip_kern<F, 0u, 0u, 0, true, false>(first, last);
         if constexpr (F == 10) {   // bior4.4 (zero taps skipped) / db5: compile-time taps
             const bool b44 = zero_mask(a.wd->dec_lo, F) == kB44DecLo && zero_mask(a.wd->dec_hi, F) == kB44DecHi;
             const int id = b44 ? 1 : 2;
@@ -1401,11 +1492,18 @@ void launch_strip_level(const LevelArgs &a, bool first, bool last)
                 const double l = ct_dec(id, false, m), h = ct_dec(id, true, m);
                 ct = std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
             }
-            if (ct && b44)
-                kern = qp2 ? strip_kern<F, kB44DecLo, kB44DecHi, 1, true>(first, last)
-                           : strip_kern<F, kB44DecLo, kB44DecHi, 1, false>(first, last);
+            if (ct && b44 && qp2 && mode == 8)   // diagnostic: no detail-subband stores
+                kern = strip_kern<F, kB44DecLo, kB44DecHi, 1, true, true, 1>(first, last);
+
+            else if (ct && b44 && qp2 && z0 && a.pipe == 8)   // the earlier all-generic tail strip (variant 25)
+                kern = strip_kern<F, kB44DecLo, kB44DecHi, 1, true, true, 0, false>(first, last);
+            else if (ct && b44)
+                kern = qp2 ? (z0 ? strip_kern<F, kB44DecLo, kB44DecHi, 1, true, true>(first, last)
+                                 : strip_kern<F, kB44DecLo, kB44DecHi, 1, false, true>(first, last))
+                           : strip_kern<F, kB44DecLo, kB44DecHi, 1, true, false>(first, last);
             else if (ct)
-                kern = qp2 ? strip_kern<F, 0u, 0u, 2, true>(first, last) : strip_kern<F, 0u, 0u, 2, false>(first, last);
+                kern = qp2 ? strip_kern<F, 0u, 0u, 2, true, true>(first, last)
+                           : strip_kern<F, 0u, 0u, 2, true, false>(first, last);
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(192), 0, a.s, a.rgb, a.rgb_stride, a.in,
                            a.plane_stride, a.LLout, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
@@ -1421,9 +1519,9 @@ void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, dim3 grid, bool fr
     auto kern = from_packed
                     ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI> : idwt_level_kernel<F, true, false, ZLO, ZHI>)
                     : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI> : idwt_level_kernel<F, false, false, ZLO, ZHI>);
-    if constexpr (F == 10) {   // bior4.4 / db5: compile-time taps
+    if constexpr (F == 10) {   // bior4.4 / db5: constant taps (run-time taps for A/B: dwt decode variant 4)
         constexpr int id = ZLO != 0 ? 1 : 2;
-        bool ct = true;
+        bool ct = a.pipe == 1 || a.pipe == 3 || a.pipe == 4 || a.pipe == 5;
         for (int m = 0; m < F; ++m) {
             const double l = ct_rec(id, false, m), h = ct_rec(id, true, m);
             ct = ct && std::memcmp(&l, &tp.lo[m], 8) == 0 && std::memcmp(&h, &tp.hi[m], 8) == 0;
@@ -1433,6 +1531,27 @@ void launch_inv_kernel(const LevelArgs &a, const Taps<F> &tp, dim3 grid, bool fr
                                          : idwt_level_kernel<F, true, false, ZLO, ZHI, id>)
                                : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id>
                                          : idwt_level_kernel<F, false, false, ZLO, ZHI, id>);
+        if (ct && a.pipe == 3)   // no wave priority for the staging (dwt decode variant 5, A/B)
+            kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI, id, 0>
+                                         : idwt_level_kernel<F, true, false, ZLO, ZHI, id, 0>)
+                               : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id, 0>
+                                         : idwt_level_kernel<F, false, false, ZLO, ZHI, id, 0>);
+        if (ct && a.pipe == 4) {   // 32 x 32 output tiles (dwt decode variant 15, A/B)
+            kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI, id, 3, 32>
+                                         : idwt_level_kernel<F, true, false, ZLO, ZHI, id, 3, 32>)
+                               : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id, 3, 32>
+                                         : idwt_level_kernel<F, false, false, ZLO, ZHI, id, 3, 32>);
+            grid.x = (unsigned)((a.hw + 31) / 32);
+            grid.y = (unsigned)((a.hh + 31) / 32);
+        }
+        if (ct && a.pipe == 5) {   // 128 x 8 output tiles (dwt decode variant 16, A/B)
+            kern = from_packed ? (to_rgb ? idwt_level_kernel<F, true, true, ZLO, ZHI, id, 3, 128>
+                                         : idwt_level_kernel<F, true, false, ZLO, ZHI, id, 3, 128>)
+                               : (to_rgb ? idwt_level_kernel<F, false, true, ZLO, ZHI, id, 3, 128>
+                                         : idwt_level_kernel<F, false, false, ZLO, ZHI, id, 3, 128>);
+            grid.x = (unsigned)((a.hw + 127) / 128);
+            grid.y = (unsigned)((a.hh + 7) / 8);
+        }
     }
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, a.s, a.packed, a.packed_stride, a.ll_off, a.off_lh, a.off_hl,
                        a.off_hh, a.in, a.plane_stride, a.lda, a.LLout, a.h, a.w, a.hh, a.hw, a.Q, tp, a.flt, rgb_out,
@@ -1607,12 +1726,12 @@ void fwd_level(int F, const LevelArgs &a, bool first, bool last)
     }
 }
 
-void strip_level(int F, const LevelArgs &a, bool first, bool last)
+void strip_level(int F, const LevelArgs &a, bool first, bool last, int mode)
 {
     switch (F) {
 #define X(n)                                                                                                       \
     case n:                                                                                                        \
-        launch_strip_level<n>(a, first, last);                                                                     \
+        launch_strip_level<n>(a, first, last, mode);                                                               \
         break;
         VCF_DWT_FOR_EACH_F(X)
 #undef X
@@ -1636,7 +1755,7 @@ void inv_level(int F, const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t
 }
 
 // ---------------------------------------------------------------------------
-// Frame pipeline over library streams (the encode's level-by-level chain)
+// Frame pipeline over library streams (dwt encode variants 13-16, decode 6-8)
 // ---------------------------------------------------------------------------
 // A 4K level 1 fills the chip; levels 3 .. l hold a few thousand waves or a
 // few hundred workgroups each, whose serial chains leave most SIMDs idle
@@ -1652,7 +1771,7 @@ void inv_level(int F, const LevelArgs &a, bool from_packed, bool to_rgb, uint8_t
 bool pipeline_default(long long n_frames, int H, int W) { return n_frames >= 2 && (long long)H * W >= (1LL << 20); }
 // (measured on C3, ABBA: encode two unstaggered chunks -7.8 %; staggering, more chunks or
 // streams, and every decode pipeline were slower -- DESIGN.md §6)
-constexpr PipeShape kEncodePipe{2, 2, false};
+constexpr PipeShape kEncodePipe{2, 2, false}, kDecodePipe{0, 0, false};
 
 #endif  // VCF_DWT_KERNELS_ONLY
 }  // namespace
@@ -1689,21 +1808,25 @@ int vcf_dwt_layout(int32_t H, int32_t W, int32_t levels, int32_t *sub_h, int32_t
     return VCF_OK;
 }
 
-// one stream's level chain of the encode (the frame pipeline calls it per
-// chunk of frames with its hook).  Levels: 1 and 2 in one band launch when
-// band12_ok (10-tap filters with compile-time taps, C3), else fused level
-// kernels; levels between the first and the last on the strip kernels
-// (F <= kMaxStripF and planes of at least 2F); levels after the first whose
-// input planes have at most kSepArea samples on the separable kernels -- one
-// thread per output beats the fused tile's three serial channels there (-2.2 %
-// on C3, ABBA); filters longer than kMaxFastF on the separable kernels alone.
-constexpr long long kSepArea = 40000;
+int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
+                      int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, void *stream)
+{
+    return vcf_dwt_dz_encode_variant(0, rgb_dev, n_frames, H, W, wavelet, levels, Q, packed_dev, workspace_dev,
+                                     stream);
+}
 
-static int encode_chain(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
+// one stream's level chain of the encode (variants 0-12; the pipelined forms
+// call it per chunk of frames with their hook)
+static int encode_chain(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                         int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, hipStream_t s,
-                        const PipeHook *hook)
+                        const PipeHook *hook, long long sep_area = 0, bool no_band = false)
 {
     int rc = VCF_OK;
+    // 10: variant 0 with the byte-wise copy-out, 11: with the earlier row-pass mapping,
+    // 12: with no raised wave priority on the fused levels (A/B)
+    const int copy_w = variant == 10 ? 1 : variant == 11 ? 4 | 8 : 4;
+    const int pipe0 = variant == 12 ? 5 : variant == 23 ? 6 : variant == 24 ? 7 : variant == 25 ? 8 : 1;
+    if (variant >= 10) variant = 0;
     Filters flt;
     if ((rc = device_filters(wavelet, flt)) != VCF_OK) return rc;
     DwtGeom g;
@@ -1716,7 +1839,10 @@ static int encode_chain(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int
     double *LL0 = D + (D - A), *LL1 = LL0 + 4LL * g.hs[1] * g.ws[1];
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *in = nullptr;
-    const bool fused = fast_filter(F);
+    const bool fused = variant == 1 || variant >= 3 || (variant == 0 && fast_filter(F));
+    if (fused && !fast_filter(F))
+        return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
+                         kMaxFastF);
     // one level on the separable kernels (column pass, then the row pass into the subbands / LL)
     auto sep_level = [&](int l) {
         const int h = g.hs[l - 1], w = g.ws[l - 1], hh = g.hs[l], hw = g.ws[l];
@@ -1738,7 +1864,7 @@ static int encode_chain(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int
     };
     int l_start = 1;
     int band_id = 0;
-    if (fused && band12_ok(g, kWavelets[wavelet], band_id)) {
+    if (fused && (variant == 0 || variant == 9) && !no_band && band12_ok(g, kWavelets[wavelet], band_id)) {
         // levels 1 and 2 in one launch: LL1 never leaves the chip; LL2 lands where level 2's would
         if ((rc = hook_wait(hook, s)) != VCF_OK) return rc;
         launch_band12(band_id, g, rgb_dev, n_frames, LL1, ws_stride, packed_dev, Q, s);
@@ -1747,67 +1873,112 @@ static int encode_chain(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int
         in = LL1;
         l_start = 3;
     }
-    for (int l = l_start; l <= levels; ++l) {
+    for (int l = l_start; fused && l <= levels; ++l) {
         double *LLout = (l & 1) ? LL0 : LL1;
+        const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
+                          g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
+                          g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s,
+                          variant == 3 ? 0 : variant == 4 ? 2 : variant == 5 ? 3 : pipe0, copy_w};
+        // strips need planes of at least 2F rows and columns (their row wrap)
+        const bool strip = F <= kMaxStripF && g.hs[l - 1] >= 2 * F && g.ws[l - 1] >= 2 * F &&
+                           ((variant >= 6 && variant <= 8) || ((variant == 0 || variant == 9) && l > 1 && l < levels));
         if (l == 1 && (rc = hook_wait(hook, s)) != VCF_OK) return rc;
-        if (!fused || (l > 1 && (long long)g.hs[l - 1] * g.ws[l - 1] <= kSepArea)) {
-            sep_level(l);
-        } else {
-            const LevelArgs a{rgb_dev, (long long)H * W * 3, in, ws_stride, LLout, packed_dev, g.packed_bytes, g.ll_off,
-                              g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], g.hs[l - 1], g.ws[l - 1], g.hs[l],
-                              g.ws[l], Q, 0, (unsigned)n_frames, flt, &kWavelets[wavelet], s};
-            // strips need planes of at least 2F rows and columns (their row wrap)
-            const bool strip = F <= kMaxStripF && g.hs[l - 1] >= 2 * F && g.ws[l - 1] >= 2 * F && l > 1 && l < levels;
-            if (strip) strip_level(F, a, false, false);
-            else fwd_level(F, a, l == 1, l == levels);
-        }
+        if (l > 1 && (long long)g.hs[l - 1] * g.ws[l - 1] <= sep_area)
+            sep_level(l);   // small levels on the separable kernels (A/B: variants 20-22)
+        else if (strip)
+            strip_level(F, a, l == 1, l == levels, variant);
+        else
+            fwd_level(F, a, l == 1, l == levels);
         in = LLout;
-        if ((rc = hip_check(hipGetLastError(), "dwt level launch")) != VCF_OK) return rc;
+        rc = hip_check(hipGetLastError(), "dwt level launch");
+        if (rc != VCF_OK) return rc;
         if (l == 1 && (rc = hook_rec(hook, s)) != VCF_OK) return rc;
+    }
+    for (int l = 1; !fused && l <= levels; ++l) {
+        sep_level(l);
+        in = (l & 1) ? LL0 : LL1;
+        rc = hip_check(hipGetLastError(), "dwt encode launch");
+        if (rc != VCF_OK) return rc;
     }
     return VCF_OK;
 }
 
-int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
-                      int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, void *stream)
+int vcf_dwt_dz_encode_variant(int variant, const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W,
+                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev,
+                              void *stream)
 {
+    if (variant < 0 || variant > 27) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    // 27: variant 0 without the fused level-1+2 band kernel (levels 1 and 2 as separate launches; A/B)
+    const bool no_band = variant == 27;
+    if (variant == 27) variant = 0;
     int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
     if (rc != VCF_OK) return rc;
     if (n_frames == 0) return VCF_OK;
     if (!workspace_dev) return set_error(VCF_ERR_INVALID, "null workspace");
     if (n_frames * 3 > 65535) return set_error(VCF_ERR_INVALID, "at most 21845 frames per call");
+    // frame pipeline (A/B: 13 = two streams and two chunks; 14 = the same staggered; 15 / 16 =
+    // two streams, four / eight chunks, staggered; 18 = three streams, four chunks, staggered;
+    // 19 = four streams, four chunks; 17 = variant 0 on the caller's stream alone)
     hipStream_t s = (hipStream_t)stream;
-    DwtGeom g;
-    dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
-    int id = 0;
+    PipeShape ps;
     // the frame pipeline pays only for the level-by-level chain: with the fused
     // level-1+2 band kernel one launch fills the chip (C3: 0.594 ms on one
     // stream vs 0.635 ms pipelined, ABBA)
-    const bool band = fast_filter(g.F) && band12_ok(g, kWavelets[wavelet], id);
-    if (!band && fast_filter(g.F) && pipeline_default(n_frames, H, W)) {
+    bool band = false;
+    {
+        DwtGeom g;
+        dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
+        int id = 0;
+        band = !no_band && band12_ok(g, kWavelets[wavelet], id);
+    }
+    if (variant == 0 && pipeline_default(n_frames, H, W) && !band) ps = kEncodePipe;
+    if (variant == 13) ps = {2, 2, false};
+    if (variant == 14) ps = {2, 2, true};
+    if (variant == 15) ps = {2, 4, true};
+    if (variant == 16) ps = {2, 8, true};
+    if (variant == 18) ps = {3, 4, true};
+    if (variant == 19) ps = {4, 4, false};
+    if (variant == 26) ps = {2, 2, false, true};   // 13 with chunk 0 on the caller's stream
+    // levels after the first whose input planes have at most 40 k samples (at 4K: level 5) run on
+    // the separable kernels: one thread per output beats the fused tile's three serial channels
+    // there (-2.2 % on C3, ABBA); 20 = none of them (the earlier schedule), 21 / 22 = up to
+    // 140 k / 600 k samples (at 4K: levels 4-5 / 3-5)
+    const long long sep_area = variant == 20 || (variant >= 1 && variant <= 12) ? 0
+                               : variant == 21                                    ? 140000
+                               : variant == 22                                    ? 600000
+                                                                                  : 40000;
+    if (variant >= 20 && pipeline_default(n_frames, H, W) && !band) ps = kEncodePipe;
+    // 23: variant 0 with the fused levels' sums started at 0.0 (no Z0, A/B)
+    // 24: variant 0 with level 1 in 512-thread tiles of 16 output rows (int16 staging)
+    // 25: variant 0 with the earlier tail strip (every row through the generic sums)
+    const int cv = variant >= 23 && variant <= 25 ? variant : 0;
+    if (variant >= 13) variant = cv;
+    if (ps.streams > 0 && fast_filter(kWavelets[wavelet].len)) {
+        DwtGeom g;
+        dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
         const long long fpx = (long long)H * W * 3, wsf = 3 * plane_doubles(g);
-        return run_pipelined(n_frames, kEncodePipe, s, [&](long long f0, long long n, hipStream_t cs, const PipeHook *hook) {
-            return encode_chain(rgb_dev + f0 * fpx, n, H, W, wavelet, levels, Q, packed_dev + f0 * g.packed_bytes,
-                                (double *)workspace_dev + f0 * wsf, cs, hook);
+        return run_pipelined(n_frames, ps, s, [&](long long f0, long long n, hipStream_t cs, const PipeHook *hook) {
+            return encode_chain(cv, rgb_dev + f0 * fpx, n, H, W, wavelet, levels, Q, packed_dev + f0 * g.packed_bytes,
+                                (double *)workspace_dev + f0 * wsf, cs, hook, sep_area, no_band);
         });
     }
-    return encode_chain(rgb_dev, n_frames, H, W, wavelet, levels, Q, packed_dev, workspace_dev, s, nullptr);
+    return encode_chain(variant, rgb_dev, n_frames, H, W, wavelet, levels, Q, packed_dev, workspace_dev, s, nullptr,
+                        sep_area, no_band);
 }
 
-// one stream's level chain of the decode: coarsest level first; the line
-// kernel (idwt_line_kernel) where line_ok, else the fused level kernels;
-// subbands shorter than F/2 (pywt's short-input branch: the coefficients wrap
-// around more than once) and filters longer than kMaxFastF on the separable
-// kernels, whose loads take any index modulo the line length
 int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                       int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, void *stream)
 {
-    int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
-    if (rc != VCF_OK) return rc;
-    if (n_frames == 0) return VCF_OK;
-    if (!workspace_dev) return set_error(VCF_ERR_INVALID, "null workspace");
-    if (n_frames * 3 > 65535) return set_error(VCF_ERR_INVALID, "at most 21845 frames per call");
-    hipStream_t s = (hipStream_t)stream;
+    return vcf_dwt_dz_decode_variant(0, packed_dev, n_frames, H, W, wavelet, levels, Q, rgb_dev, workspace_dev,
+                                     stream);
+}
+
+// one stream's level chain of the decode (variants 0-5)
+static int decode_chain(int variant, const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W,
+                        int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
+                        hipStream_t s, const PipeHook *hook, long long sep_area = 0, int line_mode = 0)
+{
+    int rc = VCF_OK;
     Filters flt;
     if ((rc = device_filters(wavelet, flt)) != VCF_OK) return rc;
     DwtGeom g;
@@ -1821,21 +1992,58 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
     const unsigned planes = (unsigned)(n_frames * 3);
     const double *prev = nullptr;
     int lda = 0;
+    // subbands shorter than F/2 (pywt's short-input branch: the coefficients
+    // wrap around more than once) run on the separable kernels, whose loads
+    // take any index modulo the line length; the fused tiles wrap once
     const bool short_lines = g.hs[levels] < F / 2 || g.ws[levels] < F / 2;
-    if (fast_filter(F) && !short_lines) {
+    const bool fused = variant == 1 || variant >= 4 || (variant == 0 && fast_filter(F) && !short_lines);
+    if (fused && !fast_filter(F))
+        return set_error(VCF_ERR_UNSUPPORTED, "filter length %d: the fused level kernels take 2..%d taps", F,
+                         kMaxFastF);
+    if (fused && short_lines)
+        return set_error(VCF_ERR_UNSUPPORTED,
+                         "level-%d subbands of %d x %d are shorter than the %s filter half-length %d: the fused "
+                         "kernels wrap once (variant 0 or 2 runs them)",
+                         levels, g.hs[levels], g.ws[levels], kWavelets[wavelet].name, F / 2);
+    if (fused) {
         for (int r = levels; r >= 1; --r) {
             const int h = g.hs[r], w = g.ws[r];
             const int oh = r > 1 ? g.hs[r - 1] : 2 * h, ow = r > 1 ? g.ws[r - 1] : 2 * w;
             double *out = (r & 1) ? P0 : P1;
             const LevelArgs a{nullptr, 0, prev, ws_stride, out, const_cast<uint8_t *>(packed_dev), g.packed_bytes,
                               g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], h, w, oh, ow, Q, lda,
-                              (unsigned)n_frames, flt, &kWavelets[wavelet], s};
+                              (unsigned)n_frames, flt, &kWavelets[wavelet], s,
+                              variant == 4 ? 2 : variant == 5 ? 3 : variant == 15 ? 4 : variant == 16 ? 5 : 1};
+            if (r > 1 && (long long)h * w <= sep_area) {   // a small level on the separable kernels (A/B)
+                if (r == levels)
+                    hipLaunchKernelGGL(idwt_rows_kernel<true>, dim3(gx(2 * w), h, planes), dim3(256), 0, s, packed_dev,
+                                       g.packed_bytes, g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2],
+                                       nullptr, 0LL, 0, A, D, ws_stride, h, w, F, Q, flt);
+                else
+                    hipLaunchKernelGGL(idwt_rows_kernel<false>, dim3(gx(2 * w), h, planes), dim3(256), 0, s,
+                                       packed_dev, g.packed_bytes, g.ll_off, g.sb_off[r][0], g.sb_off[r][1],
+                                       g.sb_off[r][2], prev, ws_stride, lda, A, D, ws_stride, h, w, F, Q, flt);
+                hipLaunchKernelGGL(idwt_cols_kernel, dim3(gx(2 * w), 2 * h, planes), dim3(256), 0, s, A, D,
+                                   ws_stride, out, ws_stride, h, 2 * w, F, flt);
+                prev = out;
+                lda = 2 * w;
+                if ((rc = hip_check(hipGetLastError(), "idwt level launch")) != VCF_OK) return rc;
+                continue;
+            }
+            if (r == 1 && (rc = hook_wait(hook, s)) != VCF_OK) return rc;
+            // line_mode: 0 = line kernel on every eligible level, 1 = none (the
+            // tiled level kernels, decode variant 17), 2 = level 1 only (18)
             int id = 0;
-            if (line_ok(kWavelets[wavelet], h, w, id)) launch_line(id, a, r == levels, r == 1, rgb_dev);
-            else inv_level(F, a, r == levels, r == 1, rgb_dev);
+            if ((variant == 0 || variant == 9) && (line_mode == 0 || (line_mode == 2 && r == 1)) &&
+                line_ok(kWavelets[wavelet], h, w, id))
+                launch_line(id, a, r == levels, r == 1, rgb_dev);
+            else
+                inv_level(F, a, r == levels, r == 1, rgb_dev);
             prev = out;
             lda = ow;
-            if ((rc = hip_check(hipGetLastError(), "idwt level launch")) != VCF_OK) return rc;
+            rc = hip_check(hipGetLastError(), "idwt level launch");
+            if (rc != VCF_OK) return rc;
+            if (r == 1 && (rc = hook_rec(hook, s)) != VCF_OK) return rc;
         }
         return VCF_OK;
     }
@@ -1854,7 +2062,8 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
                            ws_stride, h, 2 * w, F, flt);
         prev = out;
         lda = 2 * w;   // the next level trims rows/cols by indexing only h' x w'
-        if ((rc = hip_check(hipGetLastError(), "dwt decode launch")) != VCF_OK) return rc;
+        rc = hip_check(hipGetLastError(), "dwt decode launch");
+        if (rc != VCF_OK) return rc;
     }
     const int Ho = 2 * g.hs[1], Wo = 2 * g.ws[1];
     const long long npx = (long long)Ho * Wo;
@@ -1863,5 +2072,53 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
     return hip_check(hipGetLastError(), "dwt to_rgb launch");
 }
 
+int vcf_dwt_dz_decode_variant(int variant, const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W,
+                              int32_t wavelet, int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev,
+                              void *stream)
+{
+    if (variant < 0 || variant == 3 || variant > 18) return set_error(VCF_ERR_INVALID, "unknown dwt variant %d", variant);
+    // 17 / 18: variant 0 with the tiled level kernels on every level / on every level but the first
+    // (the line kernel's A/B)
+    const int line_mode = variant == 17 ? 1 : variant == 18 ? 2 : 0;
+    if (variant >= 17) variant = 0;
+    int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
+    if (rc != VCF_OK) return rc;
+    if (n_frames == 0) return VCF_OK;
+    if (!workspace_dev) return set_error(VCF_ERR_INVALID, "null workspace");
+    if (n_frames * 3 > 65535) return set_error(VCF_ERR_INVALID, "at most 21845 frames per call");
+    // frame pipeline as in the encode (A/B: 6 = two streams and two chunks; 7 = the same
+    // staggered; 8 / 10 = two streams, four / eight chunks, staggered; 11 = three streams, four
+    // chunks, staggered; 9 = variant 0 on the caller's stream alone)
+    PipeShape ps;
+    if (variant == 0 && pipeline_default(n_frames, H, W)) ps = kDecodePipe;
+    if (variant == 6) ps = {2, 2, false};
+    if (variant == 7) ps = {2, 2, true};
+    if (variant == 8) ps = {2, 4, true};
+    if (variant == 10) ps = {2, 8, true};
+    if (variant == 11) ps = {3, 4, true};
+    // 12 / 13 / 14: variant 0 with the levels after the coarsest-first order's big one whose subbands
+    // have at most 10 k / 40 k / 140 k samples on the separable kernels (4K: level 5 / 4-5 / 3-5)
+    const long long sep_area = variant == 12 ? 10000 : variant == 13 ? 40000 : variant == 14 ? 140000 : 0;
+    if (variant >= 6 && variant < 15) variant = 0;
+    {
+        DwtGeom g;
+        dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
+        const int F = g.F;
+        if (ps.streams > 0 && fast_filter(F) && !(g.hs[levels] < F / 2 || g.ws[levels] < F / 2)) {
+            const long long fpx = (long long)2 * g.hs[1] * 2 * g.ws[1] * 3, wsf = 3 * plane_doubles(g);
+            return run_pipelined(n_frames, ps, (hipStream_t)stream,
+                                 [&](long long f0, long long n, hipStream_t cs, const PipeHook *hook) {
+                                     return decode_chain(0, packed_dev + f0 * g.packed_bytes, n, H, W, wavelet,
+                                                         levels, Q, rgb_dev + f0 * fpx,
+                                                         (double *)workspace_dev + f0 * wsf, cs, hook, 0,
+                                                         line_mode);
+                                 });
+        }
+    }
+    return decode_chain(variant, packed_dev, n_frames, H, W, wavelet, levels, Q, rgb_dev, workspace_dev,
+                        (hipStream_t)stream, nullptr, sep_area, line_mode);
+}
+
 }  // extern "C"
+
 #endif  // VCF_DWT_KERNELS_ONLY

@@ -14,7 +14,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import VCF_DCT_NO_SUBBANDS, VCF_DCT_PERCEPTUAL, call
+from ._lib import VCF_DCT_NO_SUBBANDS, VCF_DCT_PERCEPTUAL, call, call_ab
 from .device import DeviceBuffer, _h
 
 __all__ = ["padded_shape", "flags_from", "encode_device", "decode_device", "encode", "decode",
@@ -44,8 +44,9 @@ def encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32,
                   variant: int = 0) -> DeviceBuffer:
     """Frames resident in HBM -> coefficient frames in HBM (asynchronous on `stream`).
 
-    variant: 0 automatic, 1 LDS-staged tile kernel, 3 column-per-lane kernel, 5 packed-fp32
-    tile kernel (see vcf_amd.h for all), -1 the generic-B kernels (any supported B, 8 included)."""
+    variant: 0 the product kernels, -1 the generic-B kernels (any supported B, 8 included), any
+    other value a kernel variant of the A/B library (include/vcf_amd_ab.h: A/B records and
+    cross-checks, not the product path)."""
     Hp, Wp = padded_shape(H, W, block_size)
     if rgb.nbytes < n_frames * H * W * 3:
         raise ValueError("input buffer too small")
@@ -55,17 +56,19 @@ def encode_device(rgb: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32,
         raise ValueError("output buffer too small")
     if variant == -1:
         call("vcf_dct_dz_encode_any", rgb.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
+    elif variant == 0:
+        call("vcf_dct_dz_encode", rgb.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
     else:
-        call("vcf_dct_dz_encode_variant", variant, rgb.ptr, n_frames, H, W, block_size, int(Q), flags,
-             out.ptr, _h(stream))
+        call_ab("vcf_dct_dz_encode_variant", variant, rgb.ptr, n_frames, H, W, block_size, int(Q), flags,
+                out.ptr, _h(stream))
     return out
 
 
 def decode_device(k: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32, flags: int = 0,
                   out: DeviceBuffer | None = None, stream=None, block_size: int = 8,
                   variant: int = 0) -> DeviceBuffer:
-    """variant: 0 automatic, 1 lane-per-block, 2 column-per-lane (see vcf_amd.h), -1 the generic-B
-    kernels (any supported B, 8 included)."""
+    """variant: 0 the product kernels, -1 the generic-B kernels (any supported B, 8 included),
+    any other value a decode variant of the A/B library (include/vcf_amd_ab.h)."""
     Hp, Wp = padded_shape(H, W, block_size)
     if k.nbytes < n_frames * Hp * Wp * 3:
         raise ValueError("input buffer too small")
@@ -75,9 +78,11 @@ def decode_device(k: DeviceBuffer, n_frames: int, H: int, W: int, Q: int = 32, f
         raise ValueError("output buffer too small")
     if variant == -1:
         call("vcf_dct_dz_decode_any", k.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
+    elif variant == 0:
+        call("vcf_dct_dz_decode", k.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr, _h(stream))
     else:
-        call("vcf_dct_dz_decode_variant", variant, k.ptr, n_frames, H, W, block_size, int(Q), flags, out.ptr,
-             _h(stream))
+        call_ab("vcf_dct_dz_decode_variant", variant, k.ptr, n_frames, H, W, block_size, int(Q), flags,
+                out.ptr, _h(stream))
     return out
 
 

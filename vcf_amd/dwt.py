@@ -64,16 +64,20 @@ def _frames(a, what):
 
 def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32, variant: int = 0):
     """HxWx3 u8 (or N of them) -> list of {subband name: indices} per frame.
-    variant: 0 automatic, 1 fused level kernels, 2 separable kernels, 3-5 fused A/B forms,
-    6 strip kernels on every level, 7 strips with sums started at 0.0, 8 diagnostic,
-    9 strips for the middle levels (what 0 picks for filters up to 10 taps); see vcf_amd.h."""
+    variant: 0 the product kernels; any other value a variant of the A/B library
+    (include/vcf_amd_ab.h: 1 fused level kernels, 2 separable kernels, 6 strip kernels on every
+    level, ...; A/B records and cross-checks, not the product path)."""
     f = _frames(rgb, "rgb")
     n, H, W, _ = f.shape
     _, pb, wb = layout(H, W, levels)
     din, dout, dws = DeviceBuffer.from_array(f), DeviceBuffer(n * pb), DeviceBuffer(n * wb)
     try:
-        L.call("vcf_dwt_dz_encode_variant", int(variant), din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q),
-               dout.ptr, dws.ptr, None)
+        if variant == 0:
+            L.call("vcf_dwt_dz_encode", din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q), dout.ptr,
+                   dws.ptr, None)
+        else:
+            L.call_ab("vcf_dwt_dz_encode_variant", int(variant), din.ptr, n, H, W, wavelet_index(wavelet), levels,
+                      int(Q), dout.ptr, dws.ptr, None)
         packed = dout.download(np.empty((n, pb), np.uint8))
     finally:
         din.free()
@@ -93,8 +97,12 @@ def decode(subbands, H: int, W: int, wavelet: str = "db5", levels: int = 5, Q: i
     Ho, Wo = 2 * shapes[0][0], 2 * shapes[0][1]
     din, dout, dws = DeviceBuffer.from_array(packed), DeviceBuffer(n * Ho * Wo * 3), DeviceBuffer(n * wb)
     try:
-        L.call("vcf_dwt_dz_decode_variant", int(variant), din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q),
-               dout.ptr, dws.ptr, None)
+        if variant == 0:
+            L.call("vcf_dwt_dz_decode", din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q), dout.ptr,
+                   dws.ptr, None)
+        else:
+            L.call_ab("vcf_dwt_dz_decode_variant", int(variant), din.ptr, n, H, W, wavelet_index(wavelet), levels,
+                      int(Q), dout.ptr, dws.ptr, None)
         out = dout.download(np.empty((n, Ho, Wo, 3), np.uint8))
     finally:
         din.free()
