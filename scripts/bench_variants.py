@@ -1,5 +1,8 @@
 """A/B the encode (or, with DECODE=1, the decode) kernel variants in one process
-(interleaved ABBA rounds, §5.4 rule 24)."""
+(interleaved ABBA rounds, §5.4 rule 24).  Variant 0 is the product library's
+kernel, the others the A/B library's (include/vcf_amd_ab.h).  DENSE=1: uniform
+random frames instead of S-smooth (every coefficient nonzero: the decode's
+worst case)."""
 import os
 import sys
 
@@ -15,7 +18,10 @@ H, W, F, Q = 2160, 3840, 64, 32
 DECODE = os.environ.get("DECODE", "0") == "1"
 variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["1", "2"])]
 Hp, Wp = D.padded_shape(H, W)
-frames = [bench.synth_frame(H, W, s) for s in range(4)]
+if os.environ.get("DENSE", "0") == "1":
+    frames = [np.random.Generator(np.random.PCG64(s)).integers(0, 256, (H, W, 3), dtype=np.uint8) for s in range(4)]
+else:
+    frames = [bench.synth_frame(H, W, s) for s in range(4)]
 din = DeviceBuffer(F * H * W * 3)
 for f in range(F):
     din.upload(frames[f % 4], offset=f * H * W * 3)

@@ -153,3 +153,22 @@ extern "C" void hb_encode_block_fold(const uint8_t *rgb, int Q, unsigned flags, 
     if (pow2) perc ? run(T{}, T{}) : run(T{}, F{});
     else perc ? run(F{}, T{}) : run(F{}, F{});
 }
+
+// the DCT-III with known-zero trailing inputs (decode zero skipping) and the
+// full one, for tests/test_block_math.py
+extern "C" void hb_dct3(int K, const double *in, double *out)
+{
+    double c[8];
+    for (int i = 0; i < 8; ++i) c[i] = in[i];
+    switch (K) {
+    case 1: vcf::dct3_8r_k<1>(c); break;
+    case 2: vcf::dct3_8r_k<2>(c); break;
+    case 3: vcf::dct3_8r_k<3>(c); break;
+    case 4: vcf::dct3_8r_k<4>(c); break;
+    case 5: vcf::dct3_8r_k<5>(c); break;
+    case 6: vcf::dct3_8r_k<6>(c); break;
+    case 7: vcf::dct3_8r_k<7>(c); break;
+    default: vcf::dct3_8r(c); break;
+    }
+    for (int i = 0; i < 8; ++i) out[i] = c[i];
+}

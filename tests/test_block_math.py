@@ -63,3 +63,25 @@ def test_block_encode_decode_vs_oracle(harness, Q, flags):
         out = np.empty((8, 8, 3), np.uint8)
         harness.hb_decode_block(_p(kin), Q, flags, _p(out))
         assert np.array_equal(out, O.decode_frame(kin, 8, 8, Q, flags)), (it, Q, flags)
+
+
+def test_dct3_zero_skipping(harness):
+    """dct3_8r_k<K> (inputs K..7 known zero) equals dct3_8r on such inputs: every
+    nonzero output bit for bit, zeros equal up to their sign (the decode
+    truncates to int16, where -0 and +0 are both 0)."""
+    pd = ctypes.POINTER(ctypes.c_double)
+    harness.hb_dct3.argtypes = [ctypes.c_int, pd, pd]
+    rng = np.random.Generator(np.random.PCG64(3))
+    for it in range(4000):
+        K = int(rng.integers(1, 9))
+        x = np.zeros(8)
+        x[:K] = rng.integers(-2048, 2048, K) * rng.choice([1.0, 0.0625, 0.5])
+        x[:K] *= rng.integers(0, 2, K)          # zeros inside the nonzero range too
+        if it % 7 == 0:
+            x[:K] = np.ldexp(rng.random(K) - 0.5, 20)   # the row pass takes non-integer inputs
+        want, got = np.empty(8), np.empty(8)
+        harness.hb_dct3(8, x.ctypes.data_as(pd), want.ctypes.data_as(pd))
+        harness.hb_dct3(K, x.ctypes.data_as(pd), got.ctypes.data_as(pd))
+        nz = (want != 0) | (got != 0)
+        assert np.array_equal(want[nz].view(np.uint64), got[nz].view(np.uint64)), (K, x, want, got)
+        assert np.array_equal(np.trunc(want), np.trunc(got))

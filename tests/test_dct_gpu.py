@@ -185,3 +185,35 @@ def test_store_policy_ab_variant_equal():
     for v in (0, 5, 7, 11, 12, 13, 14, 15, 16, 17):
         assert np.array_equal(D.encode(frames, 32, 0, variant=v), want), v
     assert np.array_equal(want[1], O.encode_frame(frames[1], 32, 0))
+
+
+@pytest.mark.parametrize("H,W", [(72, 4104), (64, 72), (61, 77)])
+@pytest.mark.parametrize("flags", [0, 1, 2])
+def test_decode_zero_skipping(H, W, flags):
+    """Index frames whose blocks carry nonzero coefficients only in their first
+    Ki rows and Kj columns (random per block, and per 8-block group so whole
+    waves share an extent) decode to the same bytes with the zero-skipping
+    product kernel, the dense kernel of the A/B library (variant 2) and the
+    oracle."""
+    rng = np.random.Generator(np.random.PCG64(H * W + flags))
+    Hp, Wp = D.padded_shape(H, W)
+    nby, nbx = Hp // 8, Wp // 8
+    for F in (2,):
+        blk = np.full((F, nby, nbx, 8, 8, 3), 128, np.uint8)
+        for f in range(F):
+            for by in range(nby):
+                for g in range(0, nbx, 8):
+                    grp = rng.random() < 0.5        # one extent for the whole group of 8 blocks
+                    Ki, Kj = rng.integers(1, 9, 2)
+                    for bx in range(g, min(g + 8, nbx)):
+                        if not grp:
+                            Ki, Kj = rng.integers(1, 9, 2)
+                        blk[f, by, bx, :Ki, :Kj] = rng.integers(100, 157, (Ki, Kj, 3))
+        if flags & 1:   # -x: blocks in place
+            k = blk.transpose(0, 1, 3, 2, 4, 5).reshape(F, Hp, Wp, 3)
+        else:           # subbands: coefficient (i, j) of block (by, bx) at (i nby + by, j nbx + bx)
+            k = blk.transpose(0, 3, 1, 4, 2, 5).reshape(F, Hp, Wp, 3)
+        k = np.ascontiguousarray(k)
+        got = D.decode(k, H, W, 32, flags)
+        assert np.array_equal(got, D.decode(k, H, W, 32, flags, variant=2))
+        assert np.array_equal(got[1], O.decode_frame(k[1], H, W, 32, flags))

@@ -113,6 +113,56 @@ VCF_HD void dct3_8r(double (&c)[8])
     c[7] = o7;
 }
 
+// dct3_8r with inputs K..7 known to be exactly zero (K = 1..8; K = 8 is
+// dct3_8r).  Every operation with a nonzero result is dct3_8r's, on the same
+// operands in the same order; an operation with a known-zero operand is
+// skipped (x + 0 = x, x - 0 = x, 0 - x = -x and 0 * c = 0 exactly).  Only the
+// sign of a zero can differ from pocketfft's (-0 for +0): a signed zero never
+// changes a nonzero sum or product, and the decode truncates to int16, where
+// both are 0 -- so the decoded bytes are identical (tests/test_dct_gpu.py).
+// The zero flags are compile-time constants after inlining: the skipped
+// branches vanish (the IDCT of a DC-only block is 2 multiplies per pass).
+struct XZ {
+    double v;
+    bool z;   // known to be exactly zero
+};
+VCF_HD XZ xz_add(XZ a, XZ b) { return b.z ? a : a.z ? b : XZ{a.v + b.v, false}; }
+VCF_HD XZ xz_sub(XZ a, XZ b) { return b.z ? a : a.z ? XZ{-b.v, false} : XZ{a.v - b.v, false}; }
+VCF_HD XZ xz_mul(double k, XZ a) { return a.z ? XZ{0.0, true} : XZ{k * a.v, false}; }
+
+template <int K>
+VCF_HD void dct3_8r_k(double (&c)[8])
+{
+    XZ x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = XZ{i < K ? c[i] : 0.0, i >= K};
+    const XZ c0 = xz_mul(VCF_SQRT2D, x[0]);   // c[0] * sqrt2 (commutes)
+    XZ t1, t2;
+    t1 = xz_add(x[1], x[7]); t2 = xz_sub(x[1], x[7]);
+    const XZ u1 = xz_add(xz_mul(VCF_TWD0, t2), xz_mul(VCF_TWD6, t1));
+    const XZ u7 = xz_sub(xz_mul(VCF_TWD0, t1), xz_mul(VCF_TWD6, t2));
+    t1 = xz_add(x[2], x[6]); t2 = xz_sub(x[2], x[6]);
+    const XZ u2 = xz_add(xz_mul(VCF_TWD1, t2), xz_mul(VCF_TWD5, t1));
+    const XZ u6 = xz_sub(xz_mul(VCF_TWD1, t1), xz_mul(VCF_TWD5, t2));
+    t1 = xz_add(x[3], x[5]); t2 = xz_sub(x[3], x[5]);
+    const XZ u3 = xz_add(xz_mul(VCF_TWD2, t2), xz_mul(VCF_TWD4, t1));
+    const XZ u5 = xz_sub(xz_mul(VCF_TWD2, t1), xz_mul(VCF_TWD4, t2));
+    const XZ c4 = xz_mul(VCF_2TW3D, x[4]);
+    const XZ tr1 = xz_add(u6, u2), h2 = xz_sub(u6, u2), tr2 = xz_add(c0, c4), h1 = xz_sub(c0, c4);
+    const XZ h0 = xz_add(tr2, tr1), h3 = xz_sub(tr2, tr1);
+    const XZ sr1 = xz_add(u7, u3), h6 = xz_sub(u7, u3), sr2 = xz_add(u1, u5), h5 = xz_sub(u1, u5);
+    const XZ h4 = xz_add(sr2, sr1), h7 = xz_sub(sr2, sr1);
+    const XZ o0 = xz_add(h0, h4), o7 = xz_sub(h0, h4);
+    const XZ tr = xz_add(xz_mul(VCF_WRD, h5), xz_mul(VCF_WID, h6));
+    const XZ ti = xz_sub(xz_mul(VCF_WRD, h6), xz_mul(VCF_WID, h5));
+    const XZ o1 = xz_add(h1, tr), o5 = xz_sub(h1, tr);
+    const XZ o2 = xz_add(ti, h2), o6 = xz_sub(ti, h2);
+    const XZ r[8] = {o0, xz_sub(o1, o2), xz_add(o2, o1), xz_add(h3, h7),
+                     xz_sub(h3, h7), xz_sub(o5, o6), xz_add(o6, o5), o7};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = r[i].z ? 0.0 : r[i].v;
+}
+
 // log2(1/s[k]) for the DCT-II reduced outputs.
 VCF_HD constexpr int dct2_inv_scale_log2(int k) { return (k & 3) == 0 ? 1 : 2; }
 

@@ -419,10 +419,16 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
     for (int C = 0; C < 3; ++C) {
         // :399-411 astype(int16) - 128, Q*k in int16 (A5); -p de-weighting (:421-435)
         double col[8];
+        // AC index bytes of the column: all 128 (coefficient 0) iff their OR
+        // and their AND are both 128 (the lane x = 0 skips its DC byte)
+        uint32_t acor = 0, acand = 0xFFu;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int kb = SUB ? sm.stage[cols_stage_off<TB, SUB>(i * 8 + x) + lb * 3 + C]
                                : sm.stage[cols_stage_off<TB, SUB>(i) + lb * 24 + x * 3 + C];
+            const uint32_t ac = (i == 0 && x == 0) ? 128u : (uint32_t)kb;
+            acor |= ac;
+            acand &= ac;
             if constexpr (DQ == 1 && !PERC) {
                 col[i] = sm.lut[kb];
                 continue;
@@ -433,6 +439,32 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
                 yv = (int16_t)(int)f;
             }
             col[i] = (double)yv;
+        }
+        // A wave whose 8 blocks are DC-only in this channel (quantized smooth
+        // content: most blocks) decodes every pixel of a block to one value:
+        // dct3_8r_k<1> per pass, the operations of dct3_8r whose results are
+        // not known zeros (vcf_dct8.h; bit-identical int16 outputs).  The
+        // branch is wave-uniform.  (64 x 4K S-smooth frames: 1.01 -> 0.756 ms;
+        // uniform-random frames, no DC-only wave: 1.187 -> 1.262 ms, the AC
+        // test; profiles/r03_dct_decode_dc_ab.log)
+        if (__ballot(acor != 128u || acand != 128u) == 0) {
+            const int kb = sm.stage[cols_stage_off<TB, SUB>(0) + lb * (SUB ? 3 : 24) + C];
+            double v;
+            if constexpr (DQ == 1 && !PERC) {
+                v = sm.lut[kb];
+            } else {
+                int16_t yv = (int16_t)__mul24(Q, kb - 128);
+                if (PERC) yv = (int16_t)(int)(float)((double)(float)yv / pweight_rt(C, 0));
+                v = (double)yv;
+            }
+            double r[8] = {v, 0, 0, 0, 0, 0, 0, 0};
+            dct3_8r_k<1>(r);   // column pass: every output sqrt2 * v
+            double q[8] = {r[0], 0, 0, 0, 0, 0, 0, 0};
+            dct3_8r_k<1>(q);   // row pass: every output sqrt2 * (sqrt2 * v)
+            const int o = (int16_t)(int)(DQ == 1 && !PERC ? q[0] : q[0] * 0.0625);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) out[C][j] = o;
+            continue;
         }
         // :440 synthesize_image (A2): axis 0 (this lane's column), then axis 1
         dct3_8r(col);
