@@ -53,6 +53,9 @@ def lib():
         L.vcfo_pocketfft_consts.argtypes = [fp, dp, fp, dp, fp, dp]
         # any block size (vcf_dct_general_oracle.cpp)
         L.vcfo_dct_supported.argtypes = [ctypes.c_int]
+        L.vcfo_dct_uses_bluestein.argtypes = [ctypes.c_int]
+        L.vcfo_cfft_f32.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.vcfo_cfft_f64.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         for n in ("vcfo_dct2_f32_n", "vcfo_dct3_f32_n"):
             getattr(L, n).argtypes = [fp, ctypes.c_int, ctypes.c_int]
         for n in ("vcfo_dct2_f64_n", "vcfo_dct3_f64_n"):
@@ -134,6 +137,23 @@ def decode_frame(k: np.ndarray, H: int, W: int, Q: int = 32, flags: int = 0) -> 
 
 def dct_supported(N: int) -> bool:
     return bool(lib().vcfo_dct_supported(int(N)))
+
+
+def dct_uses_bluestein(N: int) -> bool:
+    """pocketfft_r plans length N with Bluestein (fftblue over a cfftp of good_size_cmplx(2N-1))."""
+    return bool(lib().vcfo_dct_uses_bluestein(int(N)))
+
+
+def cfft(x, forward: bool = True):
+    """pocketfft cfftp (scipy.fft.fft; backward unnormalised) along the last axis, complex64/128."""
+    a = np.ascontiguousarray(x)
+    assert a.dtype in (np.complex64, np.complex128)
+    N = a.shape[-1]
+    b = a.reshape(-1, N).copy()
+    f = lib().vcfo_cfft_f32 if a.dtype == np.complex64 else lib().vcfo_cfft_f64
+    if f(b.ctypes.data, N, b.shape[0], 1 if forward else 0) != 0:
+        raise ValueError(f"length {N}: cfftp needs the generic passg (not restated)")
+    return b.reshape(a.shape)
 
 
 def dct_n(x, kind: int = 2, dtype=np.float32):

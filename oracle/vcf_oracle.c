@@ -69,7 +69,7 @@ static void sc_calc(size_t x, size_t n, double ang, double *re, double *im)
         if (x < n) { *re = cos((double)x * ang); *im = -sin((double)x * ang); return; }
         *re = sin((double)(2 * n - x) * ang); *im = -cos((double)(2 * n - x) * ang); return;
     }
-    x -= 4 * n;
+    x -= 2 * n;   /* the third quadrant: x in [2n, 4n] */
     if (x < n) { *re = -sin((double)x * ang); *im = -cos((double)x * ang); return; }
     *re = -cos((double)(2 * n - x) * ang); *im = -sin((double)(2 * n - x) * ang);
 }

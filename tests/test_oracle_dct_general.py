@@ -11,7 +11,9 @@ the reference:
     reconstructions bit-exact;
   * lengths with a prime factor above 5 (pocketfft radfg/radbg) 1..200 vs
     scipy, and the reference's glue at -B 7, 11, 13, 14, 21, 49, 98, 130, 200
-    (make_golden_radg.py); the Bluestein lengths pocketfft_r picks;
+    (make_golden_radg.py); the Bluestein lengths pocketfft_r picks (fftblue
+    over cfftp: scipy.fft c2c, scipy.fftpack dct/idct at all 67 lengths <= 600,
+    the glue at -B 191 and 478, make_golden_blue.py);
   * the -L search (optimize_block_size, 2D-DCT.py:533-579): the codec's host
     logic (vcf_amd/codec/dct2d.py) with the oracle standing in for the GPU
     transforms reproduces the reference's J for every candidate block size
@@ -62,12 +64,59 @@ def test_oracle_dct_radfg_radbg_lengths_vs_scipy(N):
 
 
 def test_oracle_dct_bluestein_lengths():
-    """pocketfft_r plans these lengths with Bluestein (not restated); every
-    other length 1..600 is an rfftp plan the restatement covers."""
+    """pocketfft_r plans exactly these lengths 1..600 with Bluestein; the
+    restatement covers them (fftblue over cfftp) and every rfftp length."""
     blue = set(RADG["bluestein_lengths"])
     assert blue and min(blue) == 191
+    assert blue == set(BLUE["bluestein_lengths"])
     for N in range(1, 601):
-        assert O.dct_supported(N) == (N not in blue), N
+        assert O.dct_supported(N), N
+        assert O.dct_uses_bluestein(N) == (N in blue), N
+
+
+BLUE = json.load(open(os.path.join(GOLDEN, "manifest_blue.json")))
+PASSG = {13, 169}   # cfftp lengths with a prime factor above 11 (generic passg, not restated)
+
+
+def test_oracle_cfft_vs_scipy():
+    """cfftp (the complex FFT Bluestein runs on) against scipy.fft.fft/ifft
+    under the reference's python (make_golden_blue.py), bit for bit: every
+    padded length the Bluestein plans of N <= 600 use, plus small lengths that
+    exercise each pass; ifft with norm='forward' is the unnormalised backward
+    pass."""
+    g = np.load(os.path.join(GOLDEN, "cfft_blue.npz"))
+    for N in BLUE["cfft_lengths"]:
+        for nm in ("c64", "c128"):
+            x = g[f"x_{nm}_{N}"]
+            if N in PASSG:
+                with pytest.raises(ValueError):
+                    O.cfft(x)
+                continue
+            assert np.array_equal(O.cfft(x, True), g[f"fwd_{nm}_{N}"]), (N, nm)
+            assert np.array_equal(O.cfft(x, False), g[f"bwd_{nm}_{N}"]), (N, nm)
+
+
+@pytest.mark.parametrize("N", BLUE["bluestein_lengths"])
+def test_oracle_dct_bluestein_blocks_vs_scipy(N):
+    """DCT-II/III of the Bluestein lengths (fftblue::exec_r inside T_dcst23)
+    against scipy.fftpack under the reference's python, bit for bit."""
+    g = np.load(os.path.join(GOLDEN, "blocks_blue.npz"))
+    fwd = O.dct_n(g[f"fwd_in_{N}"], 2, np.float32)
+    assert np.array_equal(fwd.view(np.uint32), g[f"fwd_out_{N}"].view(np.uint32))
+    inv = O.dct_n(g[f"inv_in_{N}"].astype(np.float64), 3, np.float64)
+    assert np.array_equal(inv.view(np.uint64), g[f"inv_out_{N}"].view(np.uint64))
+
+
+@pytest.mark.parametrize("case", BLUE["cases"], ids=lambda c: c["name"])
+def test_oracle_bluestein_block_sizes_vs_reference(case):
+    """src/2D-DCT.py encode_fn/decode_fn at -B 191 and -B 478 (2 x 239)."""
+    d = np.load(os.path.join(GOLDEN, f"dct_{case['name']}.npz"))
+    B, Q, flags = _qf(case["flags"])
+    H, W = d["rgb"].shape[:2]
+    k = O.encode_frame_b(d["rgb"], B, Q, flags)
+    assert k.shape == tuple(case["k_shape"])
+    assert np.array_equal(k, d["k"])
+    assert np.array_equal(O.decode_frame_b(d["k"], H, W, B, Q, flags), d["decoded"])
 
 
 @pytest.mark.parametrize("case", RADG["cases"], ids=lambda c: c["name"])

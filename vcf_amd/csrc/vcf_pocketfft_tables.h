@@ -59,7 +59,7 @@ void sc_calc(size_t x, size_t n, double ang, double &re, double &im)
         if (x < n) { re = std::cos(double(x) * ang); im = -std::sin(double(x) * ang); return; }
         re = std::sin(double(2 * n - x) * ang); im = -std::cos(double(2 * n - x) * ang); return;
     }
-    x -= 4 * n;
+    x -= 2 * n;   /* the third quadrant: x in [2n, 4n] */
     if (x < n) { re = -std::sin(double(x) * ang); im = -std::cos(double(x) * ang); return; }
     re = -std::cos(double(2 * n - x) * ang); im = -std::sin(double(2 * n - x) * ang);
 }
