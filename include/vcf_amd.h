@@ -117,11 +117,11 @@ int vcf_dct_dz_decode(const uint8_t *k_dev, int64_t n_frames, int32_t H, int32_t
                       int32_t block_size, int32_t Q, uint32_t flags, uint8_t *rgb_dev,
                       void *stream);
 
-/* 1 if block_size has a HIP transform: every B <= 4096 that pocketfft plans
- * with rfftp -- compiled kernels for the 38 5-smooth B <= 128 (every -L
- * candidate 2, 4, ..., 128, 2D-DCT.py:536), run-time-length kernels with the
- * generic radfg/radbg passes for the rest.  0 for the lengths pocketfft_r
- * plans with Bluestein (191, 199, 211, ...; not restated) and B > 4096. */
+/* 1 if block_size has a HIP transform: every 1 <= B <= 4096 -- compiled
+ * kernels for the 38 5-smooth B <= 128 (every -L candidate 2, 4, ..., 128,
+ * 2D-DCT.py:536), run-time-length kernels for the rest: rfftp plans with the
+ * generic radfg/radbg passes, and the lengths pocketfft_r plans with
+ * Bluestein (191, 199, 211, ...: fftblue over cfftp).  0 for B > 4096. */
 int vcf_dct_block_size_supported(int32_t block_size);
 
 /* -p's quantization tables for block size B (host only): the JPEG luma /

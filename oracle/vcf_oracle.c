@@ -41,6 +41,7 @@
  * Restates pocketfft (BSD-3-Clause, Copyright (C) 2010-2019 Max-Planck-Society);
  * license text in THIRD_PARTY_NOTICES.md.
  */
+#define _GNU_SOURCE   /* sincos */
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -54,24 +55,29 @@
 /* ------------------------------------------------------------------------ */
 static void sc_calc(size_t x, size_t n, double ang, double *re, double *im)
 {
+    /* pocketfft takes cos and sin of the same angle; gcc -O2 (the build of
+     * scipy's pocketfft the fixtures pin) fuses each pair into one glibc
+     * sincos() call, which differs from separate sin/cos in the last bit for
+     * some angles, so call it explicitly */
+    double s, c;
     x <<= 3;
     if (x < 4 * n) {
         if (x < 2 * n) {
-            if (x < n) { *re = cos((double)x * ang); *im = sin((double)x * ang); return; }
-            *re = sin((double)(2 * n - x) * ang); *im = cos((double)(2 * n - x) * ang); return;
+            if (x < n) { sincos((double)x * ang, &s, &c); *re = c; *im = s; return; }
+            sincos((double)(2 * n - x) * ang, &s, &c); *re = s; *im = c; return;
         }
         x -= 2 * n;
-        if (x < n) { *re = -sin((double)x * ang); *im = cos((double)x * ang); return; }
-        *re = -cos((double)(2 * n - x) * ang); *im = sin((double)(2 * n - x) * ang); return;
+        if (x < n) { sincos((double)x * ang, &s, &c); *re = -s; *im = c; return; }
+        sincos((double)(2 * n - x) * ang, &s, &c); *re = -c; *im = s; return;
     }
     x = 8 * n - x;
     if (x < 2 * n) {
-        if (x < n) { *re = cos((double)x * ang); *im = -sin((double)x * ang); return; }
-        *re = sin((double)(2 * n - x) * ang); *im = -cos((double)(2 * n - x) * ang); return;
+        if (x < n) { sincos((double)x * ang, &s, &c); *re = c; *im = -s; return; }
+        sincos((double)(2 * n - x) * ang, &s, &c); *re = s; *im = -c; return;
     }
     x -= 2 * n;   /* the third quadrant: x in [2n, 4n] */
-    if (x < n) { *re = -sin((double)x * ang); *im = -cos((double)x * ang); return; }
-    *re = -cos((double)(2 * n - x) * ang); *im = -sin((double)(2 * n - x) * ang);
+    if (x < n) { sincos((double)x * ang, &s, &c); *re = -s; *im = -c; return; }
+    sincos((double)(2 * n - x) * ang, &s, &c); *re = -c; *im = -s;
 }
 
 /* value of sincos_2pibyn(n)[idx] in double (before the cast to T) */

@@ -67,9 +67,8 @@ def test_padded_shape_is_host_only():
 
 @pytest.mark.parametrize("args,status", [
     (dict(H=0), L.VCF_ERR_INVALID),              # not an image
-    (dict(block_size=191), L.VCF_ERR_UNSUPPORTED),  # pocketfft plans length 191 with Bluestein (not restated)
     (dict(block_size=5000), L.VCF_ERR_UNSUPPORTED),  # beyond the run-time path's 4096
-    (dict(block_size=191, flags=2), L.VCF_ERR_UNSUPPORTED),  # -p on a Bluestein length
+    (dict(block_size=5000, flags=2), L.VCF_ERR_UNSUPPORTED),
     (dict(Q=0), L.VCF_ERR_INVALID),
     (dict(flags=8), L.VCF_ERR_INVALID),
     (dict(n_frames=-1), L.VCF_ERR_INVALID),
@@ -108,16 +107,12 @@ def test_product_never_imports_the_oracle():
 
 
 def test_block_size_coverage():
-    """-B sizes with a HIP transform: every length pocketfft plans with rfftp
-    (compiled kernels for the 5-smooth B <= 128, the run-time path for the
-    rest up to 4096); the Bluestein lengths (tests/golden/manifest_radg.json,
-    checked against scipy by tests/test_oracle_dct_general.py) are not."""
-    import json
-    from conftest import GOLDEN
-    blue = set(json.load(open(os.path.join(GOLDEN, "manifest_radg.json")))["bluestein_lengths"])
+    """-B sizes with a HIP transform: every B up to 4096 -- compiled kernels
+    for the 5-smooth B <= 128, the run-time path for the rest, rfftp plans and
+    the lengths pocketfft plans with Bluestein (tests/golden/manifest_blue.json)."""
     lib = L.lib()
     have = [b for b in range(0, 601) if lib.vcf_dct_block_size_supported(b)]
-    assert have == [b for b in range(1, 601) if b not in blue]
+    assert have == list(range(1, 601))
     assert lib.vcf_dct_block_size_supported(4096) and not lib.vcf_dct_block_size_supported(4097)
 
 

@@ -130,7 +130,7 @@ def test_codec_block_size_files_match_reference(case, tmp_path):
 def test_unsupported_block_sizes_raise():
     from vcf_amd._lib import VCFUnsupported
     rgb = _smooth(20, 20, 0)
-    for B in (191, 199, 5000):   # Bluestein lengths (not restated), beyond 4096
+    for B in (4097, 5000):   # beyond the run-time path's 4096
         assert not D.block_size_supported(B)
         with pytest.raises(VCFUnsupported):
             D.encode(rgb, 32, 0, block_size=B)
@@ -182,10 +182,34 @@ def test_runtime_block_size_int32_and_batches(B):
                               O.decode_frame_b(ku[f], H, W, B, 7, 0))
 
 
-def test_bluestein_length_unsupported():
-    rgb = np.zeros((191, 191, 3), np.uint8)
-    with pytest.raises(NotImplementedError):
-        D.encode(rgb, 32, 0, block_size=191)
+# ---- Bluestein block sizes (vcf_pocketfft_blue.h): fftblue over cfftp ----
+
+BLUE = json.load(open(os.path.join(GOLDEN, "manifest_blue.json")))
+
+
+@pytest.mark.parametrize("case", BLUE["cases"], ids=lambda c: c["name"])
+def test_bluestein_block_size_matches_reference_golden(case):
+    """The reference's own encode_fn/decode_fn at -B 191 and -B 478 (2 x 239),
+    lengths pocketfft plans with Bluestein (make_golden_blue.py), bit for bit."""
+    d = np.load(os.path.join(GOLDEN, f"dct_{case['name']}.npz"))
+    B, Q, flags = _qf(case["flags"])
+    H, W = d["rgb"].shape[:2]
+    k = D.encode(d["rgb"], Q, flags, block_size=B)
+    assert np.array_equal(k, d["k"])
+    assert np.array_equal(D.decode(d["k"], H, W, Q, flags, block_size=B), d["decoded"])
+
+
+@pytest.mark.parametrize("B", [199, 223, 271, 389, 431, 509, 613])
+@pytest.mark.parametrize("Q,flags", [(32, 0), (5, 3)])
+def test_bluestein_block_size_vs_oracle(B, Q, flags):
+    """Odd and even Bluestein lengths whose padded cfftp lengths use every
+    pass (2, 3, 4, 5, 7, 8, 11), with -x and -p: kernels vs the oracle."""
+    H, W = B + 2, B - 3
+    rng = np.random.default_rng(B + Q)
+    rgb = _smooth(H, W, B) if Q == 32 else rng.integers(0, 256, (H, W, 3), np.uint8)
+    k = D.encode(rgb, Q, flags, block_size=B)
+    assert np.array_equal(k, O.encode_frame_b(rgb, B, Q, flags))
+    assert np.array_equal(D.decode(k, H, W, Q, flags, block_size=B), O.decode_frame_b(k, H, W, B, Q, flags))
 
 
 @pytest.mark.parametrize("B", [1, 2, 3, 4, 7, 12, 16, 64, 130])

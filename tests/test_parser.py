@@ -43,7 +43,7 @@ def test_unsupported_options_raise():
     file or device work."""
     from vcf_amd.codec.dct2d import CoDec
     p = P.dct_parser()
-    for argv in (["encode", "-B", "191"], ["encode", "-B", "5000"],
+    for argv in (["encode", "-B", "5000"],
                  ["encode", "-t", "color-DCT"], ["encode", "-a", "VQ"],
                  ["encode", "-c", "PNG"], ["decode", "-f", "gaussian_blur"]):
         with pytest.raises(NotImplementedError):

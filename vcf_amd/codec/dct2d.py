@@ -9,9 +9,9 @@ span between reading the image and handing the indices to the entropy codec
 libvcf_amd.so (vcf_dct_dz_encode / vcf_dct_dz_decode); there is no CPU
 implementation of it in the product.
 
--B takes every block size the HIP path has a transform for (every B <= 4096
-that pocketfft plans with rfftp, vcf_dct_block_size_supported; not the
-Bluestein lengths, the first of which is 191), -L runs optimize_block_size
+-B takes every block size the HIP path has a transform for (every B <= 4096,
+vcf_dct_block_size_supported: pocketfft's rfftp plans and its Bluestein
+lengths, the first of which is 191), -L runs optimize_block_size
 (2D-DCT.py:533-579) with the GPU doing each candidate's analysis/synthesis.
 -t YCrCb runs exactly as -t YCoCg: 2D-DCT.py binds from_RGB/to_RGB from
 color_transforms.YCoCg at import (:22-23) and -t only picks the base class
@@ -20,7 +20,7 @@ the offset to 0 (:106-109): the GPU hands the float32 coefficients to the
 Lloyd-Max quantizer (histogram, design, encoder on the GPU,
 codec/quantizers.py) and decodes from its int16 output.  Options the HIP
 path does not implement raise NotImplementedError when the codec is
-constructed (Bluestein block sizes, other colour transforms, quantizers
+constructed (block sizes above 4096, other colour transforms, quantizers
 other than deadzone and LloydMax, filters other than no_filter, -L with
 LloydMax); entropy codecs come from ENTROPY_CODECS.
 """
@@ -111,8 +111,7 @@ class CoDec(EICCoDec):
         if not self.encoding and filt != "no_filter":
             raise NotImplementedError(f"filter {filt!r}: only no_filter is on the HIP path")
         if not D.block_size_supported(self.block_size):
-            raise NotImplementedError(f"block size {self.block_size}: the HIP path covers every B <= 4096 "
-                                      "that pocketfft plans with rfftp (not its Bluestein lengths)")
+            raise NotImplementedError(f"block size {self.block_size}: the HIP path covers 1 <= B <= 4096")
         self.entropy = make_entropy(args)
         self.file_extension = self.entropy.file_extension
         self.QSS = int(getattr(args, "QSS", 32))

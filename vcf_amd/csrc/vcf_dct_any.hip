@@ -8,8 +8,8 @@
 // lengths pocketfft factors into 4, 2, 3 and 5 up to 128: 1, 2, 3, 4, 5, 6, 8,
 // 9, 10, 12, 15, 16, ..., 120, 125, 128) or of vcf_pocketfft_rt.h (any other
 // B <= 4096 that pocketfft plans with rfftp, prime factors above 5 through its
-// generic radfg/radbg passes).  The lengths pocketfft_r plans with Bluestein
-// (the first is 191) return VCF_ERR_UNSUPPORTED.
+// generic radfg/radbg passes, and the lengths pocketfft_r plans with
+// Bluestein -- the first is 191 -- through vcf_pocketfft_blue.h).
 //
 // Mapping.  A "unit" is one channel of one BxB block.  A workgroup holds
 // U = 256/B units (encode, fp32) or 128/B units (decode, fp64), B lanes per
@@ -321,8 +321,12 @@ __device__ __forceinline__ long long coef_offset_rt(const GeomB &g, int B, int b
     return (row * g.Wp + col) * 3;
 }
 
-// scratch per workgroup: the B x B tile, then the threads' two lines of B
-__host__ __device__ constexpr long long rt_ws_per_wg(int B) { return (long long)B * B + 2LL * B * kRtThreads; }
+// scratch per workgroup: the B x B tile, then the threads' lines (two of B,
+// plus Bluestein's complex arrays), interleaved thread-fastest
+__host__ __device__ inline long long rt_ws_per_wg(const pfft::RtPlan &P)
+{
+    return (long long)P.n * P.n + pfft::rt_line_reals(P) * kRtThreads;
+}
 
 template <int M>
 __global__ __launch_bounds__(256) void dct_rt_encode_kernel(const uint8_t *__restrict__ rgb, void *__restrict__ out,
@@ -331,10 +335,10 @@ __global__ __launch_bounds__(256) void dct_rt_encode_kernel(const uint8_t *__res
                                                            const double *__restrict__ pw)
 {
     const int B = P.n, tid = threadIdx.x;
-    float *tile = ws + (long long)blockIdx.x * rt_ws_per_wg(B);
+    float *tile = ws + (long long)blockIdx.x * rt_ws_per_wg(P);
     float *lines = tile + (long long)B * B;
     const pfft::Line<float> c{lines + tid, kRtThreads}, ch{lines + (long long)B * kRtThreads + tid, kRtThreads};
-    const pfft::RtFft<float> F{mem};
+    const pfft::RtFft<float> F{mem, lines + 2LL * B * kRtThreads + tid, kRtThreads};
     for (long long u = blockIdx.x; u < g.units; u += gridDim.x) {
         long long f = 0;
         int by = 0, bx = 0, cc = 0;
@@ -390,10 +394,10 @@ __global__ __launch_bounds__(256) void dct_rt_decode_kernel(const void *__restri
                                                            const double *__restrict__ pw)
 {
     const int B = P.n, tid = threadIdx.x;
-    double *tile = ws + (long long)blockIdx.x * rt_ws_per_wg(B);
+    double *tile = ws + (long long)blockIdx.x * rt_ws_per_wg(P);
     double *lines = tile + (long long)B * B;
     const pfft::Line<double> c{lines + tid, kRtThreads}, ch{lines + (long long)B * kRtThreads + tid, kRtThreads};
-    const pfft::RtFft<double> F{mem};
+    const pfft::RtFft<double> F{mem, lines + 2LL * B * kRtThreads + tid, kRtThreads};
     for (long long u = blockIdx.x; u < g.units; u += gridDim.x) {
         long long f = 0;
         int by = 0, bx = 0, cc = 0;
@@ -436,122 +440,8 @@ __global__ __launch_bounds__(256) void dct_rt_decode_kernel(const void *__restri
     }
 }
 
-// ---- host: run-time plans (pocketfft rfftp + T_dcst23 setup) -------------
-// pocketfft_r<T0>(length)'s plan choice: Bluestein only for lengths >= 50
-// whose largest prime factor p has p*p > length, when its cost guess wins
-// (util::largest_prime_factor, cost_guess, good_size_cmplx)
-size_t rt_largest_prime_factor(size_t n)
-{
-    size_t res = 1;
-    while ((n & 1) == 0) { res = 2; n >>= 1; }
-    for (size_t x = 3; x * x <= n; x += 2)
-        while (n % x == 0) { res = x; n /= x; }
-    if (n > 1) res = n;
-    return res;
-}
-double rt_cost_guess(size_t n)
-{
-    const double lfp = 1.1;   // penalty for non-hardcoded larger factors
-    const size_t ni = n;
-    double result = 0.;
-    while ((n & 1) == 0) { result += 2; n >>= 1; }
-    for (size_t x = 3; x * x <= n; x += 2)
-        while (n % x == 0) { result += (x <= 5) ? double(x) : lfp * double(x); n /= x; }
-    if (n > 1) result += (n <= 5) ? double(n) : lfp * double(n);
-    return result * double(ni);
-}
-size_t rt_good_size_cmplx(size_t n)
-{
-    if (n <= 12) return n;
-    size_t bestfac = 2 * n;
-    for (size_t f11 = 1; f11 < bestfac; f11 *= 11)
-        for (size_t f117 = f11; f117 < bestfac; f117 *= 7)
-            for (size_t f1175 = f117; f1175 < bestfac; f1175 *= 5) {
-                size_t x = f1175;
-                while (x < n) x *= 2;
-                for (;;) {
-                    if (x < n) x *= 3;
-                    else if (x > n) {
-                        if (x < bestfac) bestfac = x;
-                        if (x & 1) break;
-                        x >>= 1;
-                    } else return n;
-                }
-            }
-    return bestfac;
-}
-bool rt_uses_bluestein(size_t n)
-{
-    const size_t tmp = (n < 50) ? 0 : rt_largest_prime_factor(n);
-    if (tmp * tmp <= n) return false;
-    const double comp1 = 0.5 * rt_cost_guess(n);
-    const double comp2 = 2 * rt_cost_guess(rt_good_size_cmplx(2 * n - 1)) * 1.5;   // pocketfft's fudge factor
-    return comp2 < comp1;
-}
-
-// lengths the run-time path covers
-bool rt_covered(int B) { return B >= 1 && B <= kRtMaxB && !rt_uses_bluestein((size_t)B); }
-
-// rfftp factorize + comp_twiddle, T_dcst23's twiddle, pypocketfft's norm_fct
-template <typename T>
-void rt_fill(int n, pfft::RtPlan &P, std::vector<T> &mem)
-{
-    P.n = n;
-    P.nf = 0;
-    int l = n;
-    if (n > 1) {
-        while (l % 4 == 0) { P.fct[P.nf++] = 4; l >>= 2; }
-        if (l % 2 == 0) {
-            l >>= 1;
-            P.fct[P.nf++] = 2;
-            std::swap(P.fct[0], P.fct[P.nf - 1]);
-        }
-        for (int d = 3; d * d <= l; d += 2)
-            while (l % d == 0) { P.fct[P.nf++] = d; l /= d; }
-        if (l > 1) P.fct[P.nf++] = l;
-    }
-    mem.clear();
-    size_t l1 = 1;
-    for (int k = 0; k < P.nf; ++k) {
-        const size_t ip = (size_t)P.fct[k], ido = (size_t)n / (l1 * ip);
-        P.tw[k] = (int)mem.size();
-        if (k < P.nf - 1) {
-            const size_t off = mem.size();
-            mem.resize(off + (ip - 1) * (ido - 1));
-            for (size_t j = 1; j < ip; ++j)
-                for (size_t i = 1; i <= (ido - 1) / 2; ++i) {
-                    T re, im;
-                    sincos_2pibyn<T>((size_t)n, j * l1 * i, re, im);
-                    mem[off + (j - 1) * (ido - 1) + 2 * i - 2] = re;
-                    mem[off + (j - 1) * (ido - 1) + 2 * i - 1] = im;
-                }
-        }
-        P.tws[k] = (int)mem.size();
-        if (ip > 5) {
-            const size_t off = mem.size();
-            mem.resize(off + 2 * ip);
-            mem[off] = T(1);
-            mem[off + 1] = T(0);
-            for (size_t i = 2, ic = 2 * ip - 2; i <= ic; i += 2, ic -= 2) {
-                T re, im;
-                sincos_2pibyn<T>((size_t)n, i / 2 * ((size_t)n / ip), re, im);
-                mem[off + i] = re;
-                mem[off + i + 1] = im;
-                mem[off + ic] = re;
-                mem[off + ic + 1] = -im;
-            }
-        }
-        l1 *= ip;
-    }
-    P.dct_tw = (int)mem.size();
-    for (int i = 0; i < n; ++i) {
-        T re, im;
-        sincos_2pibyn<T>(4 * (size_t)n, (size_t)i + 1, re, im);
-        mem.push_back(re);
-    }
-    P.norm = (int)mem.size();
-    mem.push_back(T(1 / std::sqrt((long double)(2 * n))));
-}
+// lengths the run-time path covers (plans: pfft::rt_fill, vcf_pocketfft_rt.h)
+bool rt_covered(int B) { return B >= 1 && B <= kRtMaxB; }
 
 // cv2.resize of an 8x8 uint8 table to B x B, as src/2D-DCT.py:85-90 calls it
 // (INTER_AREA for B < 8, INTER_LINEAR otherwise), restating OpenCV's scalar
@@ -713,9 +603,9 @@ int rt_plan(int n, RtPlanDev &out)
     RtPlanDev d;
     std::vector<float> mf;
     std::vector<double> md;
-    rt_fill<float>(n, d.P, mf);
+    pfft::rt_fill<float>(n, d.P, mf);
     pfft::RtPlan P2;
-    rt_fill<double>(n, P2, md);   // same offsets
+    pfft::rt_fill<double>(n, P2, md);   // same offsets
     if ((rc = hip_check(hipMalloc(&d.f32, mf.size() * sizeof(float)), "hipMalloc(rt plan)")) != VCF_OK) return rc;
     if ((rc = hip_check(hipMalloc(&d.f64, md.size() * sizeof(double)), "hipMalloc(rt plan)")) != VCF_OK) return rc;
     if ((rc = hip_check(hipMemcpy(d.f32, mf.data(), mf.size() * sizeof(float), hipMemcpyHostToDevice),
@@ -738,9 +628,9 @@ Scratch &rt_scratch_for_current_device()
 }
 
 // workgroups of a run-time-path launch: enough to fill the chip, scratch <= ~1 GiB
-unsigned rt_grid(long long units, int B, size_t esz)
+unsigned rt_grid(long long units, const pfft::RtPlan &P, size_t esz)
 {
-    const long long per = rt_ws_per_wg(B) * (long long)esz;
+    const long long per = rt_ws_per_wg(P) * (long long)esz;
     long long wgs = std::min<long long>(units, 4096);
     wgs = std::min<long long>(wgs, std::max<long long>(1, (1LL << 30) / per));
     return (unsigned)std::max<long long>(wgs, 1);
@@ -752,10 +642,10 @@ int rt_launch_encode(const uint8_t *rgb, void *out, int mode, const GeomB &g, in
     RtPlanDev pl;
     int rc = rt_plan(B, pl);
     if (rc != VCF_OK) return rc;
-    const unsigned grid = rt_grid(g.units, B, sizeof(float));
+    const unsigned grid = rt_grid(g.units, pl.P, sizeof(float));
     Scratch &scr = rt_scratch_for_current_device();
     std::lock_guard<std::mutex> lock(scr.mu);
-    rc = scr.acquire((size_t)grid * rt_ws_per_wg(B) * sizeof(float), s);
+    rc = scr.acquire((size_t)grid * rt_ws_per_wg(pl.P) * sizeof(float), s);
     if (rc != VCF_OK) return rc;
     float *ws = (float *)scr.ptr;
     if (mode == kK32) hipLaunchKernelGGL((dct_rt_encode_kernel<kK32>), dim3(grid), dim3(kRtThreads), 0, s, rgb, out, g, Q, pl.P, pl.f32, ws, pw);
@@ -772,10 +662,10 @@ int rt_launch_decode(const void *kin, void *wsout, int mode, const GeomB &g, int
     RtPlanDev pl;
     int rc = rt_plan(B, pl);
     if (rc != VCF_OK) return rc;
-    const unsigned grid = rt_grid(g.units, B, sizeof(double));
+    const unsigned grid = rt_grid(g.units, pl.P, sizeof(double));
     Scratch &scr = rt_scratch_for_current_device();
     std::lock_guard<std::mutex> lock(scr.mu);
-    rc = scr.acquire((size_t)grid * rt_ws_per_wg(B) * sizeof(double), s);
+    rc = scr.acquire((size_t)grid * rt_ws_per_wg(pl.P) * sizeof(double), s);
     if (rc != VCF_OK) return rc;
     double *ws = (double *)scr.ptr;
     if (mode == kK32) hipLaunchKernelGGL((dct_rt_decode_kernel<kK32>), dim3(grid), dim3(kRtThreads), 0, s, kin, wsout, g, Q, pl.P, pl.f64, ws, pw);
@@ -854,10 +744,7 @@ int check_any(const void *a, const void *b, int64_t n_frames, int H, int W, int 
         return set_error(VCF_ERR_INVALID, "Input image must be a 3D array (height, width, channels).");
     if (B < 1) return set_error(VCF_ERR_INVALID, "block size %d", B);
     if (slot_of(B) < 0 && !rt_covered(B))
-        return set_error(VCF_ERR_UNSUPPORTED,
-                         B > kRtMaxB ? "block size %d: the HIP path covers B <= 4096"
-                                     : "block size %d: pocketfft plans this length with Bluestein (not restated)",
-                         B);
+        return set_error(VCF_ERR_UNSUPPORTED, "block size %d: the HIP path covers B <= 4096", B);
     if (Q < 1 || (decode && mode == kU8 && Q > 32767))
         return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
     if ((flags & VCF_DCT_PERCEPTUAL) && k32)

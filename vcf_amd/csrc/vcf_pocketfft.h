@@ -61,8 +61,8 @@ constexpr Factors factorize(int len)
     return r;
 }
 
-template <typename T> __device__ __forceinline__ void PM(T &a, T &b, T c, T d) { a = c + d; b = c - d; }
-template <typename T> __device__ __forceinline__ void MULPM(T &a, T &b, T c, T d, T e, T f)
+template <typename T> __host__ __device__ __forceinline__ void PM(T &a, T &b, T c, T d) { a = c + d; b = c - d; }
+template <typename T> __host__ __device__ __forceinline__ void MULPM(T &a, T &b, T c, T d, T e, T f)
 {
     a = c * e + d * f;
     b = c * f - d * e;

@@ -1,8 +1,8 @@
 // vcf_pocketfft_rt.h -- run-time-length DCT-II / DCT-III in pocketfft's exact
 // operation order: the block transforms for the -B sizes vcf_pocketfft.h does
-// not compile in (any length pocketfft plans with rfftp, including its
-// generic radfg/radbg passes for prime factors above 5).  The lengths it
-// plans with Bluestein (pocketfft_r's cost model) are not covered.
+// not compile in: any length pocketfft plans with rfftp, including its
+// generic radfg/radbg passes for prime factors above 5, and the lengths
+// pocketfft_r's cost model plans with Bluestein (vcf_pocketfft_blue.h).
 //
 // Same restatement as vcf_pocketfft.h (rfftp factorisation, radf/radb passes,
 // copy_and_norm, T_dcst23's twiddle loops and ortho scalings), with the length
@@ -20,6 +20,16 @@
 #include <cstddef>
 
 #include "vcf_pocketfft.h"
+#include "vcf_pocketfft_blue.h"
+#include "vcf_sincos.h"
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+// host and device: the CPU harness (tests/cpu/rt_harness.hip) runs these
+// functions on the host against the oracle
+#define VCF_RT_HD __host__ __device__ __forceinline__
 
 namespace vcf {
 namespace pfft {
@@ -28,31 +38,51 @@ constexpr int kRtMaxFactors = 24;
 
 // the plan of one length: rfftp's factors and the offsets of their twiddles
 // (tw: (ip-1)(ido-1) values for all but the last factor; tws: radfg/radbg's 2 ip
-// values for factors above 5), T_dcst23's N twiddles, the norm factor
+// values for factors above 5), T_dcst23's N twiddles, the norm factor; or,
+// when blue is set, the Bluestein plan (nf = 0)
 struct RtPlan {
     int n, nf;
     int fct[kRtMaxFactors], tw[kRtMaxFactors], tws[kRtMaxFactors];
     int dct_tw, norm;
+    int blue;
+    BluePlan bl;
 };
+
+// per-thread scratch reals of a plan: the two lines c, ch of n, and for
+// Bluestein its n-element and two n2-element complex arrays
+__host__ __device__ inline long long rt_line_reals(const RtPlan &P)
+{
+    return 2LL * P.n + (P.blue ? 2LL * P.n + 4LL * P.bl.n2 : 0);
+}
 
 template <typename T>
 struct Line {
     T *p;
     int stride;
-    __device__ __forceinline__ T &operator[](size_t i) const { return p[i * (size_t)stride]; }
+    VCF_RT_HD T &operator[](size_t i) const { return p[i * (size_t)stride]; }
 };
 
 template <typename T>
-__device__ __forceinline__ bool same_line(const Line<T> &a, const Line<T> &b) { return a.p == b.p; }
+VCF_RT_HD bool same_line(const Line<T> &a, const Line<T> &b) { return a.p == b.p; }
 
 template <typename T>
 struct RtFft {
-    const T *mem;   // the plan's twiddle values
+    const T *mem;       // the plan's twiddle values
+    T *bw = nullptr;    // Bluestein scratch of this thread (rt_line_reals beyond c, ch)
+    int bstride = 1;
+
+    template <typename A>
+    VCF_RT_HD void blue(A c, const RtPlan &P, T fct, bool fwd) const
+    {
+        const size_t n = (size_t)P.n, n2 = (size_t)P.bl.n2, s = (size_t)bstride;
+        const CLine<T> tmp{bw, bstride}, akf{bw + 2 * n * s, bstride}, ch{bw + (2 * n + 2 * n2) * s, bstride};
+        blue_exec_r(mem, P.bl, c, tmp, akf, ch, fct, fwd);
+    }
 
     /* radfg: any odd factor ip > 5 (pocketfft rfftp::radfg); input in cc as
      * (ido, l1, ip), result back in cc as (ido, ip, l1), ch is scratch */
     template <typename A>
-    __device__ void radfg(size_t ido, size_t ip, size_t l1, A cc, A ch, const T *wa, const T *csarr) const
+    VCF_RT_HD void radfg(size_t ido, size_t ip, size_t l1, A cc, A ch, const T *wa, const T *csarr) const
     {
         const size_t cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
         auto CC = [&](size_t a, size_t b, size_t c) -> T & { return cc[a + ido * (b + cdim * c)]; };
@@ -149,7 +179,7 @@ struct RtFft {
     /* radbg: any odd factor ip > 5 (pocketfft rfftp::radbg); input in cc as
      * (ido, ip, l1), result in ch as (ido, l1, ip) */
     template <typename A>
-    __device__ void radbg(size_t ido, size_t ip, size_t l1, A cc, A ch, const T *wa, const T *csarr) const
+    VCF_RT_HD void radbg(size_t ido, size_t ip, size_t l1, A cc, A ch, const T *wa, const T *csarr) const
     {
         const size_t cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
         auto CC = [&](size_t a, size_t b, size_t c) -> T & { return cc[a + ido * (b + cdim * c)]; };
@@ -248,7 +278,7 @@ struct RtFft {
     }
 
     template <typename A>
-    __device__ void radf2(size_t ido, size_t l1, A cc, A ch, const T *wa) const
+    VCF_RT_HD void radf2(size_t ido, size_t l1, A cc, A ch, const T *wa) const
     {
         auto WA = [&](size_t x, size_t i) { return wa[i + x * (ido - 1)]; };
         auto CC = [&](size_t a, size_t b, size_t c) -> T & { return cc[a + ido * (b + l1 * c)]; };
@@ -271,7 +301,7 @@ struct RtFft {
     }
 
     template <typename A>
-    __device__ void radf3(size_t ido, size_t l1, A cc, A ch, const T *wa) const
+    VCF_RT_HD void radf3(size_t ido, size_t l1, A cc, A ch, const T *wa) const
     {
         const T taur = T(-0.5), taui = T(0.8660254037844386467637231707529362L);
         auto WA = [&](size_t x, size_t i) { return wa[i + x * (ido - 1)]; };
@@ -303,7 +333,7 @@ struct RtFft {
     }
 
     template <typename A>
-    __device__ void radf4(size_t ido, size_t l1, A cc, A ch, const T *wa) const
+    VCF_RT_HD void radf4(size_t ido, size_t l1, A cc, A ch, const T *wa) const
     {
         const T hsqt2 = T(0.707106781186547524400844362104849L);
         auto WA = [&](size_t x, size_t i) { return wa[i + x * (ido - 1)]; };
@@ -342,7 +372,7 @@ struct RtFft {
     }
 
     template <typename A>
-    __device__ void radf5(size_t ido, size_t l1, A cc, A ch, const T *wa) const
+    VCF_RT_HD void radf5(size_t ido, size_t l1, A cc, A ch, const T *wa) const
     {
         const T tr11 = T(0.3090169943749474241022934171828191L), ti11 = T(0.9510565162951535721164393333793821L),
                 tr12 = T(-0.8090169943749474241022934171828191L), ti12 = T(0.5877852522924731291687059546390728L);
@@ -385,14 +415,14 @@ struct RtFft {
             }
     }
 
-    __device__ static void rearrange(T &rx, T &ix, T &ry, T &iy)
+    VCF_RT_HD static void rearrange(T &rx, T &ix, T &ry, T &iy)
     {
         T t1 = rx + ry, t2 = ry - rx, t3 = ix + iy, t4 = ix - iy;
         rx = t1; ix = t3; ry = t4; iy = t2;
     }
 
     template <typename A>
-    __device__ void radb5(size_t ido, size_t l1, A cc, A ch, const T *wa) const
+    VCF_RT_HD void radb5(size_t ido, size_t l1, A cc, A ch, const T *wa) const
     {
         const T tr11 = T(0.3090169943749474241022934171828191L), ti11 = T(0.9510565162951535721164393333793821L),
                 tr12 = T(-0.8090169943749474241022934171828191L), ti12 = T(0.5877852522924731291687059546390728L);
@@ -442,7 +472,7 @@ struct RtFft {
     }
 
     template <typename A>
-    __device__ void radb2(size_t ido, size_t l1, A cc, A ch, const T *wa) const
+    VCF_RT_HD void radb2(size_t ido, size_t l1, A cc, A ch, const T *wa) const
     {
         auto WA = [&](size_t x, size_t i) { return wa[i + x * (ido - 1)]; };
         auto CC = [&](size_t a, size_t b, size_t c) -> T & { return cc[a + ido * (b + 2 * c)]; };
@@ -465,7 +495,7 @@ struct RtFft {
     }
 
     template <typename A>
-    __device__ void radb3(size_t ido, size_t l1, A cc, A ch, const T *wa) const
+    VCF_RT_HD void radb3(size_t ido, size_t l1, A cc, A ch, const T *wa) const
     {
         const T taur = T(-0.5), taui = T(0.8660254037844386467637231707529362L);
         auto WA = [&](size_t x, size_t i) { return wa[i + x * (ido - 1)]; };
@@ -498,7 +528,7 @@ struct RtFft {
     }
 
     template <typename A>
-    __device__ void radb4(size_t ido, size_t l1, A cc, A ch, const T *wa) const
+    VCF_RT_HD void radb4(size_t ido, size_t l1, A cc, A ch, const T *wa) const
     {
         const T sqrt2 = T(1.414213562373095048801688724209698L);
         auto WA = [&](size_t x, size_t i) { return wa[i + x * (ido - 1)]; };
@@ -543,7 +573,7 @@ struct RtFft {
 
 
     template <typename A>
-    __device__ void copy_and_norm(A c, A p1, size_t len, T fct) const
+    VCF_RT_HD void copy_and_norm(A c, A p1, size_t len, T fct) const
     {
         if (!same_line(p1, c)) {
             if (fct != T(1)) for (size_t i = 0; i < len; ++i) c[i] = fct * p1[i];
@@ -556,8 +586,9 @@ struct RtFft {
     // rfftp::forward: radf passes in reverse factor order (radfg leaves its
     // result in place, hence the extra swap)
     template <typename A>
-    __device__ void forward(A c, A ch, const RtPlan &P, T fct) const
+    VCF_RT_HD void forward(A c, A ch, const RtPlan &P, T fct) const
     {
+        if (P.blue) { blue(c, P, fct, true); return; }   // pocketfft_r::forward -> fftblue::exec_r
         if (P.n == 1) { c[0] *= fct; return; }
         A p1 = c, p2 = ch;
         size_t n = (size_t)P.n, nf = (size_t)P.nf, l1 = n;
@@ -580,8 +611,9 @@ struct RtFft {
 
     // rfftp::backward: radb passes in factor order
     template <typename A>
-    __device__ void backward(A c, A ch, const RtPlan &P, T fct) const
+    VCF_RT_HD void backward(A c, A ch, const RtPlan &P, T fct) const
     {
+        if (P.blue) { blue(c, P, fct, false); return; }
         if (P.n == 1) { c[0] *= fct; return; }
         A p1 = c, p2 = ch;
         size_t n = (size_t)P.n, nf = (size_t)P.nf, l1 = 1;
@@ -601,7 +633,7 @@ struct RtFft {
 
     // T_dcst23::exec(type 2, ortho, cosine): scipy.fftpack.dct(x, norm='ortho')
     template <typename A>
-    __device__ void dct2(A c, A ch, const RtPlan &P) const
+    VCF_RT_HD void dct2(A c, A ch, const RtPlan &P) const
     {
         const T sqrt2 = T(1.414213562373095048801688724209698L);
         const T *twiddle = mem + P.dct_tw;
@@ -622,7 +654,7 @@ struct RtFft {
 
     // T_dcst23::exec(type 3, ortho, cosine): scipy.fftpack.idct(x, norm='ortho')
     template <typename A>
-    __device__ void dct3(A c, A ch, const RtPlan &P) const
+    VCF_RT_HD void dct3(A c, A ch, const RtPlan &P) const
     {
         const T sqrt2 = T(1.414213562373095048801688724209698L);
         const T *twiddle = mem + P.dct_tw;
@@ -638,6 +670,124 @@ struct RtFft {
         for (size_t k = 1; k + 1 < N; k += 2) { T t = c[k]; c[k] = t - c[k + 1]; c[k + 1] = c[k + 1] + t; }
     }
 };
+
+// ---- host: run-time plans (pocketfft rfftp or fftblue + T_dcst23 setup) ---
+// pocketfft_r<T0>(length)'s plan choice: Bluestein only for lengths >= 50
+// whose largest prime factor p has p*p > length, when its cost guess wins
+// (util::largest_prime_factor, cost_guess, good_size_cmplx)
+inline size_t rt_largest_prime_factor(size_t n)
+{
+    size_t res = 1;
+    while ((n & 1) == 0) { res = 2; n >>= 1; }
+    for (size_t x = 3; x * x <= n; x += 2)
+        while (n % x == 0) { res = x; n /= x; }
+    if (n > 1) res = n;
+    return res;
+}
+inline double rt_cost_guess(size_t n)
+{
+    const double lfp = 1.1;   // penalty for non-hardcoded larger factors
+    const size_t ni = n;
+    double result = 0.;
+    while ((n & 1) == 0) { result += 2; n >>= 1; }
+    for (size_t x = 3; x * x <= n; x += 2)
+        while (n % x == 0) { result += (x <= 5) ? double(x) : lfp * double(x); n /= x; }
+    if (n > 1) result += (n <= 5) ? double(n) : lfp * double(n);
+    return result * double(ni);
+}
+inline size_t rt_good_size_cmplx(size_t n)
+{
+    if (n <= 12) return n;
+    size_t bestfac = 2 * n;
+    for (size_t f11 = 1; f11 < bestfac; f11 *= 11)
+        for (size_t f117 = f11; f117 < bestfac; f117 *= 7)
+            for (size_t f1175 = f117; f1175 < bestfac; f1175 *= 5) {
+                size_t x = f1175;
+                while (x < n) x *= 2;
+                for (;;) {
+                    if (x < n) x *= 3;
+                    else if (x > n) {
+                        if (x < bestfac) bestfac = x;
+                        if (x & 1) break;
+                        x >>= 1;
+                    } else return n;
+                }
+            }
+    return bestfac;
+}
+inline bool rt_uses_bluestein(size_t n)
+{
+    const size_t tmp = (n < 50) ? 0 : rt_largest_prime_factor(n);
+    if (tmp * tmp <= n) return false;
+    const double comp1 = 0.5 * rt_cost_guess(n);
+    const double comp2 = 2 * rt_cost_guess(rt_good_size_cmplx(2 * n - 1)) * 1.5;   // pocketfft's fudge factor
+    return comp2 < comp1;
+}
+
+// rfftp factorize + comp_twiddle (or the Bluestein plan), T_dcst23's
+// twiddle, pypocketfft's norm_fct
+template <typename T>
+inline void rt_fill(int n, RtPlan &P, std::vector<T> &mem)
+{
+    P.n = n;
+    P.nf = 0;
+    P.blue = rt_uses_bluestein((size_t)n) ? 1 : 0;
+    P.bl = BluePlan{};
+    mem.clear();
+    if (P.blue) blue_fill<T>(n, (int)rt_good_size_cmplx(2 * (size_t)n - 1), P.bl, mem);
+    int l = n;
+    if (n > 1 && !P.blue) {
+        while (l % 4 == 0) { P.fct[P.nf++] = 4; l >>= 2; }
+        if (l % 2 == 0) {
+            l >>= 1;
+            P.fct[P.nf++] = 2;
+            std::swap(P.fct[0], P.fct[P.nf - 1]);
+        }
+        for (int d = 3; d * d <= l; d += 2)
+            while (l % d == 0) { P.fct[P.nf++] = d; l /= d; }
+        if (l > 1) P.fct[P.nf++] = l;
+    }
+    size_t l1 = 1;
+    for (int k = 0; k < P.nf; ++k) {
+        const size_t ip = (size_t)P.fct[k], ido = (size_t)n / (l1 * ip);
+        P.tw[k] = (int)mem.size();
+        if (k < P.nf - 1) {
+            const size_t off = mem.size();
+            mem.resize(off + (ip - 1) * (ido - 1));
+            for (size_t j = 1; j < ip; ++j)
+                for (size_t i = 1; i <= (ido - 1) / 2; ++i) {
+                    T re, im;
+                    sincos_2pibyn<T>((size_t)n, j * l1 * i, re, im);
+                    mem[off + (j - 1) * (ido - 1) + 2 * i - 2] = re;
+                    mem[off + (j - 1) * (ido - 1) + 2 * i - 1] = im;
+                }
+        }
+        P.tws[k] = (int)mem.size();
+        if (ip > 5) {
+            const size_t off = mem.size();
+            mem.resize(off + 2 * ip);
+            mem[off] = T(1);
+            mem[off + 1] = T(0);
+            for (size_t i = 2, ic = 2 * ip - 2; i <= ic; i += 2, ic -= 2) {
+                T re, im;
+                sincos_2pibyn<T>((size_t)n, i / 2 * ((size_t)n / ip), re, im);
+                mem[off + i] = re;
+                mem[off + i + 1] = im;
+                mem[off + ic] = re;
+                mem[off + ic + 1] = -im;
+            }
+        }
+        l1 *= ip;
+    }
+    P.dct_tw = (int)mem.size();
+    for (int i = 0; i < n; ++i) {
+        T re, im;
+        sincos_2pibyn<T>(4 * (size_t)n, (size_t)i + 1, re, im);
+        mem.push_back(re);
+    }
+    P.norm = (int)mem.size();
+    mem.push_back(T(1 / std::sqrt((long double)(2 * n))));
+}
 
 }  // namespace pfft
 }  // namespace vcf

@@ -14,6 +14,7 @@
 #include "vcf_amd.h"
 #include "vcf_internal.h"
 #include "vcf_pocketfft.h"
+#include "vcf_sincos.h"
 
 namespace vcf {
 namespace {
@@ -40,48 +41,6 @@ constexpr int kTableSize = slot_off(1 << 30);   // all slots
 
 __constant__ float c_tw_f32[kTableSize];
 __constant__ double c_tw_f64[kTableSize];
-
-// ---- host: pocketfft sincos_2pibyn<T>(n)[idx].{r,i} (values in double) ----
-void sc_calc(size_t x, size_t n, double ang, double &re, double &im)
-{
-    x <<= 3;
-    if (x < 4 * n) {
-        if (x < 2 * n) {
-            if (x < n) { re = std::cos(double(x) * ang); im = std::sin(double(x) * ang); return; }
-            re = std::sin(double(2 * n - x) * ang); im = std::cos(double(2 * n - x) * ang); return;
-        }
-        x -= 2 * n;
-        if (x < n) { re = -std::sin(double(x) * ang); im = std::cos(double(x) * ang); return; }
-        re = -std::cos(double(2 * n - x) * ang); im = std::sin(double(2 * n - x) * ang); return;
-    }
-    x = 8 * n - x;
-    if (x < 2 * n) {
-        if (x < n) { re = std::cos(double(x) * ang); im = -std::sin(double(x) * ang); return; }
-        re = std::sin(double(2 * n - x) * ang); im = -std::cos(double(2 * n - x) * ang); return;
-    }
-    x -= 2 * n;   /* the third quadrant: x in [2n, 4n] */
-    if (x < n) { re = -std::sin(double(x) * ang); im = -std::cos(double(x) * ang); return; }
-    re = -std::cos(double(2 * n - x) * ang); im = -std::sin(double(2 * n - x) * ang);
-}
-
-// value pocketfft hands out for index idx of a table of length n (cast to T)
-template <typename T> void sincos_2pibyn(size_t n, size_t idx, T &re_out, T &im_out)
-{
-    const long double pi = 3.141592653589793238462643383279502884197L;
-    const double ang = double(0.25L * pi / (long double)n);
-    const size_t nval = (n + 2) / 2;
-    size_t shift = 1;
-    while ((size_t(1) << shift) * (size_t(1) << shift) < nval) ++shift;
-    const size_t mask = (size_t(1) << shift) - 1;
-    bool conj = false;
-    if (2 * idx > n) { idx = n - idx; conj = true; }
-    double r1 = 1.0, i1 = 0.0, r2 = 1.0, i2 = 0.0;
-    if (idx & mask) sc_calc(idx & mask, n, ang, r1, i1);
-    if (idx >> shift) sc_calc((idx >> shift) * (mask + 1), n, ang, r2, i2);
-    re_out = T(r1 * r2 - i1 * i2);
-    T im = T(r1 * i2 + i1 * r2);
-    im_out = conj ? -im : im;
-}
 
 // One slot: rfftp<T>::comp_twiddle values, T_dcst23's twiddle, fct.
 template <typename T> void fill_slot(int n, T *slot)

@@ -23,9 +23,9 @@ __all__ = ["padded_shape", "flags_from", "encode_device", "decode_device", "enco
 
 
 def block_size_supported(block_size: int) -> bool:
-    """True if the HIP path has a transform of this length: any B <= 4096 for which pocketfft
-    plans with rfftp (compiled kernels for the 5-smooth B <= 128, run-time plans otherwise);
-    pocketfft's Bluestein lengths (191, 199, ...) are not supported."""
+    """True if the HIP path has a transform of this length: any 1 <= B <= 4096 (compiled
+    kernels for the 5-smooth B <= 128, run-time plans otherwise -- rfftp, or Bluestein for
+    the lengths pocketfft plans that way, 191, 199, ...)."""
     return bool(_lib.lib().vcf_dct_block_size_supported(int(block_size)))
 
 
