@@ -5,6 +5,7 @@ at 8 bits, all five scanline filters (a small test-only writer forces each),
 odd sizes, multi-IDAT files; corrupt files raise; PNGs outside the covered
 set (16-bit) fall back to PIL through eic.read_image."""
 import io
+import os
 import struct
 import zlib
 
@@ -12,6 +13,7 @@ import numpy as np
 import pytest
 from PIL import Image
 
+from conftest import ROOT
 from vcf_amd.codec import eic
 
 
@@ -161,3 +163,36 @@ def test_png_writer_round_trip(shape, tmp_path):
         outs.append(p.read_bytes())
     eic.PNG_THREADS = 16
     assert outs[0] == outs[1]
+
+
+def test_libdeflate_and_zlib_paths_agree(tmp_path):
+    """The reader inflates with libdeflate when the system has it and with zlib
+    otherwise (VCF_PNG_NO_LIBDEFLATE=1 forces zlib): same pixels, same errors."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(5)
+    files = []
+    for n, (filters, split) in enumerate((([1, 2], 1), ([0, 1, 2, 3, 4], 4), ([4], 2))):
+        arr = rng.integers(0, 256, (37, 29, 3), dtype=np.uint8)
+        arr[10:20] = arr[10:11]
+        p = tmp_path / f"f{n}.png"
+        p.write_bytes(_write_png(arr, filters, idat_split=split))
+        files.append(str(p))
+    bad = tmp_path / "trailing.png"   # extra scanline data after the image: both paths take the first rows
+    arr = rng.integers(0, 256, (6, 5, 3), dtype=np.uint8)
+    png = _write_png(np.concatenate([arr, arr]), [1])
+    ihdr = struct.pack(">IIBBBBB", 5, 6, 8, 2, 0, 0, 0)
+    bad.write_bytes(png[:8] + _chunk(b"IHDR", ihdr) + png[8 + 25:])
+    files.append(str(bad))
+    code = ("import sys, numpy as np\nfrom vcf_amd.codec import eic\n"
+            "np.savez(sys.argv[1], *[eic.read_image(f)[0] for f in sys.argv[2:]])\n")
+    outs = []
+    for flag in ("0", "1"):
+        out = str(tmp_path / f"o{flag}.npz")
+        env = dict(os.environ, VCF_PNG_NO_LIBDEFLATE=flag)
+        subprocess.run([sys.executable, "-c", code, out, *files], check=True, env=env, cwd=ROOT)
+        outs.append(np.load(out))
+    for k in outs[0].files:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+    for f, k in zip(files, outs[0].files):
+        assert np.array_equal(outs[0][k], _pil_rgb(open(f, "rb").read())), f

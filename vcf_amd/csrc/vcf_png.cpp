@@ -17,10 +17,12 @@
 // entropy_image_coding.py:55-60): like 16-bit and Adam7 files they return
 // VCF_ERR_UNSUPPORTED and the caller reads them the generic way.  Chunk CRCs
 // are verified; a corrupt file is VCF_ERR_INVALID.
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -30,6 +32,74 @@
 
 namespace vcf {
 namespace {
+
+// libdeflate's decompressor and crc32, resolved once (null members: absent)
+struct Libdeflate {
+    void *(*alloc_decompressor)() = nullptr;
+    void (*free_decompressor)(void *) = nullptr;
+    int (*zlib_decompress_ex)(void *, const void *, size_t, void *, size_t, size_t *, size_t *) = nullptr;
+    uint32_t (*crc32)(uint32_t, const void *, size_t) = nullptr;
+    bool ok() const { return alloc_decompressor && free_decompressor && zlib_decompress_ex && crc32; }
+};
+
+const Libdeflate &libdeflate()
+{
+    static const Libdeflate L = [] {
+        Libdeflate l;
+        const char *off = getenv("VCF_PNG_NO_LIBDEFLATE");   // tests: force the zlib path
+        if (off && *off && *off != '0') return l;
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return l;
+        l.alloc_decompressor = reinterpret_cast<void *(*)()>(dlsym(h, "libdeflate_alloc_decompressor"));
+        l.free_decompressor = reinterpret_cast<void (*)(void *)>(dlsym(h, "libdeflate_free_decompressor"));
+        l.zlib_decompress_ex = reinterpret_cast<int (*)(void *, const void *, size_t, void *, size_t, size_t *,
+                                                        size_t *)>(dlsym(h, "libdeflate_zlib_decompress_ex"));
+        l.crc32 = reinterpret_cast<uint32_t (*)(uint32_t, const void *, size_t)>(dlsym(h, "libdeflate_crc32"));
+        return l;
+    }();
+    return L;
+}
+
+// one decompressor per thread (the III runner reads frames on a pool)
+struct Inflater {
+    void *d = nullptr;
+    ~Inflater() { if (d) libdeflate().free_decompressor(d); }
+};
+
+uint32_t chunk_crc(const uint8_t *p, size_t n)
+{
+    const Libdeflate &L = libdeflate();
+    if (L.ok()) return L.crc32(0, p, n);
+    return (uint32_t)crc32(crc32(0L, Z_NULL, 0), p, (uInt)n);
+}
+
+// the whole zlib stream of the IDAT data into out (exactly out_len bytes);
+// false: libdeflate absent or the stream not clean (the zlib path then
+// reports the precise error)
+bool inflate_libdeflate(const std::vector<std::pair<const uint8_t *, uint32_t>> &idat, uint8_t *out, size_t out_len)
+{
+    const Libdeflate &L = libdeflate();
+    if (!L.ok()) return false;
+    thread_local Inflater inf;
+    if (!inf.d) inf.d = L.alloc_decompressor();
+    if (!inf.d) return false;
+    thread_local std::vector<uint8_t> joined;
+    const uint8_t *in = idat.empty() ? nullptr : idat[0].first;
+    size_t in_len = idat.empty() ? 0 : idat[0].second;
+    if (idat.size() > 1) {
+        size_t tot = 0;
+        for (const auto &c : idat) tot += c.second;
+        joined.resize(tot);
+        size_t at = 0;
+        for (const auto &c : idat) { std::memcpy(joined.data() + at, c.first, c.second); at += c.second; }
+        in = joined.data();
+        in_len = tot;
+    }
+    if (!in) return false;
+    size_t used = 0, got = 0;
+    const int r = L.zlib_decompress_ex(inf.d, in, in_len, out, out_len, &used, &got);
+    return r == 0 && got == out_len;   // LIBDEFLATE_SUCCESS, every scanline byte
+}
 
 uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 
@@ -61,7 +131,7 @@ int parse(const uint8_t *data, int64_t n, PngHeader &h, const uint8_t **plte, ui
             return set_error(VCF_ERR_INVALID, "truncated PNG chunk");
         const uint8_t *body = data + off + 8;
         const uint32_t crc = be32(body + len);
-        if ((uint32_t)crc32(crc32(0L, Z_NULL, 0), type, 4 + len) != crc)
+        if (chunk_crc(type, 4 + (size_t)len) != crc)
             return set_error(VCF_ERR_INVALID, "broken PNG file (chunk CRC)");
         if (!std::memcmp(type, "IHDR", 4)) {
             if (len != 13) return set_error(VCF_ERR_INVALID, "bad IHDR");
@@ -102,6 +172,14 @@ int unfilter(uint8_t *row, const uint8_t *prev, size_t len, int bpp, int ftype)
     switch (ftype) {
     case 0: return VCF_OK;
     case 1:
+        if (bpp == 3) {   // the running pixel in registers: no store-to-load chain through memory
+            uint8_t a = 0, b = 0, c = 0;
+            for (size_t i = 0; i + 2 < len; i += 3) {
+                a = (uint8_t)(a + row[i]); b = (uint8_t)(b + row[i + 1]); c = (uint8_t)(c + row[i + 2]);
+                row[i] = a; row[i + 1] = b; row[i + 2] = c;
+            }
+            return VCF_OK;
+        }
         for (size_t i = bpp; i < len; ++i) row[i] = (uint8_t)(row[i] + row[i - bpp]);
         return VCF_OK;
     case 2:
@@ -197,31 +275,35 @@ int vcf_png_decode_rgb(const uint8_t *data, int64_t nbytes, uint8_t *rgb_out, in
     if ((int64_t)need > out_capacity) return set_error(VCF_ERR_INVALID, "output buffer too small");
     if (h.ctype == 3 && (!plte || plte_len % 3 != 0)) return set_error(VCF_ERR_INVALID, "palette PNG without PLTE");
 
-    // inflate all IDAT data into filtered scanlines (1 filter byte + stride)
-    std::vector<uint8_t> raw((stride + 1) * h.h);
-    z_stream zs;
-    std::memset(&zs, 0, sizeof(zs));
-    if (inflateInit(&zs) != Z_OK) return set_error(VCF_ERR_INVALID, "inflateInit failed");
-    zs.next_out = raw.data();
-    zs.avail_out = (uInt)raw.size();
-    int zr = Z_OK;
-    for (size_t c = 0; c < idat.size() && zr != Z_STREAM_END; ++c) {
-        zs.next_in = const_cast<Bytef *>(idat[c].first);
-        zs.avail_in = idat[c].second;
-        while (zs.avail_in > 0 && zs.avail_out > 0) {
-            zr = inflate(&zs, Z_NO_FLUSH);
-            if (zr == Z_STREAM_END) break;
-            if (zr != Z_OK && zr != Z_BUF_ERROR) {
-                inflateEnd(&zs);
-                return set_error(VCF_ERR_INVALID, "broken PNG data stream (zlib %d)", zr);
+    // inflate all IDAT data into filtered scanlines (1 filter byte + stride);
+    // the buffer is kept per thread (no zero fill, no fresh pages per frame)
+    thread_local std::vector<uint8_t> raw;
+    raw.resize((stride + 1) * h.h);
+    if (!inflate_libdeflate(idat, raw.data(), raw.size())) {
+        z_stream zs;
+        std::memset(&zs, 0, sizeof(zs));
+        if (inflateInit(&zs) != Z_OK) return set_error(VCF_ERR_INVALID, "inflateInit failed");
+        zs.next_out = raw.data();
+        zs.avail_out = (uInt)raw.size();
+        int zr = Z_OK;
+        for (size_t c = 0; c < idat.size() && zr != Z_STREAM_END; ++c) {
+            zs.next_in = const_cast<Bytef *>(idat[c].first);
+            zs.avail_in = idat[c].second;
+            while (zs.avail_in > 0 && zs.avail_out > 0) {
+                zr = inflate(&zs, Z_NO_FLUSH);
+                if (zr == Z_STREAM_END) break;
+                if (zr != Z_OK && zr != Z_BUF_ERROR) {
+                    inflateEnd(&zs);
+                    return set_error(VCF_ERR_INVALID, "broken PNG data stream (zlib %d)", zr);
+                }
+                if (zr == Z_BUF_ERROR) break;
             }
-            if (zr == Z_BUF_ERROR) break;
         }
+        const size_t got = raw.size() - zs.avail_out;
+        inflateEnd(&zs);
+        if (got != raw.size()) return set_error(VCF_ERR_INVALID, "image file is truncated (%zu of %zu bytes)", got,
+                                                raw.size());
     }
-    const size_t got = raw.size() - zs.avail_out;
-    inflateEnd(&zs);
-    if (got != raw.size()) return set_error(VCF_ERR_INVALID, "image file is truncated (%zu of %zu bytes)", got,
-                                            raw.size());
 
     // unfilter in place, then expand to RGB
     const uint8_t *prev = nullptr;
