@@ -241,7 +241,7 @@ def c4_block(args, world: int, rank: int, group):
     N, H, W, Q = args.c4_frames, 1080, 1920, args.QSS
     lo, hi = frame_range(N, rank, world)
     info = {"workload": (f"III C4: {N} x 1080p frames, DCT+deadzone Q={Q} + GPU entropy (-c TCBAACP, "
-                         f"{T.PRIOR_SEG}-symbol segments), frame i on rank floor(i*P/N), sizes all-gather + "
+                         f"{T.CLASS_SEG}-symbol segments, {T.PRIOR_CLASSES} prior classes), frame i on rank floor(i*P/N), sizes all-gather + "
                          f"code-stream gatherv to rank 0 over RCCL (device to device), rank 0 copies them to host"),
             "frames": N, "frame": [H, W, 3], "n_ranks": world, "frames_this_rank0": hi - lo if rank == 0 else None}
     err, comm, t_rank = None, None, float("nan")
@@ -293,7 +293,7 @@ def c4_verify(got, bases, job, N, H, W, Q, world) -> str:
     from vcf_amd import dct as D
     from vcf_amd import tcbaac as T
     from vcf_amd.device import DeviceBuffer
-    codec = T.TiledCBAACCodec(order=0, seg_len=T.PRIOR_SEG, prior=True)
+    codec = T.TiledCBAACCodec(order=0, seg_len=T.CLASS_SEG, prior=True, nclass=T.PRIOR_CLASSES)
     frames = range(N) if world > 1 else sorted({0, N // 2, N - 1})
     Hp, Wp = D.padded_shape(H, W)
     for i in frames:

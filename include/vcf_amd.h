@@ -335,6 +335,27 @@ int vcf_cbaac_tiled_encode_frames(const uint8_t *sym_dev, int64_t n_frames, int6
 int vcf_cbaac_tiled_decode_frames(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n_frames,
                                   int64_t frame_symbols, int32_t order, const uint16_t *priors_dev, int64_t seg_len,
                                   uint8_t *sym_dev, int64_t out_frame_stride, void *stream);
+/* Prior classes (container version 3; not in the reference): nclass
+ * (1 .. 256) prior rows per frame instead of one.  Segment s of a frame's
+ * `segments` takes row floor(s * nclass / segments) -- consecutive runs of
+ * segments share a row, so for DCT indices in the subband layout and nclass =
+ * 8 a row is (about) one subband row i, whose statistics differ the most --
+ * and row c = 1 + floor(hist_c[s] * 8192 / n_c) over the symbols of class c's
+ * segments (nclass = 1: the version-2 prior).  priors_dev = n_frames x nclass
+ * x 256 uint16 (frame f, class c at + 256 (f nclass + c); 8-byte aligned),
+ * hist_dev = as many uint32 of scratch; the rest as the _frames calls.  Each
+ * segment's bytes equal vcf_cbaac_encode_prior of that segment alone with
+ * its class's row. */
+int vcf_cbaac_tiled_prior_classes(const uint8_t *sym_dev, int64_t n_frames, int64_t frame_symbols,
+                                  int64_t frame_stride, int64_t seg_len, int32_t nclass, uint16_t *priors_dev,
+                                  uint32_t *hist_dev, void *stream);
+int vcf_cbaac_tiled_encode_classes(const uint8_t *sym_dev, int64_t n_frames, int64_t frame_symbols,
+                                   int64_t frame_stride, int32_t order, const uint16_t *priors_dev, int32_t nclass,
+                                   int64_t seg_len, uint8_t *out_dev, int64_t out_frame_capacity,
+                                   int64_t *seg_bytes_dev, void *ws_dev, void *stream);
+int vcf_cbaac_tiled_decode_classes(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n_frames,
+                                   int64_t frame_symbols, int32_t order, const uint16_t *priors_dev, int32_t nclass,
+                                   int64_t seg_len, uint8_t *sym_dev, int64_t out_frame_stride, void *stream);
 /* host, orders 0 / 1: vcf_cbaac_encode / _decode with every model seeded by prior (256 uint16, each >= 1) */
 int vcf_cbaac_encode_prior(const uint8_t *symbols, int64_t n, int32_t order, const uint16_t *prior, uint8_t *out,
                            int64_t out_capacity, int64_t *out_bytes, int64_t *out_bits);

@@ -5,7 +5,7 @@ one with the same calls encode_fn makes:
   read     encode_read_fn: the PNG decode (native reader, codec/eic.py)
   h2d      DeviceBuffer.from_array of the RGB frame (pageable host memory)
   dct      vcf_dct_dz_encode on the GPU (indices stay in HBM)
-  entropy  the tiled coder's kernels (prior histogram for TCBAACP, encode)
+  entropy  the tiled coder's kernels (TCBAACP: class histograms + prior rows, encode)
   d2h      segment sizes + code-stream bytes back to the host
   pack     the container (tcbaac.pack) + _shape.bin
   write    encode_write_fn (file write)
@@ -62,7 +62,13 @@ def stages_gpu_coder(c, src, out, reps):
         cap = int(lib.vcf_cbaac_tiled_bound(n, coder.seg_len))
         ob = coder.scratch.get("out", cap)
         sb = coder.scratch.get("sizes", 8 * (ns + 1))
-        if coder.prior:
+        K = coder.nclass
+        if coder.prior and K > 1:
+            pr, hist = coder.scratch.get("prior", 512 * K), coder.scratch.get("hist", 1024 * K)
+            L.call("vcf_cbaac_tiled_prior_classes", k.ptr, 1, n, n, coder.seg_len, K, pr.ptr, hist.ptr, st.handle)
+            L.call("vcf_cbaac_tiled_encode_classes", k.ptr, 1, n, n, coder.order, pr.ptr, K, coder.seg_len, ob.ptr,
+                   cap, sb.ptr, ws.ptr, st.handle)
+        elif coder.prior:
             pr, hist = coder.scratch.get("prior", 512), coder.scratch.get("hist", 1024)
             L.call("vcf_cbaac_tiled_prior", k.ptr, n, pr.ptr, hist.ptr, st.handle)
             L.call("vcf_cbaac_tiled_encode_prior", k.ptr, n, coder.order, pr.ptr, coder.seg_len, ob.ptr, cap,
@@ -74,7 +80,7 @@ def stages_gpu_coder(c, src, out, reps):
         t4 = time.perf_counter()
         prior = None
         if coder.prior:
-            prior = np.empty(256, np.uint16)
+            prior = np.empty((K, 256) if K > 1 else 256, np.uint16)
             pr.download(prior, st)
         sizes = np.empty(ns + 1, np.int64)
         sb.download(sizes, st)

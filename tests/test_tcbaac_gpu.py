@@ -143,8 +143,9 @@ def test_prior_codec_on_dct_indices():
 
 
 def test_dct_codec_with_tcbaacp_frame(tmp_path):
-    """-c TCBAACP: the DCT indices coded on the GPU with prior-seeded models;
-    the file's segments equal the host coder's, decoding gives the oracle frame."""
+    """-c TCBAACP: the DCT indices coded on the GPU with models seeded by the
+    frame's prior rows (version 3); the file's segments equal the host
+    coder's, decoding gives the oracle frame."""
     from PIL import Image
 
     from bench import synth_frame
@@ -158,8 +159,8 @@ def test_dct_codec_with_tcbaacp_frame(tmp_path):
     data = open(str(tmp_path / "enc.tadpt_arith"), "rb").read()
     k = O.encode_frame(rgb, 32, 0)
     shape, order, seg_len, sizes, payload, prior = T._parse(data)
-    assert shape == k.shape and order == 0 and seg_len == T.PRIOR_SEG
-    assert np.array_equal(prior, T.prior_of(k))
+    assert shape == k.shape and order == 0 and seg_len == T.CLASS_SEG
+    assert np.array_equal(prior, T.prior_of(k, T.PRIOR_CLASSES, seg_len))   # container version 3
     assert payload == b"".join(T.host_segments_prior(k, prior, seg_len))
     CoDec(P.parse(P.dct_parser(), ["decode", "-c", "TCBAACP"])).decode_fn(str(tmp_path / "enc"),
                                                                          str(tmp_path / "out.png"))
@@ -337,3 +338,104 @@ def test_batch_decode_frames(variant):
         L.call("vcf_cbaac_tiled_set_variant", 0)
     for f in range(F):
         assert np.array_equal(got[f * stride:f * stride + n], frames[f]), f
+
+
+# ---- version 3: prior classes ---------------------------------------------------------
+
+def _dct_indices(H=1080, W=1920, seed=5):
+    from bench import synth_frame
+    from oracle import oracle as O
+    return O.encode_frame(synth_frame(H, W, seed), 32, 0).ravel()
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("order,seg_len,nclass", [(0, 4096, 8), (0, 256, 3), (1, 4096, 8), (0, 8192, 200)])
+def test_class_prior_segments_equal_host_coder(variant, order, seg_len, nclass):
+    """Container version 3: the GPU's prior rows equal the host formula over
+    each class's segments; every segment's bytes equal
+    vcf_cbaac_encode_prior of that segment with its class's row, with one
+    wave (1) or one lane (2, order 0) per segment; both decoders invert it.
+    nclass = 200 > some frames' segment count leaves rows with no segments."""
+    from vcf_amd import _lib as L
+    rng = np.random.Generator(np.random.PCG64(seg_len + nclass))
+    lap = np.clip(np.rint(rng.laplace(128, 1.5, 300_001)), 0, 255).astype(np.uint8)
+    lap[100_000:140_000] = 128
+    for name, sym in (("dct", _dct_indices()), ("laplace", lap)):
+        try:
+            L.call("vcf_cbaac_tiled_set_variant", variant)
+            c = T.TiledCoder(order, seg_len, prior=True, nclass=nclass)
+            sizes, payload = c.encode(sym)
+            prior = T.prior_of(sym, nclass, seg_len)
+            assert np.array_equal(c.last_prior, prior), name
+            host = T.host_segments_prior(sym, prior, seg_len, order)
+            assert list(sizes) == [len(h) for h in host], name
+            assert payload == b"".join(host), name
+            assert np.array_equal(c.decode(payload, sizes, sym.size, prior), sym), name
+        finally:
+            L.call("vcf_cbaac_tiled_set_variant", 0)
+
+
+def test_class_priors_cut_the_rate_of_short_segments():
+    """On a 1080p frame's DCT indices (subband layout) 4096-symbol segments
+    with 8 prior rows cost at most 3 % over the serial stream (one prior row:
+    about +12 %), container bytes included."""
+    from vcf_amd.cbaac import encode_symbols
+    k = _dct_indices()
+    serial = len(encode_symbols(k, 0))
+    c8 = T.TiledCBAACCodec(0, T.CLASS_SEG, prior=True, nclass=T.PRIOR_CLASSES)
+    c1 = T.TiledCBAACCodec(0, T.CLASS_SEG, prior=True)
+    b8 = len(c8.compress(k.reshape(1080, 1920, 3)).getvalue())
+    b1 = len(c1.compress(k.reshape(1080, 1920, 3)).getvalue())
+    assert b8 <= 1.03 * serial, (b8, serial)
+    assert b1 > b8
+
+
+def test_frame_batch_with_classes_equals_one_by_one():
+    """FrameBatch / encode_frames_device with prior classes (one launch per
+    stage for the batch, unaligned frame starts) equals coding each frame
+    alone; the batched decode (vcf_cbaac_tiled_decode_classes) inverts it."""
+    from vcf_amd import _lib as L
+    from vcf_amd.device import DeviceBuffer
+    rng = np.random.Generator(np.random.PCG64(33))
+    n, F, seg, K = 61 * 77 * 3, 5, 1024, 4
+    frames = [np.clip(np.rint(rng.laplace(128, 0.5 + f, n)), 0, 255).astype(np.uint8) for f in range(F)]
+    buf = DeviceBuffer.from_array(np.concatenate([np.zeros(1, np.uint8)] + frames))
+    got = T.encode_frames_device(buf, F, n, 0, seg, prior=True, offset=1, nclass=K)
+    for f in range(F):
+        c = T.TiledCoder(0, seg, prior=True, nclass=K)
+        s, p = c.encode(frames[f])
+        assert list(got[f][0]) == list(s) and got[f][1] == p, f
+        assert np.array_equal(got[f][2], c.last_prior), f
+    ns = T.n_segments(n, seg)
+    payload = b"".join(e[1] for e in got)
+    offs, base = [], 0
+    for e in got:
+        offs.append(np.concatenate([[0], np.cumsum(e[0])]) + base)
+        base += len(e[1])
+    offs = np.concatenate(offs).astype(np.int64)
+    priors = np.stack([e[2] for e in got]).astype(np.uint16)
+    assert priors.shape == (F, K, 256)
+    src, doffs, dpr = (DeviceBuffer.from_array(np.frombuffer(payload, np.uint8)), DeviceBuffer.from_array(offs),
+                       DeviceBuffer.from_array(priors))
+    out = DeviceBuffer(F * n)
+    L.call("vcf_cbaac_tiled_decode_classes", src.ptr, doffs.ptr, F, n, 0, dpr.ptr, K, seg, out.ptr, n, None)
+    dec = out.download(np.empty(F * n, np.uint8))
+    assert offs.size == F * (ns + 1)
+    for f in range(F):
+        assert np.array_equal(dec[f * n:(f + 1) * n], frames[f]), f
+
+
+def test_tcbaacp_codec_is_version_3(tmp_path):
+    """-c TCBAACP writes container version 3 (8 prior rows, 4096-symbol
+    segments) and decodes it; version-2 streams still decode."""
+    import struct
+    k = _dct_indices(272, 480, 2).reshape(272, 480, 3)
+    from vcf_amd.codec.dct2d import _tcbaac_prior
+    codec = _tcbaac_prior()
+    data = codec.compress(k).getvalue()
+    shape, order, seg_len, sizes, payload, prior = T._parse(data)
+    assert struct.unpack_from("<I", data, 4 + 4 * 3 + 4)[0] == T.VERSION_CLASSES
+    assert seg_len == T.CLASS_SEG and prior.shape == (T.PRIOR_CLASSES, 256)
+    assert np.array_equal(codec.decompress(data), k)
+    v2 = T.TiledCBAACCodec(0, 8192, prior=True).compress(k).getvalue()
+    assert np.array_equal(codec.decompress(v2), k)

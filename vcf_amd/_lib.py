@@ -140,6 +140,9 @@ SIGNATURES = {
     "vcf_cbaac_tiled_trace": [_P, _I64, _I32, _I64, _P, _P, _P, _P],
     "vcf_cbaac_tiled_decode": [_P, _P, _I64, _I32, _I64, _P, _P],
     "vcf_cbaac_tiled_prior": [_P, _I64, _P, _P, _P],
+    "vcf_cbaac_tiled_prior_classes": [_P, _I64, _I64, _I64, _I64, _I32, _P, _P, _P],
+    "vcf_cbaac_tiled_encode_classes": [_P, _I64, _I64, _I64, _I32, _P, _I32, _I64, _P, _I64, _P, _P, _P],
+    "vcf_cbaac_tiled_decode_classes": [_P, _P, _I64, _I64, _I32, _P, _I32, _I64, _P, _I64, _P],
     "vcf_cbaac_tiled_encode_prior": [_P, _I64, _I32, _P, _I64, _P, _I64, _P, _P, _P],
     "vcf_cbaac_tiled_decode_prior": [_P, _P, _I64, _I32, _P, _I64, _P, _P],
     "vcf_cbaac_encode_prior": [_P, _I64, _I32, _P, _P, _I64, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],

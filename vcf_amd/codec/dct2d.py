@@ -56,13 +56,15 @@ def _tcbaac(args=None):
 
 
 def _tcbaac_prior(args=None):
-    from ..tcbaac import PRIOR_SEG, TiledCBAACCodec
+    from ..tcbaac import CLASS_SEG, PRIOR_CLASSES, TiledCBAACCodec
     return TiledCBAACCodec(getattr(args, "order", 0) if args is not None else 0,
-                           getattr(args, "segment_symbols", PRIOR_SEG) if args is not None else PRIOR_SEG, prior=True)
+                           getattr(args, "segment_symbols", CLASS_SEG) if args is not None else CLASS_SEG, prior=True,
+                           nclass=PRIOR_CLASSES)
 
 
 # TCBAAC: CBAAC in independent segments on the GPU (vcf_amd/tcbaac.py, a new container);
-# TCBAACP: the same with every segment's models seeded by the frame's order-0 prior (container version 2)
+# TCBAACP: the same with every segment's models seeded by a prior row of the frame: 8 rows, one per run of
+# segments (about one subband row each), 4096-symbol segments (container version 3)
 ENTROPY_CODECS = {"TIFF": TIFFCodec, "CBAAC": _cbaac, "CBAHC": _cbahc, "TCBAAC": _tcbaac, "TCBAACP": _tcbaac_prior}
 
 

@@ -39,7 +39,7 @@ class DeviceIII:
     """One rank's part of a frame-sharded, HBM-resident III encode."""
 
     def __init__(self, comm, rank: int, world: int, n_frames: int, H: int, W: int, Q: int = 32,
-                 seg_len: int = T.PRIOR_SEG, streams: int = 4):
+                 seg_len: int = T.CLASS_SEG, streams: int = 4, nclass: int = T.PRIOR_CLASSES):
         self.comm, self.rank, self.world = comm, int(rank), int(world)
         self.N, self.H, self.W, self.Q = int(n_frames), int(H), int(W), int(Q)
         self.lo, self.hi = frame_range(self.N, self.rank, self.world)
@@ -49,7 +49,7 @@ class DeviceIII:
         self.n_sym = self.Hp * self.Wp * 3
         self.stream = Stream()
         self.k = DeviceBuffer(max(self.n_local * self.n_sym, 1))
-        self.batch = T.FrameBatch(self.n_local, self.n_sym, 0, seg_len, prior=True)
+        self.batch = T.FrameBatch(self.n_local, self.n_sym, 0, seg_len, prior=True, nclass=nclass)
         self.send = None
         self.recv = None
         self.hstage = None

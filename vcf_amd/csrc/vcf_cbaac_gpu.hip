@@ -75,6 +75,7 @@ __device__ __forceinline__ void model_reset(Model &m, uint32_t lane)
 // reference's rules (CBAAC.py:32-36).  Short segments then stop paying the
 // model's learning cost.
 constexpr uint32_t kPriorScale = 8192;   // prior total <= 256 + 8192 < max_freq
+constexpr int32_t kMaxClasses = 256;      // prior rows per frame (container version 3)
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane);
 
@@ -328,7 +329,15 @@ __device__ __forceinline__ double rcp_exact(uint32_t t) { return rcp_nr((double)
 // out + f * cap (encode)
 struct Frames {
     int64_t sym_stride = 0, prior_stride = 0, out_stride = 0, cap = 0;
+    int32_t nclass = 1;   // prior classes: segment s of nseg takes prior row s * nclass / nseg
 };
+
+// the prior row of segment `seg` of a frame's `nseg` (container version 3:
+// nclass rows of 256, consecutive runs of segments share a row)
+__device__ __forceinline__ const uint16_t *class_prior(const uint16_t *prior, int64_t seg, int64_t nseg, int32_t nclass)
+{
+    return prior + 256 * ((seg * nclass) / nseg);
+}
 
 template <int ORDER, bool TRACE>
 __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *__restrict__ sym, int64_t n,
@@ -343,7 +352,7 @@ __global__ __launch_bounds__(64) void cbaac_tiled_encode_kernel(const uint8_t *_
         sym += f * fr.sym_stride;
         slots += f * nsf * slot_words;
         seg_bits += f * nsf;
-        if (prior) prior += f * fr.prior_stride;
+        if (prior) prior = class_prior(prior + f * fr.prior_stride, blockIdx.x, nsf, fr.nclass);
     }
     const int64_t seg = blockIdx.x;
     const uint32_t lane = threadIdx.x;
@@ -458,7 +467,7 @@ __global__ __launch_bounds__(64) void cbaac_tiled_decode_kernel(const uint8_t *_
         const int64_t f = blockIdx.y, nsf = (n + seg_len - 1) / seg_len;
         offs += f * (nsf + 1);
         out += f * fr.out_stride;
-        if (prior) prior += f * fr.prior_stride;
+        if (prior) prior = class_prior(prior + f * fr.prior_stride, blockIdx.x, nsf, fr.nclass);
     }
     const int64_t seg = blockIdx.x;
     const uint32_t lane = threadIdx.x;
@@ -625,6 +634,41 @@ __global__ __launch_bounds__(256) void cbaac_prior_kernel(const uint32_t *__rest
     prior[t] = (uint16_t)(1u + (n > 0 ? (uint32_t)((uint64_t)hist[t] * kPriorScale / (uint64_t)n) : 0u));
 }
 
+// Version 3 (prior classes): per-class histograms, one workgroup per segment
+// (its class is fixed), LDS bins, one global atomic per bin and segment
+__global__ __launch_bounds__(256) void cbaac_hist_classes_kernel(const uint8_t *__restrict__ sym, int64_t n,
+                                                                 int64_t seg_len, int32_t nclass,
+                                                                 uint32_t *__restrict__ hist, int64_t sym_stride)
+{
+    const int64_t nseg = (n + seg_len - 1) / seg_len, seg = blockIdx.x;
+    sym += (int64_t)blockIdx.y * sym_stride + seg * seg_len;   // frame blockIdx.y
+    hist += 256 * ((int64_t)blockIdx.y * nclass + (seg * nclass) / nseg);
+    const int64_t len = n - seg * seg_len < seg_len ? n - seg * seg_len : seg_len;
+    __shared__ uint32_t bins[256];
+    bins[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < len; i += 256) atomicAdd(&bins[sym[i]], 1u);
+    __syncthreads();
+    if (bins[threadIdx.x]) atomicAdd(&hist[threadIdx.x], bins[threadIdx.x]);
+}
+
+// prior row of one (frame, class): f[s] = 1 + floor(hist[s] * 8192 / n_c), n_c
+// the class's symbols (one class: the frame's n, version 2's formula)
+__global__ __launch_bounds__(256) void cbaac_prior_classes_kernel(const uint32_t *__restrict__ hist,
+                                                                  uint16_t *__restrict__ prior)
+{
+    hist += 256 * (int64_t)blockIdx.x;   // row (frame, class) blockIdx.x
+    prior += 256 * (int64_t)blockIdx.x;
+    __shared__ uint32_t part[4];
+    const uint32_t t = threadIdx.x, h = hist[t];
+    uint32_t v = h;
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if ((t & 63) == 0) part[t >> 6] = v;
+    __syncthreads();
+    const uint64_t nc = (uint64_t)part[0] + part[1] + part[2] + part[3];
+    prior[t] = (uint16_t)(1u + (nc > 0 ? (uint32_t)((uint64_t)h * kPriorScale / nc) : 0u));
+}
+
 // ---- lane-per-segment coder (order 0) ----------------------------------------------
 // One LANE per segment: a wave codes 64 segments at once, each with its own
 // model and coder state, where the kernels above spend a whole wave on one
@@ -646,9 +690,6 @@ struct LaneLds {
     uint4 E[16][2][kLW];   // [block][half][lane]: entries 8 half .. 8 half + 7 of block `block`
     uint4 C[2][kLW];       // [half][lane]: block starts 8 half .. 8 half + 7
     uint4 M[16][2];        // M[i]: 1 in the u16 entries t > i
-    uint4 E0[16][2];       // the initial model, shared
-    uint4 C0[2];
-    uint32_t bsum[16];
 };
 
 __device__ __forceinline__ uint32_t u16_of(const uint4 &v, int k)   // k compile-time
@@ -661,20 +702,12 @@ __device__ __forceinline__ uint4 add4(const uint4 &a, const uint4 &b)
     return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
-// the initial model (prior frequencies, or 256 ones) into every lane's copy, the mask table
+// every lane's initial model (its segment's prior row, or 256 ones; lanes may
+// sit in different prior classes) and the shared mask table
 __device__ __forceinline__ void lane_model_init(LaneLds &L, const uint16_t *__restrict__ prior, uint32_t lane,
                                                 uint32_t &total)
 {
-    if (lane < 16) {
-        uint32_t acc = 0, e[16];
-        for (int k = 0; k < 16; ++k) {
-            e[k] = acc;
-            acc += prior ? prior[16 * lane + k] : 1u;
-        }
-        L.E0[lane][0] = make_uint4(e[0] | e[1] << 16, e[2] | e[3] << 16, e[4] | e[5] << 16, e[6] | e[7] << 16);
-        L.E0[lane][1] = make_uint4(e[8] | e[9] << 16, e[10] | e[11] << 16, e[12] | e[13] << 16, e[14] | e[15] << 16);
-        L.bsum[lane] = acc;
-    } else if (lane < 48) {   // mask table
+    if (lane >= 16 && lane < 48) {   // mask table
         const int i = (lane - 16) >> 1, h = (lane - 16) & 1;
         uint32_t d[4];
         for (int k = 0; k < 4; ++k) {
@@ -683,25 +716,30 @@ __device__ __forceinline__ void lane_model_init(LaneLds &L, const uint16_t *__re
         }
         L.M[i][h] = make_uint4(d[0], d[1], d[2], d[3]);
     }
-    __syncthreads();
-    if (lane == 0) {
-        uint32_t acc = 0, c[16];
-        for (int b = 0; b < 16; ++b) {
-            c[b] = acc;
-            acc += L.bsum[b];
-        }
-        L.C0[0] = make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
-        L.C0[1] = make_uint4(c[8] | c[9] << 16, c[10] | c[11] << 16, c[12] | c[13] << 16, c[14] | c[15] << 16);
-        L.bsum[0] = acc;   // total (read after the barrier)
-    }
-    __syncthreads();
-    total = L.bsum[0];
+    uint32_t run = 0, c[16];
     for (int b = 0; b < 16; ++b) {
-        L.E[b][0][lane] = L.E0[b][0];
-        L.E[b][1][lane] = L.E0[b][1];
+        uint32_t acc = 0, e[16];
+        if (prior) {
+            const uint2 *q = reinterpret_cast<const uint2 *>(prior + 16 * b);   // f[16b .. 16b+15], 8-B aligned
+            const uint2 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            const uint32_t w[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+            for (int k = 0; k < 16; ++k) {
+                e[k] = acc;
+                acc += (k & 1) ? w[k >> 1] >> 16 : w[k >> 1] & 0xFFFFu;
+            }
+        } else {
+            for (int k = 0; k < 16; ++k) e[k] = k;
+            acc = 16;
+        }
+        L.E[b][0][lane] = make_uint4(e[0] | e[1] << 16, e[2] | e[3] << 16, e[4] | e[5] << 16, e[6] | e[7] << 16);
+        L.E[b][1][lane] = make_uint4(e[8] | e[9] << 16, e[10] | e[11] << 16, e[12] | e[13] << 16, e[14] | e[15] << 16);
+        c[b] = run;
+        run += acc;
     }
-    L.C[0][lane] = L.C0[0];
-    L.C[1][lane] = L.C0[1];
+    L.C[0][lane] = make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
+    L.C[1][lane] = make_uint4(c[8] | c[9] << 16, c[10] | c[11] << 16, c[12] | c[13] << 16, c[14] | c[15] << 16);
+    total = run;
+    __syncthreads();
 }
 
 // every frequency -> (f >> 1) + 1 (CBAAC.py:34-36), from the prefixes; returns the new total
@@ -790,7 +828,7 @@ __global__ __launch_bounds__(kLW) void cbaac_lane_encode_kernel(const uint8_t *_
     const int64_t start = act ? seg * seg_len : 0;
     const int64_t len = act ? (n - start < seg_len ? n - start : seg_len) : 0;
     uint32_t total;
-    lane_model_init(L, PRIOR ? prior : nullptr, lane, total);
+    lane_model_init(L, PRIOR ? class_prior(prior, act ? seg : 0, nseg, fr.nclass) : nullptr, lane, total);
     double inv = rcp_nr((double)total);
     LaneBits w;
     w.out = slots + (act ? seg : 0) * slot_words;
@@ -980,7 +1018,7 @@ __global__ __launch_bounds__(kLW) void cbaac_lane_decode_kernel(const uint8_t *_
     const int64_t start = act ? seg * seg_len : 0;
     const int64_t len = act ? (n - start < seg_len ? n - start : seg_len) : 0;
     uint32_t total;
-    lane_model_init(L, PRIOR ? prior : nullptr, lane, total);
+    lane_model_init(L, PRIOR ? class_prior(prior, act ? seg : 0, nseg, fr.nclass) : nullptr, lane, total);
     double tinv = 1.0 / (double)total;   // (unused until the first symbol; recomputed per symbol)
     (void)tinv;
     LaneReader br;
@@ -1127,7 +1165,7 @@ static bool use_lanes(int32_t order, int64_t total_segments, bool decode)
 static int tiled_encode(const uint8_t *sym_dev, int64_t n_frames, int64_t n, int64_t sym_stride, int32_t order,
                         int64_t seg_len, uint8_t *out_dev, int64_t out_capacity, int64_t *seg_bytes_dev,
                         int32_t *trace_dev, void *ws_dev, void *stream, const uint16_t *prior_dev = nullptr,
-                        int64_t prior_stride = 0)
+                        int64_t prior_stride = 0, int32_t nclass = 1)
 {
     if (int s = check_args(n, order, seg_len)) return s;
     if (n_frames < 1 || n_frames > 65535) return set_error(VCF_ERR_INVALID, "n_frames %lld (1 .. 65535)", (long long)n_frames);
@@ -1144,6 +1182,7 @@ static int tiled_encode(const uint8_t *sym_dev, int64_t n_frames, int64_t n, int
     Frames fr;
     fr.sym_stride = sym_stride;
     fr.prior_stride = prior_stride;
+    fr.nclass = nclass;
     const dim3 grid((unsigned)ns, (unsigned)n_frames);
     if (!trace_dev && use_lanes(order, ns * n_frames, false)) {   // one lane per segment
         const dim3 lg((unsigned)((ns + kLW - 1) / kLW), (unsigned)n_frames);
@@ -1185,7 +1224,7 @@ int vcf_cbaac_tiled_trace(const uint8_t *sym_dev, int64_t n, int32_t order, int6
 
 static int tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n_frames, int64_t n,
                         int32_t order, int64_t seg_len, uint8_t *sym_dev, int64_t out_stride, void *stream,
-                        const uint16_t *prior_dev, int64_t prior_stride)
+                        const uint16_t *prior_dev, int64_t prior_stride, int32_t nclass = 1)
 {
     if (int s = check_args(n, order, seg_len)) return s;
     if (n_frames < 1 || n_frames > 65535) return set_error(VCF_ERR_INVALID, "n_frames %lld (1 .. 65535)", (long long)n_frames);
@@ -1197,6 +1236,7 @@ static int tiled_decode(const uint8_t *in_dev, const int64_t *seg_offsets_dev, i
     Frames fr;
     fr.out_stride = out_stride;
     fr.prior_stride = prior_stride;
+    fr.nclass = nclass;
     const dim3 grid((unsigned)ns, (unsigned)n_frames);
     if (use_lanes(order, ns * n_frames, true)) {   // one lane per segment
         const dim3 lg((unsigned)((ns + kLW - 1) / kLW), (unsigned)n_frames);
@@ -1288,6 +1328,59 @@ int vcf_cbaac_tiled_decode_frames(const uint8_t *in_dev, const int64_t *seg_offs
         return set_error(VCF_ERR_INVALID, "priors_dev not 8-byte aligned");
     return tiled_decode(in_dev, seg_offsets_dev, n_frames, frame_symbols, order, seg_len, sym_dev, out_frame_stride,
                         stream, priors_dev, priors_dev ? 256 : 0);
+}
+
+// ---- version 3: prior classes (consecutive runs of segments share a prior row) ----
+static int check_classes(int32_t nclass, const void *priors_dev)
+{
+    if (nclass < 1 || nclass > kMaxClasses) return set_error(VCF_ERR_INVALID, "nclass %d (1 .. %d)", nclass, kMaxClasses);
+    if (priors_dev && (reinterpret_cast<uintptr_t>(priors_dev) & 7))
+        return set_error(VCF_ERR_INVALID, "priors_dev not 8-byte aligned");
+    return VCF_OK;
+}
+
+int vcf_cbaac_tiled_prior_classes(const uint8_t *sym_dev, int64_t n_frames, int64_t frame_symbols,
+                                  int64_t frame_stride, int64_t seg_len, int32_t nclass, uint16_t *priors_dev,
+                                  uint32_t *hist_dev, void *stream)
+{
+    if (int s = check_args(frame_symbols, 0, seg_len)) return s;
+    if (int s = check_classes(nclass, priors_dev)) return s;
+    if (n_frames < 1 || n_frames > 65535) return set_error(VCF_ERR_INVALID, "n_frames %lld (1 .. 65535)", (long long)n_frames);
+    if (!priors_dev || !hist_dev || (frame_symbols > 0 && !sym_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t rows = n_frames * nclass;
+    if (int s = hip_check(hipMemsetAsync(hist_dev, 0, 256 * sizeof(uint32_t) * rows, st), "hipMemsetAsync")) return s;
+    const int64_t ns = vcf_cbaac_tiled_segments(frame_symbols, seg_len);
+    if (ns > 0x7FFFFFFF) return set_error(VCF_ERR_INVALID, "too many segments");
+    if (ns > 0) {
+        cbaac_hist_classes_kernel<<<dim3((unsigned)ns, (unsigned)n_frames), 256, 0, st>>>(sym_dev, frame_symbols, seg_len,
+                                                                                          nclass, hist_dev, frame_stride);
+        if (int s = hip_check(hipGetLastError(), "cbaac_hist_classes_kernel")) return s;
+    }
+    cbaac_prior_classes_kernel<<<(unsigned)rows, 256, 0, st>>>(hist_dev, priors_dev);
+    return hip_check(hipGetLastError(), "cbaac_prior_classes_kernel");
+}
+
+int vcf_cbaac_tiled_encode_classes(const uint8_t *sym_dev, int64_t n_frames, int64_t frame_symbols,
+                                   int64_t frame_stride, int32_t order, const uint16_t *priors_dev, int32_t nclass,
+                                   int64_t seg_len, uint8_t *out_dev, int64_t out_frame_capacity,
+                                   int64_t *seg_bytes_dev, void *ws_dev, void *stream)
+{
+    if (int s = check_classes(nclass, priors_dev)) return s;
+    if (out_frame_capacity < 0) return set_error(VCF_ERR_INVALID, "negative capacity");
+    if (frame_symbols > 0 && (!out_dev || !priors_dev)) return set_error(VCF_ERR_INVALID, "null buffer");
+    return tiled_encode(sym_dev, n_frames, frame_symbols, frame_stride, order, seg_len, out_dev, out_frame_capacity,
+                        seg_bytes_dev, nullptr, ws_dev, stream, priors_dev, 256LL * nclass, nclass);
+}
+
+int vcf_cbaac_tiled_decode_classes(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n_frames,
+                                   int64_t frame_symbols, int32_t order, const uint16_t *priors_dev, int32_t nclass,
+                                   int64_t seg_len, uint8_t *sym_dev, int64_t out_frame_stride, void *stream)
+{
+    if (int s = check_classes(nclass, priors_dev)) return s;
+    if (frame_symbols > 0 && !priors_dev) return set_error(VCF_ERR_INVALID, "null prior");
+    return tiled_decode(in_dev, seg_offsets_dev, n_frames, frame_symbols, order, seg_len, sym_dev, out_frame_stride,
+                        stream, priors_dev, 256LL * nclass, nclass);
 }
 
 }  // extern "C"

@@ -22,6 +22,16 @@ n_segments, 256 uint16 prior frequencies f[s] = 1 + floor(hist[s] * 8192 / n)
 of the frame's symbols, before the segment sizes: every model of every
 segment (order 1: all 256 contexts) starts from them instead of 256 ones and adapts by the reference's rules, so short
 segments (many waves per frame) stop paying the model's learning cost.
+Version 3 (`nclass` > 1 prior classes; not in the reference): segment s of
+the frame's n_segments takes prior row floor(s * nclass / n_segments), row c
+built like version 2's over the symbols of class c's segments; after
+n_segments come uint32 nclass and per class a sparse row -- uint16 m, the m
+symbols whose frequency is not 1 (uint8 each), their m frequencies (uint16) --
+and the segment sizes as unsigned LEB128 varints (a 4096-symbol segment of DCT
+indices is ~20 bytes: a uint32 index would cost +4.8 % of the stream).
+With the DCT's subband layout and nclass = 8 a row is about one subband row,
+whose statistics differ the most: 4096-symbol segments (1519 waves for a 1080p
+frame) then cost about the serial stream's rate.
 decompress() of a malformed header returns zeros((10, 10)) like
 CBAAC.py:101-102.
 """
@@ -40,8 +50,11 @@ FILE_EXTENSION = ".tadpt_arith"
 MAGIC = b"VCFT"
 VERSION = 1
 VERSION_PRIOR = 2
+VERSION_CLASSES = 3
 DEFAULT_SEG = 1 << 17     # 48 segments for a 1080p frame, 190 for 4K
 PRIOR_SEG = 1 << 15       # version 2: 190 segments for 1080p at +2.3 % rate (profiles/r02_tcbaac_prior.jsonl)
+CLASS_SEG = 1 << 12       # version 3 (-c TCBAACP): 1519 segments for 1080p
+PRIOR_CLASSES = 8         # version 3's prior rows per frame (the 8 subband rows of the 8x8 DCT)
 
 
 def n_segments(n: int, seg_len: int = DEFAULT_SEG) -> int:
@@ -71,10 +84,13 @@ class TiledCoder:
     never interleave with another thread's on the same buffers."""
 
     def __init__(self, order: int = 0, seg_len: int = DEFAULT_SEG, stream: Stream | None = None,
-                 prior: bool = False):
+                 prior: bool = False, nclass: int = 1):
         self.order, self.seg_len, self.prior = int(order), int(seg_len), bool(prior)
+        self.nclass = int(nclass)
         if self.prior and self.order > 1:
             raise NotImplementedError("prior-seeded tiled CBAAC: orders 0 and 1")
+        if self.nclass < 1 or (self.nclass > 1 and not self.prior):
+            raise ValueError("prior classes need prior=True")
         self.stream = stream if stream is not None else Stream()
         self.scratch = _Scratch()
         self.last_prior = None     # the prior table of the last encode (prior=True)
@@ -94,7 +110,16 @@ class TiledCoder:
         cap = int(lib.vcf_cbaac_tiled_bound(n, self.seg_len))
         out = self.scratch.get("out", cap)
         sb = self.scratch.get("sizes", 8 * (ns + 1))
-        if self.prior:
+        if self.prior and self.nclass > 1:
+            K = self.nclass
+            pr, hist = self.scratch.get("prior", 512 * K), self.scratch.get("hist", 1024 * K)
+            L.call("vcf_cbaac_tiled_prior_classes", sym.address(offset), 1, int(n), int(n), self.seg_len, K, pr.ptr,
+                   hist.ptr, self.stream.handle)
+            L.call("vcf_cbaac_tiled_encode_classes", sym.address(offset), 1, int(n), int(n), self.order, pr.ptr, K,
+                   self.seg_len, out.ptr, cap, sb.ptr, ws.ptr, self.stream.handle)
+            self.last_prior = np.empty((K, 256), np.uint16)
+            pr.download(self.last_prior, self.stream)
+        elif self.prior:
             pr, hist = self.scratch.get("prior", 512), self.scratch.get("hist", 1024)
             L.call("vcf_cbaac_tiled_prior", sym.address(offset), int(n), pr.ptr, hist.ptr, self.stream.handle)
             L.call("vcf_cbaac_tiled_encode_prior", sym.address(offset), int(n), self.order, pr.ptr, self.seg_len,
@@ -164,7 +189,13 @@ class TiledCoder:
             src.upload(np.frombuffer(payload, np.uint8), self.stream)
         ob = self.scratch.get("offs", offs.nbytes)
         ob.upload(offs, self.stream)
-        if prior is not None:
+        if prior is not None and np.ndim(prior) == 2:   # version 3: prior classes
+            prior = check_prior(prior)
+            pr = self.scratch.get("prior_in", prior.nbytes)
+            pr.upload(prior, self.stream)
+            L.call("vcf_cbaac_tiled_decode_classes", src.ptr, ob.ptr, 1, int(n), self.order, pr.ptr, prior.shape[0],
+                   self.seg_len, out.ptr, int(n), self.stream.handle)
+        elif prior is not None:
             prior = check_prior(prior)
             pr = self.scratch.get("prior_in", 512)
             pr.upload(prior, self.stream)
@@ -186,10 +217,13 @@ class TiledCoder:
 
 
 def check_prior(prior) -> np.ndarray:
-    """256 uint16 frequencies, each >= 1, total below the model's max_freq
-    (so the packed 16-bit cumulative counts of the GPU model cannot overflow)."""
+    """256 uint16 frequencies (or nclass rows of them), each >= 1, every row's
+    total below the model's max_freq (so the packed 16-bit cumulative counts
+    of the GPU model cannot overflow)."""
     prior = np.ascontiguousarray(prior, np.uint16)
-    if prior.shape != (256,) or int(prior.min()) < 1 or int(prior.sum(dtype=np.int64)) >= 16384:
+    rows = prior.reshape(-1, 256) if prior.ndim in (1, 2) and prior.shape[-1] == 256 else None
+    if (rows is None or not 1 <= rows.shape[0] <= 256 or int(prior.min()) < 1
+            or int(rows.sum(axis=1, dtype=np.int64).max()) >= 16384):
         raise ValueError("bad prior table")
     return prior
 
@@ -207,12 +241,15 @@ class FrameBatch:
     the code-streams."""
 
     def __init__(self, n_frames: int, frame_symbols: int, order: int = 0, seg_len: int = PRIOR_SEG,
-                 prior: bool = True, streams: int | None = None):
+                 prior: bool = True, streams: int | None = None, nclass: int = 1):
         lib = L.lib()
         self.n_frames, self.n = int(n_frames), int(frame_symbols)
         self.order, self.seg_len, self.prior = int(order), int(seg_len), bool(prior)
+        self.nclass = int(nclass)
         if self.prior and self.order > 1:
             raise NotImplementedError("prior-seeded tiled CBAAC: orders 0 and 1")
+        if self.nclass < 1 or (self.nclass > 1 and not self.prior):
+            raise ValueError("prior classes need prior=True")
         self.ns = n_segments(self.n, self.seg_len)
         self.cap = int(lib.vcf_cbaac_tiled_bound(self.n, self.seg_len))
         self.stream = Stream()
@@ -220,8 +257,8 @@ class FrameBatch:
         self.ws = DeviceBuffer(max(int(lib.vcf_cbaac_tiled_frames_workspace(nf, self.n, self.seg_len)), 1))
         self.out = DeviceBuffer(max(self.cap * nf, 1))
         self.sizes_dev = DeviceBuffer(8 * (self.ns + 1) * nf)
-        self.prior_dev = DeviceBuffer(512 * nf)
-        self.hist = DeviceBuffer(1024 * nf)
+        self.prior_dev = DeviceBuffer(512 * nf * self.nclass)
+        self.hist = DeviceBuffer(1024 * nf * self.nclass)
         self._sizes = None
         self._priors = None
 
@@ -241,6 +278,13 @@ class FrameBatch:
         stride = self.n if frame_stride is None else int(frame_stride)
         base = sym.address(offset)
         h = self.stream.handle
+        if self.nclass > 1:
+            L.call("vcf_cbaac_tiled_prior_classes", base, self.n_frames, self.n, stride, self.seg_len, self.nclass,
+                   self.prior_dev.ptr, self.hist.ptr, h)
+            L.call("vcf_cbaac_tiled_encode_classes", base, self.n_frames, self.n, stride, self.order,
+                   self.prior_dev.ptr, self.nclass, self.seg_len, self.out.ptr, self.cap, self.sizes_dev.ptr,
+                   self.ws.ptr, h)
+            return
         if self.prior:
             L.call("vcf_cbaac_tiled_prior_frames", base, self.n_frames, self.n, stride, self.prior_dev.ptr,
                    self.hist.ptr, h)
@@ -264,7 +308,8 @@ class FrameBatch:
             if self.n_frames:
                 self.sizes_dev.download(allz, self.stream)
                 if self.prior:
-                    self._priors = np.empty((self.n_frames, 256), np.uint16)
+                    shp = (self.n_frames, self.nclass, 256) if self.nclass > 1 else (self.n_frames, 256)
+                    self._priors = np.empty(shp, np.uint16)
                     self.prior_dev.download(self._priors, self.stream)
             self.stream.synchronize()
             self._sizes = allz
@@ -294,7 +339,7 @@ class FrameBatch:
 
 def encode_frames_device(sym: DeviceBuffer, n_frames: int, frame_symbols: int, order: int = 0,
                          seg_len: int = DEFAULT_SEG, prior: bool = False, streams: int = 4,
-                         after: Stream | None = None, offset: int = 0):
+                         after: Stream | None = None, offset: int = 0, nclass: int = 1):
     """Several frames' symbols, back to back in HBM from `offset`, each coded
     as its own tiled stream (its own prior with prior=True), all of them in
     one launch per stage (FrameBatch; `streams` is accepted for the earlier
@@ -302,16 +347,77 @@ def encode_frames_device(sym: DeviceBuffer, n_frames: int, frame_symbols: int, o
     (e.g. the DCT encode's); the coder waits for its work so far (an event),
     so the caller need not synchronise it first.
     -> [(segment byte counts, payload, prior or None)]."""
-    fb = FrameBatch(n_frames, frame_symbols, order, seg_len, prior)
+    fb = FrameBatch(n_frames, frame_symbols, order, seg_len, prior, nclass=nclass)
     fb.launch(sym, offset, after)
     return fb.download()
 
 
+def _varints(v: np.ndarray) -> bytes:
+    """Unsigned LEB128 of every value (vectorised): 7 bits per byte, high bit = more."""
+    v = np.asarray(v, np.uint64)
+    cnt = np.ones(v.size, np.int64)
+    for k in range(1, 5):
+        cnt += v >= (np.uint64(1) << np.uint64(7 * k))
+    cols = np.arange(5)
+    b = ((v[:, None] >> (np.uint64(7) * cols.astype(np.uint64))) & np.uint64(0x7F)).astype(np.uint8)
+    b |= ((cols[None, :] < cnt[:, None] - 1) * 0x80).astype(np.uint8)
+    return b[cols[None, :] < cnt[:, None]].tobytes()
+
+
+def _parse_varints(data: bytes, p: int, count: int):
+    """-> (count values, the offset after them); ValueError if the data end first."""
+    if count == 0:
+        return np.zeros(0, np.int64), p
+    raw = np.frombuffer(data, np.uint8, min(len(data) - p, 5 * count), p)
+    ends = np.flatnonzero(raw < 0x80)
+    if ends.size < count:
+        raise ValueError("segment index")
+    stop = int(ends[count - 1]) + 1
+    raw = raw[:stop].astype(np.uint64)
+    grp = np.concatenate([[0], np.cumsum(raw[:-1] < 0x80)])
+    start = np.concatenate([[0], ends[:count - 1] + 1])
+    pos = np.arange(stop) - start[grp]
+    if int(pos.max()) > 4:
+        raise ValueError("segment index")
+    vals = np.zeros(count, np.uint64)
+    np.add.at(vals, grp, (raw & np.uint64(0x7F)) << (np.uint64(7) * pos.astype(np.uint64)))
+    return vals.astype(np.int64), p + stop
+
+
+def _sparse_rows(prior: np.ndarray) -> bytes:
+    """Version 3's prior rows: per row uint16 m, m uint8 symbols, m uint16 frequencies (those != 1)."""
+    out = [struct.pack("<I", prior.shape[0])]
+    for row in prior:
+        sy = np.flatnonzero(row != 1).astype(np.uint8)
+        out += [struct.pack("<H", sy.size), sy.tobytes(), row[sy].astype("<u2").tobytes()]
+    return b"".join(out)
+
+
+def _parse_sparse_rows(data: bytes, p: int):
+    (K,) = struct.unpack_from("<I", data, p)
+    if not 1 <= K <= 256:
+        raise ValueError(f"{K} prior classes")
+    p += 4
+    prior = np.ones((K, 256), np.uint16)
+    for c in range(K):
+        (m,) = struct.unpack_from("<H", data, p)
+        if m > 256 or p + 2 + 3 * m > len(data):
+            raise ValueError("prior row")
+        sy = np.frombuffer(data, np.uint8, m, p + 2)
+        prior[c, sy] = np.frombuffer(data, "<u2", m, p + 2 + m)
+        p += 2 + 3 * m
+    return check_prior(prior), p
+
+
 def pack(shape, order: int, seg_len: int, seg_bytes, payload: bytes, prior=None) -> bytes:
+    """The container: version 1 (prior None), 2 (one 256-entry prior) or 3 (nclass x 256 priors)."""
     seg_bytes = np.asarray(seg_bytes, np.int64)
     head = np.array([len(shape), *shape], np.uint32).tobytes()
-    version = VERSION if prior is None else VERSION_PRIOR
+    classes = prior is not None and np.ndim(prior) == 2
+    version = VERSION if prior is None else (VERSION_CLASSES if classes else VERSION_PRIOR)
     head += MAGIC + struct.pack("<IIII", version, order, seg_len, seg_bytes.size)
+    if classes:   # version 3: sparse prior rows, the segment sizes as LEB128 varints
+        return head + _sparse_rows(check_prior(prior)) + _varints(seg_bytes) + payload
     if prior is not None:
         head += check_prior(prior).astype("<u2").tobytes()
     head += seg_bytes.astype(np.uint32).tobytes()
@@ -333,7 +439,7 @@ def _parse(data: bytes):
     if data[p:p + 4] != MAGIC:
         raise ValueError("not a tiled CBAAC stream")
     version, order, seg_len, ns = struct.unpack_from("<IIII", data, p + 4)
-    if version not in (VERSION, VERSION_PRIOR):
+    if version not in (VERSION, VERSION_PRIOR, VERSION_CLASSES):
         raise ValueError(f"version {version}")
     if order > 1:                       # the GPU coder's orders (both versions)
         raise ValueError(f"order {order}")
@@ -344,8 +450,12 @@ def _parse(data: bytes):
     if version == VERSION_PRIOR:
         prior = check_prior(np.frombuffer(data, "<u2", 256, p))
         p += 512
-    seg_bytes = np.frombuffer(data, np.uint32, ns, p).astype(np.int64)
-    p += 4 * ns
+    if version == VERSION_CLASSES:
+        prior, p = _parse_sparse_rows(data, p)
+        seg_bytes, p = _parse_varints(data, p, ns)
+    else:
+        seg_bytes = np.frombuffer(data, np.uint32, ns, p).astype(np.int64)
+        p += 4 * ns
     payload = data[p:]
     n = int(np.prod(shape)) if nd else 1
     if n_segments(n, seg_len) != ns or int(seg_bytes.sum()) != len(payload):
@@ -359,10 +469,11 @@ class TiledCBAACCodec:
 
     file_extension = FILE_EXTENSION
 
-    def __init__(self, order: int = 0, seg_len: int = DEFAULT_SEG, prior: bool = False):
+    def __init__(self, order: int = 0, seg_len: int = DEFAULT_SEG, prior: bool = False, nclass: int = 1):
         self.ORDER = int(order)
         self.seg_len = int(seg_len)
         self.prior = bool(prior)
+        self.nclass = int(nclass)
         self._coder = None
         self._make = threading.Lock()
 
@@ -370,7 +481,7 @@ class TiledCBAACCodec:
     def coder(self) -> TiledCoder:
         with self._make:
             if self._coder is None:
-                self._coder = TiledCoder(self.ORDER, self.seg_len, prior=self.prior)
+                self._coder = TiledCoder(self.ORDER, self.seg_len, prior=self.prior, nclass=self.nclass)
             return self._coder
 
     def compress(self, img: np.ndarray, fn=None) -> io.BytesIO:
@@ -419,29 +530,44 @@ def host_segments(sym: np.ndarray, order: int = 0, seg_len: int = DEFAULT_SEG):
     return [encode_symbols(sym[i:i + seg_len], order) for i in range(0, sym.size, seg_len)]
 
 
-def prior_of(sym: np.ndarray) -> np.ndarray:
-    """The version-2 prior of a frame's symbols, on the host (what
-    vcf_cbaac_tiled_prior computes on the GPU)."""
+def prior_of(sym: np.ndarray, nclass: int = 1, seg_len: int | None = None) -> np.ndarray:
+    """The version-2 prior of a frame's symbols (nclass = 1), or version 3's
+    nclass rows for segments of seg_len, on the host (what
+    vcf_cbaac_tiled_prior / _prior_classes compute on the GPU)."""
     sym = np.ascontiguousarray(sym, np.uint8).ravel()
-    hist = np.bincount(sym, minlength=256).astype(np.uint64)
-    n = max(sym.size, 1)
-    return (1 + hist * 8192 // n).astype(np.uint16)
+    if nclass == 1:
+        hist = np.bincount(sym, minlength=256).astype(np.uint64)
+        n = max(sym.size, 1)
+        return (1 + hist * 8192 // n).astype(np.uint16)
+    ns = n_segments(sym.size, seg_len)
+    rows = np.ones((nclass, 256), np.uint16)
+    for c in range(nclass):
+        segs = [s for s in range(ns) if s * nclass // ns == c]
+        if not segs:
+            continue
+        part = sym[segs[0] * seg_len:(segs[-1] + 1) * seg_len]
+        hist = np.bincount(part, minlength=256).astype(np.uint64)
+        rows[c] = (1 + hist * 8192 // max(part.size, 1)).astype(np.uint16)
+    return rows
 
 
 def host_segments_prior(sym: np.ndarray, prior, seg_len: int = DEFAULT_SEG, order: int = 0):
     """vcf_cbaac_encode_prior on every segment: what each segment of a
-    version-2 stream must equal."""
+    version-2 stream (one prior) or version-3 stream (prior rows: segment s of
+    ns takes row s * nclass // ns) must equal."""
     import ctypes
     prior = check_prior(prior)
     sym = np.ascontiguousarray(sym, np.uint8).ravel()
     lib = L.lib()
     res = []
+    ns = n_segments(sym.size, seg_len)
     for i in range(0, sym.size, seg_len):
         seg = np.ascontiguousarray(sym[i:i + seg_len])
+        row = np.ascontiguousarray(prior[(i // seg_len) * prior.shape[0] // ns]) if prior.ndim == 2 else prior
         cap = int(lib.vcf_cbaac_bound(seg.size))
         out = np.empty(cap, np.uint8)
         nb, bits = ctypes.c_int64(), ctypes.c_int64()
-        L.call("vcf_cbaac_encode_prior", seg.ctypes.data, seg.size, order, prior.ctypes.data, out.ctypes.data, cap,
+        L.call("vcf_cbaac_encode_prior", seg.ctypes.data, seg.size, order, row.ctypes.data, out.ctypes.data, cap,
                ctypes.byref(nb), ctypes.byref(bits))
         res.append(out[:nb.value].tobytes())
     return res
