@@ -356,6 +356,15 @@ int vcf_cbaac_tiled_encode_classes(const uint8_t *sym_dev, int64_t n_frames, int
 int vcf_cbaac_tiled_decode_classes(const uint8_t *in_dev, const int64_t *seg_offsets_dev, int64_t n_frames,
                                    int64_t frame_symbols, int32_t order, const uint16_t *priors_dev, int32_t nclass,
                                    int64_t seg_len, uint8_t *sym_dev, int64_t out_frame_stride, void *stream);
+/* host: version 3's container pieces for a batch of frames -- the segment
+ * sizes of each row as unsigned LEB128 varints (row r's bytes end at
+ * out[row_end[r]]), and each frame's nclass prior rows stored sparsely
+ * (uint32 nclass; per row uint16 m, the m symbols with a frequency != 1, their
+ * m uint16 frequencies; frame f's bytes end at out[frame_end[f]]). */
+int vcf_leb128_encode_rows(const int64_t *v, int64_t rows, int64_t cols, uint8_t *out, int64_t capacity,
+                           int64_t *row_end);
+int vcf_prior_rows_sparse(const uint16_t *priors, int64_t frames, int32_t nclass, uint8_t *out, int64_t capacity,
+                          int64_t *frame_end);
 /* host, orders 0 / 1: vcf_cbaac_encode / _decode with every model seeded by prior (256 uint16, each >= 1) */
 int vcf_cbaac_encode_prior(const uint8_t *symbols, int64_t n, int32_t order, const uint16_t *prior, uint8_t *out,
                            int64_t out_capacity, int64_t *out_bytes, int64_t *out_bits);

@@ -103,7 +103,7 @@ def test_zero_frames_and_errors():
     with pytest.raises(ValueError):
         D.encode(np.zeros((8, 8), np.uint8))
     with pytest.raises(NotImplementedError):
-        D.encode(np.zeros((16, 16, 3), np.uint8), 32, block_size=191)   # a Bluestein length
+        D.encode(np.zeros((16, 16, 3), np.uint8), 32, block_size=4097)   # beyond the run-time path
     with pytest.raises(ValueError):
         D.decode(np.zeros((8, 8, 3), np.uint8), 8, 8, 40000)
 

@@ -147,6 +147,8 @@ SIGNATURES = {
     "vcf_cbaac_tiled_decode_prior": [_P, _P, _I64, _I32, _P, _I64, _P, _P],
     "vcf_cbaac_encode_prior": [_P, _I64, _I32, _P, _P, _I64, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     "vcf_cbaac_decode_prior": [_P, _I64, _I64, _I32, _P, _P],
+    "vcf_leb128_encode_rows": [_P, _I64, _I64, _P, _I64, _P],
+    "vcf_prior_rows_sparse": [_P, _I64, _I32, _P, _I64, _P],
     "vcf_comm_unique_id": [_P, _SZ],
     "vcf_comm_init": [ctypes.POINTER(_P), _P, ctypes.c_int, ctypes.c_int],
     "vcf_comm_init_timeout": [ctypes.POINTER(_P), _P, ctypes.c_int, ctypes.c_int, _I64],

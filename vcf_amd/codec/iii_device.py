@@ -86,7 +86,7 @@ class DeviceIII:
             self.batch.launch(self.k, after=self.stream)
         seg, totals, priors = self.batch.sizes()          # waits for the coder
         t = mark("entropy", t)
-        headers = [self.batch.header(f, self.shape) for f in range(self.n_local)]
+        headers = self.batch.headers(self.shape)
         local_sizes = np.array([len(h) + int(totals[f]) for f, h in enumerate(headers)], np.int64)
         nbytes = int(local_sizes.sum())
         send = self._buf("send", nbytes)

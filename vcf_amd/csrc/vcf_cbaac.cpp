@@ -326,4 +326,61 @@ int vcf_cbaac_model_trace(const uint8_t *symbols, int64_t n, int32_t order, int3
     return VCF_OK;
 }
 
+/* Container version 3 index pieces (vcf_amd/tcbaac.py), per row of values:
+ * the segment sizes as unsigned LEB128 varints, row r's bytes ending at
+ * out[row_end[r]]. */
+int vcf_leb128_encode_rows(const int64_t *v, int64_t rows, int64_t cols, uint8_t *out, int64_t capacity,
+                           int64_t *row_end)
+{
+    if (rows < 0 || cols < 0 || capacity < 0) return set_error(VCF_ERR_INVALID, "negative size");
+    if ((rows * cols > 0 && (!v || !out)) || (rows > 0 && !row_end)) return set_error(VCF_ERR_INVALID, "null buffer");
+    int64_t o = 0;
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int64_t c = 0; c < cols; ++c) {
+            uint64_t x = (uint64_t)v[r * cols + c];
+            if (v[r * cols + c] < 0) return set_error(VCF_ERR_INVALID, "negative value");
+            do {
+                if (o >= capacity) return set_error(VCF_ERR_INVALID, "output buffer too small");
+                const uint8_t b = (uint8_t)(x & 0x7F);
+                x >>= 7;
+                out[o++] = x ? (uint8_t)(b | 0x80) : b;
+            } while (x);
+        }
+        row_end[r] = o;
+    }
+    return VCF_OK;
+}
+
+/* Version 3's prior rows of `frames` frames (nclass x 256 uint16 each): per
+ * frame uint32 nclass, then per row uint16 m and the m symbols whose
+ * frequency is not 1 (uint8, ascending) and their m frequencies (uint16);
+ * frame f's bytes end at out[frame_end[f]]. */
+int vcf_prior_rows_sparse(const uint16_t *priors, int64_t frames, int32_t nclass, uint8_t *out, int64_t capacity,
+                          int64_t *frame_end)
+{
+    if (frames < 0 || nclass < 1 || capacity < 0) return set_error(VCF_ERR_INVALID, "bad size");
+    if (frames > 0 && (!priors || !out || !frame_end)) return set_error(VCF_ERR_INVALID, "null buffer");
+    int64_t o = 0;
+    auto put = [&](uint32_t v, int nb) -> bool {
+        if (o + nb > capacity) return false;
+        for (int i = 0; i < nb; ++i) out[o++] = (uint8_t)(v >> (8 * i));
+        return true;
+    };
+    for (int64_t f = 0; f < frames; ++f) {
+        if (!put((uint32_t)nclass, 4)) return set_error(VCF_ERR_INVALID, "output buffer too small");
+        for (int32_t c = 0; c < nclass; ++c) {
+            const uint16_t *row = priors + (f * nclass + c) * 256;
+            uint32_t m = 0;
+            for (int s = 0; s < 256; ++s) m += row[s] != 1;
+            if (!put(m, 2)) return set_error(VCF_ERR_INVALID, "output buffer too small");
+            for (int s = 0; s < 256; ++s)
+                if (row[s] != 1 && !put((uint32_t)s, 1)) return set_error(VCF_ERR_INVALID, "output buffer too small");
+            for (int s = 0; s < 256; ++s)
+                if (row[s] != 1 && !put(row[s], 2)) return set_error(VCF_ERR_INVALID, "output buffer too small");
+        }
+        frame_end[f] = o;
+    }
+    return VCF_OK;
+}
+
 }  // extern "C"

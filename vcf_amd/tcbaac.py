@@ -325,6 +325,23 @@ class FrameBatch:
         seg, _, pri = self.sizes()
         return pack(tuple(shape), self.order, self.seg_len, seg[f], b"", None if pri is None else pri[f])
 
+    def headers(self, shape) -> list:
+        """Every frame's header (== header(f, shape)), built for the whole
+        batch at once: version 3's varint indexes and sparse prior rows as a
+        few array operations over all frames instead of a pack() per frame."""
+        seg, _, pri = self.sizes()
+        if pri is None or pri.ndim != 3:
+            return [self.header(f, shape) for f in range(self.n_frames)]
+        F, K = pri.shape[:2]
+        fixed = (np.array([len(shape), *shape], np.uint32).tobytes() + MAGIC +
+                 struct.pack("<IIII", VERSION_CLASSES, self.order, self.seg_len, self.ns))
+        check_prior(pri.reshape(-1, 256))
+        rb, rend = _sparse_rows_batch(pri)
+        vb, vend = _varints_rows(seg)
+        rst = np.concatenate([[0], rend[:-1]])
+        vst = np.concatenate([[0], vend[:-1]])
+        return [fixed + rb[rst[f]:rend[f]] + vb[vst[f]:vend[f]] for f in range(F)]
+
     def download(self):
         """-> [(segment byte counts, payload bytes, prior or None)] per frame."""
         seg, totals, pri = self.sizes()
@@ -352,16 +369,30 @@ def encode_frames_device(sym: DeviceBuffer, n_frames: int, frame_symbols: int, o
     return fb.download()
 
 
+def _varints_rows(v: np.ndarray):
+    """Unsigned LEB128 varints (7 bits per byte, high bit = more) of each row
+    of a 2-D array (vcf_leb128_encode_rows) -> (bytes, end offset of each row)."""
+    v = np.ascontiguousarray(v, np.int64)
+    out = np.empty(max(5 * v.size, 1), np.uint8)
+    ends = np.zeros(v.shape[0], np.int64)
+    L.call("vcf_leb128_encode_rows", v.ctypes.data, v.shape[0], v.shape[1], out.ctypes.data, out.size,
+           ends.ctypes.data)
+    return out[:int(ends[-1]) if ends.size else 0].tobytes(), ends
+
+
 def _varints(v: np.ndarray) -> bytes:
-    """Unsigned LEB128 of every value (vectorised): 7 bits per byte, high bit = more."""
-    v = np.asarray(v, np.uint64)
-    cnt = np.ones(v.size, np.int64)
-    for k in range(1, 5):
-        cnt += v >= (np.uint64(1) << np.uint64(7 * k))
-    cols = np.arange(5)
-    b = ((v[:, None] >> (np.uint64(7) * cols.astype(np.uint64))) & np.uint64(0x7F)).astype(np.uint8)
-    b |= ((cols[None, :] < cnt[:, None] - 1) * 0x80).astype(np.uint8)
-    return b[cols[None, :] < cnt[:, None]].tobytes()
+    return _varints_rows(np.asarray(v, np.int64).reshape(1, -1))[0]
+
+
+def _sparse_rows_batch(pri: np.ndarray):
+    """Version 3's sparse prior rows of every frame of an (F, K, 256) array
+    (vcf_prior_rows_sparse) -> (bytes, end offset of each frame)."""
+    pri = np.ascontiguousarray(pri, np.uint16)
+    F, K = pri.shape[:2]
+    out = np.empty(F * (4 + K * (2 + 3 * 256)), np.uint8)
+    ends = np.zeros(F, np.int64)
+    L.call("vcf_prior_rows_sparse", pri.ctypes.data, F, K, out.ctypes.data, out.size, ends.ctypes.data)
+    return out[:int(ends[-1]) if F else 0].tobytes(), ends
 
 
 def _parse_varints(data: bytes, p: int, count: int):
@@ -386,11 +417,7 @@ def _parse_varints(data: bytes, p: int, count: int):
 
 def _sparse_rows(prior: np.ndarray) -> bytes:
     """Version 3's prior rows: per row uint16 m, m uint8 symbols, m uint16 frequencies (those != 1)."""
-    out = [struct.pack("<I", prior.shape[0])]
-    for row in prior:
-        sy = np.flatnonzero(row != 1).astype(np.uint8)
-        out += [struct.pack("<H", sy.size), sy.tobytes(), row[sy].astype("<u2").tobytes()]
-    return b"".join(out)
+    return _sparse_rows_batch(np.asarray(prior)[None])[0]
 
 
 def _parse_sparse_rows(data: bytes, p: int):
