@@ -175,7 +175,7 @@ def test_device_iii_single_rank_rccl():
     stages = {}
     sizes, got = job.run(rgb, stages)
     assert set(stages) == {"dct_dz", "entropy", "pack", "sizes_allgather", "gatherv", "d2h_rank0"}
-    codec = T.TiledCBAACCodec(order=0, seg_len=1024, prior=True)
+    codec = T.TiledCBAACCodec(order=0, seg_len=1024, prior=True, nclass=T.PRIOR_CLASSES)   # DeviceIII default
     for i, f in enumerate(frames):
         k = O.encode_frame(f, 32, 0)
         want = codec.compress(k).getvalue()

@@ -439,3 +439,20 @@ def test_tcbaacp_codec_is_version_3(tmp_path):
     assert np.array_equal(codec.decompress(data), k)
     v2 = T.TiledCBAACCodec(0, 8192, prior=True).compress(k).getvalue()
     assert np.array_equal(codec.decompress(v2), k)
+
+
+def test_frame_batch_headers_equal_pack():
+    """FrameBatch.headers (the whole batch's version-3 headers from two native
+    calls) equals pack() of every frame, and header + payload decodes."""
+    from vcf_amd.device import DeviceBuffer
+    rng = np.random.Generator(np.random.PCG64(8))
+    shape, F = (16, 40, 3), 6
+    n = int(np.prod(shape))
+    frames = np.clip(np.rint(rng.laplace(128, 2.0, (F, n))), 0, 255).astype(np.uint8)
+    fb = T.FrameBatch(F, n, 0, 256, prior=True, nclass=3)
+    fb.launch(DeviceBuffer.from_array(frames))
+    heads = fb.headers(shape)
+    got = fb.download()
+    for f in range(F):
+        assert heads[f] == fb.header(f, shape) == T.pack(shape, 0, 256, got[f][0], b"", got[f][2]), f
+        assert np.array_equal(T.TiledCBAACCodec(0, 256).decompress(heads[f] + got[f][1]), frames[f].reshape(shape))
