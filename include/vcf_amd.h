@@ -412,6 +412,24 @@ int vcf_png_encode_rgb(const uint8_t *rgb, int32_t H, int32_t W, int32_t level, 
                        int64_t out_capacity, int64_t *out_bytes);
 int64_t vcf_png_encode_bound(int32_t H, int32_t W);
 
+/* ---- TIFF strip deflate on the GPU (TIFF.py:23-31, the default -c) ----------
+ * zlib.compress(strip, level) for every strip of a batch of frames, byte for
+ * byte (zlib 1.2.11 deflate_slow, windowBits 15, memLevel 8): what
+ * tifffile.imwrite(..., compression='zlib') stores per RowsPerStrip strip
+ * (TIFF.py:29; host path vcf_amd/codec/tiff.py _deflate_strips).  Frame f is
+ * in_dev[f*frame_bytes, (f+1)*frame_bytes), cut into strips of strip_bytes
+ * (the last one shorter); strip s = f*spf + k, spf = vcf_zlib_strip_count,
+ * is written to out_dev + s*slot_bytes and its length to sizes_dev[s]
+ * (-1: slot too small).  level 4..9 (VCF_ERR_UNSUPPORTED otherwise);
+ * strip_bytes <= 65536 (tifffile's strips for rows up to 64 KB);
+ * slot_bytes a multiple of 4 >= vcf_zlib_bound(strip_bytes); ws_dev holds
+ * vcf_zlib_workspace(total strips) bytes.  All pointers 4-byte aligned. */
+int64_t vcf_zlib_bound(int64_t strip_bytes);
+int64_t vcf_zlib_workspace(int64_t n_strips);
+int64_t vcf_zlib_strip_count(int64_t frame_bytes, int32_t strip_bytes);
+int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes, int32_t strip_bytes, int32_t level,
+                    uint8_t *out_dev, int64_t slot_bytes, int32_t *sizes_dev, void *ws_dev, void *stream);
+
 /* ---- deadzone quantizer plug-in (deadzone.py:95-117, assumption A5) ---------- */
 
 /* k[i] = (int32)(x[i] / Q), truncation toward zero; the division is float32

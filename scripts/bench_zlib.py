@@ -1,0 +1,85 @@
+"""TIFF strip deflate (TIFF.py:29: tifffile -> zlib level 6 per ~64 KB strip):
+GPU vcf_zlib_strips vs the host path (system zlib on a thread pool), on the
+index frames the DCT encode leaves in HBM (1080p and 4K, S-smooth content, Q=32)
+and on raw RGB frames.  Every GPU strip is checked against zlib.compress.
+Prints one JSON line per workload."""
+import argparse
+import json
+import os
+import sys
+import time
+import zlib
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--threads", type=int, default=16)
+    args = ap.parse_args()
+    from bench import synth_frame
+    from vcf_amd import _lib as L
+    from vcf_amd import dct
+    from vcf_amd.codec.tiff import strip_layout
+    from vcf_amd.device import DeviceBuffer, Event, Stream
+    st = Stream()
+    for name, (H, W), kind in [("dct_1080p", (1080, 1920), "dct"), ("dct_4k", (2160, 3840), "dct"),
+                               ("rgb_1080p", (1080, 1920), "rgb")]:
+        n = args.frames if H == 1080 else max(1, args.frames // 4)
+        base = np.stack([synth_frame(H, W, s) for s in range(4)])
+        frames = base[np.arange(n) % 4]
+        if kind == "dct":
+            frames = np.concatenate([dct.encode(frames[i:i + 16], Q=32) for i in range(0, n, 16)])
+        flat = np.ascontiguousarray(frames.reshape(n, -1))
+        fb = flat.shape[1]
+        _, _, sb = strip_layout(frames.shape[1:], 1)
+        spf = int(L.lib().vcf_zlib_strip_count(fb, sb))
+        total = spf * n
+        slot = int(L.lib().vcf_zlib_bound(sb))
+        d = DeviceBuffer.from_array(flat)
+        out = DeviceBuffer(total * slot)
+        sizes = DeviceBuffer(total * 4)
+        ws = DeviceBuffer(int(L.lib().vcf_zlib_workspace(total)))
+        e0, e1 = Event(), Event()
+        ms = []
+        for r in range(args.reps + 1):
+            e0.record(st)
+            L.call("vcf_zlib_strips", d.ptr, n, fb, sb, 6, out.ptr, slot, sizes.ptr, ws.ptr, st.handle)
+            e1.record(st)
+            st.synchronize()
+            if r:
+                ms.append(e0.elapsed_ms(e1))
+            print(f"{name} rep {r}: {e0.elapsed_ms(e1):.2f} ms", file=sys.stderr, flush=True)
+        sz = sizes.download(np.empty(total, np.int32))
+        slots = out.download(np.empty(total * slot, np.uint8))
+        # check every strip of frames 0 and n-1, and a sample elsewhere
+        chk = sorted(set(list(range(spf)) + list(range((n - 1) * spf, total)) + list(range(0, total, 37))))
+        ok = all(slots[s * slot:s * slot + sz[s]].tobytes() ==
+                 zlib.compress(flat[s // spf, (s % spf) * sb:(s % spf + 1) * sb].tobytes(), 6) for s in chk)
+        # host: zlib on a thread pool over the same strips
+        strips = [flat[f, k * sb:(k + 1) * sb] for f in range(n) for k in range(spf)]
+        with ThreadPoolExecutor(args.threads) as ex:
+            t = time.perf_counter()
+            comp = list(ex.map(lambda c: zlib.compress(c, 6), strips))
+            host_s = time.perf_counter() - t
+        gms = float(np.median(ms))
+        print(json.dumps({"workload": f"{name}: {n} frames, {total} strips of {sb} B, zlib level 6",
+                          "gpu_ms": round(gms, 3), "gpu_GBps": round(flat.nbytes / gms / 1e6, 2),
+                          "host_ms": round(host_s * 1e3, 2), "host_threads": args.threads,
+                          "host_GBps": round(flat.nbytes / host_s / 1e9, 3),
+                          "speedup": round(host_s * 1e3 / gms, 2),
+                          "ratio": round(flat.nbytes / max(1, int(sz.sum())), 2),
+                          "bytes_equal_zlib": bool(ok and sum(map(len, comp)) == int(sz.sum())),
+                          "strips_checked": len(chk)}), flush=True)
+        for b in (d, out, sizes, ws):
+            b.free()
+
+
+if __name__ == "__main__":
+    main()

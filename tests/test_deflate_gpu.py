@@ -1,0 +1,96 @@
+"""GPU TIFF strip deflate (vcf_zlib_strips, csrc/vcf_deflate.hip) against
+zlib.compress, byte for byte, and the TIFF files around the strips against the
+host writer (the reference's TIFF.py:29 via tifffile -> zlib level 6)."""
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(n, shape, seed, kind="image"):
+    rng = np.random.default_rng(seed)
+    out = []
+    for f in range(n):
+        if kind == "image":
+            H, W, C = shape
+            y = np.arange(H)[:, None, None]
+            x = np.arange(W)[None, :, None]
+            a = 128 + 60 * np.sin(x / (37 + f) + np.arange(C)) + 50 * np.cos(y / 23.0 - f) + rng.normal(0, 4, shape)
+            out.append(np.clip(a, 0, 255).astype(np.uint8))
+        elif kind == "random":
+            out.append(rng.integers(0, 256, shape, dtype=np.uint8))
+        else:   # DCT-index-like: mostly 128 with sparse values
+            a = np.full(shape, 128, np.uint8)
+            m = rng.random(shape) < 0.03
+            a[m] = rng.integers(100, 160, int(m.sum()))
+            out.append(a)
+    return np.stack(out)
+
+
+def _check(frames, strip_bytes, level=6):
+    from vcf_amd.device import DeviceBuffer
+    from vcf_amd.zlib_gpu import StripDeflater
+    n = frames.shape[0]
+    flat = frames.reshape(n, -1)
+    d = DeviceBuffer.from_array(flat)
+    got = StripDeflater().deflate_device(d, n, flat.shape[1], strip_bytes, level)
+    for f in range(n):
+        b = flat[f].tobytes()
+        want = [zlib.compress(b[i:i + strip_bytes], level) for i in range(0, len(b), strip_bytes)]
+        assert len(got[f]) == len(want)
+        for k, (g, w) in enumerate(zip(got[f], want)):
+            assert g == w, (f, k, len(g), len(w))
+
+
+@pytest.mark.parametrize("kind", ["image", "random", "sparse"])
+def test_strips_equal_zlib(kind):
+    _check(_frames(3, (40, 300, 3), 1, kind), 11 * 900)
+
+
+@pytest.mark.parametrize("strip", [65536, 65300, 65280, 65274, 1, 2, 3, 258, 4096])
+def test_strip_lengths(strip):
+    _check(_frames(2, (48, 700, 3), 2, "image"), strip)
+
+
+@pytest.mark.parametrize("level", [4, 5, 7, 8, 9])
+def test_levels(level):
+    _check(_frames(1, (30, 1000, 3), 3, "image"), 65536, level)
+
+
+def test_1080p_dct_frame_equals_host_tiff():
+    """A 1080p frame of DCT indices (the C2 path): the GPU TIFF equals the host writer's bytes."""
+    from bench import synth_frame
+    from vcf_amd.codec.tiff import imwrite_bytes
+    from vcf_amd.device import DeviceBuffer
+    from vcf_amd.zlib_gpu import tiff_frames_device
+    from vcf_amd import dct
+    rgb = np.stack([synth_frame(1080, 1920, s) for s in (1, 2)])
+    k = dct.encode(rgb, Q=32)
+    d = DeviceBuffer.from_array(np.ascontiguousarray(k))
+    files = tiff_frames_device(d, 2, k.shape[1:], np.uint8)
+    for f in range(2):
+        assert files[f] == imwrite_bytes(k[f])
+
+
+def test_u16_and_gray():
+    from vcf_amd.codec.tiff import imwrite_bytes
+    from vcf_amd.device import DeviceBuffer
+    from vcf_amd.zlib_gpu import tiff_frames_device
+    rng = np.random.default_rng(5)
+    a = (rng.integers(0, 600, (3, 70, 130, 3))).astype(np.uint16)
+    files = tiff_frames_device(DeviceBuffer.from_array(a), 3, a.shape[1:], np.uint16)
+    assert all(files[f] == imwrite_bytes(a[f]) for f in range(3))
+    g = rng.integers(120, 136, (2, 300, 333), dtype=np.uint8)
+    files = tiff_frames_device(DeviceBuffer.from_array(g), 2, g.shape[1:], np.uint8)
+    assert all(files[f] == imwrite_bytes(g[f]) for f in range(2))
+
+
+def test_unsupported():
+    from vcf_amd import _lib as L
+    from vcf_amd.device import DeviceBuffer
+    d = DeviceBuffer(1 << 20)
+    for level, strip in ((1, 4096), (6, 65537), (0, 4096)):
+        with pytest.raises(Exception):
+            L.call("vcf_zlib_strips", d.ptr, 1, 8192, strip, level, d.ptr, 1 << 17, d.ptr, d.ptr, None)

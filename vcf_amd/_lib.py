@@ -126,6 +126,10 @@ SIGNATURES = {
     "vcf_png_decode_rgb": [_P, _I64, _P, _I64],
     "vcf_png_encode_rgb": [_P, _I32, _I32, _I32, _I32, _P, _I64, ctypes.POINTER(_I64)],
     "vcf_png_encode_bound": [_I32, _I32],
+    "vcf_zlib_bound": [_I64],
+    "vcf_zlib_workspace": [_I64],
+    "vcf_zlib_strip_count": [_I64, _I32],
+    "vcf_zlib_strips": [_P, _I64, _I64, _I32, _I32, _P, _I64, _P, _P, _P],
     "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],
     "vcf_deadzone_dequantize": [_P, _I32, _I64, _I32, _P, _P],
     "vcf_cbaac_tiled_set_variant": [_I32],
@@ -201,7 +205,8 @@ def lib():
             L.vcf_cbahc_bound.restype = ctypes.c_int64
             L.vcf_png_encode_bound.restype = ctypes.c_int64
             for name in ("vcf_cbaac_tiled_segments", "vcf_cbaac_tiled_workspace", "vcf_cbaac_tiled_bound",
-                         "vcf_cbaac_tiled_frames_workspace"):
+                         "vcf_cbaac_tiled_frames_workspace", "vcf_zlib_bound", "vcf_zlib_workspace",
+                         "vcf_zlib_strip_count"):
                 getattr(L, name).restype = ctypes.c_int64
             _lib = L
     return _lib

@@ -50,6 +50,16 @@ def _deflate_strips(data: memoryview, strip_bytes: int, nstrips: int, level: int
     return [zlib.compress(c, level) for c in chunks]
 
 
+def strip_layout(shape, itemsize: int = 1):
+    """(rows per strip, strips, bytes per full strip) tifffile 2021.7.2 uses
+    for an H x W [x C] array: RowsPerStrip = 65536 // row bytes, at least 1."""
+    H, W = shape[0], shape[1]
+    C = shape[2] if len(shape) > 2 else 1
+    row_bytes = W * C * itemsize
+    rps = max(1, min(H, 65536 // max(1, row_bytes)))
+    return rps, (H + rps - 1) // rps, rps * row_bytes
+
+
 def imwrite_bytes(img: np.ndarray, level: int = ZLIB_LEVEL) -> bytes:
     """tifffile.imwrite(BytesIO, img, compression='zlib') for HxWxC u8/u16."""
     a = np.ascontiguousarray(img)
@@ -61,15 +71,22 @@ def imwrite_bytes(img: np.ndarray, level: int = ZLIB_LEVEL) -> bytes:
         a = a[:, :, None]
     if a.ndim != 3:
         raise ValueError("TIFF writer expects an H x W [x C] array")
-    H, W, C = a.shape
-    isz = a.dtype.itemsize
-    row_bytes = W * C * isz
-    rps = max(1, min(H, 65536 // max(1, row_bytes)))
-    nstrips = (H + rps - 1) // rps
-    comp = _deflate_strips(memoryview(a.reshape(-1).view(np.uint8)), rps * row_bytes, nstrips, level)
+    rps, nstrips, strip_bytes = strip_layout(a.shape, a.dtype.itemsize)
+    comp = _deflate_strips(memoryview(a.reshape(-1).view(np.uint8)), strip_bytes, nstrips, level)
+    return container(img.shape, a.dtype, comp)
+
+
+def container(shape, dtype, comp) -> bytes:
+    """The TIFF file around already-deflated strips (tifffile's byte layout)."""
+    H, W = shape[0], shape[1]
+    C = shape[2] if len(shape) > 2 else 1
+    isz = np.dtype(dtype).itemsize
+    rps, nstrips, _ = strip_layout((H, W, C), isz)
+    if len(comp) != nstrips:
+        raise ValueError(f"{len(comp)} strips for a {H}x{W}x{C} image, expected {nstrips}")
     counts = [len(c) for c in comp]
 
-    desc = json.dumps({"shape": list(img.shape)}).encode() + b"\x00"
+    desc = json.dumps({"shape": list(shape)}).encode() + b"\x00"
     photometric = 2 if C == 3 else 1      # RGB for 3 samples, else minisblack
     tags = []   # (code, type, count, payload bytes or int)
     tags.append((256, 4, 1, W))

@@ -1,0 +1,122 @@
+"""GPU deflate of TIFF strips: the reference's default entropy stage
+(TIFF.py:23-31, tifffile.imwrite(..., compression='zlib')) with the strips
+deflated on the GPU, byte for byte what zlib.compress(strip, 6) returns
+(libvcf_amd.so: vcf_zlib_strips; algorithm in csrc/vcf_deflate.h).
+
+Frames already in HBM (the DCT/DWT kernels' index frames) are deflated where
+they are; only the compressed strips come back: the per-strip streams are
+packed on the device (vcf_copy_pieces) and copied to the host in one piece.
+The TIFF file around them is vcf_amd.codec.tiff.container, the same writer
+the host path uses, so the files are identical.
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+
+from . import _lib as L
+from .device import DeviceBuffer, Stream, copy_pieces
+
+LEVEL = 6   # tifffile 2021.7.2's zlib level (vcf_amd/codec/tiff.py ZLIB_LEVEL)
+
+
+def strip_count(frame_bytes: int, strip_bytes: int) -> int:
+    return int(L.lib().vcf_zlib_strip_count(int(frame_bytes), int(strip_bytes)))
+
+
+def bound(strip_bytes: int) -> int:
+    return int(L.lib().vcf_zlib_bound(int(strip_bytes)))
+
+
+class StripDeflater:
+    """Deflates every strip of a batch of device-resident frames.  Scratch
+    buffers grow on demand and are reused; calls are serialised (one set of
+    scratch, one stream)."""
+
+    def __init__(self):
+        self._bufs = {}
+        self._stream = None
+        self._lock = threading.Lock()
+
+    def _buf(self, name: str, nbytes: int) -> DeviceBuffer:
+        b = self._bufs.get(name)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                b.free()
+            b = self._bufs[name] = DeviceBuffer(max(int(nbytes), 16))
+        return b
+
+    def deflate_device(self, src: DeviceBuffer, n_frames: int, frame_bytes: int, strip_bytes: int,
+                       level: int = LEVEL, offset: int = 0, stream: Stream | None = None):
+        """-> list over frames of lists of strip streams (bytes).  `src` holds
+        n_frames frames of frame_bytes bytes from byte `offset`; work on
+        `stream` (default: the deflater's own) is complete before the call
+        returns."""
+        with self._lock:
+            if stream is None:
+                if self._stream is None:
+                    self._stream = Stream()
+                stream = self._stream
+            spf = strip_count(frame_bytes, strip_bytes)
+            total = spf * int(n_frames)
+            if total == 0:
+                return [[] for _ in range(int(n_frames))]
+            slot = bound(strip_bytes)
+            out = self._buf("out", total * slot)
+            sizes = self._buf("sizes", total * 4)
+            ws = self._buf("ws", int(L.lib().vcf_zlib_workspace(total)))
+            L.call("vcf_zlib_strips", src.address(offset), int(n_frames), int(frame_bytes), int(strip_bytes),
+                   int(level), out.ptr, slot, sizes.ptr, ws.ptr, stream.handle)
+            sz = np.empty(total, np.int32)
+            sizes.download(sz, stream)
+            stream.synchronize()
+            if (sz < 0).any():
+                raise RuntimeError("vcf_zlib_strips: a strip overflowed its slot")
+            # pack the streams on the device, one download
+            offs = np.zeros(total + 1, np.int64)
+            np.cumsum(sz, out=offs[1:])
+            table = np.empty((total, 3), np.int64)
+            table[:, 0] = np.arange(total, dtype=np.int64) * slot
+            table[:, 1] = offs[:-1]
+            table[:, 2] = sz
+            tb = self._buf("table", table.nbytes)
+            tb.upload(table, stream)
+            packed = self._buf("packed", int(offs[-1]))
+            copy_pieces(out, tb, total, packed, stream)
+            host = np.empty(int(offs[-1]), np.uint8)
+            if host.size:
+                packed.download(host, stream)
+            stream.synchronize()
+            blob = host.tobytes()
+            return [[blob[offs[f * spf + k]:offs[f * spf + k + 1]] for k in range(spf)] for f in range(int(n_frames))]
+
+    def close(self):
+        for b in self._bufs.values():
+            b.free()
+        self._bufs.clear()
+
+
+_default = None
+
+
+def deflater() -> StripDeflater:
+    global _default
+    if _default is None:
+        _default = StripDeflater()
+    return _default
+
+
+def tiff_frames_device(src: DeviceBuffer, n_frames: int, shape, dtype=np.uint8, offset: int = 0,
+                       stream: Stream | None = None) -> list:
+    """TIFF files (bytes) of n_frames device-resident H x W [x C] u8/u16
+    arrays, identical to vcf_amd.codec.tiff.imwrite_bytes of each (TIFF.py:29)."""
+    from .codec.tiff import container, strip_layout
+    dt = np.dtype(dtype)
+    if dt not in (np.uint8, np.uint16):
+        raise ValueError(f"current type = {dt}")   # TIFF.py:27
+    shape = tuple(int(s) for s in shape)
+    frame_bytes = int(np.prod(shape)) * dt.itemsize
+    _, _, strip_bytes = strip_layout(shape if len(shape) == 3 else shape + (1,), dt.itemsize)
+    strips = deflater().deflate_device(src, n_frames, frame_bytes, strip_bytes, LEVEL, offset, stream)
+    return [container(shape, dt, s) for s in strips]
