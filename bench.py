@@ -220,11 +220,12 @@ def c4_frame(bases, i: int) -> np.ndarray:
     return bases[i % len(bases)] + np.uint8((i // len(bases)) * 7 % 256)
 
 
-def c4_block(args, world: int, rank: int, group):
+def c4_block(args, world: int, rank: int, group, entropy: str = "TCBAACP"):
     """Config C4 of BASELINE.json: III over a 256-frame 1080p sequence,
     frame-sharded across the ranks, end to end on the GPU with the exchange
     (vcf_amd/codec/iii_device.py): DCT+deadzone, the GPU entropy stage
-    (-c TCBAACP), per-frame sizes all-gathered and the code-streams gathered
+    (-c TCBAACP, or with entropy="TIFF" the reference's default -c TIFF: every
+    strip deflated on the GPU exactly as zlib), per-frame sizes all-gathered and the code-streams gathered
     to rank 0 over RCCL (device to device).  Timed like the headline:
     barrier + device sync on both sides, max over ranks.  Rank 0 checks what
     it gathered: every frame's container equals that frame coded on its own
@@ -240,8 +241,10 @@ def c4_block(args, world: int, rank: int, group):
     from vcf_amd.rccl import Communicator
     N, H, W, Q = args.c4_frames, 1080, 1920, args.QSS
     lo, hi = frame_range(N, rank, world)
-    info = {"workload": (f"III C4: {N} x 1080p frames, DCT+deadzone Q={Q} + GPU entropy (-c TCBAACP, "
-                         f"{T.CLASS_SEG}-symbol segments, {T.PRIOR_CLASSES} prior classes), frame i on rank floor(i*P/N), sizes all-gather + "
+    ent = (f"-c TCBAACP, {T.CLASS_SEG}-symbol segments, {T.PRIOR_CLASSES} prior classes" if entropy == "TCBAACP"
+           else "-c TIFF, the reference's default: every ~64 KB strip deflated on the GPU byte-exact with zlib level 6")
+    info = {"workload": (f"III C4: {N} x 1080p frames, DCT+deadzone Q={Q} + GPU entropy ({ent}), frame i on rank "
+                         f"floor(i*P/N), sizes all-gather + "
                          f"code-stream gatherv to rank 0 over RCCL (device to device), rank 0 copies them to host"),
             "frames": N, "frame": [H, W, 3], "n_ranks": world, "frames_this_rank0": hi - lo if rank == 0 else None}
     err, comm, t_rank = None, None, float("nan")
@@ -252,7 +255,7 @@ def c4_block(args, world: int, rank: int, group):
             rgb.upload(c4_frame(bases, i), offset=j * H * W * 3)
         comm = Communicator(group if world > 1 else HostGroup(0, 1), timeout_s=args.c4_timeout)
         info["backend"] = "rccl" if world > 1 else "rccl (single rank: the root's device copy)"
-        job = DeviceIII(comm, rank, world, N, H, W, Q)
+        job = DeviceIII(comm, rank, world, N, H, W, Q, entropy=entropy)
         for _ in range(args.c4_warmup):
             job.run(rgb)
         group.barrier()
@@ -268,7 +271,7 @@ def c4_block(args, world: int, rank: int, group):
         if rank == 0:
             info["code_bytes"] = int(sizes.sum())
             info["bits_per_symbol"] = round(8 * int(sizes.sum()) / (N * job.n_sym), 5)
-            info["verified"] = c4_verify(got, bases, job, N, H, W, Q, world)
+            info["verified"] = c4_verify(got, bases, job, N, H, W, Q, world, entropy)
     except Exception as e:   # reported in the block; the headline line still prints
         err = f"{type(e).__name__}: {e}"
     finally:
@@ -288,11 +291,24 @@ def c4_block(args, world: int, rank: int, group):
     return info
 
 
-def c4_verify(got, bases, job, N, H, W, Q, world) -> str:
-    """Rank 0: the gathered containers against per-frame coding on this GPU."""
+def c4_verify(got, bases, job, N, H, W, Q, world, entropy="TCBAACP") -> str:
+    """Rank 0: the gathered containers against per-frame coding on this GPU
+    (TIFF: against the host TIFF writer, system zlib, of the frame's indices)."""
     from vcf_amd import dct as D
     from vcf_amd import tcbaac as T
     from vcf_amd.device import DeviceBuffer
+    if entropy == "TIFF":
+        from vcf_amd.codec.tiff import imread_bytes, imwrite_bytes
+        frames = range(N) if world > 1 else sorted({0, N // 2, N - 1})
+        for i in frames:
+            k = D.encode(c4_frame(bases, i), Q)
+            if got[i] != imwrite_bytes(k):
+                return f"MISMATCH at frame {i}"
+            if i in (0, N - 1) and not np.array_equal(imread_bytes(got[i]), k):
+                return f"decode MISMATCH at frame {i}"
+        what = "every frame" if world > 1 else f"frames {list(frames)}"
+        return (f"ok: {what} equal to the host TIFF writer's file (system zlib) of the frame's indices; "
+                f"frames 0 and {N - 1} read back to them")
     codec = T.TiledCBAACCodec(order=0, seg_len=T.CLASS_SEG, prior=True, nclass=T.PRIOR_CLASSES)
     frames = range(N) if world > 1 else sorted({0, N // 2, N - 1})
     Hp, Wp = D.padded_shape(H, W)
@@ -344,6 +360,7 @@ def main():
     ap.add_argument("--variant", type=int, default=0, help="encode kernel (0 = automatic)")
     ap.add_argument("--c4-frames", type=int, default=256, help="frames of the C4 block (0 disables it)")
     ap.add_argument("--c4-steps", type=int, default=2)
+    ap.add_argument("--no-c4-tiff", action="store_true", help="skip the C4 block with -c TIFF (GPU deflate)")
     ap.add_argument("--c4-warmup", type=int, default=1)
     ap.add_argument("--c4-timeout", type=float, default=90.0, help="seconds before an RCCL call is aborted")
     args = ap.parse_args()
@@ -402,6 +419,8 @@ def main():
     # C4 (III, 256 x 1080p, frame-sharded, with the RCCL exchange): after the
     # headline's timed region, reported in its own block
     c4 = c4_block(args, world, rank, group) if args.c4_frames > 0 else None
+    # the same with the reference's default entropy codec, -c TIFF (GPU deflate)
+    c4t = c4_block(args, world, rank, group, "TIFF") if args.c4_frames > 0 and not args.no_c4_tiff else None
 
     # after the timed region (an idle GPU during seconds of CPU work would start
     # the timed steps at low clocks): parity spot check of the timed kernel's
@@ -451,6 +470,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "c4_e2e_with_gather": c4,
+            "c4_tiff_e2e_with_gather": c4t,
         }
         print(json.dumps(out), flush=True)
     group.close()

@@ -423,7 +423,8 @@ int64_t vcf_png_encode_bound(int32_t H, int32_t W);
  * (-1: slot too small).  level 4..9 (VCF_ERR_UNSUPPORTED otherwise);
  * strip_bytes <= 65536 (tifffile's strips for rows up to 64 KB);
  * slot_bytes a multiple of 4 >= vcf_zlib_bound(strip_bytes); ws_dev holds
- * vcf_zlib_workspace(total strips) bytes.  All pointers 4-byte aligned. */
+ * vcf_zlib_workspace(total strips) bytes (16-byte aligned; out_dev and
+ * sizes_dev 4-byte aligned). */
 int64_t vcf_zlib_bound(int64_t strip_bytes);
 int64_t vcf_zlib_workspace(int64_t n_strips);
 int64_t vcf_zlib_strip_count(int64_t frame_bytes, int32_t strip_bytes);

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--only", default="", help="comma-separated workload names")
     args = ap.parse_args()
     from bench import synth_frame
     from vcf_amd import _lib as L
@@ -29,11 +30,20 @@ def main():
     from vcf_amd.codec.tiff import strip_layout
     from vcf_amd.device import DeviceBuffer, Event, Stream
     st = Stream()
-    for name, (H, W), kind in [("dct_1080p", (1080, 1920), "dct"), ("dct_4k", (2160, 3840), "dct"),
-                               ("rgb_1080p", (1080, 1920), "rgb")]:
+    from bench import c4_frame
+    sets = [("dct_1080p", (1080, 1920), "dct"), ("dct_c4_1080p", (1080, 1920), "c4"), ("dct_4k", (2160, 3840), "dct"),
+            ("rgb_1080p", (1080, 1920), "rgb")]
+    if args.only:
+        sets = [t for t in sets if t[0] in args.only.split(",")]
+    for name, (H, W), kind in sets:
         n = args.frames if H == 1080 else max(1, args.frames // 4)
-        base = np.stack([synth_frame(H, W, s) for s in range(4)])
-        frames = base[np.arange(n) % 4]
+        if kind == "c4":   # bench.py's C4 sequence (shifted S-smooth frames, u8 wrap)
+            bases = [synth_frame(H, W, seed=100 + s) for s in range(4)]
+            frames = np.stack([c4_frame(bases, i) for i in range(n)])
+            kind = "dct"
+        else:
+            base = np.stack([synth_frame(H, W, s) for s in range(4)])
+            frames = base[np.arange(n) % 4]
         if kind == "dct":
             frames = np.concatenate([dct.encode(frames[i:i + 16], Q=32) for i in range(0, n, 16)])
         flat = np.ascontiguousarray(frames.reshape(n, -1))

@@ -94,3 +94,27 @@ def test_unsupported():
     for level, strip in ((1, 4096), (6, 65537), (0, 4096)):
         with pytest.raises(Exception):
             L.call("vcf_zlib_strips", d.ptr, 1, 8192, strip, level, d.ptr, 1 << 17, d.ptr, d.ptr, None)
+
+
+def test_device_iii_tiff_equals_host_writer():
+    """The C4 data path with the reference's default -c TIFF
+    (vcf_amd/codec/iii_device.py, entropy="TIFF"): every gathered file equals
+    the host TIFF writer's (system zlib) for the frame's indices, and reads back."""
+    from vcf_amd.codec.iii_device import DeviceIII
+    from vcf_amd.codec.tiff import imread_bytes, imwrite_bytes
+    from vcf_amd import dct
+    from vcf_amd.device import DeviceBuffer
+    rng = np.random.default_rng(3)
+    for n, H, W in ((5, 61, 77), (3, 200, 1000)):
+        y = np.arange(H)[:, None, None]
+        x = np.arange(W)[None, :, None]
+        frames = np.stack([np.clip(128 + 50 * np.sin(x / (19 + f) + y / 31.0 + np.arange(3)) +
+                                   rng.normal(0, 6, (H, W, 3)), 0, 255).astype(np.uint8) for f in range(n)])
+        job = DeviceIII(None, 0, 1, n, H, W, 32, entropy="TIFF")
+        stages = {}
+        sizes, got = job.run(DeviceBuffer.from_array(frames), stages)
+        k = dct.encode(frames, Q=32)
+        for i in range(n):
+            want = imwrite_bytes(k[i])
+            assert got[i] == want and sizes[i] == len(want), (n, i)
+            assert np.array_equal(imread_bytes(got[i]), k[i])

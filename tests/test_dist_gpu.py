@@ -196,6 +196,7 @@ def test_bench_c4_block_small():
                         "--warmup", "1", "--settle-max-s", "0", "--no-cpu-baseline", "--c4-frames", "6"],
                        env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-2000:]
-    c4 = json.loads(p.stdout.strip().splitlines()[-1])["c4_e2e_with_gather"]
-    assert "error" not in c4, c4
-    assert c4["value"] > 0 and c4["verified"].startswith("ok"), c4
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    for key in ("c4_e2e_with_gather", "c4_tiff_e2e_with_gather"):
+        c4 = line[key]
+        assert "error" not in c4 and c4["value"] > 0 and c4["verified"].startswith("ok"), c4

@@ -8,12 +8,15 @@ chunk never leaves the GPU until its code-streams are final:
 
   1. one launch of the fused DCT + deadzone kernel over the rank's chunk
      (vcf_dct_dz_encode), indices stay in HBM;
-  2. the GPU entropy stage: every frame's indices coded as a prior-seeded
-     tiled CBAAC stream (`-c TCBAACP`, vcf_amd/tcbaac.py), all frames in
-     one launch per stage; only the small segment index comes to the host;
-  3. every frame's container (header + segments, exactly the bytes
-     `TiledCBAACCodec.compress_device` returns for it) is assembled in a
-     device send buffer;
+  2. the GPU entropy stage, all frames in one launch per stage, only the
+     small size tables coming to the host: either every frame's indices
+     coded as a prior-seeded tiled CBAAC stream (`-c TCBAACP`,
+     vcf_amd/tcbaac.py), or -- the reference's default `-c TIFF` -- every
+     TIFF strip of every frame deflated exactly as zlib would
+     (vcf_amd/zlib_gpu.py);
+  3. every frame's file (header + payload: exactly the bytes
+     `TiledCBAACCodec.compress_device`, resp. the TIFF writer, returns for
+     it) is assembled in a device send buffer;
   4. the exchange: per-frame container sizes all-gathered
      (ncclAllGather), the containers gathered to rank 0 device to device
      (vcf_comm_gatherv: one ncclSend per peer, P-1 receives on rank 0, each
@@ -31,15 +34,18 @@ import numpy as np
 
 from .. import dct as D
 from .. import tcbaac as T
+from .. import zlib_gpu as Z
 from ..device import DeviceBuffer, HostBuffer, Stream, copy_dtod, copy_pieces
 from .shard import frame_range
+from .tiff import container_prefix, strip_layout
 
 
 class DeviceIII:
     """One rank's part of a frame-sharded, HBM-resident III encode."""
 
     def __init__(self, comm, rank: int, world: int, n_frames: int, H: int, W: int, Q: int = 32,
-                 seg_len: int = T.CLASS_SEG, streams: int = 4, nclass: int = T.PRIOR_CLASSES):
+                 seg_len: int = T.CLASS_SEG, streams: int = 4, nclass: int = T.PRIOR_CLASSES,
+                 entropy: str = "TCBAACP"):
         self.comm, self.rank, self.world = comm, int(rank), int(world)
         self.N, self.H, self.W, self.Q = int(n_frames), int(H), int(W), int(Q)
         self.lo, self.hi = frame_range(self.N, self.rank, self.world)
@@ -49,7 +55,15 @@ class DeviceIII:
         self.n_sym = self.Hp * self.Wp * 3
         self.stream = Stream()
         self.k = DeviceBuffer(max(self.n_local * self.n_sym, 1))
-        self.batch = T.FrameBatch(self.n_local, self.n_sym, 0, seg_len, prior=True, nclass=nclass)
+        if entropy not in ("TCBAACP", "TIFF"):
+            raise ValueError(f"entropy codec {entropy!r}: TCBAACP or TIFF")
+        self.entropy = entropy
+        if entropy == "TIFF":
+            self.batch = None
+            self.zd = Z.StripDeflater()
+            self.strip_bytes = strip_layout(self.shape, 1)[2]
+        else:
+            self.batch = T.FrameBatch(self.n_local, self.n_sym, 0, seg_len, prior=True, nclass=nclass)
         self.send = None
         self.recv = None
         self.hstage = None
@@ -82,12 +96,33 @@ class DeviceIII:
         if self.n_local:
             D.encode_device(rgb, self.n_local, self.H, self.W, self.Q, 0, out=self.k, stream=self.stream)
         t = mark("dct_dz", t)
-        if self.n_local:
-            self.batch.launch(self.k, after=self.stream)
-        seg, totals, priors = self.batch.sizes()          # waits for the coder
-        t = mark("entropy", t)
-        headers = self.batch.headers(self.shape)
-        local_sizes = np.array([len(h) + int(totals[f]) for f, h in enumerate(headers)], np.int64)
+        if self.entropy == "TIFF":
+            # the TIFF files: header (built on the host from the strip sizes) + the strips as deflated
+            if self.n_local:
+                self.zd.launch(self.k, self.n_local, self.n_sym, self.strip_bytes, Z.LEVEL, 0, self.stream)
+                sz = self.zd.sizes().astype(np.int64).reshape(self.n_local, -1)
+            else:
+                sz = np.zeros((0, 1), np.int64)
+            t = mark("entropy", t)
+            headers = [container_prefix(self.shape, np.uint8, sz[f]) for f in range(self.n_local)]
+            pay_buf = self.zd.out if self.n_local else None
+            spf = sz.shape[1]
+            pay_src = (np.arange(self.n_local * spf, dtype=np.int64) * self.zd.slot if self.n_local else
+                       np.zeros(0, np.int64)).reshape(self.n_local, spf)
+            pay_len = sz
+        else:
+            if self.n_local:
+                self.batch.launch(self.k, after=self.stream)
+            seg, totals, priors = self.batch.sizes()          # waits for the coder
+            t = mark("entropy", t)
+            headers = self.batch.headers(self.shape)
+            pay_buf = self.batch.out
+            pay_src = np.zeros((self.n_local, 1), np.int64)
+            pay_len = np.zeros((self.n_local, 1), np.int64)
+            for f in range(self.n_local):
+                pbuf, poff, pn = self.batch.payload(f)
+                pay_src[f, 0], pay_len[f, 0] = poff, pn
+        local_sizes = np.array([len(h) + int(pay_len[f].sum()) for f, h in enumerate(headers)], np.int64)
         nbytes = int(local_sizes.sum())
         send = self._buf("send", nbytes)
         if self.n_local:
@@ -96,20 +131,22 @@ class DeviceIII:
             hb = np.frombuffer(b"".join(headers), np.uint8)
             hst = self._buf("hstage", hb.size)
             hst.upload(hb, self.stream)
+            npay = pay_len.shape[1]
             hdr_tab = np.empty((self.n_local, 3), np.int64)
-            pay_tab = np.empty((self.n_local, 3), np.int64)
+            pay_tab = np.empty((self.n_local, npay, 3), np.int64)
             off = hoff = 0
             for f, h in enumerate(headers):
-                pbuf, poff, pn = self.batch.payload(f)
                 hdr_tab[f] = (hoff, off, len(h))
-                pay_tab[f] = (poff, off + len(h), pn)
-                off += len(h) + pn
+                off += len(h)
                 hoff += len(h)
-            tab = np.concatenate([hdr_tab, pay_tab]).ravel()
+                for j in range(npay):
+                    pay_tab[f, j] = (pay_src[f, j], off, pay_len[f, j])
+                    off += int(pay_len[f, j])
+            tab = np.concatenate([hdr_tab.ravel(), pay_tab.ravel()])
             tb = self._buf("table", tab.nbytes)
             tb.upload(tab, self.stream)
             copy_pieces(hst, tb, self.n_local, send, self.stream)
-            copy_pieces(self.batch.out, _View(tb, hdr_tab.nbytes), self.n_local, send, self.stream)
+            copy_pieces(pay_buf, _View(tb, hdr_tab.nbytes), self.n_local * npay, send, self.stream)
         t = mark("pack", t)
         sizes = self._all_gather_sizes(local_sizes)
         t = mark("sizes_allgather", t)

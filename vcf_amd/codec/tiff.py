@@ -78,13 +78,20 @@ def imwrite_bytes(img: np.ndarray, level: int = ZLIB_LEVEL) -> bytes:
 
 def container(shape, dtype, comp) -> bytes:
     """The TIFF file around already-deflated strips (tifffile's byte layout)."""
+    return container_prefix(shape, dtype, [len(c) for c in comp]) + b"".join(comp)
+
+
+def container_prefix(shape, dtype, counts) -> bytes:
+    """Every byte of the TIFF file before its strip data (header, IFD, tag
+    values, padding to the 16-byte aligned data offset), for strips of the
+    given compressed sizes stored back to back after it."""
     H, W = shape[0], shape[1]
     C = shape[2] if len(shape) > 2 else 1
     isz = np.dtype(dtype).itemsize
     rps, nstrips, _ = strip_layout((H, W, C), isz)
-    if len(comp) != nstrips:
-        raise ValueError(f"{len(comp)} strips for a {H}x{W}x{C} image, expected {nstrips}")
-    counts = [len(c) for c in comp]
+    counts = [int(c) for c in counts]
+    if len(counts) != nstrips:
+        raise ValueError(f"{len(counts)} strips for a {H}x{W}x{C} image, expected {nstrips}")
 
     desc = json.dumps({"shape": list(shape)}).encode() + b"\x00"
     photometric = 2 if C == 3 else 1      # RGB for 3 samples, else minisblack
@@ -142,8 +149,6 @@ def container(shape, dtype, comp) -> bytes:
     out += struct.pack("<I", 0)
     out += ool
     out += b"\x00" * (data_off - len(out))
-    for c in comp:
-        out += c
     return bytes(out)
 
 

@@ -3,24 +3,32 @@
 // (TIFF.py:29 -> tifffile.imwrite(..., compression='zlib') -> zlib level 6,
 // one stream per RowsPerStrip strip; the host path is vcf_amd/codec/tiff.py).
 //
-// One wave (64 lanes, one workgroup) per strip; two strips per CU (76 KB LDS
-// each).  Three phases per strip:
-//   A  hash-chain order for all positions at once: every position 0..n-3 is
-//      bucketed by its zlib hash, stably (histogram, scan, ordered scatter in
-//      groups of 64 with an exact same-hash lane mask).  sorted[] lists the
-//      positions bucket by bucket in increasing order, idx[p] is p's slot,
-//      so zlib's chain of p -- earlier positions with p's hash, newest first --
-//      is sorted[idx[p]-1], sorted[idx[p]-2], ... while the hash stays p's.
-//   B  the strip is copied into LDS (the bytes past its end as zlib's window
-//      holds them) and the wave runs deflate_slow (vcf_deflate.h) with
-//      uniform state; longest_match evaluates the chain head with one
-//      wave-wide 256-byte compare and, when that is not already a nice match,
-//      up to 64 candidates at a time, one per lane.
-//   C  per block: trees built by lane 0 (trees.c restated), the block and
-//      tree headers written serially, the symbols packed in parallel (64 per
-//      step: per-lane code bits, prefix sum of their lengths, LDS OR into
-//      staging words, whole words stored).
-// The wave ends with the adler32 trailer; sizes_dev[s] = the stream's length.
+// zlib's serial loop is split where its data dependences allow (DESIGN.md
+// §4.9; the restatement and its proofs of equivalence are vcf_deflate.h):
+//   K1 zlib_head_kernel, one wave per strip: the hash insertion of every
+//      position in order -- hd[p] = zlib's head[] when p is inserted (the
+//      newest earlier position with p's hash, 0 = NIL), i.e. the hash
+//      chains, which do not depend on the parse -- and the adler32 sums.
+//      64 positions per step with an exact same-hash lane mask; the 32768
+//      heads in LDS.
+//   K2 zlib_match_kernel, one thread per position, 256 per workgroup and
+//      1024 positions per workgroup: longest_match at p for both chain
+//      limits deflate_slow can use (max_chain, and max_chain >> 2 once
+//      prev_length >= good_match).  Every call whose result can matter has
+//      the early-exit threshold min(nice, lookahead), independent of
+//      prev_length (vcf_deflate.h), so two (length, distance) pairs per
+//      position carry all of it; "found" is length > prev_length, decided
+//      in K3.  The window (32 KB back + the workgroup's span) in LDS, the
+//      chains walked through hd[] (L2), the bytes past the strip's end as
+//      zlib's window holds them (zeros, or after its one slide the stale
+//      copy 32 KB back).
+//   K3 zlib_parse_kernel, one wave per strip: deflate_slow with uniform state
+//      over 512-position register windows of hd[], the K2 results and the
+//      bytes; per block the trees built by lane 0 (trees.c restated), the
+//      block and tree headers written serially, the symbols packed 64 at a
+//      time (per-lane code bits, prefix sum of their lengths, LDS OR into
+//      staging words, whole words stored); the adler32 trailer.
+// sizes_dev[s] = the stream's length.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,24 +43,17 @@ namespace {
 
 using namespace dfl;
 
-constexpr int kWinBytes = MAX_STRIP + 320;      // strip + the window bytes past its end
-constexpr int kStgWords = 128;                  // staging for one 64-symbol step (<= 3072 + 31 bits)
-constexpr int64_t kWsPerStrip = (int64_t)MAX_STRIP * 2 * 2 + (int64_t)LIT_BUFSIZE * 4;   // idx, sorted, symbols
-
-struct DflSmem {
-    union {
-        uint32_t cnt[1 << 14];                  // phase A: 32768 u16 counters, packed in pairs
-        uint32_t win32[kWinBytes / 4];          // phase B/C: the window
-    } u;
-    uint16_t lfreq[HEAP_SIZE], ldad[HEAP_SIZE], llen[HEAP_SIZE], lcode[L_CODES + 2];
-    uint16_t dfreq[2 * D_CODES + 1], ddad[2 * D_CODES + 1], dlen[2 * D_CODES + 1], dcode[D_CODES + 2];
-    uint16_t bfreq[2 * BL_CODES + 1], bdad[2 * BL_CODES + 1], blen[2 * BL_CODES + 1], bcode[BL_CODES + 2];
-    int16_t heap[HEAP_SIZE];
-    uint8_t depth[HEAP_SIZE];
-    uint16_t bl_count[MAX_BITS + 1];
-    uint32_t stg[kStgWords];
-    uint32_t bcast[4];
-};
+constexpr int kStgWords = 128;       // bit staging for one 64-symbol step (<= 3072 + 31 bits)
+constexpr int kChunk = 1024;         // K2: positions per workgroup
+constexpr int kK2Threads = 256;
+constexpr int kK2Win = WSIZE + kChunk + MAX_MATCH + 64;   // K2's LDS window
+// workspace per strip: hd u16, full- and reduced-chain results u32, symbols u32, adler sums
+constexpr int64_t kHdOff = 0;
+constexpr int64_t kRfOff = kHdOff + (int64_t)MAX_STRIP * 2;
+constexpr int64_t kRrOff = kRfOff + (int64_t)MAX_STRIP * 4;
+constexpr int64_t kSymOff = kRrOff + (int64_t)MAX_STRIP * 4;
+constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;
+constexpr int64_t kWsPerStrip = kSumOff + 16;
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -76,36 +77,210 @@ __device__ __forceinline__ uint32_t excl_scan(uint32_t v, uint32_t &total)
     total = (uint32_t)__shfl(incl, 63, 64);
     return incl - v;
 }
-__device__ __forceinline__ uint32_t wave_max(uint32_t v)
-{
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
-    return v;
-}
 template <class T>
 __device__ __forceinline__ T ld_l2(const T *p)   // coherent with the other lanes' earlier stores (not via L1)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-struct Wave {
-    DflSmem &sm;
+struct Strip {
     const uint8_t *src;
     uint32_t n;
-    uint16_t *idx, *sorted;
+    uint8_t *ws;
+};
+__device__ __forceinline__ Strip strip_of(const uint8_t *in, int64_t frame_bytes, int32_t strip_bytes, int32_t spf,
+                                          uint8_t *ws, int64_t s)
+{
+    const int64_t f = s / spf, k = s - f * spf;
+    const int64_t off = k * (int64_t)strip_bytes;
+    return {in + f * frame_bytes + off, (uint32_t)min((int64_t)strip_bytes, frame_bytes - off), ws + s * kWsPerStrip};
+}
+
+// ---- K1: hash chains (zlib's head[] at each insertion) and adler32 sums ----
+struct HeadSmem {
+    uint16_t head[1 << 15];
+    uint8_t stage[kChunk + 64];
+};
+
+__global__ __launch_bounds__(64) void zlib_head_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+                                                      int32_t strip_bytes, int32_t spf, uint8_t *__restrict__ ws,
+                                                      int64_t s0)
+{
+    __shared__ __attribute__((aligned(16))) HeadSmem sm;
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0 + blockIdx.x);
+    uint16_t *hd = reinterpret_cast<uint16_t *>(S.ws + kHdOff);
+    const uint32_t lane = lane_id(), n = S.n;
+    const uint32_t np = n >= 3 ? n - 2 : 0;   // positions 0..n-3 are inserted
+    for (uint32_t i = lane; i < (1u << 14); i += 64) reinterpret_cast<uint32_t *>(sm.head)[i] = 0;
+    uint64_t sb = 0, swb = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
+        wave_sync();   // the previous chunk's stage reads are done
+        for (uint32_t j = lane; j < (uint32_t)kChunk + 2; j += 64) {
+            const uint32_t p = c0 + j;
+            const uint32_t b = p < n ? S.src[p] : 0u;
+            sm.stage[j] = (uint8_t)b;
+            if (j < (uint32_t)kChunk) {
+                sb += b;
+                swb += (uint64_t)(p < n ? n - p : 0u) * b;
+            }
+        }
+        wave_sync();
+        for (uint32_t g = 0; g < (uint32_t)kChunk && c0 + g < np; g += 64) {
+            const uint32_t p = c0 + g + lane, j = g + lane;
+            const bool v = p < np;
+            const uint32_t h = ((uint32_t)sm.stage[j] << 10 ^ (uint32_t)sm.stage[j + 1] << 5 ^ sm.stage[j + 2]) & 0x7fffu;
+            uint64_t rem = __ballot(v), mine = 0;
+            while (rem) {   // exact same-hash masks, one distinct hash per round
+                const uint32_t l = (uint32_t)__ffsll((unsigned long long)rem) - 1;
+                const uint32_t hl = lane_val(h, l);
+                const uint64_t m = __ballot(v && h == hl);
+                if (v && h == hl) mine = m;
+                rem &= ~m;
+            }
+            if (v) {
+                const uint64_t lower = mine & ((1ull << lane) - 1);
+                hd[p] = (uint16_t)(lower ? c0 + g + 63 - (uint32_t)__clzll((long long)lower) : (uint32_t)sm.head[h]);
+            }
+            wave_sync();
+            if (v && (mine >> lane) == 1) sm.head[h] = (uint16_t)p;   // the group's newest with this hash
+            wave_sync();
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        sb += __shfl_xor(sb, d, 64);
+        swb += __shfl_xor(swb, d, 64);
+    }
+    if (lane == 0) {
+        uint64_t *sums = reinterpret_cast<uint64_t *>(S.ws + kSumOff);
+        sums[0] = sb;
+        sums[1] = swb;
+    }
+}
+
+// ---- K2: longest_match at every position, both chain limits ----------------
+__global__ __launch_bounds__(kK2Threads) void zlib_match_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+                                                               int32_t strip_bytes, int32_t spf, int32_t level,
+                                                               uint8_t *__restrict__ ws, int64_t s0)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t win32[kK2Win / 4 + 4];
+    uint8_t *win = reinterpret_cast<uint8_t *>(win32);
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0 + blockIdx.y);
+    const uint32_t n = S.n, p0 = blockIdx.x * kChunk;
+    const uint32_t np = n >= 3 ? n - 2 : 0;
+    if (p0 >= np) return;
+    Config cfg;
+    level_config(level, cfg);
+    const uint16_t *hd = reinterpret_cast<const uint16_t *>(S.ws + kHdOff);
+    uint32_t *rf = reinterpret_cast<uint32_t *>(S.ws + kRfOff);
+    uint32_t *rr = reinterpret_cast<uint32_t *>(S.ws + kRrOff);
+    // window [w0, w0 + span): 32 KB back (every candidate is > p - MAX_DIST) and the
+    // chunk's strings; past n the bytes zlib's window holds there: zeros before its
+    // slide, after it (at strstart >= S_post) the stale copy WSIZE back
+    const uint32_t w0 = p0 > (uint32_t)WSIZE ? p0 - WSIZE : 0u;
+    const uint32_t wend = min(np, p0 + kChunk) + MAX_MATCH + 16;
+    const uint32_t slide_at = n == (uint32_t)MAX_STRIP ? WSIZE + MAX_DIST + 1 : WSIZE + MAX_DIST;
+    for (uint32_t p = w0 + threadIdx.x; p < wend; p += kK2Threads) win[p - w0] = p < n ? S.src[p] : 0u;
+    __syncthreads();
+    const uint32_t cfull = (uint32_t)cfg.chain, cred = (uint32_t)cfg.chain >> 2;
+    for (uint32_t p = p0 + threadIdx.x; p < min(np, p0 + kChunk); p += kK2Threads) {
+        uint32_t cur = hd[p];
+        uint32_t rfull = 0, rred = 0;
+        if (cur != 0 && p - cur <= (uint32_t)MAX_DIST) {
+            const uint32_t nice = min((uint32_t)cfg.nice, n - p);
+            const uint32_t limit = p > (uint32_t)MAX_DIST ? p - MAX_DIST : 0u;
+            const bool tail = p + MAX_MATCH + 16 > n;     // compares may read past the end
+            const bool post = p >= slide_at;              // ... as zlib's window holds it after the slide
+            uint32_t bf = 0, bfp = 0, br = 0, brp = 0;
+            uint32_t k = 0;
+            for (;;) {
+                // common prefix of the strings at cur and p, capped at MAX_MATCH
+                uint32_t len = 0;
+                if (!tail) {
+                    const uint32_t a = cur - w0, b = p - w0;
+                    while (len < (uint32_t)MAX_MATCH) {
+                        uint32_t x = 0, q = 0;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint32_t aa = a + len + 4 * u, bb = b + len + 4 * u;
+                            const uint32_t va = __builtin_amdgcn_alignbyte(win32[(aa >> 2) + 1], win32[aa >> 2], aa & 3);
+                            const uint32_t vb = __builtin_amdgcn_alignbyte(win32[(bb >> 2) + 1], win32[bb >> 2], bb & 3);
+                            if (x == 0) {
+                                x = va ^ vb;
+                                q = 4 * u;
+                            }
+                        }
+                        if (x) {
+                            len += q + ((uint32_t)__builtin_ctz(x) >> 3);
+                            break;
+                        }
+                        len += 16;
+                    }
+                    len = min(len, (uint32_t)MAX_MATCH);
+                } else {
+                    auto vb = [&](uint32_t P) -> uint32_t {
+                        if (P < n) return win[P - w0];
+                        return post ? (uint32_t)win[P - WSIZE - w0] : 0u;
+                    };
+                    while (len < (uint32_t)MAX_MATCH && vb(cur + len) == vb(p + len)) ++len;
+                }
+                if (len > bf) {
+                    bf = len;
+                    bfp = cur;
+                    if (k < cred) {
+                        br = len;
+                        brp = cur;
+                    }
+                    if (len >= nice) break;
+                }
+                if (++k >= cfull) break;
+                cur = hd[cur];
+                if (cur <= limit) break;
+            }
+            if (bf) rfull = bf << 16 | (p - bfp);
+            if (br) rred = br << 16 | (p - brp);
+        }
+        rf[p] = rfull;
+        rr[p] = rred;
+    }
+}
+
+// ---- K3: the parse, the trees, the bits ------------------------------------
+struct ParseSmem {
+    uint16_t lfreq[HEAP_SIZE], ldad[HEAP_SIZE], llen[HEAP_SIZE], lcode[L_CODES + 2];
+    uint16_t dfreq[2 * D_CODES + 1], ddad[2 * D_CODES + 1], dlen[2 * D_CODES + 1], dcode[D_CODES + 2];
+    uint16_t bfreq[2 * BL_CODES + 1], bdad[2 * BL_CODES + 1], blen[2 * BL_CODES + 1], bcode[BL_CODES + 2];
+    int16_t heap[HEAP_SIZE];
+    uint8_t depth[HEAP_SIZE];
+    uint16_t bl_count[MAX_BITS + 1];
+    uint32_t stg[kStgWords];
+    uint32_t lhist[L_CODES], dhist[D_CODES];   // the block's symbol counts (counted at flush)
+    uint32_t bcast[4];
+};
+
+struct Wave {
+    ParseSmem &sm;
+    const uint8_t *src;
+    uint32_t n;
+    const uint16_t *hd;
+    const uint32_t *rf, *rr;
     uint32_t *syms;
     uint32_t *out32;
     uint32_t out_words;           // slot capacity in words
+    uint32_t good;                // cfg.good: the reduced-chain results from prev_length >= good
     uint32_t bitpos = 0;          // bits written so far (uniform)
     uint32_t nsym = 0;            // symbols of the current block (uniform)
-    uint32_t wbase = 0xffffffffu, idxw = 0;   // idx[wbase + lane]
-    uint32_t last_ip = 0;
+    // 512-position windows: lane l holds positions base + 8l .. base + 8l + 7
+    uint32_t base = 0x80000000u;  // p - base >= 512: not loaded
+    uint4 hv, fv0, fv1, rv0, rv1;
+    uint32_t bv0, bv1;
     bool overflow = false;
     BlockTrees T;
 
-    __device__ Wave(DflSmem &s, const uint8_t *in, uint32_t len, uint16_t *ix, uint16_t *so, uint32_t *sy,
-                    uint32_t *o, uint32_t ow)
-        : sm(s), src(in), n(len), idx(ix), sorted(so), syms(sy), out32(o), out_words(ow)
+    __device__ Wave(ParseSmem &s, const uint8_t *in, uint32_t len, const uint8_t *w, uint32_t g, uint32_t *o,
+                    uint32_t ow)
+        : sm(s), src(in), n(len), hd(reinterpret_cast<const uint16_t *>(w + kHdOff)),
+          rf(reinterpret_cast<const uint32_t *>(w + kRfOff)), rr(reinterpret_cast<const uint32_t *>(w + kRrOff)),
+          syms(reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(w) + kSymOff)), out32(o), out_words(ow), good(g)
     {
         T.l = {sm.lfreq, sm.ldad, sm.llen, sm.lcode, L_CODES, MAX_BITS, 0, 0};
         T.d = {sm.dfreq, sm.ddad, sm.dlen, sm.dcode, D_CODES, MAX_BITS, 1, 0};
@@ -115,14 +290,32 @@ struct Wave {
         T.w.bl_count = sm.bl_count;
     }
 
-    __device__ uint8_t *win() { return reinterpret_cast<uint8_t *>(sm.u.win32); }
-    __device__ uint32_t wbyte(uint32_t p) { return win()[p]; }
-    __device__ uint32_t hash_at(uint32_t p) { return ((wbyte(p) << 10) ^ (wbyte(p + 1) << 5) ^ wbyte(p + 2)) & 0x7fffu; }
-    // 4 window bytes from any byte offset: two aligned LDS words and a funnel shift
-    __device__ uint32_t ld4(uint32_t a)
+    // ---- the windows ---------------------------------------------------
+    __device__ void window(uint32_t p)
     {
-        const uint32_t w0 = sm.u.win32[a >> 2], w1 = sm.u.win32[(a >> 2) + 1];
-        return __builtin_amdgcn_alignbyte(w1, w0, a & 3);
+        if (p - base < 512u) return;
+        base = p & ~7u;
+        const uint32_t q = base + 8 * lane_id();
+        hv = *reinterpret_cast<const uint4 *>(hd + q);
+        fv0 = *reinterpret_cast<const uint4 *>(rf + q);
+        fv1 = *reinterpret_cast<const uint4 *>(rf + q + 4);
+        rv0 = *reinterpret_cast<const uint4 *>(rr + q);
+        rv1 = *reinterpret_cast<const uint4 *>(rr + q + 4);
+        uint32_t b[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = q + j < n ? src[q + j] : 0u;
+        bv0 = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+        bv1 = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+    }
+    __device__ static uint32_t pick4(const uint4 &v, uint32_t l, uint32_t e)   // dword e (0..3) of lane l
+    {
+        const uint32_t a = lane_val(v.x, l), b = lane_val(v.y, l), c = lane_val(v.z, l), d = lane_val(v.w, l);
+        return e == 0 ? a : e == 1 ? b : e == 2 ? c : d;
+    }
+    __device__ uint32_t u32_at(const uint4 &v0, const uint4 &v1, uint32_t p)
+    {
+        const uint32_t off = p - base, l = off >> 3, e = off & 7;
+        return e < 4 ? pick4(v0, l, e) : pick4(v1, l, e - 4);
     }
 
     // ---- bit output ----------------------------------------------------
@@ -195,120 +388,68 @@ struct Wave {
     }
 
     // ---- deflate_slow's Ops ----------------------------------------------
-    __device__ uint32_t byte(uint32_t p) { return wbyte(p); }
-    __device__ uint32_t idx_at(uint32_t p)
+    __device__ uint32_t byte(uint32_t p)
     {
-        const uint32_t b = p & ~63u;
-        if (b != wbase) {
-            wbase = b;
-            const uint32_t q = b + lane_id();
-            idxw = q < n ? ld_l2(idx + q) : 0u;
-        }
-        return lane_val(idxw, p - b);
+        window(p);
+        const uint32_t off = p - base, l = off >> 3, e = off & 7;
+        const uint32_t w = e < 4 ? lane_val(bv0, l) : lane_val(bv1, l);
+        return (w >> ((e & 3) * 8)) & 0xffu;
     }
+    // zlib's head[] as p is inserted (0 = NIL)
     __device__ uint32_t head(uint32_t p)
     {
-        const uint32_t ip = idx_at(p);
-        last_ip = ip;
-        if (ip == 0) return 0;
-        const uint32_t c = uni(ld_l2(sorted + (ip - 1)));
-        return hash_at(c) == hash_at(p) ? c : 0u;
+        window(p);
+        const uint32_t off = p - base, l = off >> 3, e = off & 7;
+        const uint32_t w = pick4(hv, l, e >> 1);
+        return (w >> ((e & 1) * 16)) & 0xffffu;
     }
-    __device__ void slide()
+    __device__ void slide() {}   // K2 compared against the slid window already
+    // longest_match from K2: the full chain's result, or the reduced chain's once prev_len >= good
+    __device__ bool longest(uint32_t p, uint32_t, uint32_t prev_len, uint32_t, uint32_t, uint32_t, uint32_t &len,
+                            uint32_t &pos)
     {
-        for (uint32_t P = n + lane_id(); P < n + MAX_MATCH; P += 64) win()[P] = win()[P - WSIZE];
-        wave_sync();
-    }
-    // common prefix of the strings at a and b, up to MAX_MATCH: one wave-wide compare
-    __device__ uint32_t wave_lcp(uint32_t a, uint32_t b)
-    {
-        const uint32_t x = ld4(a + 4 * lane_id()) ^ ld4(b + 4 * lane_id());
-        const uint64_t m = __ballot(x != 0);
-        if (m) {
-            const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
-            return 4 * f + ((uint32_t)__builtin_ctz(lane_val(x, f)) >> 3);
-        }
-        uint32_t l = 256;
-        if (wbyte(a + 256) == wbyte(b + 256)) l = wbyte(a + 257) == wbyte(b + 257) ? 258 : 257;
-        return l;
-    }
-    __device__ uint32_t lane_lcp(uint32_t a, uint32_t b)
-    {
-        uint32_t l = 0;
-        while (l < (uint32_t)MAX_MATCH) {
-            const uint32_t x = ld4(a + l) ^ ld4(b + l);
-            if (x) {
-                l += (uint32_t)__builtin_ctz(x) >> 3;
-                break;
-            }
-            l += 4;
-        }
-        return min(l, (uint32_t)MAX_MATCH);
-    }
-    // longest_match: the first candidate (chain order) reaching max(nice, prev_len+1),
-    // else the first reaching the longest length found, if longer than prev_len
-    __device__ bool longest(uint32_t p, uint32_t hd, uint32_t prev_len, uint32_t chain, uint32_t nice,
-                            uint32_t limit, uint32_t &len, uint32_t &pos)
-    {
-        const uint32_t T = max(nice, prev_len + 1);
-        const uint32_t l1 = wave_lcp(hd, p);
-        if (l1 >= T) {
-            len = l1;
-            pos = hd;
-            return true;
-        }
-        const uint32_t hp = hash_at(p), ip = last_ip;
-        uint32_t best = prev_len, bpos = 0;
-        bool found = false;
-        for (uint32_t b = 0; b < chain; b += 64) {
-            const uint32_t gk = b + lane_id();
-            bool v = gk < chain && gk < ip;
-            uint32_t c = v ? (uint32_t)ld_l2(sorted + (ip - 1 - gk)) : 0u;
-            v = v && (gk == 0 || c > limit) && hash_at(c) == hp;
-            const uint64_t stop = __ballot(!v);
-            const uint32_t nv = stop ? (uint32_t)__ffsll((unsigned long long)stop) - 1 : 64u;
-            v = lane_id() < nv;
-            const uint32_t l = v ? (gk == 0 ? l1 : lane_lcp(c, p)) : 0u;
-            const uint64_t hit = __ballot(v && l >= T);
-            if (hit) {
-                const uint32_t k = (uint32_t)__ffsll((unsigned long long)hit) - 1;
-                len = lane_val(l, k);
-                pos = lane_val(c, k);
-                return true;
-            }
-            const uint32_t m = uni(wave_max(l));
-            if (m > best) {
-                const uint32_t k = (uint32_t)__ffsll((unsigned long long)__ballot(v && l == m)) - 1;
-                best = m;
-                bpos = lane_val(c, k);
-                found = true;
-            }
-            if (nv < 64) break;
-        }
-        len = best;
-        pos = bpos;
-        return found;
+        window(p);
+        const uint32_t r = prev_len >= good ? u32_at(rv0, rv1, p) : u32_at(fv0, fv1, p);
+        len = r >> 16;
+        pos = p - (r & 0xffffu);
+        return len > prev_len;
     }
     __device__ bool tally(uint32_t dist, uint32_t lc)
     {
-        if (lane_id() == 0) {
-            syms[nsym] = dist << 8 | lc;
-            dfl::tally(T, dist, lc);
-        }
+        if (lane_id() == 0) syms[nsym] = dist << 8 | lc;   // counted at flush
         ++nsym;
         return nsym == (uint32_t)LIT_BUFSIZE - 1;
     }
     __device__ void init_freqs()
     {
-        for (uint32_t i = lane_id(); i < (uint32_t)L_CODES; i += 64) sm.lfreq[i] = i == END_BLOCK ? 1 : 0;
-        if (lane_id() < (uint32_t)D_CODES) sm.dfreq[lane_id()] = 0;
+        for (uint32_t i = lane_id(); i < (uint32_t)L_CODES; i += 64) sm.lhist[i] = 0;
+        if (lane_id() < (uint32_t)D_CODES) sm.dhist[lane_id()] = 0;
         if (lane_id() < (uint32_t)BL_CODES) sm.bfreq[lane_id()] = 0;
+        wave_sync();
+    }
+    // _tr_tally's counts for the whole block at once (LDS atomics), then init_block's END_BLOCK
+    __device__ void count_block()
+    {
+        for (uint32_t i = lane_id(); i < nsym; i += 64) {
+            const uint32_t sy = ld_l2(syms + i), dist = sy >> 8, lc = sy & 0xff;
+            if (dist == 0) {
+                atomicAdd(&sm.lhist[lc], 1u);
+            } else {
+                atomicAdd(&sm.lhist[length_code((int)lc) + 257], 1u);
+                atomicAdd(&sm.dhist[dist_code((int)(dist - 1))], 1u);
+            }
+        }
+        wave_sync();
+        for (uint32_t i = lane_id(); i < (uint32_t)L_CODES; i += 64)
+            sm.lfreq[i] = (uint16_t)(sm.lhist[i] + (i == END_BLOCK ? 1u : 0u));
+        if (lane_id() < (uint32_t)D_CODES) sm.dfreq[lane_id()] = (uint16_t)sm.dhist[lane_id()];
         wave_sync();
     }
     __device__ void flush(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
     {
         __threadfence();   // the block's symbols (lane 0's stores) before the other lanes read them
         wave_sync();
+        count_block();
         if (lane_id() == 0) {
             int max_blindex = 0;
             const int kind = plan_block(T, stored_len, buf_ok, max_blindex);
@@ -333,7 +474,7 @@ struct Wave {
         if (kind == 0) {
             for (uint32_t i = 0; i < stored_len; i += 64) {
                 const uint32_t q = i + lane_id();
-                emit_par(q < stored_len ? wbyte(block_start + q) : 0u, q < stored_len ? 8u : 0u);
+                emit_par(q < stored_len ? (uint32_t)src[block_start + q] : 0u, q < stored_len ? 8u : 0u);
             }
         } else {
             if (kind == 1) {
@@ -362,106 +503,28 @@ struct Wave {
     }
 };
 
-// Phase A: sorted[] / idx[] (the chains of every position) and the adler32 sums
-__device__ void hash_order(DflSmem &sm, const uint8_t *src, uint32_t n, uint16_t *idx, uint16_t *sorted)
+__global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+                                                       int32_t strip_bytes, int32_t spf, int32_t level,
+                                                       uint8_t *__restrict__ out, int64_t slot_bytes,
+                                                       int32_t *__restrict__ sizes, uint8_t *__restrict__ ws,
+                                                       int64_t s0)
 {
+    __shared__ __attribute__((aligned(16))) ParseSmem sm;
+    const int64_t s = s0 + blockIdx.x;
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s);
     const uint32_t lane = lane_id();
-    for (uint32_t i = lane; i < (1u << 14); i += 64) sm.u.cnt[i] = 0;
-    wave_sync();
-    const uint32_t np = n >= 3 ? n - 2 : 0;   // positions 0..n-3 are inserted
-    auto hash_g = [&](uint32_t p) {
-        return (((uint32_t)src[p] << 10) ^ ((uint32_t)src[p + 1] << 5) ^ (uint32_t)src[p + 2]) & 0x7fffu;
-    };
-    for (uint32_t p = lane; p < np; p += 64) {
-        const uint32_t h = hash_g(p);
-        atomicAdd(&sm.u.cnt[h >> 1], 1u << ((h & 1) * 16));
-    }
-    wave_sync();
-    // exclusive scan of the 32768 counters (each < 65536 in total: u16 starts)
-    uint32_t s = 0;
-    for (uint32_t i = 0; i < 256; ++i) {
-        const uint32_t w = sm.u.cnt[lane * 256 + i];
-        s += (w & 0xffffu) + (w >> 16);
-    }
-    uint32_t tot;
-    uint32_t run = excl_scan(s, tot);
-    for (uint32_t i = 0; i < 256; ++i) {
-        const uint32_t w = sm.u.cnt[lane * 256 + i];
-        const uint32_t c0 = w & 0xffffu, c1 = w >> 16;
-        sm.u.cnt[lane * 256 + i] = run | ((run + c0) << 16);
-        run += c0 + c1;
-    }
-    wave_sync();
-    // ordered scatter, 64 positions at a time
-    for (uint32_t p0 = 0; p0 < np; p0 += 64) {
-        const uint32_t p = p0 + lane;
-        const bool v = p < np;
-        const uint32_t h = v ? hash_g(p) : 0u;
-        uint64_t rem = __ballot(v), mine = 0;
-        while (rem) {
-            const uint32_t l = (uint32_t)__ffsll((unsigned long long)rem) - 1;
-            const uint32_t hl = lane_val(h, l);
-            const uint64_t m = __ballot(v && h == hl);
-            if (v && h == hl) mine = m;
-            rem &= ~m;
-        }
-        if (v) {
-            const uint32_t rank = (uint32_t)__popcll(mine & ((1ull << lane) - 1));
-            const uint32_t sh = (h & 1) * 16;
-            const uint32_t slot = ((sm.u.cnt[h >> 1] >> sh) & 0xffffu) + rank;
-            idx[p] = (uint16_t)slot;
-            sorted[slot] = (uint16_t)p;
-            if (rank == 0) atomicAdd(&sm.u.cnt[h >> 1], (uint32_t)__popcll(mine) << sh);
-        }
-        wave_sync();
-    }
-    __threadfence();
-    wave_sync();
-}
-
-__global__ __launch_bounds__(64) void zlib_strips_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
-                                                        int32_t strip_bytes, int32_t spf, int32_t level,
-                                                        uint8_t *__restrict__ out, int64_t slot_bytes,
-                                                        int32_t *__restrict__ sizes, uint8_t *__restrict__ ws)
-{
-    __shared__ __attribute__((aligned(16))) DflSmem sm;
-    const int64_t s = blockIdx.x;
-    const int64_t f = s / spf, k = s - f * spf;
-    const int64_t off = k * (int64_t)strip_bytes;
-    const uint32_t n = (uint32_t)min((int64_t)strip_bytes, frame_bytes - off);
-    const uint8_t *src = in + f * frame_bytes + off;
-    uint8_t *w = ws + s * kWsPerStrip;
-    uint16_t *idx = reinterpret_cast<uint16_t *>(w);
-    uint16_t *sorted = idx + MAX_STRIP;
-    uint32_t *syms = reinterpret_cast<uint32_t *>(sorted + MAX_STRIP);
     Config cfg;
     level_config(level, cfg);
-
-    hash_order(sm, src, n, idx, sorted);
-
-    // adler32 sums; the window: the strip, then zeros (fill_window's high_water zeroing)
-    const uint32_t lane = lane_id();
-    uint64_t sb = 0, swb = 0;
-    uint8_t *win = reinterpret_cast<uint8_t *>(sm.u.win32);
-    for (uint32_t p = lane; p < (uint32_t)kWinBytes; p += 64) {
-        const uint32_t b = p < n ? src[p] : 0u;
-        win[p] = (uint8_t)b;
-        sb += b;
-        swb += (uint64_t)(n - min(p, n)) * b;
-    }
-    for (int d = 32; d >= 1; d >>= 1) {
-        sb += __shfl_xor(sb, d, 64);
-        swb += __shfl_xor(swb, d, 64);
-    }
     for (uint32_t i = lane; i < (uint32_t)kStgWords; i += 64) sm.stg[i] = 0;
-    Wave wv(sm, src, n, idx, sorted, syms, reinterpret_cast<uint32_t *>(out + s * slot_bytes),
+    Wave wv(sm, S.src, S.n, S.ws, (uint32_t)cfg.good, reinterpret_cast<uint32_t *>(out + s * slot_bytes),
             (uint32_t)(slot_bytes >> 2));
-    wv.init_freqs();   // includes the barrier for the window and the staging words
+    wv.init_freqs();   // includes the barrier for the staging words
 
     const uint32_t hdr = zlib_header(level);
     wv.emit_par(lane == 0 ? ((hdr >> 8) | ((hdr & 0xffu) << 8)) : 0u, lane == 0 ? 16u : 0u);
-    deflate_slow(wv, n, cfg);
-    const uint32_t ad = adler32_from_sums(sb, swb, n);
+    deflate_slow(wv, S.n, cfg);
+    const uint64_t *sums = reinterpret_cast<const uint64_t *>(S.ws + kSumOff);
+    const uint32_t ad = adler32_from_sums(sums[0], sums[1], S.n);
     const uint32_t be = (ad >> 24) | ((ad >> 8) & 0xff00u) | ((ad << 8) & 0xff0000u) | (ad << 24);
     wv.emit_par(lane == 0 ? be : 0u, lane == 0 ? 32u : 0u);
     if (wv.bitpos & 31) wv.store_words(wv.bitpos >> 5, 1);
@@ -507,16 +570,29 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     if (slot_bytes < vcf_zlib_bound(strip_bytes) || (slot_bytes & 3))
         return set_error(VCF_ERR_INVALID, "slot_bytes %lld: need a multiple of 4 >= vcf_zlib_bound(%d) = %lld",
                          (long long)slot_bytes, strip_bytes, (long long)vcf_zlib_bound(strip_bytes));
-    if (((uintptr_t)out_dev & 3) || ((uintptr_t)ws_dev & 3) || ((uintptr_t)sizes_dev & 3))
-        return set_error(VCF_ERR_INVALID, "out_dev, sizes_dev and ws_dev must be 4-byte aligned");
+    if (((uintptr_t)out_dev & 3) || ((uintptr_t)ws_dev & 15) || ((uintptr_t)sizes_dev & 3))
+        return set_error(VCF_ERR_INVALID, "out_dev and sizes_dev must be 4-byte aligned, ws_dev 16-byte aligned");
     if (n_frames == 0 || frame_bytes == 0) return VCF_OK;
     const int64_t spf = vcf_zlib_strip_count(frame_bytes, strip_bytes);
     const int64_t total = spf * n_frames;
-    if (total > (int64_t)INT32_MAX) return set_error(VCF_ERR_INVALID, "too many strips");
-    hipLaunchKernelGGL(zlib_strips_kernel, dim3((unsigned)total), dim3(64), 0, (hipStream_t)stream, in_dev,
-                       frame_bytes, strip_bytes, (int32_t)spf, level, out_dev, slot_bytes, sizes_dev,
-                       (uint8_t *)ws_dev);
-    return hip_check(hipGetLastError(), "zlib_strips_kernel launch");
+    hipStream_t st = (hipStream_t)stream;
+    const int chunks = (int)((std::min<int64_t>(strip_bytes, frame_bytes) + kChunk - 1) / kChunk);
+    for (int64_t s0 = 0; s0 < total; s0 += 65535) {   // grid limits: strips [s0, s0 + cnt) per round
+        const unsigned cnt = (unsigned)std::min<int64_t>(65535, total - s0);
+        hipLaunchKernelGGL(zlib_head_kernel, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
+                           (int32_t)spf, (uint8_t *)ws_dev, s0);
+        int rc = hip_check(hipGetLastError(), "zlib_head_kernel launch");
+        if (rc != VCF_OK) return rc;
+        hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, st, in_dev,
+                           frame_bytes, strip_bytes, (int32_t)spf, level, (uint8_t *)ws_dev, s0);
+        rc = hip_check(hipGetLastError(), "zlib_match_kernel launch");
+        if (rc != VCF_OK) return rc;
+        hipLaunchKernelGGL(zlib_parse_kernel, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
+                           (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, (uint8_t *)ws_dev, s0);
+        rc = hip_check(hipGetLastError(), "zlib_parse_kernel launch");
+        if (rc != VCF_OK) return rc;
+    }
+    return VCF_OK;
 }
 
 }  // extern "C"

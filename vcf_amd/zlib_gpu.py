@@ -47,6 +47,39 @@ class StripDeflater:
             b = self._bufs[name] = DeviceBuffer(max(int(nbytes), 16))
         return b
 
+    def launch(self, src: DeviceBuffer, n_frames: int, frame_bytes: int, strip_bytes: int, level: int = LEVEL,
+               offset: int = 0, stream: Stream | None = None) -> None:
+        """Queue the deflate of every strip on `stream` (default: the
+        deflater's own); strip s's stream then sits at byte s * slot of
+        `out`.  sizes() waits for it.  The caller holds the deflater (one
+        batch at a time)."""
+        if stream is None:
+            if self._stream is None:
+                self._stream = Stream()
+            stream = self._stream
+        self.stream = stream
+        self.spf = strip_count(frame_bytes, strip_bytes)
+        self.n_frames = int(n_frames)
+        self.total = self.spf * self.n_frames
+        self.slot = bound(strip_bytes)
+        if self.total == 0:
+            return
+        self.out = self._buf("out", self.total * self.slot)
+        self._sizes = self._buf("sizes", self.total * 4)
+        ws = self._buf("ws", int(L.lib().vcf_zlib_workspace(self.total)))
+        L.call("vcf_zlib_strips", src.address(offset), int(n_frames), int(frame_bytes), int(strip_bytes),
+               int(level), self.out.ptr, self.slot, self._sizes.ptr, ws.ptr, stream.handle)
+
+    def sizes(self) -> np.ndarray:
+        """Compressed size of every strip of the last launch (int32, frame-major)."""
+        sz = np.empty(self.total, np.int32)
+        if self.total:
+            self._sizes.download(sz, self.stream)
+        self.stream.synchronize()
+        if (sz < 0).any():
+            raise RuntimeError("vcf_zlib_strips: a strip overflowed its slot")
+        return sz
+
     def deflate_device(self, src: DeviceBuffer, n_frames: int, frame_bytes: int, strip_bytes: int,
                        level: int = LEVEL, offset: int = 0, stream: Stream | None = None):
         """-> list over frames of lists of strip streams (bytes).  `src` holds
@@ -54,25 +87,11 @@ class StripDeflater:
         `stream` (default: the deflater's own) is complete before the call
         returns."""
         with self._lock:
-            if stream is None:
-                if self._stream is None:
-                    self._stream = Stream()
-                stream = self._stream
-            spf = strip_count(frame_bytes, strip_bytes)
-            total = spf * int(n_frames)
+            self.launch(src, n_frames, frame_bytes, strip_bytes, level, offset, stream)
+            total, spf, slot, stream = self.total, self.spf, self.slot, self.stream
             if total == 0:
                 return [[] for _ in range(int(n_frames))]
-            slot = bound(strip_bytes)
-            out = self._buf("out", total * slot)
-            sizes = self._buf("sizes", total * 4)
-            ws = self._buf("ws", int(L.lib().vcf_zlib_workspace(total)))
-            L.call("vcf_zlib_strips", src.address(offset), int(n_frames), int(frame_bytes), int(strip_bytes),
-                   int(level), out.ptr, slot, sizes.ptr, ws.ptr, stream.handle)
-            sz = np.empty(total, np.int32)
-            sizes.download(sz, stream)
-            stream.synchronize()
-            if (sz < 0).any():
-                raise RuntimeError("vcf_zlib_strips: a strip overflowed its slot")
+            sz = self.sizes()
             # pack the streams on the device, one download
             offs = np.zeros(total + 1, np.int64)
             np.cumsum(sz, out=offs[1:])
@@ -83,7 +102,7 @@ class StripDeflater:
             tb = self._buf("table", table.nbytes)
             tb.upload(table, stream)
             packed = self._buf("packed", int(offs[-1]))
-            copy_pieces(out, tb, total, packed, stream)
+            copy_pieces(self.out, tb, total, packed, stream)
             host = np.empty(int(offs[-1]), np.uint8)
             if host.size:
                 packed.download(host, stream)
