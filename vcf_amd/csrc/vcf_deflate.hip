@@ -5,23 +5,28 @@
 //
 // zlib's serial loop is split where its data dependences allow (DESIGN.md
 // §4.9; the restatement and its proofs of equivalence are vcf_deflate.h):
-//   K1 zlib_head_kernel, one wave per strip: the hash insertion of every
-//      position in order -- hd[p] = zlib's head[] when p is inserted (the
-//      newest earlier position with p's hash, 0 = NIL), i.e. the hash
-//      chains, which do not depend on the parse -- and the adler32 sums.
-//      64 positions per step with an exact same-hash lane mask; the 32768
-//      heads in LDS.
-//   K2 zlib_match_kernel, one thread per position, 256 per workgroup and
-//      1024 positions per workgroup: longest_match at p for both chain
-//      limits deflate_slow can use (max_chain, and max_chain >> 2 once
-//      prev_length >= good_match).  Every call whose result can matter has
-//      the early-exit threshold min(nice, lookahead), independent of
-//      prev_length (vcf_deflate.h), so two (length, distance) pairs per
-//      position carry all of it; "found" is length > prev_length, decided
-//      in K3.  The window (32 KB back + the workgroup's span) in LDS, the
-//      chains walked through hd[] (L2), the bytes past the strip's end as
-//      zlib's window holds them (zeros, or after its one slide the stale
-//      copy 32 KB back).
+//   K1 zlib_order_kernel, one wave per strip: the positions 0..n-3 bucketed
+//      by zlib's hash, stably (histogram, scan, ordered scatter 64 positions
+//      at a time with an exact same-hash lane mask; 32768 counters in LDS).
+//      zlib inserts every position, in order, and a position's hash depends
+//      on its 3 bytes only, so the hash chains do not depend on the parse:
+//      the chain of p is the earlier positions of p's bucket, newest first
+//      -- contiguous in sorted[].  A second ordered pass writes hd[p], the
+//      chain's head (zlib's head[] as p is inserted).  Also the adler32 sums.
+//   K2 zlib_match_kernel, 16 consecutive positions per thread, 4096 per
+//      workgroup: longest_match at p for both chain limits deflate_slow can
+//      use (max_chain, and max_chain >> 2 once prev_length >= good_match).
+//      Every call whose result can matter has the early-exit threshold
+//      min(nice, lookahead), independent of prev_length (vcf_deflate.h), so
+//      two (length, distance) pairs per position carry all of it; "found" is
+//      length > prev_length, decided in K3.  K2a resolves a position from
+//      its chain head alone when that is exact (a nice match, or inside a
+//      run of one byte value reaching max_chain back) and lists the others;
+//      K2b walks the listed chains, one position per wave, 64 candidates
+//      from sorted[] per step, zlib's scan_end test before a full compare.
+//      The window (32 KB back + the span, K2b the whole strip) in LDS, the
+//      bytes past the strip's end as zlib's window holds them (zeros, or
+//      after its one slide the stale copy 32 KB back).
 //   K3 zlib_parse_kernel, one wave per strip: deflate_slow with uniform state
 //      over 512-position register windows of hd[], the K2 results and the
 //      bytes; per block the trees built by lane 0 (trees.c restated), the
@@ -44,16 +49,30 @@ namespace {
 using namespace dfl;
 
 constexpr int kStgWords = 128;       // bit staging for one 64-symbol step (<= 3072 + 31 bits)
-constexpr int kChunk = 1024;         // K2: positions per workgroup
+constexpr int kStage = 1024;         // K1: bytes staged per step
 constexpr int kK2Threads = 256;
+constexpr int kPer = 16;             // K2: consecutive positions per thread
+constexpr int kChunk = kK2Threads * kPer;                 // K2: positions per workgroup
 constexpr int kK2Win = WSIZE + kChunk + MAX_MATCH + 64;   // K2's LDS window
-// workspace per strip: hd u16, full- and reduced-chain results u32, symbols u32, adler sums
-constexpr int64_t kHdOff = 0;
-constexpr int64_t kRfOff = kHdOff + (int64_t)MAX_STRIP * 2;
+// workspace per strip: idx (u16; K2 turns it into hd, zlib's head[] per position),
+// sorted (u16), hd (u16), K2's worklist (u16), full- and reduced-chain results (u32),
+// symbols (u32), adler sums
+constexpr int64_t kIdxOff = 0;
+constexpr int64_t kSortOff = kIdxOff + (int64_t)MAX_STRIP * 2;
+constexpr int64_t kHdOff = kSortOff + (int64_t)MAX_STRIP * 2;
+constexpr int64_t kListOff = kHdOff + (int64_t)MAX_STRIP * 2;
+constexpr int64_t kRfOff = kListOff + (int64_t)MAX_STRIP * 2;
 constexpr int64_t kRrOff = kRfOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSymOff = kRrOff + (int64_t)MAX_STRIP * 4;
-constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;
-constexpr int64_t kWsPerStrip = kSumOff + 16;
+constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;   // adler sums (2 x u64), worklist length (u32)
+constexpr int64_t kWsPerStrip = kSumOff + 32;
+constexpr int kK2bThreads = 1024;    // K2b: 16 waves per strip, one listed position per wave at a time
+// A strip is parsed LAZY (on demand, zlib's order of work) when K1 finds fewer than
+// one distinct hash per kLazyDiv positions among its 64-position groups: such
+// repetitive content leaves most positions inside long matches, which zlib -- and
+// the lazy parse -- never search, while K2 would search them all.  Both orders
+// produce the same bytes; only the time differs.
+constexpr uint32_t kLazyDiv = 4;
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -88,6 +107,10 @@ struct Strip {
     uint32_t n;
     uint8_t *ws;
 };
+__device__ __forceinline__ bool strip_lazy(const Strip &S)
+{
+    return *reinterpret_cast<const uint32_t *>(S.ws + kSumOff + 20) != 0;
+}
 __device__ __forceinline__ Strip strip_of(const uint8_t *in, int64_t frame_bytes, int32_t strip_bytes, int32_t spf,
                                           uint8_t *ws, int64_t s)
 {
@@ -96,41 +119,114 @@ __device__ __forceinline__ Strip strip_of(const uint8_t *in, int64_t frame_bytes
     return {in + f * frame_bytes + off, (uint32_t)min((int64_t)strip_bytes, frame_bytes - off), ws + s * kWsPerStrip};
 }
 
-// ---- K1: hash chains (zlib's head[] at each insertion) and adler32 sums ----
-struct HeadSmem {
-    uint16_t head[1 << 15];
-    uint8_t stage[kChunk + 64];
+// ---- K1: hash-bucket order of the positions, and the adler32 sums ----------
+// sorted[] lists the positions 0..n-3 bucket by bucket (buckets in hash order,
+// positions increasing inside a bucket) and idx[p] is p's slot, so zlib's chain
+// of p -- the earlier positions with p's hash, newest first -- is
+// sorted[idx[p]-1], sorted[idx[p]-2], ... while the hash stays p's; hd[p] is
+// its first element (zlib's head[] as p is inserted, 0 = NIL).
+struct OrderSmem {
+    uint32_t cnt[1 << 14];              // 32768 u16 counters / cursors, packed in pairs
+    uint8_t stage[kStage + 64];
 };
 
-__global__ __launch_bounds__(64) void zlib_head_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
-                                                      int32_t strip_bytes, int32_t spf, uint8_t *__restrict__ ws,
-                                                      int64_t s0)
+__device__ __forceinline__ void stage_chunk(uint8_t *stage, const uint8_t *src, uint32_t n, uint32_t c0)
 {
-    __shared__ __attribute__((aligned(16))) HeadSmem sm;
+    for (uint32_t j = lane_id(); j < (uint32_t)kStage + 2; j += 64) {
+        const uint32_t p = c0 + j;
+        stage[j] = p < n ? src[p] : 0u;
+    }
+}
+
+__global__ __launch_bounds__(64) void zlib_order_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+                                                       int32_t strip_bytes, int32_t spf, uint8_t *__restrict__ ws,
+                                                       int64_t s0)
+{
+    __shared__ __attribute__((aligned(16))) OrderSmem sm;
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0 + blockIdx.x);
+    uint16_t *idx = reinterpret_cast<uint16_t *>(S.ws + kIdxOff);
+    uint16_t *sorted = reinterpret_cast<uint16_t *>(S.ws + kSortOff);
     uint16_t *hd = reinterpret_cast<uint16_t *>(S.ws + kHdOff);
     const uint32_t lane = lane_id(), n = S.n;
     const uint32_t np = n >= 3 ? n - 2 : 0;   // positions 0..n-3 are inserted
-    for (uint32_t i = lane; i < (1u << 14); i += 64) reinterpret_cast<uint32_t *>(sm.head)[i] = 0;
+    for (uint32_t i = lane; i < (1u << 14); i += 64) sm.cnt[i] = 0;
     uint64_t sb = 0, swb = 0;
-    for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
-        wave_sync();   // the previous chunk's stage reads are done
-        for (uint32_t j = lane; j < (uint32_t)kChunk + 2; j += 64) {
-            const uint32_t p = c0 + j;
-            const uint32_t b = p < n ? S.src[p] : 0u;
-            sm.stage[j] = (uint8_t)b;
-            if (j < (uint32_t)kChunk) {
-                sb += b;
-                swb += (uint64_t)(p < n ? n - p : 0u) * b;
+    // histogram of the hashes (and the adler32 sums)
+    for (uint32_t c0 = 0; c0 < n; c0 += kStage) {
+        wave_sync();
+        stage_chunk(sm.stage, S.src, n, c0);
+        wave_sync();
+        for (uint32_t j = lane; j < (uint32_t)kStage; j += 64) {
+            const uint32_t p = c0 + j, b = sm.stage[j];
+            sb += b;
+            swb += (uint64_t)(p < n ? n - p : 0u) * b;
+            if (p < np) {
+                const uint32_t h = ((uint32_t)b << 10 ^ (uint32_t)sm.stage[j + 1] << 5 ^ sm.stage[j + 2]) & 0x7fffu;
+                atomicAdd(&sm.cnt[h >> 1], 1u << ((h & 1) * 16));
             }
         }
+    }
+    wave_sync();
+    // exclusive scan of the 32768 counters (each total < 65536: u16 starts)
+    uint32_t tsum = 0;
+    for (uint32_t i = 0; i < 256; ++i) {
+        const uint32_t w = sm.cnt[lane * 256 + i];
+        tsum += (w & 0xffffu) + (w >> 16);
+    }
+    uint32_t tot;
+    uint32_t run = excl_scan(tsum, tot);
+    for (uint32_t i = 0; i < 256; ++i) {
+        const uint32_t w = sm.cnt[lane * 256 + i];
+        const uint32_t c0 = w & 0xffffu, c1 = w >> 16;
+        const uint32_t st = run | ((run + c0) << 16);
+        sm.cnt[lane * 256 + i] = st;
+        run += c0 + c1;
+    }
+    // ordered scatter, 64 positions at a time, exact same-hash lane masks
+    uint32_t distinct = 0;   // sum over the groups of their distinct hashes
+    for (uint32_t c0 = 0; c0 < np; c0 += kStage) {
         wave_sync();
-        for (uint32_t g = 0; g < (uint32_t)kChunk && c0 + g < np; g += 64) {
+        stage_chunk(sm.stage, S.src, n, c0);
+        wave_sync();
+        for (uint32_t g = 0; g < (uint32_t)kStage && c0 + g < np; g += 64) {
             const uint32_t p = c0 + g + lane, j = g + lane;
             const bool v = p < np;
             const uint32_t h = ((uint32_t)sm.stage[j] << 10 ^ (uint32_t)sm.stage[j + 1] << 5 ^ sm.stage[j + 2]) & 0x7fffu;
             uint64_t rem = __ballot(v), mine = 0;
-            while (rem) {   // exact same-hash masks, one distinct hash per round
+            while (rem) {   // one distinct hash per round
+                ++distinct;
+                const uint32_t l = (uint32_t)__ffsll((unsigned long long)rem) - 1;
+                const uint32_t hl = lane_val(h, l);
+                const uint64_t m = __ballot(v && h == hl);
+                if (v && h == hl) mine = m;
+                rem &= ~m;
+            }
+            if (v) {
+                const uint32_t rank = (uint32_t)__popcll(mine & ((1ull << lane) - 1));
+                const uint32_t sh = (h & 1) * 16;
+                const uint32_t slot = ((sm.cnt[h >> 1] >> sh) & 0xffffu) + rank;
+                idx[p] = (uint16_t)slot;
+                sorted[slot] = (uint16_t)p;
+                if (rank == 0) atomicAdd(&sm.cnt[h >> 1], (uint32_t)__popcll(mine) << sh);
+            }
+            wave_sync();
+        }
+    }
+    // hd[p]: zlib's head[] as p is inserted -- the newest earlier position with
+    // p's hash (0 = NIL, as zlib's position 0 is), from a last-position table and
+    // the group's own same-hash lanes; K2 reads it coalesced
+    for (uint32_t i = lane; i < (1u << 14); i += 64) sm.cnt[i] = 0;
+    uint16_t *last = reinterpret_cast<uint16_t *>(sm.cnt);
+    for (uint32_t c0 = 0; c0 < np; c0 += kStage) {
+        wave_sync();
+        stage_chunk(sm.stage, S.src, n, c0);
+        wave_sync();
+        for (uint32_t g = 0; g < (uint32_t)kStage && c0 + g < np; g += 64) {
+            const uint32_t p = c0 + g + lane, j = g + lane;
+            const bool v = p < np;
+            const uint32_t h = ((uint32_t)sm.stage[j] << 10 ^ (uint32_t)sm.stage[j + 1] << 5 ^ sm.stage[j + 2]) & 0x7fffu;
+            uint64_t rem = __ballot(v), mine = 0;
+            while (rem) {
                 const uint32_t l = (uint32_t)__ffsll((unsigned long long)rem) - 1;
                 const uint32_t hl = lane_val(h, l);
                 const uint64_t m = __ballot(v && h == hl);
@@ -139,10 +235,10 @@ __global__ __launch_bounds__(64) void zlib_head_kernel(const uint8_t *__restrict
             }
             if (v) {
                 const uint64_t lower = mine & ((1ull << lane) - 1);
-                hd[p] = (uint16_t)(lower ? c0 + g + 63 - (uint32_t)__clzll((long long)lower) : (uint32_t)sm.head[h]);
+                hd[p] = (uint16_t)(lower ? c0 + g + 63 - (uint32_t)__clzll((long long)lower) : (uint32_t)last[h]);
             }
             wave_sync();
-            if (v && (mine >> lane) == 1) sm.head[h] = (uint16_t)p;   // the group's newest with this hash
+            if (v && (mine >> lane) == 1) last[h] = (uint16_t)p;   // the group's newest with this hash
             wave_sync();
         }
     }
@@ -154,10 +250,17 @@ __global__ __launch_bounds__(64) void zlib_head_kernel(const uint8_t *__restrict
         uint64_t *sums = reinterpret_cast<uint64_t *>(S.ws + kSumOff);
         sums[0] = sb;
         sums[1] = swb;
+        *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 16) = 0;   // K2's worklist length
+        *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = distinct * kLazyDiv < np ? 1u : 0u;   // parse order
     }
 }
 
 // ---- K2: longest_match at every position, both chain limits ----------------
+// A thread takes kPer consecutive positions.  zlib's own shortcuts, exact:
+// a candidate can only beat the best length L so far if it matches at bytes
+// L-1 and L (longest_match's scan_end test), and when the first candidate of
+// p+1 is the first candidate of p plus one, its common prefix is p's minus
+// one (one byte is checked when p's reached the MAX_MATCH cap).
 __global__ __launch_bounds__(kK2Threads) void zlib_match_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
                                                                int32_t strip_bytes, int32_t spf, int32_t level,
                                                                uint8_t *__restrict__ ws, int64_t s0)
@@ -167,80 +270,256 @@ __global__ __launch_bounds__(kK2Threads) void zlib_match_kernel(const uint8_t *_
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0 + blockIdx.y);
     const uint32_t n = S.n, p0 = blockIdx.x * kChunk;
     const uint32_t np = n >= 3 ? n - 2 : 0;
-    if (p0 >= np) return;
+    if (p0 >= np || strip_lazy(S)) return;
     Config cfg;
     level_config(level, cfg);
     const uint16_t *hd = reinterpret_cast<const uint16_t *>(S.ws + kHdOff);
+    uint16_t *list = reinterpret_cast<uint16_t *>(S.ws + kListOff);
+    uint32_t *nlist = reinterpret_cast<uint32_t *>(S.ws + kSumOff + 16);
     uint32_t *rf = reinterpret_cast<uint32_t *>(S.ws + kRfOff);
     uint32_t *rr = reinterpret_cast<uint32_t *>(S.ws + kRrOff);
-    // window [w0, w0 + span): 32 KB back (every candidate is > p - MAX_DIST) and the
+    // window [w0, wend): 32 KB back (every candidate is > p - MAX_DIST) and the
     // chunk's strings; past n the bytes zlib's window holds there: zeros before its
-    // slide, after it (at strstart >= S_post) the stale copy WSIZE back
+    // slide, after it (at strstart >= slide_at) the stale copy WSIZE back
     const uint32_t w0 = p0 > (uint32_t)WSIZE ? p0 - WSIZE : 0u;
     const uint32_t wend = min(np, p0 + kChunk) + MAX_MATCH + 16;
     const uint32_t slide_at = n == (uint32_t)MAX_STRIP ? WSIZE + MAX_DIST + 1 : WSIZE + MAX_DIST;
-    for (uint32_t p = w0 + threadIdx.x; p < wend; p += kK2Threads) win[p - w0] = p < n ? S.src[p] : 0u;
+    if ((((uintptr_t)(S.src + w0)) & 3) == 0 && wend <= n) {
+        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(S.src + w0);
+        for (uint32_t q = threadIdx.x; q < (wend - w0 + 3) / 4; q += kK2Threads)
+            win32[q] = w0 + 4 * q + 4 <= n ? s32[q] : 0u;
+        for (uint32_t q = threadIdx.x; q < 4; q += kK2Threads) win32[(wend - w0 + 3) / 4 + q] = 0;
+    } else {
+        for (uint32_t p = w0 + threadIdx.x; p < wend + 16; p += kK2Threads) win[p - w0] = p < n ? S.src[p] : 0u;
+    }
     __syncthreads();
-    const uint32_t cfull = (uint32_t)cfg.chain, cred = (uint32_t)cfg.chain >> 2;
-    for (uint32_t p = p0 + threadIdx.x; p < min(np, p0 + kChunk); p += kK2Threads) {
-        uint32_t cur = hd[p];
+    const uint32_t cfull = (uint32_t)cfg.chain;
+    auto ld4 = [&](uint32_t a) {
+        return __builtin_amdgcn_alignbyte(win32[(a >> 2) + 1], win32[a >> 2], a & 3);
+    };
+    auto lcp_fast = [&](uint32_t a, uint32_t b, uint32_t from) -> uint32_t {   // window offsets; from: bytes known equal
+        uint32_t len = from;
+        while (len < (uint32_t)MAX_MATCH) {
+            uint32_t x = 0, q = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t xu = ld4(a + len + 4 * u) ^ ld4(b + len + 4 * u);
+                if (x == 0) {
+                    x = xu;
+                    q = 4 * u;
+                }
+            }
+            if (x) {
+                len += q + ((uint32_t)__builtin_ctz(x) >> 3);
+                break;
+            }
+            len += 16;
+        }
+        return min(len, (uint32_t)MAX_MATCH);
+    };
+    // the thread's positions' chain heads (zlib's head[] as each is inserted), one round of loads
+    const uint32_t pbeg = p0 + threadIdx.x * kPer;
+    const uint32_t pn = pbeg < np ? min((uint32_t)kPer, np - pbeg) : 0u;
+    uint32_t c1v[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) c1v[u] = (uint32_t)u < pn ? (uint32_t)hd[pbeg + u] : 0u;
+    uint32_t prev_c = 0, prev_l = 0;   // the previous position's first candidate and its common prefix
+    // run: how many bytes before p equal p's (counted up to cfull)
+    uint32_t run = 0;
+    if (pn) {
+        const uint32_t b = win[pbeg - w0];
+        while (run < cfull && pbeg - run > w0 && win[pbeg - run - 1 - w0] == b) ++run;
+    }
+#pragma unroll 1
+    for (uint32_t u = 0; u < pn; ++u) {
+        const uint32_t p = pbeg + u;
+        if (u) run = win[p - w0] == win[p - 1 - w0] ? min(run + 1, cfull) : 0u;
+        // (register arrays indexed by a loop variable: select through a switch-free scan)
+        uint32_t cur = 0;
+#pragma unroll
+        for (int t = 0; t < kPer; ++t)
+            if ((uint32_t)t == u) cur = c1v[t];
         uint32_t rfull = 0, rred = 0;
         if (cur != 0 && p - cur <= (uint32_t)MAX_DIST) {
             const uint32_t nice = min((uint32_t)cfg.nice, n - p);
-            const uint32_t limit = p > (uint32_t)MAX_DIST ? p - MAX_DIST : 0u;
             const bool tail = p + MAX_MATCH + 16 > n;     // compares may read past the end
             const bool post = p >= slide_at;              // ... as zlib's window holds it after the slide
-            uint32_t bf = 0, bfp = 0, br = 0, brp = 0;
-            uint32_t k = 0;
-            for (;;) {
-                // common prefix of the strings at cur and p, capped at MAX_MATCH
-                uint32_t len = 0;
-                if (!tail) {
-                    const uint32_t a = cur - w0, b = p - w0;
-                    while (len < (uint32_t)MAX_MATCH) {
-                        uint32_t x = 0, q = 0;
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const uint32_t aa = a + len + 4 * u, bb = b + len + 4 * u;
-                            const uint32_t va = __builtin_amdgcn_alignbyte(win32[(aa >> 2) + 1], win32[aa >> 2], aa & 3);
-                            const uint32_t vb = __builtin_amdgcn_alignbyte(win32[(bb >> 2) + 1], win32[bb >> 2], bb & 3);
-                            if (x == 0) {
-                                x = va ^ vb;
-                                q = 4 * u;
-                            }
-                        }
-                        if (x) {
-                            len += q + ((uint32_t)__builtin_ctz(x) >> 3);
-                            break;
-                        }
-                        len += 16;
-                    }
-                    len = min(len, (uint32_t)MAX_MATCH);
-                } else {
-                    auto vb = [&](uint32_t P) -> uint32_t {
-                        if (P < n) return win[P - w0];
-                        return post ? (uint32_t)win[P - WSIZE - w0] : 0u;
-                    };
-                    while (len < (uint32_t)MAX_MATCH && vb(cur + len) == vb(p + len)) ++len;
-                }
-                if (len > bf) {
-                    bf = len;
-                    bfp = cur;
-                    if (k < cred) {
-                        br = len;
-                        brp = cur;
-                    }
-                    if (len >= nice) break;
-                }
-                if (++k >= cfull) break;
-                cur = hd[cur];
-                if (cur <= limit) break;
+            auto vb = [&](uint32_t P) -> uint32_t {
+                if (P < n) return win[P - w0];
+                return post ? (uint32_t)win[P - WSIZE - w0] : 0u;
+            };
+            auto lcp = [&](uint32_t c, uint32_t from) -> uint32_t {
+                if (!tail) return lcp_fast(c - w0, p - w0, from);
+                uint32_t len = from;
+                while (len < (uint32_t)MAX_MATCH && vb(c + len) == vb(p + len)) ++len;
+                return len;
+            };
+            uint32_t len;
+            if (!tail && cur == prev_c + 1 && prev_l > 0) {
+                len = prev_l < (uint32_t)MAX_MATCH ? prev_l - 1 : lcp(cur, MAX_MATCH - 1);
+            } else {
+                len = lcp(cur, 0);
+            }
+            prev_c = cur;
+            prev_l = len;
+            uint32_t bf = len, bfp = cur, br = len, brp = cur;
+            // Inside a run of one byte value b reaching cfull positions back with
+            // len >= 3 (p's bytes are b b b), the chain's first cfull candidates are
+            // p-1, ..., p-cfull (the only positions there, all b b b: p's hash) and
+            // each matches exactly up to the run's end, as the first does: no walk.
+            const bool in_run = cur == p - 1 && run >= cfull && len >= 3;
+            if (len < nice && !in_run && hd[cur] > (p > (uint32_t)MAX_DIST ? p - MAX_DIST : 0u)) {
+                // the rest of the chain may hold a longer match: K2b walks it (rf/rr keep
+                // the first candidate meanwhile)
+                list[atomicAdd(nlist, 1u)] = (uint16_t)p;
             }
             if (bf) rfull = bf << 16 | (p - bfp);
             if (br) rred = br << 16 | (p - brp);
+        } else {
+            prev_c = 0;
+            prev_l = 0;
         }
         rf[p] = rfull;
         rr[p] = rred;
+    }
+}
+
+// ---- K2b: the listed positions' chains, 64 candidates per wave step ----------
+// One workgroup of 16 waves per strip, the whole strip in LDS; a wave takes one
+// listed position at a time.  Lane t evaluates candidate k = 1 + t (+64 per
+// round) of the chain; only a candidate matching p at bytes len1-1 and len1 can
+// beat the first candidate's length len1 (longest_match's scan_end test), so
+// only those do the full compare.  The reductions keep zlib's order: the first
+// candidate reaching nice, else the first reaching the longest length.
+__global__ __launch_bounds__(kK2bThreads) void zlib_chain_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+                                                                int32_t strip_bytes, int32_t spf, int32_t level,
+                                                                uint8_t *__restrict__ ws, int64_t s0)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t win32[(MAX_STRIP + MAX_MATCH + 64) / 4];
+    uint8_t *win = reinterpret_cast<uint8_t *>(win32);
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0 + blockIdx.x);
+    const uint32_t n = S.n;
+    const uint32_t cnt = *reinterpret_cast<const uint32_t *>(S.ws + kSumOff + 16);
+    if (cnt == 0 || strip_lazy(S)) return;
+    Config cfg;
+    level_config(level, cfg);
+    const uint16_t *idx = reinterpret_cast<const uint16_t *>(S.ws + kIdxOff);
+    const uint16_t *sorted = reinterpret_cast<const uint16_t *>(S.ws + kSortOff);
+    const uint16_t *list = reinterpret_cast<const uint16_t *>(S.ws + kListOff);
+    uint32_t *rf = reinterpret_cast<uint32_t *>(S.ws + kRfOff);
+    uint32_t *rr = reinterpret_cast<uint32_t *>(S.ws + kRrOff);
+    const uint32_t wend = min(n + MAX_MATCH + 32, (uint32_t)(MAX_STRIP + MAX_MATCH + 60));
+    if (((uintptr_t)S.src & 3) == 0) {
+        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(S.src);
+        for (uint32_t q = threadIdx.x; q < wend / 4; q += kK2bThreads) win32[q] = 4 * q + 4 <= n ? s32[q] : 0u;
+        __syncthreads();
+        for (uint32_t p = (n & ~3u) + threadIdx.x; p < min(n, (n & ~3u) + 4); p += kK2bThreads) win[p] = S.src[p];
+    } else {
+        for (uint32_t p = threadIdx.x; p < wend; p += kK2bThreads) win[p] = p < n ? S.src[p] : 0u;
+    }
+    __syncthreads();
+    const uint32_t slide_at = n == (uint32_t)MAX_STRIP ? WSIZE + MAX_DIST + 1 : WSIZE + MAX_DIST;
+    const uint32_t cfull = (uint32_t)cfg.chain, cred = (uint32_t)cfg.chain >> 2;
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    for (uint32_t i = wave; i < cnt; i += kK2bThreads / 64) {
+        const uint32_t p = list[i];
+        const uint32_t ip = idx[p];
+        const uint32_t hp = ((uint32_t)win[p] << 10 ^ (uint32_t)win[p + 1] << 5 ^ win[p + 2]) & 0x7fffu;
+        const uint32_t r1 = rf[p], len1 = r1 >> 16, c1 = p - (r1 & 0xffffu);
+        const uint32_t nice = min((uint32_t)cfg.nice, n - p);
+        const uint32_t limit = p > (uint32_t)MAX_DIST ? p - MAX_DIST : 0u;
+        const bool post = p >= slide_at;
+        auto vb = [&](uint32_t P) -> uint32_t {   // the window as zlib's longest_match reads it
+            if (P < n) return win[P];
+            return post ? (uint32_t)win[P - WSIZE] : 0u;
+        };
+        const bool tail = p + MAX_MATCH + 16 > n;
+        auto lcp = [&](uint32_t c) -> uint32_t {
+            uint32_t len = 0;
+            if (!tail) {
+                while (len < (uint32_t)MAX_MATCH) {
+                    uint32_t x = 0, q = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t a = c + len + 4 * u, b = p + len + 4 * u;
+                        const uint32_t xu = __builtin_amdgcn_alignbyte(win32[(a >> 2) + 1], win32[a >> 2], a & 3) ^
+                                            __builtin_amdgcn_alignbyte(win32[(b >> 2) + 1], win32[b >> 2], b & 3);
+                        if (x == 0) {
+                            x = xu;
+                            q = 4 * u;
+                        }
+                    }
+                    if (x) {
+                        len += q + ((uint32_t)__builtin_ctz(x) >> 3);
+                        break;
+                    }
+                    len += 16;
+                }
+                return min(len, (uint32_t)MAX_MATCH);
+            }
+            while (len < (uint32_t)MAX_MATCH && vb(c + len) == vb(p + len)) ++len;
+            return len;
+        };
+        uint32_t bf = len1, bfp = c1, br = len1, brp = c1;
+        bool done_f = false, done_r = false;   // a nice match found (the scans stop there)
+        for (uint32_t k0 = 1; k0 < cfull && !done_f; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            const bool in_arr = k < cfull && k + 1 <= ip;   // slot ip-1-k >= 0
+            const uint32_t c = in_arr ? (uint32_t)sorted[ip - 1 - k] : 0u;
+            // still p's bucket (its hash) and newer than the limit
+            const bool in_chain = in_arr && c > limit &&
+                                  (((uint32_t)win[c] << 10 ^ (uint32_t)win[c + 1] << 5 ^ win[c + 2]) & 0x7fffu) == hp;
+            const uint64_t stop = __ballot(!in_chain);
+            const uint32_t nv = stop ? (uint32_t)__ffsll((unsigned long long)stop) - 1 : 64u;
+            const bool v = lane < nv;
+            // scan_end against the first candidate: only then can the match be longer than len1
+            const bool cand = v && (len1 == 0 || (vb(c + len1) == vb(p + len1) && vb(c + len1 - 1) == vb(p + len1 - 1)));
+            const uint32_t l = cand ? lcp(c) : 0u;
+            // full chain: the first reaching nice, else the first reaching the longest length
+            const uint64_t hit = __ballot(cand && l > bf && l >= nice);
+            uint32_t m = l;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor(m, d, 64));
+            const uint32_t hk = hit ? (uint32_t)__ffsll((unsigned long long)hit) - 1 : 64u;
+            // the reduced chain (k < cred), evaluated before the full one moves on
+            if (!done_r && k0 < cred) {
+                const bool inr = cand && k < cred;
+                const uint64_t hr = __ballot(inr && l > br && l >= nice);
+                if (hr) {
+                    const uint32_t t = (uint32_t)__ffsll((unsigned long long)hr) - 1;
+                    br = lane_val(l, t);
+                    brp = lane_val(c, t);
+                    done_r = true;
+                } else {
+                    uint32_t mr = inr ? l : 0u;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) mr = max(mr, (uint32_t)__shfl_xor(mr, d, 64));
+                    mr = uni(mr);
+                    if (mr > br) {
+                        const uint32_t t = (uint32_t)__ffsll((unsigned long long)__ballot(inr && l == mr)) - 1;
+                        br = mr;
+                        brp = lane_val(c, t);
+                    }
+                }
+            }
+            if (hk < 64) {
+                bf = lane_val(l, hk);
+                bfp = lane_val(c, hk);
+                done_f = true;
+            } else {
+                m = uni(m);
+                if (m > bf) {
+                    const uint32_t t = (uint32_t)__ffsll((unsigned long long)__ballot(cand && l == m)) - 1;
+                    bf = m;
+                    bfp = lane_val(c, t);
+                }
+            }
+            if (nv < 64) break;
+        }
+        if (lane == 0) {
+            rf[p] = bf << 16 | (p - bfp);
+            rr[p] = br << 16 | (p - brp);
+        }
     }
 }
 
@@ -257,6 +536,12 @@ struct ParseSmem {
     uint32_t bcast[4];
 };
 
+// LAZY (strips K1 found repetitive, kLazyDiv below): zlib's own order of work --
+// the strip in LDS and longest_match evaluated only where deflate_slow calls it
+// (the chain head with one wave-wide compare, then 64 candidates of sorted[] per
+// step, one per lane), so positions inside long matches cost nothing.  Otherwise
+// the K2 results are read from register windows.  Same bytes either way.
+template <bool LAZY>
 struct Wave {
     ParseSmem &sm;
     const uint8_t *src;
@@ -275,6 +560,11 @@ struct Wave {
     uint32_t bv0, bv1;
     bool overflow = false;
     BlockTrees T;
+    // LAZY: the window in LDS, the bucket order, and a 512-position window of idx[]
+    uint8_t *lwin = nullptr;
+    const uint16_t *idx = nullptr, *sorted = nullptr;
+    uint32_t ibase = 0x80000000u;
+    uint4 iv;
 
     __device__ Wave(ParseSmem &s, const uint8_t *in, uint32_t len, const uint8_t *w, uint32_t g, uint32_t *o,
                     uint32_t ow)
@@ -297,6 +587,7 @@ struct Wave {
         base = p & ~7u;
         const uint32_t q = base + 8 * lane_id();
         hv = *reinterpret_cast<const uint4 *>(hd + q);
+        if constexpr (LAZY) return;
         fv0 = *reinterpret_cast<const uint4 *>(rf + q);
         fv1 = *reinterpret_cast<const uint4 *>(rf + q + 4);
         rv0 = *reinterpret_cast<const uint4 *>(rr + q);
@@ -390,6 +681,7 @@ struct Wave {
     // ---- deflate_slow's Ops ----------------------------------------------
     __device__ uint32_t byte(uint32_t p)
     {
+        if constexpr (LAZY) return lwin[p];
         window(p);
         const uint32_t off = p - base, l = off >> 3, e = off & 7;
         const uint32_t w = e < 4 ? lane_val(bv0, l) : lane_val(bv1, l);
@@ -403,11 +695,105 @@ struct Wave {
         const uint32_t w = pick4(hv, l, e >> 1);
         return (w >> ((e & 1) * 16)) & 0xffffu;
     }
-    __device__ void slide() {}   // K2 compared against the slid window already
-    // longest_match from K2: the full chain's result, or the reduced chain's once prev_len >= good
-    __device__ bool longest(uint32_t p, uint32_t, uint32_t prev_len, uint32_t, uint32_t, uint32_t, uint32_t &len,
-                            uint32_t &pos)
+    __device__ void slide()   // fill_window's slide: past the end, the stale copy WSIZE back
     {
+        if constexpr (LAZY) {
+            for (uint32_t P = n + lane_id(); P < n + MAX_MATCH; P += 64) lwin[P] = lwin[P - WSIZE];
+            wave_sync();
+        }   // (K2 compared against the slid window already)
+    }
+    __device__ uint32_t ld4(uint32_t a)
+    {
+        const uint32_t *w32 = reinterpret_cast<const uint32_t *>(lwin);
+        return __builtin_amdgcn_alignbyte(w32[(a >> 2) + 1], w32[a >> 2], a & 3);
+    }
+    __device__ uint32_t hash_at(uint32_t q) { return ((uint32_t)lwin[q] << 10 ^ (uint32_t)lwin[q + 1] << 5 ^ lwin[q + 2]) & 0x7fffu; }
+    // common prefix of the strings at a and b, up to MAX_MATCH: one wave-wide compare
+    __device__ uint32_t wave_lcp(uint32_t a, uint32_t b)
+    {
+        const uint32_t x = ld4(a + 4 * lane_id()) ^ ld4(b + 4 * lane_id());
+        const uint64_t m = __ballot(x != 0);
+        if (m) {
+            const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
+            return 4 * f + ((uint32_t)__builtin_ctz(lane_val(x, f)) >> 3);
+        }
+        uint32_t l = 256;
+        if (lwin[a + 256] == lwin[b + 256]) l = lwin[a + 257] == lwin[b + 257] ? 258 : 257;
+        return l;
+    }
+    __device__ uint32_t lane_lcp(uint32_t a, uint32_t b)   // one lane, 16 bytes per step
+    {
+        uint32_t l = 0;
+        while (l < (uint32_t)MAX_MATCH) {
+            const uint32_t x0 = ld4(a + l) ^ ld4(b + l), x1 = ld4(a + l + 4) ^ ld4(b + l + 4);
+            const uint32_t x2 = ld4(a + l + 8) ^ ld4(b + l + 8), x3 = ld4(a + l + 12) ^ ld4(b + l + 12);
+            if (x0 | x1 | x2 | x3) {
+                l += x0 ? 0 : x1 ? 4 : x2 ? 8 : 12;
+                l += (uint32_t)__builtin_ctz(x0 ? x0 : x1 ? x1 : x2 ? x2 : x3) >> 3;
+                break;
+            }
+            l += 16;
+        }
+        return min(l, (uint32_t)MAX_MATCH);
+    }
+    __device__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
+                            uint32_t limit, uint32_t &len, uint32_t &pos)
+    {
+        if constexpr (LAZY) {
+            // the first candidate (chain order) reaching max(nice, prev_len+1), else the
+            // first reaching the longest length found, if longer than prev_len
+            const uint32_t Tn = max(nice, prev_len + 1);
+            const uint32_t l1 = wave_lcp(hdp, p);
+            if (l1 >= Tn) {
+                len = l1;
+                pos = hdp;
+                return true;
+            }
+            const uint32_t hp = hash_at(p);
+            uint32_t ip;
+            {   // idx[p] from its window
+                if (p - ibase >= 512u) {
+                    ibase = p & ~7u;
+                    iv = *reinterpret_cast<const uint4 *>(idx + ibase + 8 * lane_id());
+                }
+                const uint32_t off = p - ibase, e = off & 7;
+                ip = (pick4(iv, off >> 3, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
+            }
+            uint32_t best = prev_len, bpos = 0;
+            bool found = false;
+            for (uint32_t b = 0; b < chain; b += 64) {
+                const uint32_t gk = b + lane_id();
+                bool v = gk < chain && gk < ip;
+                const uint32_t c = v ? (uint32_t)sorted[ip - 1 - gk] : 0u;
+                v = v && (gk == 0 || c > limit) && hash_at(c) == hp;
+                const uint64_t stop = __ballot(!v);
+                const uint32_t nv = stop ? (uint32_t)__ffsll((unsigned long long)stop) - 1 : 64u;
+                v = lane_id() < nv;
+                const uint32_t l = v ? (gk == 0 ? l1 : lane_lcp(c, p)) : 0u;
+                const uint64_t hit = __ballot(v && l >= Tn);
+                if (hit) {
+                    const uint32_t k = (uint32_t)__ffsll((unsigned long long)hit) - 1;
+                    len = lane_val(l, k);
+                    pos = lane_val(c, k);
+                    return true;
+                }
+                uint32_t m = l;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor(m, d, 64));
+                m = uni(m);
+                if (m > best) {
+                    const uint32_t k = (uint32_t)__ffsll((unsigned long long)__ballot(v && l == m)) - 1;
+                    best = m;
+                    bpos = lane_val(c, k);
+                    found = true;
+                }
+                if (nv < 64) break;
+            }
+            len = best;
+            pos = bpos;
+            return found;
+        }
+        // the K2 results: the full chain's, or the reduced chain's once prev_len >= good
         window(p);
         const uint32_t r = prev_len >= good ? u32_at(rv0, rv1, p) : u32_at(fv0, fv1, p);
         len = r >> 16;
@@ -503,22 +889,50 @@ struct Wave {
     }
 };
 
+template <bool LAZY>
+struct ParseShared {
+    ParseSmem sm;
+};
+template <>
+struct ParseShared<true> {
+    ParseSmem sm;
+    uint32_t win32[(MAX_STRIP + 320) / 4];   // the strip, then the window bytes past its end
+};
+
+template <bool LAZY>
 __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
                                                        int32_t strip_bytes, int32_t spf, int32_t level,
                                                        uint8_t *__restrict__ out, int64_t slot_bytes,
                                                        int32_t *__restrict__ sizes, uint8_t *__restrict__ ws,
                                                        int64_t s0)
 {
-    __shared__ __attribute__((aligned(16))) ParseSmem sm;
+    __shared__ __attribute__((aligned(16))) ParseShared<LAZY> sh;
+    ParseSmem &sm = sh.sm;
     const int64_t s = s0 + blockIdx.x;
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s);
+    if (strip_lazy(S) != LAZY) return;   // the other kernel codes this strip
     const uint32_t lane = lane_id();
     Config cfg;
     level_config(level, cfg);
     for (uint32_t i = lane; i < (uint32_t)kStgWords; i += 64) sm.stg[i] = 0;
-    Wave wv(sm, S.src, S.n, S.ws, (uint32_t)cfg.good, reinterpret_cast<uint32_t *>(out + s * slot_bytes),
-            (uint32_t)(slot_bytes >> 2));
-    wv.init_freqs();   // includes the barrier for the staging words
+    Wave<LAZY> wv(sm, S.src, S.n, S.ws, (uint32_t)cfg.good, reinterpret_cast<uint32_t *>(out + s * slot_bytes),
+                  (uint32_t)(slot_bytes >> 2));
+    if constexpr (LAZY) {
+        // the window: the strip, then zeros (fill_window's high_water zeroing)
+        uint8_t *win = reinterpret_cast<uint8_t *>(sh.win32);
+        if (((uintptr_t)S.src & 3) == 0) {
+            const uint32_t *s32 = reinterpret_cast<const uint32_t *>(S.src);
+            for (uint32_t q = lane; q < (MAX_STRIP + 320) / 4; q += 64) sh.win32[q] = 4 * q + 4 <= S.n ? s32[q] : 0u;
+            wave_sync();
+            for (uint32_t p = (S.n & ~3u) + lane; p < S.n; p += 64) win[p] = S.src[p];
+        } else {
+            for (uint32_t p = lane; p < (uint32_t)(MAX_STRIP + 320); p += 64) win[p] = p < S.n ? S.src[p] : 0u;
+        }
+        wv.lwin = win;
+        wv.idx = reinterpret_cast<const uint16_t *>(S.ws + kIdxOff);
+        wv.sorted = reinterpret_cast<const uint16_t *>(S.ws + kSortOff);
+    }
+    wv.init_freqs();   // includes the barrier for the staging words and the window
 
     const uint32_t hdr = zlib_header(level);
     wv.emit_par(lane == 0 ? ((hdr >> 8) | ((hdr & 0xffu) << 8)) : 0u, lane == 0 ? 16u : 0u);
@@ -579,17 +993,25 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     const int chunks = (int)((std::min<int64_t>(strip_bytes, frame_bytes) + kChunk - 1) / kChunk);
     for (int64_t s0 = 0; s0 < total; s0 += 65535) {   // grid limits: strips [s0, s0 + cnt) per round
         const unsigned cnt = (unsigned)std::min<int64_t>(65535, total - s0);
-        hipLaunchKernelGGL(zlib_head_kernel, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
+        hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
                            (int32_t)spf, (uint8_t *)ws_dev, s0);
-        int rc = hip_check(hipGetLastError(), "zlib_head_kernel launch");
+        int rc = hip_check(hipGetLastError(), "zlib_order_kernel launch");
         if (rc != VCF_OK) return rc;
         hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, st, in_dev,
                            frame_bytes, strip_bytes, (int32_t)spf, level, (uint8_t *)ws_dev, s0);
         rc = hip_check(hipGetLastError(), "zlib_match_kernel launch");
         if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_parse_kernel, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
+        hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt), dim3(kK2bThreads), 0, st, in_dev, frame_bytes, strip_bytes,
+                           (int32_t)spf, level, (uint8_t *)ws_dev, s0);
+        rc = hip_check(hipGetLastError(), "zlib_chain_kernel launch");
+        if (rc != VCF_OK) return rc;
+        hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
                            (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, (uint8_t *)ws_dev, s0);
         rc = hip_check(hipGetLastError(), "zlib_parse_kernel launch");
+        if (rc != VCF_OK) return rc;
+        hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
+                           (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, (uint8_t *)ws_dev, s0);
+        rc = hip_check(hipGetLastError(), "zlib_parse_kernel (lazy) launch");
         if (rc != VCF_OK) return rc;
     }
     return VCF_OK;
