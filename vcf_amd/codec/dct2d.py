@@ -26,6 +26,7 @@ LloydMax); entropy codecs come from ENTROPY_CODECS.
 """
 from __future__ import annotations
 
+import io
 import logging
 import struct
 from concurrent.futures import ThreadPoolExecutor
@@ -402,6 +403,16 @@ class CoDec(EICCoDec):
                 f.write(struct.pack("iii", H, W, 3))
             return self.encode_write_fn(self.compress(k), out_fn)
 
+        # -c TIFF (the default): a batch's strips are deflated on the GPU from the
+        # indices in HBM (vcf_amd/zlib_gpu.py, byte-exact with zlib), so only the
+        # files come back; a single frame (encode_fn) keeps the host thread pool
+        gpu_tiff = isinstance(self.entropy, TIFFCodec) and TIFFCodec.gpu_batches
+
+        def _write_file(out_fn, blob):
+            with open(f"{out_fn}_shape.bin", "wb") as f:
+                f.write(struct.pack("iii", H, W, 3))
+            return self.encode_write_fn(io.BytesIO(blob), out_fn)
+
         try:
             with ThreadPoolExecutor(max_workers=io_threads) as pool:
                 reads = {0: [pool.submit(_read, 0, i) for i in range(len(batches[0]))]}
@@ -416,6 +427,13 @@ class CoDec(EICCoDec):
                     # this slot's pinned output is still read by batch b-2's deflates
                     for i, f in writes.pop(b - 2, []):
                         sizes[i] = f.result()
+                    if gpu_tiff:
+                        from .. import zlib_gpu
+                        dout, st = enc.run_device(b, len(chunk))
+                        files = zlib_gpu.tiff_frames_device(dout, len(chunk), (Hp, Wp, 3), np.uint8, stream=st)
+                        writes[b] = [(b * batch + i, pool.submit(_write_file, chunk[i][1], files[i]))
+                                     for i in range(len(chunk))]
+                        continue
                     ks = enc.run(b, len(chunk))
                     writes[b] = [(b * batch + i, pool.submit(_write, chunk[i][1], ks[i])) for i in range(len(chunk))]
                 for lst in writes.values():

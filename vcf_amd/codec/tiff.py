@@ -200,6 +200,9 @@ def imread_bytes(buf: bytes) -> np.ndarray:
 class TIFFCodec:
     """The reference's TIFF entropy stage: compress(ndarray) -> BytesIO
     (seeked to 0, TIFF.py:23-31), decompress(bytes) -> ndarray (:33-39)."""
+    # batches of frames whose indices sit in HBM (dct2d.CoDec.encode_fns) deflate
+    # their strips on the GPU, byte-exact with zlib (vcf_amd/zlib_gpu.py)
+    gpu_batches = True
 
     file_extension = ".tif"
 

@@ -93,6 +93,15 @@ class StagedEncoder:
         st.synchronize()
         return s["hout"].array[:n]
 
+    def run_device(self, b: int, n: int):
+        """Queue the encode of slot b%2's n pinned frames and leave the indices
+        in HBM: -> (device output, the slot's stream); nothing is downloaded."""
+        s = self.slot(b)
+        st = s["stream"]
+        _lib.call("vcf_memcpy_htod", s["din"].ptr, s["hin"].ptr, n * self.H * self.W * 3, st.handle)
+        self.launch(s["din"], n, s["dout"], st)
+        return s["dout"], st
+
     def close(self):
         for s in self.slots:
             for k in ("hin", "hout", "din", "dout"):
