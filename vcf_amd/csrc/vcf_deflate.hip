@@ -750,6 +750,9 @@ struct Wave {
                 return true;
             }
             const uint32_t hp = hash_at(p);
+            // only a candidate longer than F = max(prev_len, the head's length) can change the
+            // result, and such a one matches at bytes F-1 and F (longest_match's scan_end test)
+            const uint32_t F = max(prev_len, l1);
             uint32_t ip;
             {   // idx[p] from its window
                 if (p - ibase >= 512u) {
@@ -769,7 +772,8 @@ struct Wave {
                 const uint64_t stop = __ballot(!v);
                 const uint32_t nv = stop ? (uint32_t)__ffsll((unsigned long long)stop) - 1 : 64u;
                 v = lane_id() < nv;
-                const uint32_t l = v ? (gk == 0 ? l1 : lane_lcp(c, p)) : 0u;
+                const bool cand = v && gk != 0 && lwin[c + F] == lwin[p + F] && lwin[c + F - 1] == lwin[p + F - 1];
+                const uint32_t l = v ? (gk == 0 ? l1 : cand ? lane_lcp(c, p) : 0u) : 0u;
                 const uint64_t hit = __ballot(v && l >= Tn);
                 if (hit) {
                     const uint32_t k = (uint32_t)__ffsll((unsigned long long)hit) - 1;
