@@ -427,6 +427,9 @@ int64_t vcf_png_encode_bound(int32_t H, int32_t W);
  * sizes_dev 4-byte aligned). */
 int64_t vcf_zlib_bound(int64_t strip_bytes);
 int64_t vcf_zlib_workspace(int64_t n_strips);
+/* the largest strip_bytes vcf_zlib_strips takes (65536: frames with rows of
+ * more than 64 KB -- 1-row strips past 21845 RGB pixels -- stay on the host writer) */
+int32_t vcf_zlib_max_strip(void);
 int64_t vcf_zlib_strip_count(int64_t frame_bytes, int32_t strip_bytes);
 int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes, int32_t strip_bytes, int32_t level,
                     uint8_t *out_dev, int64_t slot_bytes, int32_t *sizes_dev, void *ws_dev, void *stream);
@@ -457,6 +460,27 @@ int vcf_ycrcb_to_rgb(const uint8_t *ycrcb_dev, int64_t n_px, uint8_t *rgb_dev, v
 int vcf_ycrcb_dz_encode(const uint8_t *rgb_dev, int64_t n_px, int32_t Q, uint16_t *k_dev, void *stream);
 /* YCrCb.decode (:53-72): Q * k in uint16, int16, uint8, to_RGB, clip. */
 int vcf_ycrcb_dz_decode(const uint16_t *k_dev, int64_t n_px, int32_t Q, uint8_t *rgb_dev, void *stream);
+
+/* ---- the stand-alone pixel codecs YCoCg.py and deadzone.py -------------------
+ * YCoCg.encode (src/YCoCg.py:33-56) with -a deadzone: img.astype(int16),
+ * from_RGB into int16 (A4, truncated toward zero), += offset 0 (:27-28),
+ * deadzone (x / Q) truncated (A5), astype(uint16).  n_px pixels of 3
+ * interleaved channels; k_dev n_px * 3 uint16. */
+int vcf_ycocg_dz_encode(const uint8_t *rgb_dev, int64_t n_px, int32_t Q, uint16_t *k_dev, void *stream);
+/* YCoCg.decode (:58-85): astype(int16), Q * k in int16 (1 <= Q <= 32767, else
+ * VCF_ERR_UNSUPPORTED), to_RGB in int16 (A4, wrapping), clip(0, 255), uint8. */
+int vcf_ycocg_dz_decode(const uint16_t *k_dev, int64_t n_px, int32_t Q, uint8_t *rgb_dev, void *stream);
+/* YCoCg.py with -a LloydMax (:29-30, offset [-128, 0, 0]): the int16 YCoCg
+ * image (A4) with offset0 added to Y, for the LloydMax entry points below; and
+ * back: Y - offset0, to_RGB in int16, clip(0, 255), uint8. */
+int vcf_ycocg_i16_from_rgb(const uint8_t *rgb_dev, int64_t n_px, int32_t offset0, int16_t *out_dev, void *stream);
+int vcf_ycocg_i16_to_rgb(const int16_t *in_dev, int64_t n_px, int32_t offset0, uint8_t *rgb_dev, void *stream);
+/* deadzone.encode (src/deadzone.py:67-79): astype(int16), (x / Q) truncated,
+ * astype(uint8), elementwise over n bytes. */
+int vcf_dz_u8_encode(const uint8_t *x_dev, int64_t n, int32_t Q, uint8_t *k_dev, void *stream);
+/* deadzone.decode (:81-93): Q * k in uint8 (wrapping; 1 <= Q <= 255, the
+ * Python-int-times-uint8 result type, else VCF_ERR_UNSUPPORTED). */
+int vcf_dz_u8_decode(const uint8_t *k_dev, int64_t n, int32_t Q, uint8_t *y_dev, void *stream);
 
 /* LloydMax (src/LloydMax.py:75-143).  Per channel c of an n_px x channels
  * array: counts = numpy.histogram(x[..., c], bins=max-min+1, range=(min, max))

@@ -136,3 +136,63 @@ def ycrcb_dz_decode(k: np.ndarray, Q: int) -> np.ndarray:
     y = ((np.asarray(k, np.uint16).astype(np.int64) * int(Q)) & 0xFFFF).astype(np.uint16)
     y = y.astype(np.int16).astype(np.uint8)
     return ycrcb_to_rgb(y)
+
+
+# ---- YCoCg.py / deadzone.py as stand-alone codecs (A4, A5) ----
+def ycocg_i16(rgb: np.ndarray) -> np.ndarray:
+    """YCoCg.encode (src/YCoCg.py:36-38): img.astype(int16), then color_transforms.YCoCg.from_RGB
+    (A4: the float64 matrix products stored into empty_like(int16), i.e. truncated toward zero)."""
+    a = np.asarray(rgb).astype(np.int16)
+    R, G, B = a[..., 0], a[..., 1], a[..., 2]
+    o = np.empty_like(a)
+    o[..., 0] = R / 4 + G / 2 + B / 4
+    o[..., 1] = R / 2 - B / 2
+    o[..., 2] = -R / 4 + G / 2 - B / 4
+    return o
+
+
+def ycocg_i16_to_rgb(y: np.ndarray) -> np.ndarray:
+    """YCoCg.decode (:73-84): to_RGB in int16 (A4, wrapping), clip(0, 255), astype(uint8)."""
+    Y, Co, Cg = (np.asarray(y, np.int64)[..., c] for c in range(3))
+    o = np.stack([Y + Co - Cg, Y + Cg, Y - Co - Cg], axis=-1)
+    o = ((o + 32768) % 65536 - 32768).astype(np.int16)
+    return np.clip(o, 0, 255).astype(np.uint8)
+
+
+def ycocg_dz_encode(rgb: np.ndarray, Q: int) -> np.ndarray:
+    """YCoCg.encode (:33-56) with -a deadzone: int16 YCoCg, += [0,0,0], (x/Q).astype(int32) (A5), uint16."""
+    x = ycocg_i16(rgb)
+    return (x / Q).astype(np.int32).astype(np.uint16)
+
+
+def ycocg_dz_decode(k: np.ndarray, Q: int) -> np.ndarray:
+    """YCoCg.decode (:58-85): astype(int16), Q * k in int16 (wrapping), -= 0, to_RGB, clip."""
+    k16 = np.asarray(k, np.uint16).astype(np.int16).astype(np.int64)
+    y = ((k16 * int(Q) + 32768) % 65536 - 32768).astype(np.int16)
+    return ycocg_i16_to_rgb(y)
+
+
+def ycocg_lm_encode(rgb: np.ndarray, Q: int, lo: int, hi: int):
+    """YCoCg.encode with -a LloydMax: offset [-128, 0, 0] (:29-30) added to Y, LloydMax.quantize_fn,
+    astype(uint16) -> (k, [centroids])."""
+    x = ycocg_i16(rgb)
+    x[..., 0] = (x[..., 0].astype(np.int32) - 128).astype(np.int16)
+    k, cents = lm_quantize(x, Q, lo, hi)
+    return k.astype(np.uint16), cents
+
+
+def ycocg_lm_decode(k: np.ndarray, cents) -> np.ndarray:
+    """YCoCg.decode with -a LloydMax: astype(int16), centroids into int16, Y + 128, to_RGB, clip."""
+    y = lm_dequantize(np.asarray(k).astype(np.int16), cents)
+    y[..., 0] = (y[..., 0].astype(np.int32) + 128).astype(np.int16)
+    return ycocg_i16_to_rgb(y)
+
+
+def dz_u8_encode(img: np.ndarray, Q: int) -> np.ndarray:
+    """deadzone.encode (src/deadzone.py:67-79): astype(int16), (x/Q).astype(int32) (A5), astype(uint8)."""
+    return (np.asarray(img).astype(np.int16) / Q).astype(np.int32).astype(np.uint8)
+
+
+def dz_u8_decode(k: np.ndarray, Q: int) -> np.ndarray:
+    """deadzone.decode (:81-93): Q * k with k uint8 and Q a Python int <= 255 -> uint8 (wrapping)."""
+    return ((np.asarray(k, np.uint8).astype(np.int64) * int(Q)) & 0xFF).astype(np.uint8)

@@ -177,3 +177,22 @@ def test_staged_pipeline_equals_single_frames(tmp_path, n, batch):
         assert sizes[i] == m
         assert open(out + ".tif", "rb").read() == open(ref + ".tif", "rb").read()
         assert open(out + "_shape.bin", "rb").read() == open(ref + "_shape.bin", "rb").read()
+
+
+def test_staged_pipeline_wide_rows_keep_host_writer(tmp_path):
+    """Frames whose rows exceed 64 KB (1-row TIFF strips past 21845 px) are
+    beyond the GPU deflate's strips: encode_fns writes them with the host
+    writer, and the files still equal encode_fn's."""
+    from vcf_amd import zlib_gpu
+    from vcf_amd.codec.dct2d import CoDec
+    assert not zlib_gpu.covers((8, 21848, 3)) and zlib_gpu.covers((8, 21840, 3))
+    rng = np.random.default_rng(5)
+    pairs = []
+    for i in range(3):
+        src = _png(tmp_path / f"in_{i}.png", rng.integers(0, 256, (9, 21850, 3), dtype=np.uint8))
+        pairs.append((src, str(tmp_path / f"enc_{i}")))
+    sizes = CoDec(_args("encode")).encode_fns(pairs, batch=2, io_threads=2)
+    for i, (src, out) in enumerate(pairs):
+        ref = str(tmp_path / f"ref_{i}")
+        assert sizes[i] == CoDec(_args("encode")).encode_fn(src, ref)
+        assert open(out + ".tif", "rb").read() == open(ref + ".tif", "rb").read()

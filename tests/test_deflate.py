@@ -57,6 +57,15 @@ def _cases():
     }
 
 
+def test_harness_slide_nil_head(dh):
+    """slide_hash's NIL mapping of the head entry at input position wsize
+    (ADVICE round 3): zlib writes a literal at strstart 65274 there."""
+    from deflate_cases import slide_nil_strip
+    b = slide_nil_strip()
+    for level in (4, 5, 6, 7, 8, 9):
+        assert dh(b, level) == zlib.compress(b, level), level
+
+
 @pytest.mark.parametrize("level", [6, 4, 5, 7, 8, 9])
 def test_harness_equals_zlib(dh, level):
     for name, b in _cases().items():

@@ -54,6 +54,21 @@ def test_strip_lengths(strip):
     _check(_frames(2, (48, 700, 3), 2, "image"), strip)
 
 
+def test_slide_nil_head():
+    """zlib's slide_hash maps the head entry at input position wsize to NIL
+    (tests/deflate_cases.py): the GPU must emit zlib's literal there."""
+    from deflate_cases import slide_nil_strip
+    from vcf_amd.device import DeviceBuffer
+    from vcf_amd.zlib_gpu import StripDeflater
+    b = np.frombuffer(slide_nil_strip(), np.uint8)
+    frames = np.stack([b, b[::-1].copy()])
+    d = DeviceBuffer.from_array(frames)
+    for level in (4, 6, 9):
+        got = StripDeflater().deflate_device(d, 2, b.size, b.size, level)
+        assert got[0][0] == zlib.compress(b.tobytes(), level), level
+        assert got[1][0] == zlib.compress(b[::-1].tobytes(), level), level
+
+
 @pytest.mark.parametrize("level", [4, 5, 7, 8, 9])
 def test_levels(level):
     _check(_frames(1, (30, 1000, 3), 3, "image"), 65536, level)

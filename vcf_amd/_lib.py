@@ -98,6 +98,12 @@ SIGNATURES = {
     "vcf_ycrcb_to_rgb": [_P, _I64, _P, _P],
     "vcf_ycrcb_dz_encode": [_P, _I64, _I32, _P, _P],
     "vcf_ycrcb_dz_decode": [_P, _I64, _I32, _P, _P],
+    "vcf_ycocg_dz_encode": [_P, _I64, _I32, _P, _P],
+    "vcf_ycocg_dz_decode": [_P, _I64, _I32, _P, _P],
+    "vcf_ycocg_i16_from_rgb": [_P, _I64, _I32, _P, _P],
+    "vcf_ycocg_i16_to_rgb": [_P, _I64, _I32, _P, _P],
+    "vcf_dz_u8_encode": [_P, _I64, _I32, _P, _P],
+    "vcf_dz_u8_decode": [_P, _I64, _I32, _P, _P],
     "vcf_lm_levels": [_I32, _I32, _I32],
     "vcf_lm_histogram": [_P, _I32, _I64, _I32, _I32, _I32, _P, _P],
     "vcf_lm_design": [_P, _I32, _I32, _I32, _P],
@@ -128,6 +134,7 @@ SIGNATURES = {
     "vcf_png_encode_bound": [_I32, _I32],
     "vcf_zlib_bound": [_I64],
     "vcf_zlib_workspace": [_I64],
+    "vcf_zlib_max_strip": [],
     "vcf_zlib_strip_count": [_I64, _I32],
     "vcf_zlib_strips": [_P, _I64, _I64, _I32, _I32, _P, _I64, _P, _P, _P],
     "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],

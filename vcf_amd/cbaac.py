@@ -73,3 +73,10 @@ class CBAACCodec:
             return np.zeros((10, 10), np.uint8)    # CBAAC.py:101-102
         n = int(np.prod(shape))
         return decode_symbols(data[4 + 4 * nd:], n, self.ORDER).reshape(shape)
+
+    # the reference's public names (CBAAC.py:81, :97; compress/decompress wrap them, :152-156)
+    def compress_fn(self, img, fn):
+        return self.compress(img, fn)
+
+    def decompress_fn(self, compressed_bytes, fn):
+        return self.decompress(compressed_bytes, fn)

@@ -73,3 +73,10 @@ class CBAHCCodec:
             meta = _NoGlobals(f).load()
         n = int(np.prod(shape))
         return decode_symbols(bytes(data), int(meta["nbits"]), n, int(meta["order"])).reshape(shape)
+
+    # the reference's public names (CBAHC.py:169, :226; compress/decompress wrap them, :223, :278)
+    def compress_fn(self, img, fn):
+        return self.compress(img, fn)
+
+    def decompress_fn(self, compressed_img, fn):
+        return self.decompress(compressed_img, fn)

@@ -11,4 +11,4 @@ from vcf_amd.codec.dct2d import CoDec  # noqa: E402
 from vcf_amd.codec.main import main  # noqa: E402
 
 if __name__ == "__main__":
-    main(P.dct_parser(quantizer=P.quantizer_of(sys.argv[1:])), CoDec)
+    main(P.dct_parser(quantizer=P.quantizer_of(sys.argv[1:]), entropy=P.entropy_of(sys.argv[1:])), CoDec)

@@ -12,4 +12,4 @@ from vcf_amd.codec.dwt2d import CoDec  # noqa: E402
 from vcf_amd.codec.main import main  # noqa: E402
 
 if __name__ == "__main__":
-    main(P.dwt_parser(), CoDec)
+    main(P.dwt_parser(entropy=P.entropy_of(sys.argv[1:])), CoDec)

@@ -15,4 +15,4 @@ from vcf_amd.codec.main import main  # noqa: E402
 if __name__ == "__main__":
     # the reference imports the -T codec module, whose options join the parser
     t = P.parse(P.iii_parser(), sys.argv[1:]).transform if len(sys.argv) > 1 else "2D-DCT"
-    main(P.iii_parser(transform=t), CoDec)
+    main(P.iii_parser(transform=t, entropy=P.entropy_of(sys.argv[1:])), CoDec)

@@ -19,4 +19,4 @@ if __name__ == "__main__":
     pre = argparse.ArgumentParser(add_help=False)
     pre.add_argument("--st", dest="space_transform", type=str, default="2D-DCT")
     st = pre.parse_known_args()[0].space_transform
-    main(P.ipp_parser(space_transform=st), codec_class(st))
+    main(P.ipp_parser(space_transform=st, entropy=P.entropy_of(sys.argv[1:])), codec_class(st))

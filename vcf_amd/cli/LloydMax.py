@@ -11,4 +11,4 @@ from vcf_amd.codec.main import main  # noqa: E402
 from vcf_amd.codec.pixel import LloydMaxCoDec  # noqa: E402
 
 if __name__ == "__main__":
-    main(P.lloydmax_parser(), LloydMaxCoDec)
+    main(P.lloydmax_parser(entropy=P.entropy_of(sys.argv[1:])), LloydMaxCoDec)

@@ -407,6 +407,11 @@ class CoDec(EICCoDec):
         # indices in HBM (vcf_amd/zlib_gpu.py, byte-exact with zlib), so only the
         # files come back; a single frame (encode_fn) keeps the host thread pool
         gpu_tiff = isinstance(self.entropy, TIFFCodec) and TIFFCodec.gpu_batches
+        if gpu_tiff:
+            from .. import zlib_gpu
+            # rows over 64 KB (1-row strips past 21845 px) are beyond the GPU deflate's
+            # strips: those frames keep the host writer
+            gpu_tiff = zlib_gpu.covers((Hp, Wp, 3), 1)
 
         def _write_file(out_fn, blob):
             with open(f"{out_fn}_shape.bin", "wb") as f:

@@ -62,6 +62,9 @@ class DeviceIII:
             self.batch = None
             self.zd = Z.StripDeflater()
             self.strip_bytes = strip_layout(self.shape, 1)[2]
+            if not Z.covers(self.shape, 1):
+                raise NotImplementedError(f"{self.Wp}-pixel rows: TIFF strips of {self.strip_bytes} bytes are beyond "
+                                          f"the GPU deflate's {Z.max_strip()}; use the file path (dct2d.encode_fns)")
         else:
             self.batch = T.FrameBatch(self.n_local, self.n_sym, 0, seg_len, prior=True, nclass=nclass)
         self.send = None

@@ -80,12 +80,39 @@ def add_eic(enc, dec):
                      help=f"Output image (default: {DECODED})", default=f"{DECODED}")
 
 
-def add_filter(enc, dec):
-    """no_filter.py:14-17 (entropy codec choice lives in the filter module)."""
+def add_filter(enc, dec, entropy: str = DEFAULT_EIC):
+    """no_filter.py:14-21 (entropy codec choice lives in the filter module; the
+    module -c names is imported there, and CBAHC.py adds --order on import)."""
     enc.add_argument("-c", "--entropy_image_codec",
                      help=f"Entropy Image Codec (default: {DEFAULT_EIC})", default=DEFAULT_EIC)
     dec.add_argument("-c", "--entropy_image_codec",
                      help=f"Entropy Image Codec (default: {DEFAULT_EIC})", default=DEFAULT_EIC)
+    if entropy == "CBAHC":
+        add_order_cbahc(enc, dec)
+
+
+DEFAULT_ORDER = 0                       # CBAHC.py:13
+
+
+def add_order_cbahc(enc, dec):
+    """CBAHC.py:13-16 (at import time)."""
+    for p in (enc, dec):
+        p.add_argument("--order", type=int, help=f"Context model order (default: {DEFAULT_ORDER})",
+                       default=DEFAULT_ORDER)
+
+
+def add_order_cbaac(enc, dec):
+    """CBAAC.py:158-164 (only when CBAAC.py itself is the program: as a -c
+    module its CoDec reads getattr(args, 'order', 0), :76)."""
+    for p in (enc, dec):
+        p.add_argument("--order", type=int, default=0, help="Context order")
+
+
+def entropy_of(argv) -> str:
+    """Pre-parse -c/--entropy_image_codec, as the reference's import chain does (no_filter.py:20-21)."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("-c", "--entropy_image_codec", default=DEFAULT_EIC)
+    return pre.parse_known_args(argv)[0].entropy_image_codec
 
 
 def add_deadzone(enc, dec):
@@ -170,31 +197,32 @@ def add_iii(enc, dec):
 
 
 def dct_parser(description: str = "Exploiting spatial redundancy with the 2D Discrete Cosine "
-                                  "Transform of constant block size.", quantizer: str = DEFAULT_QUANTIZER):
-    """The parser `python 2D-DCT.py ...` ends up with (the codec chain -a names)."""
+                                  "Transform of constant block size.", quantizer: str = DEFAULT_QUANTIZER,
+               entropy: str = DEFAULT_EIC):
+    """The parser `python 2D-DCT.py ...` ends up with (the codec chain -a and -c name)."""
     p, enc, dec = base_parser(description)
     add_dct(enc, dec)
     add_ycocg(enc, dec)
     add_quantizer(enc, dec, quantizer)
-    add_filter(enc, dec)
+    add_filter(enc, dec, entropy)
     add_eic(enc, dec)
     return p
 
 
 def dwt_parser(description: str = "Exploiting spatial redundancy with the 2D dyadic Discrete Wavelet "
-                                  "Transform."):
+                                  "Transform.", entropy: str = DEFAULT_EIC):
     """`python 2D-DWT.py ...` (2D-DWT.py -> YCoCg.py -> deadzone.py -> no_filter.py -> TIFF.py)."""
     p, enc, dec = base_parser(description)
     add_dwt(enc, dec)
     add_ycocg(enc, dec)
     add_deadzone(enc, dec)
-    add_filter(enc, dec)
+    add_filter(enc, dec, entropy)
     add_eic(enc, dec)
     return p
 
 
 def iii_parser(description: str = "III coding: runs a 2D image codec for each image of a sequence.",
-               transform: str = "2D-DCT"):
+               transform: str = "2D-DCT", entropy: str = DEFAULT_EIC):
     """`python III.py ...` (III.py + the chain of the 2D codec it imports)."""
     p, enc, dec = base_parser(description)
     add_iii(enc, dec)
@@ -204,27 +232,67 @@ def iii_parser(description: str = "III coding: runs a 2D image codec for each im
         add_dct(enc, dec)
     add_ycocg(enc, dec)
     add_deadzone(enc, dec)
-    add_filter(enc, dec)
+    add_filter(enc, dec, entropy)
     add_eic(enc, dec)
     return p
 
 
-def lloydmax_parser(description: str = "Image quantization using a LloydMax quantizer."):
+def lloydmax_parser(description: str = "Image quantization using a LloydMax quantizer.",
+                    entropy: str = DEFAULT_EIC):
     """`python LloydMax.py ...` (LloydMax.py -> no_filter.py -> TIFF.py)."""
     p, enc, dec = base_parser(description)
     add_lloydmax(enc, dec)
-    add_filter(enc, dec)
+    add_filter(enc, dec, entropy)
     add_eic(enc, dec)
     return p
 
 
 def ycrcb_parser(description: str = "Exploiting color (perceptual) redundancy with the YCrCb transform.",
-                 quantizer: str = DEFAULT_QUANTIZER):
+                 quantizer: str = DEFAULT_QUANTIZER, entropy: str = DEFAULT_EIC):
     """`python YCrCb.py ...` (YCrCb.py -> <quantizer>.py -> no_filter.py -> TIFF.py)."""
     p, enc, dec = base_parser(description)
     add_ycocg(enc, dec)        # YCrCb.py:17-19 adds the same -a option
     add_quantizer(enc, dec, quantizer)
-    add_filter(enc, dec)
+    add_filter(enc, dec, entropy)
+    add_eic(enc, dec)
+    return p
+
+
+def ycocg_parser(description: str = "Exploiting color (perceptual) redundancy with the YCoCg transform.",
+                 quantizer: str = DEFAULT_QUANTIZER, entropy: str = DEFAULT_EIC):
+    """`python YCoCg.py ...` (YCoCg.py:15-21 -> <quantizer>.py -> no_filter.py -> TIFF.py)."""
+    return ycrcb_parser(description, quantizer, entropy)
+
+
+def deadzone_parser(description: str = "Image quantization using a deadzone scalar quantizer.",
+                    entropy: str = DEFAULT_EIC):
+    """`python deadzone.py ...` (deadzone.py:32-35 -> no_filter.py -> TIFF.py)."""
+    p, enc, dec = base_parser(description)
+    add_deadzone(enc, dec)
+    add_filter(enc, dec, entropy)
+    add_eic(enc, dec)
+    return p
+
+
+def tiff_parser(description: str = "Entropy Encoding of images using TIFF (Tag Image File Format). "):
+    """`python TIFF.py ...` (TIFF.py -> entropy_image_coding.py)."""
+    p, enc, dec = base_parser(description)
+    add_eic(enc, dec)
+    return p
+
+
+def cbaac_parser(description: str = "Context-based adaptive arithmetic coding"):
+    """`python CBAAC.py ...` (CBAAC.py -> entropy_image_coding.py, then --order, :158-164)."""
+    p, enc, dec = base_parser(description)
+    add_eic(enc, dec)
+    add_order_cbaac(enc, dec)
+    return p
+
+
+def cbahc_parser(description: str = "\n# Huffman adaptativo\n"):
+    """`python CBAHC.py ...` (CBAHC.py:13-16 --order, then entropy_image_coding.py)."""
+    p, enc, dec = base_parser(description)
+    add_order_cbahc(enc, dec)
     add_eic(enc, dec)
     return p
 
@@ -270,7 +338,7 @@ IPP_SEARCH = 8
 
 
 def ipp_parser(description: str = "IPP hybrid video coding using motion compensation and DCT.",
-               space_transform: str = "2D-DCT"):
+               space_transform: str = "2D-DCT", entropy: str = DEFAULT_EIC):
     """`python IPP_DCT.py ...` over the 2D-DCT chain (or, --st 2D-DWT, the 2D-DWT one)."""
     p, enc, dec = base_parser(description)
     if space_transform == "2D-DWT":
@@ -279,7 +347,7 @@ def ipp_parser(description: str = "IPP hybrid video coding using motion compensa
         add_dct(enc, dec)
     add_ycocg(enc, dec)
     add_deadzone(enc, dec)
-    add_filter(enc, dec)
+    add_filter(enc, dec, entropy)
     add_eic(enc, dec)
     add_ipp(enc, dec)
     return p

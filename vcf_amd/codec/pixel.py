@@ -154,3 +154,168 @@ class YCrCbCoDec(_PixelCoDec):
             y = rgb.download(np.empty((H, W, 3), np.uint8))
             rgb.free()
         return self.decode_write_fn(self.filter(y), out_fn)
+
+
+class YCoCgCoDec(_PixelCoDec):
+    """YCoCg.CoDec (src/YCoCg.py:23-85), the stand-alone colour codec and the
+    reference's default -t, over -a deadzone (one fused kernel per direction)
+    or -a LloydMax (the int16 YCoCg image through the quantizer plug-in)."""
+
+    def __init__(self, args):
+        super().__init__(args)
+        self.lm = make_quantizer(args)
+        # :27-30: residues centred at zero for deadzone, Y - 128 otherwise
+        self.offset = np.array([0, 0, 0]) if self.lm is None else np.array([-128, 0, 0])
+
+    def quantize(self, img, fn="/tmp/encoded"):
+        if self.lm is not None:
+            return self.lm.quantize(img, fn)
+        from .. import quant
+        return quant.deadzone_quantize(img, self.QSS)
+
+    def dequantize(self, k, fn="/tmp/encoded"):
+        if self.lm is not None:
+            return self.lm.dequantize(k, fn)
+        from .. import quant
+        return quant.deadzone_dequantize(k, self.QSS)
+
+    def encode_fn(self, in_fn, out_fn):
+        """:33-56: int16, from_RGB, + offset, quantize, astype(uint16), compress, write."""
+        img = self.encode_read_fn(in_fn)
+        self._check(img)
+        H, W = img.shape[:2]
+        if self.lm is None:
+            k = PL.ycocg_dz_encode(img, self.QSS)
+        else:
+            from .._lib import call
+            src = DeviceBuffer.from_array(img)
+            ycc = DeviceBuffer(max(H * W * 3 * 2, 1))
+            call("vcf_ycocg_i16_from_rgb", src.ptr, H * W, int(self.offset[0]), ycc.ptr, None)
+            src.free()
+            # k = empty_like(int16) <- searchsorted indices (0..N-1), astype(uint16): the same values
+            dk = self.lm.quantize_device(ycc, np.int16, H * W, 3, np.uint16)
+            ycc.free()
+            self._take_codebook()
+            k = dk.download(np.empty((H, W, 3), np.uint16))
+            dk.free()
+        return self.encode_write_fn(self.compress(k), out_fn)
+
+    def decode_fn(self, in_fn, out_fn):
+        """:58-85: decompress, astype(int16), dequantize, - offset, to_RGB, clip, uint8, filter, write."""
+        k = self.decompress(self.decode_read_fn(in_fn))
+        if k.ndim != 3 or k.shape[2] != 3:
+            raise ValueError(f"index array of shape {k.shape}: expected H x W x 3")
+        H, W = k.shape[:2]
+        if self.lm is None:
+            y = PL.ycocg_dz_decode(np.ascontiguousarray(k, dtype=np.uint16), self.QSS)
+        else:
+            from .._lib import call
+            # y = empty_like(k.astype(int16)) <- centroids truncated into int16
+            dk = DeviceBuffer.from_array(np.ascontiguousarray(k.astype(np.int16)))
+            yc = self.lm.dequantize_device(dk, np.int16, H * W, 3, np.int16)
+            dk.free()
+            rgb = DeviceBuffer(max(H * W * 3, 1))
+            call("vcf_ycocg_i16_to_rgb", yc.ptr, H * W, int(self.offset[0]), rgb.ptr, None)
+            yc.free()
+            y = rgb.download(np.empty((H, W, 3), np.uint8))
+            rgb.free()
+        return self.decode_write_fn(self.filter(y), out_fn)
+
+
+class DeadzoneCoDec(_PixelCoDec):
+    """deadzone.CoDec (src/deadzone.py:39-117) run as its own codec: the image
+    quantized directly (int16, (x / Q) truncated, uint8) and back (Q * k in
+    uint8), elementwise on the GPU."""
+
+    def __init__(self, args, min_index_val=0, max_index_val=255):
+        super().__init__(args)
+        self.lm = None
+        self.min_index_val, self.max_index_val = min_index_val, max_index_val
+
+    def quantize(self, img, fn="/tmp/encoded"):
+        from .. import quant
+        return quant.deadzone_quantize(img, self.QSS)
+
+    def dequantize(self, k, fn="/tmp/encoded"):
+        from .. import quant
+        return quant.deadzone_dequantize(k, self.QSS)
+
+    def encode_fn(self, in_fn, out_fn):
+        """:67-79: astype(int16), quantize, astype(uint8), compress, write."""
+        img = self.encode_read_fn(in_fn)
+        if img.dtype != np.uint8:
+            raise NotImplementedError(f"{img.dtype} images: the HIP path takes u8 images")
+        k = PL.dz_u8_encode(img, self.QSS)
+        return self.encode_write_fn(self.compress(k), out_fn)
+
+    def decode_fn(self, in_fn, out_fn):
+        """:81-93: decompress, dequantize (Q * k in uint8), filter, write."""
+        k = self.decompress(self.decode_read_fn(in_fn))
+        if k.dtype != np.uint8:
+            raise NotImplementedError(f"{k.dtype} indices: deadzone.py writes uint8")
+        if self.QSS > 255:
+            raise NotImplementedError(f"QSS {self.QSS}: Q * k is uint8 only for Q <= 255 (numpy value-based "
+                                      "casting); the HIP path covers that case")
+        y = PL.dz_u8_decode(k, self.QSS)
+        return self.decode_write_fn(self.filter(y), out_fn)
+
+
+class EntropyImageCoDec(EICCoDec):
+    """An entropy codec run on the image itself: TIFF.py, CBAAC.py and
+    CBAHC.py as stand-alone codecs (entropy_image_coding.CoDec.encode/decode,
+    :81-86 / :117-121: read, compress, write; read, decompress, write)."""
+
+    codec_name = "TIFF"
+
+    def __init__(self, args):
+        super().__init__(args)
+        from argparse import Namespace
+        self.entropy = make_entropy(Namespace(**{**vars(args), "entropy_image_codec": self.codec_name}))
+        self.file_extension = self.entropy.file_extension
+
+    def compress(self, img, fn="/tmp/encoded"):
+        if self.codec_name == "CBAHC":
+            return self.entropy.compress(img, fn)
+        return self.entropy.compress(img)
+
+    def decompress(self, codestream, fn="/tmp/encoded"):
+        if self.codec_name == "CBAHC":
+            return self.entropy.decompress(codestream, fn)
+        return self.entropy.decompress(codestream)
+
+    def compress_fn(self, img, fn):
+        return self.compress(img, fn)
+
+    def decompress_fn(self, codestream, fn):
+        return self.decompress(codestream, fn)
+
+    def encode_fn(self, in_fn, out_fn):
+        img = self.encode_read_fn(in_fn)
+        return self.encode_write_fn(self.compress(img), out_fn)
+
+    def decode_fn(self, in_fn, out_fn):
+        img = self.decompress(self.decode_read_fn(in_fn))
+        if self.codec_name == "CBAAC":
+            img = np.asarray(img).astype(np.uint8)      # CBAAC.py:112
+        return self.decode_write_fn(img, out_fn)
+
+    def encode(self):
+        return self.encode_fn("/tmp/original.png", "/tmp/encoded")
+
+    def decode(self):
+        return self.decode_fn("/tmp/encoded", "/tmp/decoded.png")
+
+
+class TIFFImageCoDec(EntropyImageCoDec):
+    """TIFF.CoDec (src/TIFF.py:16-39)."""
+    codec_name = "TIFF"
+
+
+class CBAACImageCoDec(EntropyImageCoDec):
+    """CBAAC.CoDec (src/CBAAC.py:72-156) with --order (:158-166)."""
+    codec_name = "CBAAC"
+
+
+class CBAHCImageCoDec(EntropyImageCoDec):
+    """CBAHC.CoDec (src/CBAHC.py:158-283) with --order (:14-16)."""
+    codec_name = "CBAHC"

@@ -5,7 +5,10 @@
 // (tifffile.imwrite(..., compression='zlib') -> one zlib stream per ~64 KB
 // strip at level 6); the host path (vcf_amd/codec/tiff.py) calls system zlib.
 //
-// What is restated, and from where (zlib 1.2.11; its algorithm, not its text):
+// What is restated, and from where (zlib 1.2.11, Jean-loup Gailly and Mark
+// Adler, zlib licence -- see THIRD_PARTY_NOTICES.md).  The trees.c part is a
+// close transliteration of zlib's own functions (same control flow and
+// variable roles, so that every tie and overflow resolves as zlib's does):
 //   * deflate.c deflate_slow: lazy evaluation, the TOO_FAR rule, the hash
 //     insertion of every position, FLUSH_BLOCK after lit_bufsize-1 symbols;
 //     fill_window's one slide for strips longer than wsize+MAX_DIST (the
@@ -455,7 +458,8 @@ VD_HD inline uint32_t adler32_from_sums(uint64_t sum_b, uint64_t sum_wb, uint64_
 //   bool tally(dist, lc)                 _tr_tally; true when lit_bufsize-1 symbols are buffered
 //   void flush(stored_len, buf_ok, block_start, last)   _tr_flush_block
 // Positions are input offsets throughout; zlib's window offsets differ from
-// them by the slide, which every distance, TOO_FAR and limit test is invariant to.
+// them by the slide, which every distance, TOO_FAR and limit test is invariant
+// to -- except the NIL mapping of the head entry at input WSIZE, handled below.
 template <class Ops>
 VD_HD inline void deflate_slow(Ops &ops, uint32_t n, const Config &cfg)
 {
@@ -480,6 +484,11 @@ VD_HD inline void deflate_slow(Ops &ops, uint32_t n, const Config &cfg)
         }
         uint32_t hash_head = 0;
         if (lookahead >= (uint32_t)MIN_MATCH) hash_head = ops.head(strstart);
+        // slide_hash maps every head entry m <= wsize (window offsets) to NIL:
+        // input position WSIZE is window offset 0 after the slide, and is not
+        // searched even though its distance from strstart = wsize + MAX_DIST
+        // is exactly MAX_DIST (earlier entries are farther than MAX_DIST anyway)
+        if (slid && hash_head <= (uint32_t)WSIZE) hash_head = 0;
         prev_length = match_length;
         prev_match = match_start;
         match_length = MIN_MATCH - 1;

@@ -965,6 +965,8 @@ int64_t vcf_zlib_bound(int64_t strip_bytes)
     return (b + 15) / 16 * 16 + 16;
 }
 
+int32_t vcf_zlib_max_strip(void) { return dfl::MAX_STRIP; }
+
 int64_t vcf_zlib_workspace(int64_t n_strips) { return n_strips < 0 ? -1 : n_strips * kWsPerStrip; }
 
 int64_t vcf_zlib_strip_count(int64_t frame_bytes, int32_t strip_bytes)

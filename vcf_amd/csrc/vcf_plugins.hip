@@ -124,6 +124,137 @@ __global__ __launch_bounds__(kThreads) void ycrcb_dz_decode_kernel(const uint16_
     }
 }
 
+// ---- YCoCg.py and deadzone.py, the stand-alone pixel codecs ----------------
+// YCoCg.encode (src/YCoCg.py:33-56) with -a deadzone: img.astype(int16),
+// from_RGB into an int16 array (A4: Y = R/4 + G/2 + B/4, Co = R/2 - B/2,
+// Cg = -R/4 + G/2 - B/4 in float64 -- exact quarter multiples -- stored with
+// the C cast, i.e. truncated toward zero), += offset [0, 0, 0] (:27-28),
+// deadzone (x / Q).astype(int32) (A5: float64 true division of small
+// integers, which truncates exactly like integer division), astype(uint16)
+// (negative indices wrap).  Four pixels per thread: 12 bytes in, 24 out.
+__device__ __forceinline__ void ycocg_i16(int r, int g, int b, int &y, int &co, int &cg)
+{
+    y = (r + 2 * g + b) / 4;     // C division truncates toward zero, as the int16 store does
+    co = (r - b) / 2;
+    cg = (-r + 2 * g - b) / 4;
+}
+
+__global__ __launch_bounds__(kThreads) void ycocg_dz_encode_kernel(const uint8_t *__restrict__ rgb, int64_t n_px,
+                                                                   int Q, uint16_t *__restrict__ k)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 4 * p < n_px; p += stride) {
+        const int64_t p0 = 4 * p;
+        const int np = (int)min((int64_t)4, n_px - p0);
+        uint8_t px[12];
+        if (np == 4 && (((uintptr_t)(rgb + 3 * p0)) & 3) == 0) {
+            const uint32_t *s = reinterpret_cast<const uint32_t *>(rgb + 3 * p0);
+#pragma unroll
+            for (int w = 0; w < 3; ++w) {
+                const uint32_t v = s[w];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) px[4 * w + j] = (uint8_t)(v >> (8 * j));
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 12; ++j) px[j] = j < 3 * np ? rgb[3 * p0 + j] : 0;
+        }
+        uint16_t o[12];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int c[3];
+            ycocg_i16(px[3 * i], px[3 * i + 1], px[3 * i + 2], c[0], c[1], c[2]);
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) o[3 * i + ch] = (uint16_t)(int32_t)(c[ch] / Q);
+        }
+        if (np == 4 && (((uintptr_t)(k + 3 * p0)) & 7) == 0) {
+            uint2 *d = reinterpret_cast<uint2 *>(k + 3 * p0);
+#pragma unroll
+            for (int w = 0; w < 3; ++w)
+                d[w] = make_uint2((uint32_t)o[4 * w] | (uint32_t)o[4 * w + 1] << 16,
+                                  (uint32_t)o[4 * w + 2] | (uint32_t)o[4 * w + 3] << 16);
+        } else {
+            for (int j = 0; j < 3 * np; ++j) k[3 * p0 + j] = o[j];
+        }
+    }
+}
+
+// YCoCg.decode (:58-85): k.astype(int16), deadzone Q * k (int16 x Python int
+// stays int16 under numpy 1.26's value-based casting: wraps), -= offset 0,
+// to_RGB in int16 (A4: R = Y + Co - Cg, G = Y + Cg, B = Y - Co - Cg, each
+// wrapping), clip(0, 255), astype(uint8).
+__global__ __launch_bounds__(kThreads) void ycocg_dz_decode_kernel(const uint16_t *__restrict__ k, int64_t n_px,
+                                                                   int Q, uint8_t *__restrict__ rgb)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_px; p += stride) {
+        int v[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = (int16_t)(uint16_t)((uint32_t)Q * k[3 * p + c]);
+        const int r = (int16_t)(v[0] + v[1] - v[2]), g = (int16_t)(v[0] + v[2]), b = (int16_t)(v[0] - v[1] - v[2]);
+        rgb[3 * p] = (uint8_t)sat8(r);
+        rgb[3 * p + 1] = (uint8_t)sat8(g);
+        rgb[3 * p + 2] = (uint8_t)sat8(b);
+    }
+}
+
+// YCoCg.py with -a LloydMax: the int16 YCoCg image + offset [-128, 0, 0]
+// (:29-30) for the quantizer plug-in, and back (the dequantized int16 image
+// - offset, to_RGB in int16, clip, uint8).
+__global__ __launch_bounds__(kThreads) void ycocg_i16_from_rgb_kernel(const uint8_t *__restrict__ rgb, int64_t n_px,
+                                                                      int off0, int16_t *__restrict__ out)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_px; p += stride) {
+        int y, co, cg;
+        ycocg_i16(rgb[3 * p], rgb[3 * p + 1], rgb[3 * p + 2], y, co, cg);
+        out[3 * p] = (int16_t)(y + off0);
+        out[3 * p + 1] = (int16_t)co;
+        out[3 * p + 2] = (int16_t)cg;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void ycocg_i16_to_rgb_kernel(const int16_t *__restrict__ in, int64_t n_px,
+                                                                    int off0, uint8_t *__restrict__ rgb)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_px; p += stride) {
+        const int y = (int16_t)(in[3 * p] - off0), co = in[3 * p + 1], cg = in[3 * p + 2];
+        rgb[3 * p] = (uint8_t)sat8((int16_t)(y + co - cg));
+        rgb[3 * p + 1] = (uint8_t)sat8((int16_t)(y + cg));
+        rgb[3 * p + 2] = (uint8_t)sat8((int16_t)(y - co - cg));
+    }
+}
+
+// deadzone.encode (src/deadzone.py:67-79): img.astype(int16), (x / Q).astype(int32)
+// (A5), astype(uint8); decode (:81-93): Q * k in uint8 (value-based casting of
+// a Python int Q <= 255 against uint8 keeps uint8: wraps).  Elementwise over
+// n bytes, 16 per thread.
+template <bool ENC>
+__global__ __launch_bounds__(kThreads) void dz_u8_kernel(const uint8_t *__restrict__ x, int64_t n, int Q,
+                                                         uint8_t *__restrict__ y)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; 16 * p < n; p += stride) {
+        const int64_t b0 = 16 * p;
+        auto f = [&](uint32_t v) -> uint32_t { return ENC ? (uint32_t)((int)v / Q) & 0xffu : ((uint32_t)Q * v) & 0xffu; };
+        if (b0 + 16 <= n && (((uintptr_t)(x + b0) | (uintptr_t)(y + b0)) & 15) == 0) {
+            const uint4 in = *reinterpret_cast<const uint4 *>(x + b0);
+            uint32_t w[4] = {in.x, in.y, in.z, in.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t o = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o |= f((w[i] >> (8 * j)) & 0xffu) << (8 * j);
+                w[i] = o;
+            }
+            *reinterpret_cast<uint4 *>(y + b0) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            for (int64_t q = b0; q < min(n, b0 + 16); ++q) y[q] = (uint8_t)f(x[q]);
+        }
+    }
+}
+
 // ---- numpy.histogram(x[..., c], bins=n, range=(lo, hi)), numpy 1.26 --------
 // bin_type BT = result_type(lo, hi, x): float32 for float32 x, float64 for
 // integer x.  keep = lo <= x <= hi; f = ((x - lo) / (hi - lo)) * n in BT;
@@ -353,6 +484,72 @@ int vcf_ycrcb_dz_decode(const uint16_t *k_dev, int64_t n_px, int32_t Q, uint8_t 
     hipLaunchKernelGGL(ycrcb_dz_decode_kernel, dim3(grid_for(n_px)), dim3(kThreads), 0, (hipStream_t)stream, k_dev,
                        n_px, Q, rgb_dev);
     return hip_check(hipGetLastError(), "ycrcb_dz_decode_kernel launch");
+}
+
+int vcf_ycocg_dz_encode(const uint8_t *rgb_dev, int64_t n_px, int32_t Q, uint16_t *k_dev, void *stream)
+{
+    if (n_px < 0) return set_error(VCF_ERR_INVALID, "n_px < 0");
+    if (Q < 1) return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
+    if (n_px == 0) return VCF_OK;
+    if (!rgb_dev || !k_dev) return set_error(VCF_ERR_INVALID, "null buffer");
+    hipLaunchKernelGGL(ycocg_dz_encode_kernel, dim3(grid_for(n_px, 16)), dim3(kThreads), 0, (hipStream_t)stream,
+                       rgb_dev, n_px, Q, k_dev);
+    return hip_check(hipGetLastError(), "ycocg_dz_encode_kernel launch");
+}
+
+int vcf_ycocg_dz_decode(const uint16_t *k_dev, int64_t n_px, int32_t Q, uint8_t *rgb_dev, void *stream)
+{
+    if (n_px < 0) return set_error(VCF_ERR_INVALID, "n_px < 0");
+    if (Q < 1 || Q > 32767)
+        return set_error(VCF_ERR_UNSUPPORTED, "quantization step %d: int16 dequantization needs 1 <= Q <= 32767", Q);
+    if (n_px == 0) return VCF_OK;
+    if (!rgb_dev || !k_dev) return set_error(VCF_ERR_INVALID, "null buffer");
+    hipLaunchKernelGGL(ycocg_dz_decode_kernel, dim3(grid_for(n_px)), dim3(kThreads), 0, (hipStream_t)stream, k_dev,
+                       n_px, Q, rgb_dev);
+    return hip_check(hipGetLastError(), "ycocg_dz_decode_kernel launch");
+}
+
+int vcf_ycocg_i16_from_rgb(const uint8_t *rgb_dev, int64_t n_px, int32_t offset0, int16_t *out_dev, void *stream)
+{
+    if (n_px < 0) return set_error(VCF_ERR_INVALID, "n_px < 0");
+    if (n_px == 0) return VCF_OK;
+    if (!rgb_dev || !out_dev) return set_error(VCF_ERR_INVALID, "null buffer");
+    hipLaunchKernelGGL(ycocg_i16_from_rgb_kernel, dim3(grid_for(n_px)), dim3(kThreads), 0, (hipStream_t)stream,
+                       rgb_dev, n_px, offset0, out_dev);
+    return hip_check(hipGetLastError(), "ycocg_i16_from_rgb_kernel launch");
+}
+
+int vcf_ycocg_i16_to_rgb(const int16_t *in_dev, int64_t n_px, int32_t offset0, uint8_t *rgb_dev, void *stream)
+{
+    if (n_px < 0) return set_error(VCF_ERR_INVALID, "n_px < 0");
+    if (n_px == 0) return VCF_OK;
+    if (!rgb_dev || !in_dev) return set_error(VCF_ERR_INVALID, "null buffer");
+    hipLaunchKernelGGL(ycocg_i16_to_rgb_kernel, dim3(grid_for(n_px)), dim3(kThreads), 0, (hipStream_t)stream, in_dev,
+                       n_px, offset0, rgb_dev);
+    return hip_check(hipGetLastError(), "ycocg_i16_to_rgb_kernel launch");
+}
+
+int vcf_dz_u8_encode(const uint8_t *x_dev, int64_t n, int32_t Q, uint8_t *k_dev, void *stream)
+{
+    if (n < 0) return set_error(VCF_ERR_INVALID, "n < 0");
+    if (Q < 1) return set_error(VCF_ERR_INVALID, "quantization step %d out of range", Q);
+    if (n == 0) return VCF_OK;
+    if (!x_dev || !k_dev) return set_error(VCF_ERR_INVALID, "null buffer");
+    hipLaunchKernelGGL(dz_u8_kernel<true>, dim3(grid_for(n, 64)), dim3(kThreads), 0, (hipStream_t)stream, x_dev, n,
+                       Q, k_dev);
+    return hip_check(hipGetLastError(), "dz_u8_kernel launch");
+}
+
+int vcf_dz_u8_decode(const uint8_t *k_dev, int64_t n, int32_t Q, uint8_t *y_dev, void *stream)
+{
+    if (n < 0) return set_error(VCF_ERR_INVALID, "n < 0");
+    if (Q < 1 || Q > 255)
+        return set_error(VCF_ERR_UNSUPPORTED, "quantization step %d: uint8 dequantization needs 1 <= Q <= 255", Q);
+    if (n == 0) return VCF_OK;
+    if (!k_dev || !y_dev) return set_error(VCF_ERR_INVALID, "null buffer");
+    hipLaunchKernelGGL(dz_u8_kernel<false>, dim3(grid_for(n, 64)), dim3(kThreads), 0, (hipStream_t)stream, k_dev, n,
+                       Q, y_dev);
+    return hip_check(hipGetLastError(), "dz_u8_kernel launch");
 }
 
 int vcf_lm_levels(int32_t Q_step, int32_t min_val, int32_t max_val)

@@ -109,6 +109,53 @@ def ycrcb_dz_decode(k: np.ndarray, Q: int) -> np.ndarray:
         dout.free()
 
 
+# ---- YCoCg.py and deadzone.py, the stand-alone pixel codecs --------------------
+def _map(fn: str, a: np.ndarray, out_dtype, n: int, Q: int) -> np.ndarray:
+    out = np.empty(a.shape, out_dtype)
+    if n == 0:
+        call(fn, None, 0, int(Q), None, None)   # argument checks only
+        return out
+    din, dout = DeviceBuffer.from_array(a), DeviceBuffer(out.nbytes)
+    try:
+        call(fn, din.ptr, n, int(Q), dout.ptr, None)
+        return dout.download(out)
+    finally:
+        din.free()
+        dout.free()
+
+
+def ycocg_dz_encode(rgb: np.ndarray, Q: int) -> np.ndarray:
+    """YCoCg.encode (src/YCoCg.py:33-56) with -a deadzone: u8 RGB -> uint16 indices."""
+    rgb = _rgb(rgb, "rgb")
+    if rgb.dtype != np.uint8:
+        raise TypeError("rgb must be uint8")
+    return _map("vcf_ycocg_dz_encode", rgb, np.uint16, rgb.shape[0] * rgb.shape[1], Q)
+
+
+def ycocg_dz_decode(k: np.ndarray, Q: int) -> np.ndarray:
+    """YCoCg.decode (:58-85) with -a deadzone: uint16 indices -> u8 RGB."""
+    k = _rgb(k, "k")
+    if k.dtype != np.uint16:
+        raise TypeError("k must be uint16 (YCoCg.py:50)")
+    return _map("vcf_ycocg_dz_decode", k, np.uint8, k.shape[0] * k.shape[1], Q)
+
+
+def dz_u8_encode(img: np.ndarray, Q: int) -> np.ndarray:
+    """deadzone.encode (src/deadzone.py:67-79): u8 image -> u8 indices (any shape)."""
+    img = np.ascontiguousarray(img)
+    if img.dtype != np.uint8:
+        raise TypeError("img must be uint8")
+    return _map("vcf_dz_u8_encode", img, np.uint8, img.size, Q)
+
+
+def dz_u8_decode(k: np.ndarray, Q: int) -> np.ndarray:
+    """deadzone.decode (:81-93): u8 indices -> Q * k in uint8."""
+    k = np.ascontiguousarray(k)
+    if k.dtype != np.uint8:
+        raise TypeError("k must be uint8 (deadzone.py:76)")
+    return _map("vcf_dz_u8_decode", k, np.uint8, k.size, Q)
+
+
 # ---- LloydMax ----------------------------------------------------------------
 def lm_levels(Q: int, min_val: int, max_val: int) -> int:
     return call("vcf_lm_levels", int(Q), int(min_val), int(max_val))

@@ -29,6 +29,19 @@ def bound(strip_bytes: int) -> int:
     return int(L.lib().vcf_zlib_bound(int(strip_bytes)))
 
 
+def max_strip() -> int:
+    """The largest strip the GPU deflate takes (vcf_zlib_max_strip: 65536 bytes)."""
+    return int(L.lib().vcf_zlib_max_strip())
+
+
+def covers(shape, itemsize: int = 1) -> bool:
+    """True when tifffile's strips of an H x W [x C] array fit the GPU deflate
+    (rows of at most 64 KB; wider frames keep the host TIFF writer)."""
+    from .codec.tiff import strip_layout
+    shape = tuple(int(s) for s in shape)
+    return strip_layout(shape if len(shape) == 3 else shape + (1,), itemsize)[2] <= max_strip()
+
+
 class StripDeflater:
     """Deflates every strip of a batch of device-resident frames.  Scratch
     buffers grow on demand and are reused; calls are serialised (one set of
