@@ -132,4 +132,4 @@ def test_device_iii_tiff_equals_host_writer():
         for i in range(n):
             want = imwrite_bytes(k[i])
             assert got[i] == want and sizes[i] == len(want), (n, i)
-            assert np.array_equal(imread_bytes(got[i]), k[i])
+            assert np.array_equal(imread_bytes(bytes(got[i])), k[i])

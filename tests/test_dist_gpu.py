@@ -134,6 +134,7 @@ def test_bench_two_ranks_without_launcher():
     assert p.returncode == 0, p.stderr[-2000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 8 and line["value"] > 0
+    _check_c4_blocks(line)
 
 
 def test_bench_two_ranks_under_torchrun():
@@ -154,6 +155,22 @@ def test_bench_two_ranks_under_torchrun():
     assert len(lines) == 1, p.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 8 and line["value"] > 0
+    _check_c4_blocks(line)
+
+
+def _check_c4_blocks(line):
+    """At world 2 the C4 blocks either ran on two GPUs (times, every stage's
+    maximum over ranks, every frame verified) or -- two ranks on this box's one
+    GPU -- say explicitly that they were skipped; never an RCCL error string."""
+    from vcf_amd.device import device_count
+    for key in ("c4_e2e_with_gather", "c4_tiff_e2e_with_gather"):
+        b = line[key]
+        assert "error" not in b, b
+        if device_count() < 2:
+            assert b["skipped"].startswith("ranks share a device"), b
+        else:
+            assert b["ms"] > 0 and b["verified"].startswith("ok"), b
+            assert b["frames_per_rank"] == [128, 128] and set(b["stages_ms_max"]) == set(b["slowest_rank"])
 
 
 def test_device_iii_single_rank_rccl():
@@ -180,7 +197,7 @@ def test_device_iii_single_rank_rccl():
         k = O.encode_frame(f, 32, 0)
         want = codec.compress(k).getvalue()
         assert got[i] == want and sizes[i] == len(want), i
-        assert np.array_equal(codec.decompress(got[i]), k), i
+        assert np.array_equal(codec.decompress(bytes(got[i])), k), i
     sizes2, got2 = job.run(rgb)                  # reusable: same bytes again
     assert got2 == got and list(sizes2) == list(sizes)
     comm.close()

@@ -37,7 +37,7 @@ from .. import tcbaac as T
 from .. import zlib_gpu as Z
 from ..device import DeviceBuffer, HostBuffer, Stream, copy_dtod, copy_pieces
 from .shard import frame_range
-from .tiff import container_prefix, strip_layout
+from .tiff import container_prefixes, strip_layout
 
 
 class DeviceIII:
@@ -83,8 +83,9 @@ class DeviceIII:
     def run(self, rgb: DeviceBuffer, stages: dict | None = None):
         """Encode this rank's frames (rgb: n_local frames, H x W x 3 u8, back
         to back) and gather every frame's container on rank 0.
-        -> (per-frame container sizes of all N frames, list of N container
-        bytes on rank 0 / None elsewhere).  With `stages`, each stage is
+        -> (per-frame container sizes of all N frames, list of N containers on
+        rank 0 -- memoryviews into the page-locked receive buffer, valid until
+        the next run -- / None elsewhere).  With `stages`, each stage is
         synchronised and its seconds are added under its name (diagnostic:
         the syncs cost a little)."""
         def mark(name, t0):
@@ -107,7 +108,10 @@ class DeviceIII:
             else:
                 sz = np.zeros((0, 1), np.int64)
             t = mark("entropy", t)
-            headers = [container_prefix(self.shape, np.uint8, sz[f]) for f in range(self.n_local)]
+            # every frame's TIFF prefix at once (only the strip offsets / byte counts differ)
+            hdr = container_prefixes(self.shape, np.uint8, sz) if self.n_local else np.zeros((0, 0), np.uint8)
+            hlen = np.full(self.n_local, hdr.shape[1], np.int64)
+            hb = hdr.reshape(-1)
             pay_buf = self.zd.out if self.n_local else None
             spf = sz.shape[1]
             pay_src = (np.arange(self.n_local * spf, dtype=np.int64) * self.zd.slot if self.n_local else
@@ -119,33 +123,30 @@ class DeviceIII:
             seg, totals, priors = self.batch.sizes()          # waits for the coder
             t = mark("entropy", t)
             headers = self.batch.headers(self.shape)
+            hlen = np.array([len(h) for h in headers], np.int64)
+            hb = np.frombuffer(b"".join(headers), np.uint8)
             pay_buf = self.batch.out
             pay_src = np.zeros((self.n_local, 1), np.int64)
             pay_len = np.zeros((self.n_local, 1), np.int64)
             for f in range(self.n_local):
                 pbuf, poff, pn = self.batch.payload(f)
                 pay_src[f, 0], pay_len[f, 0] = poff, pn
-        local_sizes = np.array([len(h) + int(pay_len[f].sum()) for f, h in enumerate(headers)], np.int64)
+        local_sizes = hlen + pay_len.sum(axis=1)
         nbytes = int(local_sizes.sum())
         send = self._buf("send", nbytes)
         if self.n_local:
             # headers (staged from the host) and payloads (in the coder's output)
-            # land back to back in the send buffer: two gather-copy launches
-            hb = np.frombuffer(b"".join(headers), np.uint8)
+            # land back to back in the send buffer: two gather-copy launches, their
+            # piece tables computed in whole arrays
             hst = self._buf("hstage", hb.size)
             hst.upload(hb, self.stream)
             npay = pay_len.shape[1]
-            hdr_tab = np.empty((self.n_local, 3), np.int64)
-            pay_tab = np.empty((self.n_local, npay, 3), np.int64)
-            off = hoff = 0
-            for f, h in enumerate(headers):
-                hdr_tab[f] = (hoff, off, len(h))
-                off += len(h)
-                hoff += len(h)
-                for j in range(npay):
-                    pay_tab[f, j] = (pay_src[f, j], off, pay_len[f, j])
-                    off += int(pay_len[f, j])
-            tab = np.concatenate([hdr_tab.ravel(), pay_tab.ravel()])
+            frame_off = np.concatenate([[0], np.cumsum(local_sizes)[:-1]])
+            hdr_tab = np.stack([np.concatenate([[0], np.cumsum(hlen)[:-1]]), frame_off, hlen], axis=1)
+            pay_dst = (frame_off + hlen)[:, None] + np.concatenate(
+                [np.zeros((self.n_local, 1), np.int64), np.cumsum(pay_len, axis=1)[:, :-1]], axis=1)
+            pay_tab = np.stack([pay_src, pay_dst, pay_len], axis=2)
+            tab = np.concatenate([hdr_tab.ravel(), pay_tab.ravel()]).astype(np.int64)
             tb = self._buf("table", tab.nbytes)
             tb.upload(tab, self.stream)
             copy_pieces(hst, tb, self.n_local, send, self.stream)
@@ -171,10 +172,10 @@ class DeviceIII:
             if total:
                 recv.download(blob, self.stream)
             self.stream.synchronize()
-            out, off = [], 0
-            for s in sizes:
-                out.append(blob[off:off + int(s)].tobytes())
-                off += int(s)
+            # views into the page-locked buffer (valid until the next run), no per-frame copies
+            mv = memoryview(blob)
+            ends = np.cumsum(sizes)
+            out = [mv[int(e - s):int(e)] for s, e in zip(sizes, ends)]
         else:
             self.stream.synchronize()
         mark("d2h_rank0", t)

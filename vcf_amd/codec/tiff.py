@@ -152,6 +152,31 @@ def container_prefix(shape, dtype, counts) -> bytes:
     return bytes(out)
 
 
+def container_prefixes(shape, dtype, counts) -> np.ndarray:
+    """container_prefix for a batch of equal-shaped frames at once: counts is
+    (n_frames, strips) compressed sizes -> (n_frames, prefix bytes) uint8, row
+    f equal to container_prefix(shape, dtype, counts[f]).  Only the
+    StripOffsets / StripByteCounts values differ between the frames, so the
+    prefix is built once and those two arrays are filled in vectorised."""
+    counts = np.asarray(counts, np.int64)
+    n, ns = counts.shape
+    tmpl = container_prefix(shape, dtype, [0] * ns)
+    data_off = len(tmpl)
+    nt = struct.unpack("<H", tmpl[8:10])[0]
+    pos = {}
+    for i in range(nt):
+        e = 10 + 12 * i
+        code, _, count = struct.unpack("<HHI", tmpl[e:e + 8])
+        if code in (273, 279):
+            pos[code] = e + 8 if 4 * count <= 4 else struct.unpack("<I", tmpl[e + 8:e + 12])[0]
+    out = np.tile(np.frombuffer(tmpl, np.uint8), (n, 1))
+    offs = np.full((n, ns), data_off, np.int64)
+    offs[:, 1:] += np.cumsum(counts[:, :-1], axis=1)
+    for code, v in ((273, offs), (279, counts)):
+        out[:, pos[code]:pos[code] + 4 * ns] = v.astype("<u4").view(np.uint8).reshape(n, 4 * ns)
+    return out
+
+
 def _read_ifd(buf: bytes):
     bo = {b"II": "<", b"MM": ">"}.get(buf[:2])
     if bo is None or struct.unpack(bo + "H", buf[2:4])[0] != 42:

@@ -42,6 +42,7 @@
 #include "vcf_amd.h"
 #include "vcf_deflate.h"
 #include "vcf_internal.h"
+#include "vcf_pipeline.h"
 
 namespace vcf {
 namespace {
@@ -66,6 +67,23 @@ constexpr int64_t kRrOff = kRfOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSymOff = kRrOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;   // adler sums (2 x u64), worklist length (u32)
 constexpr int64_t kWsPerStrip = kSumOff + 32;
+// Rounds: at most kRound strips share one workspace slot; up to kZSlots rounds
+// are in flight at once on library streams (round r on stream r % kZSlots,
+// after round r - kZSlots, which used the same slot), so one round's
+// latency-bound tail -- a few strips' serial parses -- overlaps the next
+// rounds' work.  Workspace: kZSlots x kRound x kWsPerStrip < 4 GB.
+constexpr int64_t kRound = 1200;
+constexpr int kZSlots = 3;
+static_assert(kZSlots <= kAuxStreams, "one library stream per slot");
+struct ZRounds {
+    int64_t rounds, per, slots;
+    explicit ZRounds(int64_t total)
+    {
+        rounds = std::max<int64_t>(1, (total + kRound - 1) / kRound);
+        per = (total + rounds - 1) / rounds;
+        slots = std::min<int64_t>(kZSlots, rounds);
+    }
+};
 constexpr int kK2bThreads = 1024;    // K2b: 16 waves per strip, one listed position per wave at a time
 // A strip is parsed LAZY (on demand, zlib's order of work) when K1 finds fewer than
 // one distinct hash per kLazyDiv positions among its 64-position groups: such
@@ -111,12 +129,15 @@ __device__ __forceinline__ bool strip_lazy(const Strip &S)
 {
     return *reinterpret_cast<const uint32_t *>(S.ws + kSumOff + 20) != 0;
 }
+// strip s of the batch; its workspace is slot s - s0 of the round's workspace
+// (rounds of at most kRound strips reuse one workspace)
 __device__ __forceinline__ Strip strip_of(const uint8_t *in, int64_t frame_bytes, int32_t strip_bytes, int32_t spf,
-                                          uint8_t *ws, int64_t s)
+                                          uint8_t *ws, int64_t s0, int64_t s)
 {
     const int64_t f = s / spf, k = s - f * spf;
     const int64_t off = k * (int64_t)strip_bytes;
-    return {in + f * frame_bytes + off, (uint32_t)min((int64_t)strip_bytes, frame_bytes - off), ws + s * kWsPerStrip};
+    return {in + f * frame_bytes + off, (uint32_t)min((int64_t)strip_bytes, frame_bytes - off),
+            ws + (s - s0) * kWsPerStrip};
 }
 
 // ---- K1: hash-bucket order of the positions, and the adler32 sums ----------
@@ -138,15 +159,29 @@ __device__ __forceinline__ void stage_chunk(uint8_t *stage, const uint8_t *src, 
     }
 }
 
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c)   // zlib UPDATE_HASH x3
+{
+    return (a << 10 ^ b << 5 ^ c) & 0x7fffu;
+}
+
+// One wave per strip.  Pass 1: the hash histogram (and the adler32 sums);
+// exclusive scan; pass 2: the ordered scatter, 256 positions (four 64-lane
+// sub-groups) per step: within a sub-group the same-hash lane masks give each
+// position its rank, the first lane of each hash (the leader) adds the
+// sub-group's count to the bucket cursor with one LDS atomic returning the old
+// cursor -- the four sub-groups' atomics issue back to back and execute in
+// order, so a later sub-group sees an earlier one's update -- and the other
+// lanes take the leader's old cursor by ds_bpermute.  hd[] (zlib's head[] as
+// p is inserted) is zlib_head_kernel's: every position in parallel from
+// sorted[idx[p]-1].
 __global__ __launch_bounds__(64) void zlib_order_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
                                                        int32_t strip_bytes, int32_t spf, uint8_t *__restrict__ ws,
                                                        int64_t s0)
 {
     __shared__ __attribute__((aligned(16))) OrderSmem sm;
-    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0 + blockIdx.x);
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s0 + blockIdx.x);
     uint16_t *idx = reinterpret_cast<uint16_t *>(S.ws + kIdxOff);
     uint16_t *sorted = reinterpret_cast<uint16_t *>(S.ws + kSortOff);
-    uint16_t *hd = reinterpret_cast<uint16_t *>(S.ws + kHdOff);
     const uint32_t lane = lane_id(), n = S.n;
     const uint32_t np = n >= 3 ? n - 2 : 0;   // positions 0..n-3 are inserted
     for (uint32_t i = lane; i < (1u << 14); i += 64) sm.cnt[i] = 0;
@@ -161,7 +196,7 @@ __global__ __launch_bounds__(64) void zlib_order_kernel(const uint8_t *__restric
             sb += b;
             swb += (uint64_t)(p < n ? n - p : 0u) * b;
             if (p < np) {
-                const uint32_t h = ((uint32_t)b << 10 ^ (uint32_t)sm.stage[j + 1] << 5 ^ sm.stage[j + 2]) & 0x7fffu;
+                const uint32_t h = hash3(b, sm.stage[j + 1], sm.stage[j + 2]);
                 atomicAdd(&sm.cnt[h >> 1], 1u << ((h & 1) * 16));
             }
         }
@@ -182,64 +217,55 @@ __global__ __launch_bounds__(64) void zlib_order_kernel(const uint8_t *__restric
         sm.cnt[lane * 256 + i] = st;
         run += c0 + c1;
     }
-    // ordered scatter, 64 positions at a time, exact same-hash lane masks
-    uint32_t distinct = 0;   // sum over the groups of their distinct hashes
+    // ordered scatter
+    uint32_t distinct = 0;   // sum over the 64-position groups of their distinct hashes
+    const uint64_t lt = (1ull << lane) - 1;
     for (uint32_t c0 = 0; c0 < np; c0 += kStage) {
         wave_sync();
         stage_chunk(sm.stage, S.src, n, c0);
         wave_sync();
-        for (uint32_t g = 0; g < (uint32_t)kStage && c0 + g < np; g += 64) {
-            const uint32_t p = c0 + g + lane, j = g + lane;
-            const bool v = p < np;
-            const uint32_t h = ((uint32_t)sm.stage[j] << 10 ^ (uint32_t)sm.stage[j + 1] << 5 ^ sm.stage[j + 2]) & 0x7fffu;
-            uint64_t rem = __ballot(v), mine = 0;
-            while (rem) {   // one distinct hash per round
-                ++distinct;
-                const uint32_t l = (uint32_t)__ffsll((unsigned long long)rem) - 1;
-                const uint32_t hl = lane_val(h, l);
-                const uint64_t m = __ballot(v && h == hl);
-                if (v && h == hl) mine = m;
-                rem &= ~m;
+        for (uint32_t g = 0; g < (uint32_t)kStage && c0 + g < np; g += 256) {
+            uint32_t h[4], rank[4], cntj[4], old[4];
+            uint64_t mine[4];
+            bool v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t j = g + 64 * q + lane;
+                v[q] = c0 + j < np && j < (uint32_t)kStage;
+                h[q] = hash3(sm.stage[j], sm.stage[j + 1], sm.stage[j + 2]);
             }
-            if (v) {
-                const uint32_t rank = (uint32_t)__popcll(mine & ((1ull << lane) - 1));
-                const uint32_t sh = (h & 1) * 16;
-                const uint32_t slot = ((sm.cnt[h >> 1] >> sh) & 0xffffu) + rank;
-                idx[p] = (uint16_t)slot;
-                sorted[slot] = (uint16_t)p;
-                if (rank == 0) atomicAdd(&sm.cnt[h >> 1], (uint32_t)__popcll(mine) << sh);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint64_t rem = __ballot(v[q]), m0 = 0;
+                while (rem) {   // one distinct hash per round
+                    ++distinct;
+                    const uint32_t l = (uint32_t)__ffsll((unsigned long long)rem) - 1;
+                    const uint32_t hl = lane_val(h[q], l);
+                    const uint64_t m = __ballot(v[q] && h[q] == hl);
+                    if (v[q] && h[q] == hl) m0 = m;
+                    rem &= ~m;
+                }
+                mine[q] = m0;
+                rank[q] = (uint32_t)__popcll(m0 & lt);
+                cntj[q] = (uint32_t)__popcll(m0);
             }
-            wave_sync();
-        }
-    }
-    // hd[p]: zlib's head[] as p is inserted -- the newest earlier position with
-    // p's hash (0 = NIL, as zlib's position 0 is), from a last-position table and
-    // the group's own same-hash lanes; K2 reads it coalesced
-    for (uint32_t i = lane; i < (1u << 14); i += 64) sm.cnt[i] = 0;
-    uint16_t *last = reinterpret_cast<uint16_t *>(sm.cnt);
-    for (uint32_t c0 = 0; c0 < np; c0 += kStage) {
-        wave_sync();
-        stage_chunk(sm.stage, S.src, n, c0);
-        wave_sync();
-        for (uint32_t g = 0; g < (uint32_t)kStage && c0 + g < np; g += 64) {
-            const uint32_t p = c0 + g + lane, j = g + lane;
-            const bool v = p < np;
-            const uint32_t h = ((uint32_t)sm.stage[j] << 10 ^ (uint32_t)sm.stage[j + 1] << 5 ^ sm.stage[j + 2]) & 0x7fffu;
-            uint64_t rem = __ballot(v), mine = 0;
-            while (rem) {
-                const uint32_t l = (uint32_t)__ffsll((unsigned long long)rem) - 1;
-                const uint32_t hl = lane_val(h, l);
-                const uint64_t m = __ballot(v && h == hl);
-                if (v && h == hl) mine = m;
-                rem &= ~m;
+            // the leaders' cursor updates, back to back (LDS executes them in order)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                old[q] = 0;
+                if (v[q] && rank[q] == 0) old[q] = atomicAdd(&sm.cnt[h[q] >> 1], cntj[q] << ((h[q] & 1) * 16));
             }
-            if (v) {
-                const uint64_t lower = mine & ((1ull << lane) - 1);
-                hd[p] = (uint16_t)(lower ? c0 + g + 63 - (uint32_t)__clzll((long long)lower) : (uint32_t)last[h]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int leader = mine[q] ? __ffsll((unsigned long long)mine[q]) - 1 : (int)lane;
+                const uint32_t o = (uint32_t)__shfl((int)old[q], leader, 64);
+                if (v[q]) {
+                    const uint32_t p = c0 + g + 64 * q + lane;
+                    const uint32_t slot = ((o >> ((h[q] & 1) * 16)) & 0xffffu) + rank[q];
+                    idx[p] = (uint16_t)slot;
+                    sorted[slot] = (uint16_t)p;
+                }
             }
-            wave_sync();
-            if (v && (mine >> lane) == 1) last[h] = (uint16_t)p;   // the group's newest with this hash
-            wave_sync();
         }
     }
     for (int d = 32; d >= 1; d >>= 1) {
@@ -255,6 +281,43 @@ __global__ __launch_bounds__(64) void zlib_order_kernel(const uint8_t *__restric
     }
 }
 
+// hd[p]: zlib's head[] as p is inserted -- the newest earlier position with
+// p's hash, i.e. the bucket's previous slot sorted[idx[p]-1] when that slot is
+// still p's bucket (same hash), else NIL (0, which zlib's position 0 also is).
+// Every position in parallel: kHdPer consecutive positions per thread.
+constexpr int kHdThreads = 256, kHdPer = 8;
+__global__ __launch_bounds__(kHdThreads) void zlib_head_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+                                                              int32_t strip_bytes, int32_t spf,
+                                                              uint8_t *__restrict__ ws, int64_t s0)
+{
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s0 + blockIdx.y);
+    const uint32_t np = S.n >= 3 ? S.n - 2 : 0;
+    const uint32_t p0 = (blockIdx.x * kHdThreads + threadIdx.x) * kHdPer;
+    if (p0 >= np) return;
+    const uint16_t *idx = reinterpret_cast<const uint16_t *>(S.ws + kIdxOff);
+    const uint16_t *sorted = reinterpret_cast<const uint16_t *>(S.ws + kSortOff);
+    uint16_t *hd = reinterpret_cast<uint16_t *>(S.ws + kHdOff);
+    const uint32_t pn = min((uint32_t)kHdPer, np - p0);
+    uint32_t b[kHdPer + 2], q[kHdPer];
+#pragma unroll
+    for (int u = 0; u < kHdPer + 2; ++u) b[u] = (uint32_t)u < pn + 2 ? S.src[p0 + u] : 0u;
+#pragma unroll
+    for (int u = 0; u < kHdPer; ++u) {
+        const uint32_t i = (uint32_t)u < pn ? (uint32_t)idx[p0 + u] : 0u;
+        q[u] = i ? (uint32_t)sorted[i - 1] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kHdPer; ++u) {
+        if ((uint32_t)u >= pn) break;
+        uint32_t r = 0;
+        if (q[u] && q[u] < p0 + u) {   // an earlier slot holds an earlier position; same bucket iff same hash
+            const uint32_t hq = hash3(S.src[q[u]], S.src[q[u] + 1], S.src[q[u] + 2]);
+            if (hq == hash3(b[u], b[u + 1], b[u + 2])) r = q[u];
+        }
+        hd[p0 + u] = (uint16_t)r;
+    }
+}
+
 // ---- K2: longest_match at every position, both chain limits ----------------
 // A thread takes kPer consecutive positions.  zlib's own shortcuts, exact:
 // a candidate can only beat the best length L so far if it matches at bytes
@@ -267,7 +330,7 @@ __global__ __launch_bounds__(kK2Threads) void zlib_match_kernel(const uint8_t *_
 {
     __shared__ __attribute__((aligned(16))) uint32_t win32[kK2Win / 4 + 4];
     uint8_t *win = reinterpret_cast<uint8_t *>(win32);
-    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0 + blockIdx.y);
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s0 + blockIdx.y);
     const uint32_t n = S.n, p0 = blockIdx.x * kChunk;
     const uint32_t np = n >= 3 ? n - 2 : 0;
     if (p0 >= np || strip_lazy(S)) return;
@@ -397,7 +460,7 @@ __global__ __launch_bounds__(kK2bThreads) void zlib_chain_kernel(const uint8_t *
 {
     __shared__ __attribute__((aligned(16))) uint32_t win32[(MAX_STRIP + MAX_MATCH + 64) / 4];
     uint8_t *win = reinterpret_cast<uint8_t *>(win32);
-    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0 + blockIdx.x);
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s0 + blockIdx.x);
     const uint32_t n = S.n;
     const uint32_t cnt = *reinterpret_cast<const uint32_t *>(S.ws + kSumOff + 16);
     if (cnt == 0 || strip_lazy(S)) return;
@@ -524,17 +587,28 @@ __global__ __launch_bounds__(kK2bThreads) void zlib_chain_kernel(const uint8_t *
 }
 
 // ---- K3: the parse, the trees, the bits ------------------------------------
+// The trees' Freq and Code share storage, as in zlib's ct_data union: a tree's
+// codes are written by gen_codes after its last frequency read, and the next
+// block's counts start from zero after its last code read.  The block's symbol
+// counts go straight into the frequency arrays (packed 16-bit LDS adds).
 struct ParseSmem {
-    uint16_t lfreq[HEAP_SIZE], ldad[HEAP_SIZE], llen[HEAP_SIZE], lcode[L_CODES + 2];
-    uint16_t dfreq[2 * D_CODES + 1], ddad[2 * D_CODES + 1], dlen[2 * D_CODES + 1], dcode[D_CODES + 2];
-    uint16_t bfreq[2 * BL_CODES + 1], bdad[2 * BL_CODES + 1], blen[2 * BL_CODES + 1], bcode[BL_CODES + 2];
+    uint16_t lfreq[HEAP_SIZE + 1], ldad[HEAP_SIZE], llen[HEAP_SIZE];
+    uint16_t dfreq[2 * D_CODES + 1 + 1], ddad[2 * D_CODES + 1], dlen[2 * D_CODES + 1];
+    uint16_t bfreq[2 * BL_CODES + 1 + 1], bdad[2 * BL_CODES + 1], blen[2 * BL_CODES + 1];
     int16_t heap[HEAP_SIZE];
     uint8_t depth[HEAP_SIZE];
     uint16_t bl_count[MAX_BITS + 1];
     uint32_t stg[kStgWords];
-    uint32_t lhist[L_CODES], dhist[D_CODES];   // the block's symbol counts (counted at flush)
     uint32_t bcast[4];
 };
+static_assert(offsetof(ParseSmem, lfreq) % 4 == 0, "packed adds into lfreq");
+// the lazy parse's sliding window of the strip: [wbase, wbase + kLazyWin) holds
+// every byte longest_match can read at the current position (back to
+// p - MAX_DIST, ahead to p + MAX_MATCH + 62); the parse shifts it forward in
+// 256-byte steps, so four strips (window + ParseSmem <= 40 KB) fit a CU
+constexpr uint32_t kLazyWin = 34560;
+constexpr uint32_t kLazyAhead = 320;
+static_assert(kLazyWin >= MAX_DIST + kLazyAhead + 1024, "window too short for its shifts");
 
 // LAZY (strips K1 found repetitive, kLazyDiv below): zlib's own order of work --
 // the strip in LDS and longest_match evaluated only where deflate_slow calls it
@@ -560,8 +634,10 @@ struct Wave {
     uint32_t bv0, bv1;
     bool overflow = false;
     BlockTrees T;
-    // LAZY: the window in LDS, the bucket order, and a 512-position window of idx[]
-    uint8_t *lwin = nullptr;
+    // LAZY: the sliding window in LDS, the bucket order, and a 512-position window of idx[]
+    uint8_t *lwin = nullptr;      // window byte i is input position wbase + i
+    uint32_t wbase = 0;
+    bool wslid = false;           // zlib's window has slid: the bytes past n are the stale copy WSIZE back
     const uint16_t *idx = nullptr, *sorted = nullptr;
     uint32_t ibase = 0x80000000u;
     uint4 iv;
@@ -572,9 +648,9 @@ struct Wave {
           rf(reinterpret_cast<const uint32_t *>(w + kRfOff)), rr(reinterpret_cast<const uint32_t *>(w + kRrOff)),
           syms(reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(w) + kSymOff)), out32(o), out_words(ow), good(g)
     {
-        T.l = {sm.lfreq, sm.ldad, sm.llen, sm.lcode, L_CODES, MAX_BITS, 0, 0};
-        T.d = {sm.dfreq, sm.ddad, sm.dlen, sm.dcode, D_CODES, MAX_BITS, 1, 0};
-        T.bl = {sm.bfreq, sm.bdad, sm.blen, sm.bcode, BL_CODES, MAX_BL_BITS, 2, 0};
+        T.l = {sm.lfreq, sm.ldad, sm.llen, sm.lfreq, L_CODES, MAX_BITS, 0, 0};
+        T.d = {sm.dfreq, sm.ddad, sm.dlen, sm.dfreq, D_CODES, MAX_BITS, 1, 0};
+        T.bl = {sm.bfreq, sm.bdad, sm.blen, sm.bfreq, BL_CODES, MAX_BL_BITS, 2, 0};
         T.w.heap = sm.heap;
         T.w.depth = sm.depth;
         T.w.bl_count = sm.bl_count;
@@ -681,7 +757,10 @@ struct Wave {
     // ---- deflate_slow's Ops ----------------------------------------------
     __device__ uint32_t byte(uint32_t p)
     {
-        if constexpr (LAZY) return lwin[p];
+        if constexpr (LAZY) {
+            ensure(p);
+            return lwin[p - wbase];
+        }
         window(p);
         const uint32_t off = p - base, l = off >> 3, e = off & 7;
         const uint32_t w = e < 4 ? lane_val(bv0, l) : lane_val(bv1, l);
@@ -698,16 +777,43 @@ struct Wave {
     __device__ void slide()   // fill_window's slide: past the end, the stale copy WSIZE back
     {
         if constexpr (LAZY) {
-            for (uint32_t P = n + lane_id(); P < n + MAX_MATCH; P += 64) lwin[P] = lwin[P - WSIZE];
+            wslid = true;
+            for (uint32_t P = max(n, wbase) + lane_id(); P < min(n + MAX_MATCH, wbase + kLazyWin); P += 64)
+                lwin[P - wbase] = src[P - WSIZE];
             wave_sync();
         }   // (K2 compared against the slid window already)
     }
-    __device__ uint32_t ld4(uint32_t a)
+    // the byte zlib's window holds at input position P (P < wbase + kLazyWin):
+    // the strip, then zeros (fill_window's high_water zeroing) or, once slid, the stale copy
+    __device__ uint32_t win_src(uint32_t P) const
+    {
+        return P < n ? (uint32_t)src[P] : (wslid && P - WSIZE < n ? (uint32_t)src[P - WSIZE] : 0u);
+    }
+    __device__ void fill(uint32_t from, uint32_t to)   // window bytes of input positions [from, to)
+    {
+        for (uint32_t P = from + lane_id(); P < to; P += 64) lwin[P - wbase] = (uint8_t)win_src(P);
+    }
+    // keep [p - MAX_DIST, p + kLazyAhead) in the window: shift it forward when p runs ahead
+    __device__ void ensure(uint32_t p)
+    {
+        if (p + kLazyAhead <= wbase + kLazyWin) return;
+        const uint32_t nb = (p > (uint32_t)MAX_DIST ? p - MAX_DIST : 0u) & ~255u;
+        const uint32_t d = nb - wbase;   // > 0, a multiple of 256
+        uint4 *w = reinterpret_cast<uint4 *>(lwin);
+        // forward copy in increasing order: chunk k reads at >= d + 1024 k, writes below d + 1024 k
+        for (uint32_t o = 16 * lane_id(); o < kLazyWin - d; o += 1024) w[o >> 4] = w[(o + d) >> 4];
+        wave_sync();
+        const uint32_t old_end = wbase + kLazyWin;
+        wbase = nb;
+        fill(old_end, nb + kLazyWin);
+        wave_sync();
+    }
+    __device__ uint32_t ld4(uint32_t a)   // window offsets
     {
         const uint32_t *w32 = reinterpret_cast<const uint32_t *>(lwin);
         return __builtin_amdgcn_alignbyte(w32[(a >> 2) + 1], w32[a >> 2], a & 3);
     }
-    __device__ uint32_t hash_at(uint32_t q) { return ((uint32_t)lwin[q] << 10 ^ (uint32_t)lwin[q + 1] << 5 ^ lwin[q + 2]) & 0x7fffu; }
+    __device__ uint32_t hash_at(uint32_t q) { return hash3(lwin[q], lwin[q + 1], lwin[q + 2]); }   // window offset
     // common prefix of the strings at a and b, up to MAX_MATCH: one wave-wide compare
     __device__ uint32_t wave_lcp(uint32_t a, uint32_t b)
     {
@@ -742,14 +848,16 @@ struct Wave {
         if constexpr (LAZY) {
             // the first candidate (chain order) reaching max(nice, prev_len+1), else the
             // first reaching the longest length found, if longer than prev_len
+            ensure(p);
+            const uint32_t wp = p - wbase;   // window offsets from here on (every candidate is >= wbase)
             const uint32_t Tn = max(nice, prev_len + 1);
-            const uint32_t l1 = wave_lcp(hdp, p);
+            const uint32_t l1 = wave_lcp(hdp - wbase, wp);
             if (l1 >= Tn) {
                 len = l1;
                 pos = hdp;
                 return true;
             }
-            const uint32_t hp = hash_at(p);
+            const uint32_t hp = hash_at(wp);
             // only a candidate longer than F = max(prev_len, the head's length) can change the
             // result, and such a one matches at bytes F-1 and F (longest_match's scan_end test)
             const uint32_t F = max(prev_len, l1);
@@ -768,12 +876,14 @@ struct Wave {
                 const uint32_t gk = b + lane_id();
                 bool v = gk < chain && gk < ip;
                 const uint32_t c = v ? (uint32_t)sorted[ip - 1 - gk] : 0u;
-                v = v && (gk == 0 || c > limit) && hash_at(c) == hp;
+                v = v && (gk == 0 || c > limit);
+                const uint32_t wc = v ? c - wbase : 0u;
+                v = v && hash_at(wc) == hp;
                 const uint64_t stop = __ballot(!v);
                 const uint32_t nv = stop ? (uint32_t)__ffsll((unsigned long long)stop) - 1 : 64u;
                 v = lane_id() < nv;
-                const bool cand = v && gk != 0 && lwin[c + F] == lwin[p + F] && lwin[c + F - 1] == lwin[p + F - 1];
-                const uint32_t l = v ? (gk == 0 ? l1 : cand ? lane_lcp(c, p) : 0u) : 0u;
+                const bool cand = v && gk != 0 && lwin[wc + F] == lwin[wp + F] && lwin[wc + F - 1] == lwin[wp + F - 1];
+                const uint32_t l = v ? (gk == 0 ? l1 : cand ? lane_lcp(wc, wp) : 0u) : 0u;
                 const uint64_t hit = __ballot(v && l >= Tn);
                 if (hit) {
                     const uint32_t k = (uint32_t)__ffsll((unsigned long long)hit) - 1;
@@ -812,10 +922,14 @@ struct Wave {
     }
     __device__ void init_freqs()
     {
-        for (uint32_t i = lane_id(); i < (uint32_t)L_CODES; i += 64) sm.lhist[i] = 0;
-        if (lane_id() < (uint32_t)D_CODES) sm.dhist[lane_id()] = 0;
+        for (uint32_t i = lane_id(); i < (uint32_t)L_CODES; i += 64) sm.lfreq[i] = 0;
+        if (lane_id() < (uint32_t)D_CODES) sm.dfreq[lane_id()] = 0;
         if (lane_id() < (uint32_t)BL_CODES) sm.bfreq[lane_id()] = 0;
         wave_sync();
+    }
+    __device__ static void add16(uint16_t *a, uint32_t i)   // a[i]++ as a packed 32-bit LDS add (no carry: < 65536)
+    {
+        atomicAdd(reinterpret_cast<uint32_t *>(a) + (i >> 1), 1u << ((i & 1) * 16));
     }
     // _tr_tally's counts for the whole block at once (LDS atomics), then init_block's END_BLOCK
     __device__ void count_block()
@@ -823,16 +937,14 @@ struct Wave {
         for (uint32_t i = lane_id(); i < nsym; i += 64) {
             const uint32_t sy = ld_l2(syms + i), dist = sy >> 8, lc = sy & 0xff;
             if (dist == 0) {
-                atomicAdd(&sm.lhist[lc], 1u);
+                add16(sm.lfreq, lc);
             } else {
-                atomicAdd(&sm.lhist[length_code((int)lc) + 257], 1u);
-                atomicAdd(&sm.dhist[dist_code((int)(dist - 1))], 1u);
+                add16(sm.lfreq, (uint32_t)length_code((int)lc) + 257);
+                add16(sm.dfreq, (uint32_t)dist_code((int)(dist - 1)));
             }
         }
         wave_sync();
-        for (uint32_t i = lane_id(); i < (uint32_t)L_CODES; i += 64)
-            sm.lfreq[i] = (uint16_t)(sm.lhist[i] + (i == END_BLOCK ? 1u : 0u));
-        if (lane_id() < (uint32_t)D_CODES) sm.dfreq[lane_id()] = (uint16_t)sm.dhist[lane_id()];
+        if (lane_id() == 0) sm.lfreq[END_BLOCK] += 1;   // init_block's END_BLOCK count
         wave_sync();
     }
     __device__ void flush(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
@@ -869,11 +981,11 @@ struct Wave {
         } else {
             if (kind == 1) {
                 for (uint32_t i = lane_id(); i < (uint32_t)L_CODES; i += 64) {
-                    sm.lcode[i] = (uint16_t)static_lcode((int)i);
+                    sm.lfreq[i] = (uint16_t)static_lcode((int)i);   // (Code shares Freq's storage)
                     sm.llen[i] = (uint16_t)static_llen((int)i);
                 }
                 if (lane_id() < (uint32_t)D_CODES) {
-                    sm.dcode[lane_id()] = (uint16_t)static_dcode((int)lane_id());
+                    sm.dfreq[lane_id()] = (uint16_t)static_dcode((int)lane_id());
                     sm.dlen[lane_id()] = 5;
                 }
                 wave_sync();
@@ -882,10 +994,10 @@ struct Wave {
                 const uint32_t q = i + lane_id();
                 uint64_t v = 0;
                 int nb = 0;
-                if (q < nsym) symbol_bits(ld_l2(syms + q), sm.lcode, sm.llen, sm.dcode, sm.dlen, v, nb);
+                if (q < nsym) symbol_bits(ld_l2(syms + q), sm.lfreq, sm.llen, sm.dfreq, sm.dlen, v, nb);
                 emit_par(v, (uint32_t)nb);
             }
-            emit_par(lane_id() == 0 ? sm.lcode[END_BLOCK] : 0u, lane_id() == 0 ? sm.llen[END_BLOCK] : 0u);
+            emit_par(lane_id() == 0 ? sm.lfreq[END_BLOCK] : 0u, lane_id() == 0 ? sm.llen[END_BLOCK] : 0u);
         }
         nsym = 0;
         init_freqs();
@@ -900,8 +1012,9 @@ struct ParseShared {
 template <>
 struct ParseShared<true> {
     ParseSmem sm;
-    uint32_t win32[(MAX_STRIP + 320) / 4];   // the strip, then the window bytes past its end
+    uint32_t win32[kLazyWin / 4];   // the sliding window of the strip (Wave::ensure)
 };
+static_assert(sizeof(ParseShared<true>) <= 40960, "four lazy-parse workgroups per CU");
 
 template <bool LAZY>
 __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
@@ -913,7 +1026,7 @@ __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restric
     __shared__ __attribute__((aligned(16))) ParseShared<LAZY> sh;
     ParseSmem &sm = sh.sm;
     const int64_t s = s0 + blockIdx.x;
-    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s);
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s);
     if (strip_lazy(S) != LAZY) return;   // the other kernel codes this strip
     const uint32_t lane = lane_id();
     Config cfg;
@@ -922,15 +1035,15 @@ __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restric
     Wave<LAZY> wv(sm, S.src, S.n, S.ws, (uint32_t)cfg.good, reinterpret_cast<uint32_t *>(out + s * slot_bytes),
                   (uint32_t)(slot_bytes >> 2));
     if constexpr (LAZY) {
-        // the window: the strip, then zeros (fill_window's high_water zeroing)
+        // the window's first kLazyWin bytes: the strip, then zeros (fill_window's high_water zeroing)
         uint8_t *win = reinterpret_cast<uint8_t *>(sh.win32);
         if (((uintptr_t)S.src & 3) == 0) {
             const uint32_t *s32 = reinterpret_cast<const uint32_t *>(S.src);
-            for (uint32_t q = lane; q < (MAX_STRIP + 320) / 4; q += 64) sh.win32[q] = 4 * q + 4 <= S.n ? s32[q] : 0u;
+            for (uint32_t q = lane; q < kLazyWin / 4; q += 64) sh.win32[q] = 4 * q + 4 <= S.n ? s32[q] : 0u;
             wave_sync();
-            for (uint32_t p = (S.n & ~3u) + lane; p < S.n; p += 64) win[p] = S.src[p];
+            for (uint32_t p = (S.n & ~3u) + lane; p < min(S.n, kLazyWin); p += 64) win[p] = S.src[p];
         } else {
-            for (uint32_t p = lane; p < (uint32_t)(MAX_STRIP + 320); p += 64) win[p] = p < S.n ? S.src[p] : 0u;
+            for (uint32_t p = lane; p < kLazyWin; p += 64) win[p] = p < S.n ? S.src[p] : 0u;
         }
         wv.lwin = win;
         wv.idx = reinterpret_cast<const uint16_t *>(S.ws + kIdxOff);
@@ -967,7 +1080,12 @@ int64_t vcf_zlib_bound(int64_t strip_bytes)
 
 int32_t vcf_zlib_max_strip(void) { return dfl::MAX_STRIP; }
 
-int64_t vcf_zlib_workspace(int64_t n_strips) { return n_strips < 0 ? -1 : n_strips * kWsPerStrip; }
+int64_t vcf_zlib_workspace(int64_t n_strips)
+{
+    if (n_strips < 0) return -1;
+    const ZRounds zr(n_strips);
+    return zr.slots * zr.per * kWsPerStrip;
+}
 
 int64_t vcf_zlib_strip_count(int64_t frame_bytes, int32_t strip_bytes)
 {
@@ -997,30 +1115,58 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     const int64_t total = spf * n_frames;
     hipStream_t st = (hipStream_t)stream;
     const int chunks = (int)((std::min<int64_t>(strip_bytes, frame_bytes) + kChunk - 1) / kChunk);
-    for (int64_t s0 = 0; s0 < total; s0 += 65535) {   // grid limits: strips [s0, s0 + cnt) per round
-        const unsigned cnt = (unsigned)std::min<int64_t>(65535, total - s0);
-        hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
-                           (int32_t)spf, (uint8_t *)ws_dev, s0);
+    const unsigned hd_blocks = (unsigned)((std::min<int64_t>(strip_bytes, frame_bytes) + kHdThreads * kHdPer - 1) /
+                                          (kHdThreads * kHdPer));
+    auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws, hipStream_t rs) -> int {
+        hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64), 0, rs, in_dev, frame_bytes, strip_bytes,
+                           (int32_t)spf, ws, s0);
         int rc = hip_check(hipGetLastError(), "zlib_order_kernel launch");
         if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, st, in_dev,
-                           frame_bytes, strip_bytes, (int32_t)spf, level, (uint8_t *)ws_dev, s0);
+        hipLaunchKernelGGL(zlib_head_kernel, dim3(hd_blocks, cnt), dim3(kHdThreads), 0, rs, in_dev, frame_bytes,
+                           strip_bytes, (int32_t)spf, ws, s0);
+        rc = hip_check(hipGetLastError(), "zlib_head_kernel launch");
+        if (rc != VCF_OK) return rc;
+        hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, rs, in_dev,
+                           frame_bytes, strip_bytes, (int32_t)spf, level, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_match_kernel launch");
         if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt), dim3(kK2bThreads), 0, st, in_dev, frame_bytes, strip_bytes,
-                           (int32_t)spf, level, (uint8_t *)ws_dev, s0);
+        hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt), dim3(kK2bThreads), 0, rs, in_dev, frame_bytes, strip_bytes,
+                           (int32_t)spf, level, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_chain_kernel launch");
         if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
-                           (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, (uint8_t *)ws_dev, s0);
+        hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3(cnt), dim3(64), 0, rs, in_dev, frame_bytes, strip_bytes,
+                           (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_parse_kernel launch");
         if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
-                           (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, (uint8_t *)ws_dev, s0);
-        rc = hip_check(hipGetLastError(), "zlib_parse_kernel (lazy) launch");
-        if (rc != VCF_OK) return rc;
+        hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3(cnt), dim3(64), 0, rs, in_dev, frame_bytes, strip_bytes,
+                           (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
+        return hip_check(hipGetLastError(), "zlib_parse_kernel (lazy) launch");
+    };
+    const ZRounds zr(total);
+    uint8_t *ws = (uint8_t *)ws_dev;
+    if (zr.rounds == 1) return round(0, (unsigned)total, ws, st);
+    // rounds in flight on library streams, forked from the caller's stream and joined back to it
+    AuxStreams &ax = aux_for_current_device();
+    std::lock_guard<std::mutex> lock(ax.mu);
+    int rc = ax.init();
+    if (rc != VCF_OK) return rc;
+    if ((rc = hip_check(hipEventRecord(ax.fork, st), "hipEventRecord")) != VCF_OK) return rc;
+    for (int j = 0; j < zr.slots; ++j)
+        if ((rc = hip_check(hipStreamWaitEvent(ax.s[j], ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
+    for (int64_t r = 0; r < zr.rounds && rc == VCF_OK; ++r) {
+        const int64_t s0 = r * zr.per;
+        if (s0 >= total) break;
+        const int j = (int)(r % zr.slots);
+        rc = round(s0, (unsigned)std::min<int64_t>(zr.per, total - s0), ws + (int64_t)j * zr.per * kWsPerStrip,
+                   ax.s[j]);
     }
-    return VCF_OK;
+    // join every library stream even after an error, so the caller's stream never runs ahead
+    for (int j = 0; j < zr.slots; ++j) {
+        int r2 = hip_check(hipEventRecord(ax.join[j], ax.s[j]), "hipEventRecord");
+        if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(st, ax.join[j], 0), "hipStreamWaitEvent");
+        if (rc == VCF_OK) rc = r2;
+    }
+    return rc;
 }
 
 }  // extern "C"
