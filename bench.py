@@ -360,6 +360,104 @@ def c4_verify(got, bases, job, N, H, W, Q, world, entropy="TCBAACP") -> str:
     return f"ok: {what} equal to the frame coded alone; frames 0 and {N - 1} decode to their indices"
 
 
+def c5_frame(base, i: int, H: int, W: int) -> np.ndarray:
+    """Frame i of the C5 sequence: a window of a larger S-smooth picture panning
+    by (2i mod 41, 3i mod 53) pixels, so the motion search finds real vectors."""
+    dy, dx = (2 * i) % 41, (3 * i) % 53
+    return np.ascontiguousarray(base[dy:dy + H, dx:dx + W])
+
+
+def c5_block(args, world: int, rank: int, group):
+    """Config C5 of BASELINE.json: IPP_DCT over a 64-frame 4K sequence, GOP 10,
+    full search bs 16 / S 8, 2D-DCT + deadzone + the default -c TIFF, GOPs
+    sharded across the ranks, end to end on the GPU
+    (vcf_amd/codec/ipp_device.py: the rank's GOPs in lock step, batched DCT,
+    GPU TIFF deflate and DCT decode per step, files gathered to rank 0 over
+    RCCL).  Timed like the headline (barrier + device sync, max over ranks).
+    Returns the block dict; never raises."""
+    from vcf_amd.codec.ipp_device import DeviceIPP
+    from vcf_amd.comm import HostGroup
+    from vcf_amd.device import DeviceBuffer, device_count, synchronize
+    from vcf_amd.rccl import Communicator
+    N, H, W, Q, G = args.c5_frames, 2160, 3840, args.QSS, 10
+    info = {"workload": (f"IPP_DCT C5: {N} x 4K frames (panning S-smooth), GOP {G}, full search bs 16 / S 8, "
+                         f"residual 2D-DCT + deadzone Q={Q} + -c TIFF (GPU deflate, zlib level 6), GOP g on rank "
+                         "floor(g*P/G), the rank's GOPs in lock step, files gathered to rank 0 over RCCL"),
+            "frames": N, "frame": [H, W, 3], "gop": G, "n_ranks": world}
+    if world > 1 and device_count() < world:
+        info["skipped"] = (f"ranks share a device ({world} ranks on {device_count()} GPU(s)): RCCL refuses two "
+                           "ranks on one GPU, so the C5 exchange runs only with one GPU per rank")
+        return info
+    err, comm, t_rank, stages, job = None, None, float("nan"), {}, None
+    try:
+        base = synth_frame(H + 48, W + 64, seed=500)
+        comm = Communicator(group if world > 1 else HostGroup(0, 1), timeout_s=args.c4_timeout)
+        job = DeviceIPP(comm, rank, world, N, H, W, Q, G, 16, 8, False)
+        rgb = DeviceBuffer(max(job.n_local * H * W * 3, 1))
+        for j, i in enumerate(range(job.lo, job.hi)):
+            rgb.upload(c5_frame(base, i, H, W), offset=j * H * W * 3)
+        for _ in range(args.c5_warmup):
+            job.run(rgb)
+        group.barrier()
+        synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.c5_steps):
+            sizes, got, mvs = job.run(rgb)
+        synchronize()
+        t_rank = (time.perf_counter() - t0) / args.c5_steps
+        job.run(rgb, stages)
+        info["frames_this_rank0"] = job.n_local if rank == 0 else None
+        if rank == 0:
+            info["code_bytes"] = int(sizes.sum())
+            info["bits_per_pixel"] = round(8 * int(sizes.sum()) / (N * H * W), 5)
+            info["_check"] = (got, mvs, base)   # verified after the timed regions (rank 0, N = 1)
+    except Exception as e:   # reported in the block; the headline line still prints
+        err = f"{type(e).__name__}: {e}"
+    finally:
+        if comm is not None:
+            try:
+                comm.close()
+            except Exception:
+                pass
+    times = group.all_gather_f64(t_rank) if world > 1 else [t_rank]
+    keys = ("gop_loop", "sizes_d2h", "pack", "sizes_allgather", "gatherv", "d2h_rank0")
+    rows = [group.all_gather_f64(stages.get(k, float("nan"))) if world > 1 else [stages.get(k, float("nan"))]
+            for k in keys]
+    info["stages_ms_max"] = {k: round(float(np.nanmax(r)) * 1e3, 3) for k, r in zip(keys, rows)
+                             if np.isfinite(r).any()}
+    if err is None and all(np.isfinite(times)):
+        tmax = max(times)
+        info.update(ms=round(tmax * 1e3, 3), steps=args.c5_steps, warmup=args.c5_warmup,
+                    value=round(N * H * W / tmax / 1e6, 1), unit="Mpixels/s", frames_per_s=round(N / tmax, 1))
+    else:
+        info["error"] = err or "another rank failed"
+    return info
+
+
+def c5_check(info, Q: int) -> None:
+    """The checker leg (rank 0, N = 1, beside cpu_baseline): frames 0 and 1 of the
+    C5 block's first GOP against the reference's GOP loop restated by the C oracle
+    (IPP_DCT.py:397-575: the I-frame's indices; the P-frame's full-search motion
+    field, compensation, residual and indices), files compared byte for byte with
+    the host TIFF writer's.  Replaces the block's private _check entry."""
+    chk = info.pop("_check", None) if info else None
+    if chk is None:
+        return
+    from oracle import oracle as O
+    from vcf_amd.codec.tiff import imwrite_bytes
+    got, mvs, base = chk
+    H, W = info["frame"][:2]
+    f0, f1 = c5_frame(base, 0, H, W), c5_frame(base, 1, H, W)
+    k0 = O.encode_frame(f0, Q)
+    ref = O.decode_frame(k0, H, W, Q)
+    mv = O.ipp_block_matching(ref, f1, 16, 8, False)
+    k1 = O.encode_frame(O.ipp_residual(f1, O.ipp_motion_compensate(ref, mv, 16)), Q)
+    ok = (bytes(got[0]) == imwrite_bytes(k0) and bytes(got[1]) == imwrite_bytes(k1) and
+          np.array_equal(np.asarray(mvs[0]), np.asarray(mv)))
+    info["verified"] = ("ok: frames 0 (I) and 1 (P) equal the host TIFF writer's files of the reference GOP "
+                        "loop's indices (C oracle), frame 1's motion field equal" if ok else "MISMATCH")
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc pass (if it matches)."""
     p = os.path.join(ROOT, "profiles", "pmc_encode_4k.json")
@@ -394,6 +492,9 @@ def main():
     ap.add_argument("--no-c4-tiff", action="store_true", help="skip the C4 block with -c TIFF (GPU deflate)")
     ap.add_argument("--c4-warmup", type=int, default=1)
     ap.add_argument("--c4-timeout", type=float, default=90.0, help="seconds before an RCCL call is aborted")
+    ap.add_argument("--c5-frames", type=int, default=64, help="4K frames of the C5 block (0 disables it)")
+    ap.add_argument("--c5-steps", type=int, default=2)
+    ap.add_argument("--c5-warmup", type=int, default=1)
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -452,6 +553,8 @@ def main():
     c4 = c4_block(args, world, rank, group) if args.c4_frames > 0 else None
     # the same with the reference's default entropy codec, -c TIFF (GPU deflate)
     c4t = c4_block(args, world, rank, group, "TIFF") if args.c4_frames > 0 and not args.no_c4_tiff else None
+    # C5 (IPP_DCT, 64 x 4K, GOP 10, full search, -c TIFF on the GPU deflate, GOP-sharded)
+    c5 = c5_block(args, world, rank, group) if args.c5_frames > 0 else None
 
     # after the timed region (an idle GPU during seconds of CPU work would start
     # the timed steps at low clocks): parity spot check of the timed kernel's
@@ -462,6 +565,9 @@ def main():
         cpu, k_ref = cpu_baseline(distinct[0], Q, args.cpu_budget)
         k_gpu = dout.download(np.empty((Hp, Wp, 3), np.uint8))
         parity = "bit-exact vs oracle (frame 0)" if np.array_equal(k_gpu, k_ref) else "MISMATCH"
+        c5_check(c5, Q)
+    elif c5 is not None:
+        c5.pop("_check", None)
 
     workload = (f"dct_dz_encode {H}x{W}x3 u8 RGB frames (4K), B=8, YCoCg, deadzone Q={Q}, "
                 f"subband layout, {F} frames/step/GPU resident in HBM")
@@ -502,6 +608,7 @@ def main():
             "parity": parity,
             "c4_e2e_with_gather": c4,
             "c4_tiff_e2e_with_gather": c4t,
+            "c5_e2e_with_gather": c5,
         }
         print(json.dumps(out), flush=True)
     group.close()

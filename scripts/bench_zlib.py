@@ -70,8 +70,12 @@ def main():
         slots = out.download(np.empty(total * slot, np.uint8))
         # check every strip of frames 0 and n-1, and a sample elsewhere
         chk = sorted(set(list(range(spf)) + list(range((n - 1) * spf, total)) + list(range(0, total, 37))))
-        ok = all(slots[s * slot:s * slot + sz[s]].tobytes() ==
-                 zlib.compress(flat[s // spf, (s % spf) * sb:(s % spf + 1) * sb].tobytes(), 6) for s in chk)
+        bad = [s for s in chk if slots[s * slot:s * slot + sz[s]].tobytes() !=
+               zlib.compress(flat[s // spf, (s % spf) * sb:(s % spf + 1) * sb].tobytes(), 6)]
+        ok = not bad
+        if bad:
+            print(f"{name}: {len(bad)} of {len(chk)} checked strips differ from zlib, first {bad[:12]}",
+                  file=sys.stderr, flush=True)
         # host: zlib on a thread pool over the same strips
         strips = [flat[f, k * sb:(k + 1) * sb] for f in range(n) for k in range(spf)]
         with ThreadPoolExecutor(args.threads) as ex:

@@ -1,0 +1,28 @@
+"""Diagnostic: deflate the C4 workload once and dump every strip's size and a
+checksum of its bytes (compare runs with VCF_ZLIB_SLOTS=1 and =3)."""
+import sys, os, zlib
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import synth_frame, c4_frame
+from vcf_amd import _lib as L, dct
+from vcf_amd.codec.tiff import strip_layout
+from vcf_amd.device import DeviceBuffer, Stream
+n, H, W = int(sys.argv[1]), 1080, 1920
+bases = [synth_frame(H, W, seed=100 + s) for s in range(4)]
+frames = np.concatenate([dct.encode(np.stack([c4_frame(bases, i) for i in range(f, min(n, f + 16))]), Q=32)
+                         for f in range(0, n, 16)])
+flat = np.ascontiguousarray(frames.reshape(n, -1))
+fb = flat.shape[1]; _, _, sb = strip_layout(frames.shape[1:], 1)
+spf = int(L.lib().vcf_zlib_strip_count(fb, sb)); total = spf * n; slot = int(L.lib().vcf_zlib_bound(sb))
+d = DeviceBuffer.from_array(flat); out = DeviceBuffer(total * slot); sizes = DeviceBuffer(total * 4)
+ws = DeviceBuffer(int(L.lib().vcf_zlib_workspace(total))); st = Stream()
+L.call("vcf_zlib_strips", d.ptr, n, fb, sb, 6, out.ptr, slot, sizes.ptr, ws.ptr, st.handle)
+st.synchronize()
+sz = sizes.download(np.empty(total, np.int32))
+o = out.download(np.empty(total * slot, np.uint8))
+crc = np.array([zlib.crc32(o[s * slot:s * slot + sz[s]].tobytes()) for s in range(total)], np.uint32)
+np.savez(sys.argv[2], sz=sz, crc=crc)
+bad = [s for s in range(total) if o[s * slot:s * slot + sz[s]].tobytes() !=
+       zlib.compress(flat[s // spf, (s % spf) * sb:(s % spf + 1) * sb].tobytes(), 6)]
+print(f"{sys.argv[2]}: total {total}, bad {len(bad)}: {bad[:40]}", flush=True)

@@ -247,3 +247,46 @@ def test_ipp_over_2d_dwt_matches_oracle_loop(tmp_path):
     r = subprocess.run([sys.executable, cli, "encode", "-i", pat, "-O", str(tmp_path / "c" / "v")] + flags,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def _ipp_loop_indices(frames, gop, bs, sr, fast, Q):
+    """_ipp_loop's per-frame index arrays (what each frame's .tif holds) and motion fields."""
+    ks, mvs = [], []
+    for g0 in range(0, len(frames), gop):
+        H, W = frames[g0].shape[:2]
+        k = O.encode_frame(frames[g0], Q)
+        ks.append(k)
+        ref = O.decode_frame(k, H, W, Q)
+        for p in range(1, min(gop, len(frames) - g0)):
+            mv = O.ipp_block_matching(ref, frames[g0 + p], bs, sr, fast)
+            comp = O.ipp_motion_compensate(ref, mv, bs)
+            k = O.encode_frame(O.ipp_residual(frames[g0 + p], comp), Q)
+            ks.append(k)
+            ref = O.ipp_reconstruct(comp, O.decode_frame(k, H, W, Q))
+            mvs.append(mv)
+    return ks, mvs
+
+
+@pytest.mark.parametrize("fast", [False, True], ids=["full", "tss"])
+@pytest.mark.parametrize("n,gop,H,W", [(7, 3, 72, 96), (10, 4, 64, 80), (5, 10, 48, 64)])
+def test_device_ipp_equals_reference_loop(n, gop, H, W, fast):
+    """The HBM-resident C5 path (vcf_amd/codec/ipp_device.py: GOPs in lock step,
+    batched DCT + GPU TIFF deflate): every gathered file equals the host TIFF
+    writer's file of the reference loop's indices for that frame, and the motion
+    fields are the reference loop's (IPP_DCT.py:397-575 restated by the oracle)."""
+    from vcf_amd.codec.ipp_device import DeviceIPP
+    from vcf_amd.codec.tiff import imread_bytes, imwrite_bytes
+    from vcf_amd.device import DeviceBuffer
+    frames = _moving(H, W, n, 17 + n)
+    job = DeviceIPP(None, 0, 1, n, H, W, 32, gop, 16, 8, fast)
+    stages = {}
+    sizes, got, mvs = job.run(DeviceBuffer.from_array(np.stack(frames)), stages)
+    ks, want_mv = _ipp_loop_indices(frames, gop, 16, 8, fast, 32)
+    assert len(got) == n and len(mvs) == len(want_mv)
+    for i in range(n):
+        want = imwrite_bytes(ks[i])
+        assert bytes(got[i]) == want and sizes[i] == len(want), i
+        assert np.array_equal(imread_bytes(bytes(got[i])), ks[i])
+    for a, b in zip(mvs, want_mv):
+        assert np.array_equal(a, b)
+    assert set(stages) >= {"gop_loop", "pack", "gatherv"}

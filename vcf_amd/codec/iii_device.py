@@ -67,18 +67,8 @@ class DeviceIII:
                                           f"the GPU deflate's {Z.max_strip()}; use the file path (dct2d.encode_fns)")
         else:
             self.batch = T.FrameBatch(self.n_local, self.n_sym, 0, seg_len, prior=True, nclass=nclass)
-        self.send = None
-        self.recv = None
-        self.hstage = None
-        self.table = None
-        self.host = None
-
-    def _buf(self, name: str, nbytes: int) -> DeviceBuffer:
-        b = getattr(self, name)
-        if b is None or b.nbytes < nbytes:
-            b = DeviceBuffer(max(nbytes, 1))
-            setattr(self, name, b)
-        return b
+        self.exchange = Exchange(comm, self.rank, self.world, self.N, lambda r: frame_range(self.N, r, self.world),
+                                 self.stream)
 
     def run(self, rgb: DeviceBuffer, stages: dict | None = None):
         """Encode this rank's frames (rgb: n_local frames, H x W x 3 u8, back
@@ -131,6 +121,37 @@ class DeviceIII:
             for f in range(self.n_local):
                 pbuf, poff, pn = self.batch.payload(f)
                 pay_src[f, 0], pay_len[f, 0] = poff, pn
+        return self.exchange.run(hb, hlen, pay_buf, pay_src, pay_len, mark, t)
+
+
+class Exchange:
+    """The containers of one rank's frames packed into a device send buffer
+    and gathered to rank 0: per-frame sizes all-gathered
+    (ncclAllGather), the containers gathered device to device
+    (vcf_comm_gatherv: one ncclSend per peer, each over its own xGMI link),
+    then one copy to rank 0's page-locked host buffer.  Rank r holds the
+    global frames ranges(r) = [lo, hi) (contiguous, rank order)."""
+
+    def __init__(self, comm, rank: int, world: int, N: int, ranges, stream: Stream):
+        self.comm, self.rank, self.world, self.N = comm, int(rank), int(world), int(N)
+        self.ranges = ranges
+        self.lo, self.hi = ranges(self.rank)
+        self.n_local = self.hi - self.lo
+        self.stream = stream
+        self.send = self.recv = self.hstage = self.table = self.host = None
+
+    def _buf(self, name: str, nbytes: int) -> DeviceBuffer:
+        b = getattr(self, name)
+        if b is None or b.nbytes < nbytes:
+            b = DeviceBuffer(max(nbytes, 1))
+            setattr(self, name, b)
+        return b
+
+    def run(self, hb: np.ndarray, hlen: np.ndarray, pay_buf, pay_src: np.ndarray, pay_len: np.ndarray, mark, t):
+        """hb: every local frame's header bytes back to back (hlen[f] each);
+        frame f's payload is pay_len[f, j] bytes at pay_src[f, j] of pay_buf,
+        j in order.  -> (sizes of all N containers, rank 0's list of N
+        memoryviews into the page-locked receive buffer / None)."""
         local_sizes = hlen + pay_len.sum(axis=1)
         nbytes = int(local_sizes.sum())
         send = self._buf("send", nbytes)
@@ -154,8 +175,7 @@ class DeviceIII:
         t = mark("pack", t)
         sizes = self._all_gather_sizes(local_sizes)
         t = mark("sizes_allgather", t)
-        counts = np.array([sizes[slice(*frame_range(self.N, r, self.world))].sum() for r in range(self.world)],
-                          np.int64)
+        counts = np.array([sizes[slice(*self.ranges(r))].sum() for r in range(self.world)], np.int64)
         total = int(counts.sum())
         recv = self._buf("recv", total) if self.rank == 0 else None
         if self.comm is not None:
@@ -189,7 +209,7 @@ class DeviceIII:
         rows = self.comm.all_gather_i64(full)
         out = np.zeros(self.N, np.int64)
         for r in range(self.world):
-            rlo, rhi = frame_range(self.N, r, self.world)
+            rlo, rhi = self.ranges(r)
             out[rlo:rhi] = rows[r, rlo:rhi]
         return out
 

@@ -81,7 +81,12 @@ struct ZRounds {
     {
         rounds = std::max<int64_t>(1, (total + kRound - 1) / kRound);
         per = (total + rounds - 1) / rounds;
-        slots = std::min<int64_t>(kZSlots, rounds);
+        static const int max_slots = [] {   // VCF_ZLIB_SLOTS (A/B diagnostics): 1 = rounds in series
+            const char *e = getenv("VCF_ZLIB_SLOTS");
+            const int v = e ? atoi(e) : kZSlots;
+            return v < 1 ? 1 : v > kZSlots ? kZSlots : v;
+        }();
+        slots = std::min<int64_t>(max_slots, rounds);
     }
 };
 constexpr int kK2bThreads = 1024;    // K2b: 16 waves per strip, one listed position per wave at a time
@@ -93,6 +98,19 @@ constexpr int kK2bThreads = 1024;    // K2b: 16 waves per strip, one listed posi
 constexpr uint32_t kLazyDiv = 4;
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+#ifndef VCF_ZLIB_PROF
+#define VCF_ZLIB_PROF 0
+#endif
+#if VCF_ZLIB_PROF
+// diagnostic build only (scripts/zprof_build.sh): per-phase clock totals of the parse kernels
+// [0] lazy total, [1] lazy longest, [2] lazy flush, [3] longest calls, [4] chain rounds,
+// [5] window shifts, [6] lazy strips, [7] K3 (non-lazy) total
+__device__ unsigned long long g_zprof[8];
+#define VCF_ZPROF_COUNT(x) (++(x))
+#else
+#define VCF_ZPROF_COUNT(x) ((void)0)
+#endif
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint32_t lane_val(uint32_t v, uint32_t l)
 {
@@ -799,6 +817,7 @@ struct Wave {
         if (p + kLazyAhead <= wbase + kLazyWin) return;
         const uint32_t nb = (p > (uint32_t)MAX_DIST ? p - MAX_DIST : 0u) & ~255u;
         const uint32_t d = nb - wbase;   // > 0, a multiple of 256
+        VCF_ZPROF_COUNT(n_shift);
         uint4 *w = reinterpret_cast<uint4 *>(lwin);
         // forward copy in increasing order: chunk k reads at >= d + 1024 k, writes below d + 1024 k
         for (uint32_t o = 16 * lane_id(); o < kLazyWin - d; o += 1024) w[o >> 4] = w[(o + d) >> 4];
@@ -842,8 +861,36 @@ struct Wave {
         }
         return min(l, (uint32_t)MAX_MATCH);
     }
+#if VCF_ZLIB_PROF
+    unsigned long long t_longest = 0, t_flush = 0, n_longest = 0, n_rounds = 0, n_shift = 0;
     __device__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
                             uint32_t limit, uint32_t &len, uint32_t &pos)
+    {
+        const unsigned long long t0 = clock64();
+        const bool r = longest_impl(p, hdp, prev_len, chain, nice, limit, len, pos);
+        t_longest += clock64() - t0;
+        ++n_longest;
+        return r;
+    }
+    __device__ void flush(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
+    {
+        const unsigned long long t0 = clock64();
+        flush_impl(stored_len, buf_ok, block_start, last);
+        t_flush += clock64() - t0;
+    }
+#else
+    __device__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
+                            uint32_t limit, uint32_t &len, uint32_t &pos)
+    {
+        return longest_impl(p, hdp, prev_len, chain, nice, limit, len, pos);
+    }
+    __device__ void flush(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
+    {
+        flush_impl(stored_len, buf_ok, block_start, last);
+    }
+#endif
+    __device__ bool longest_impl(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
+                                 uint32_t limit, uint32_t &len, uint32_t &pos)
     {
         if constexpr (LAZY) {
             // the first candidate (chain order) reaching max(nice, prev_len+1), else the
@@ -873,6 +920,7 @@ struct Wave {
             uint32_t best = prev_len, bpos = 0;
             bool found = false;
             for (uint32_t b = 0; b < chain; b += 64) {
+                VCF_ZPROF_COUNT(n_rounds);
                 const uint32_t gk = b + lane_id();
                 bool v = gk < chain && gk < ip;
                 const uint32_t c = v ? (uint32_t)sorted[ip - 1 - gk] : 0u;
@@ -947,7 +995,7 @@ struct Wave {
         if (lane_id() == 0) sm.lfreq[END_BLOCK] += 1;   // init_block's END_BLOCK count
         wave_sync();
     }
-    __device__ void flush(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
+    __device__ void flush_impl(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
     {
         __threadfence();   // the block's symbols (lane 0's stores) before the other lanes read them
         wave_sync();
@@ -1053,7 +1101,26 @@ __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restric
 
     const uint32_t hdr = zlib_header(level);
     wv.emit_par(lane == 0 ? ((hdr >> 8) | ((hdr & 0xffu) << 8)) : 0u, lane == 0 ? 16u : 0u);
+#if VCF_ZLIB_PROF
+    const unsigned long long tp0 = clock64();
+#endif
     deflate_slow(wv, S.n, cfg);
+#if VCF_ZLIB_PROF
+    if (lane == 0) {
+        const unsigned long long tp = clock64() - tp0;
+        if (LAZY) {
+            atomicAdd(&g_zprof[0], tp);
+            atomicAdd(&g_zprof[1], wv.t_longest);
+            atomicAdd(&g_zprof[2], wv.t_flush);
+            atomicAdd(&g_zprof[3], wv.n_longest);
+            atomicAdd(&g_zprof[4], wv.n_rounds);
+            atomicAdd(&g_zprof[5], wv.n_shift);
+            atomicAdd(&g_zprof[6], 1ull);
+        } else {
+            atomicAdd(&g_zprof[7], tp);
+        }
+    }
+#endif
     const uint64_t *sums = reinterpret_cast<const uint64_t *>(S.ws + kSumOff);
     const uint32_t ad = adler32_from_sums(sums[0], sums[1], S.n);
     const uint32_t be = (ad >> 24) | ((ad >> 8) & 0xff00u) | ((ad << 8) & 0xff0000u) | (ad << 24);
@@ -1079,6 +1146,18 @@ int64_t vcf_zlib_bound(int64_t strip_bytes)
 }
 
 int32_t vcf_zlib_max_strip(void) { return dfl::MAX_STRIP; }
+
+#if VCF_ZLIB_PROF
+int vcf_zlib_prof_read(unsigned long long *host8, int reset)
+{
+    int rc = hip_check(hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_zprof), sizeof(g_zprof)), "hipMemcpyFromSymbol");
+    if (rc == VCF_OK && reset) {
+        static const unsigned long long z[8] = {};
+        rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_zprof), z, sizeof(z)), "hipMemcpyToSymbol");
+    }
+    return rc;
+}
+#endif
 
 int64_t vcf_zlib_workspace(int64_t n_strips)
 {

@@ -29,6 +29,11 @@ def bound(strip_bytes: int) -> int:
     return int(L.lib().vcf_zlib_bound(int(strip_bytes)))
 
 
+def workspace(n_strips: int) -> int:
+    """Workspace bytes of one vcf_zlib_strips call over n_strips strips."""
+    return int(L.lib().vcf_zlib_workspace(int(n_strips)))
+
+
 def max_strip() -> int:
     """The largest strip the GPU deflate takes (vcf_zlib_max_strip: 65536 bytes)."""
     return int(L.lib().vcf_zlib_max_strip())
