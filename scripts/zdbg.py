@@ -26,3 +26,8 @@ np.savez(sys.argv[2], sz=sz, crc=crc)
 bad = [s for s in range(total) if o[s * slot:s * slot + sz[s]].tobytes() !=
        zlib.compress(flat[s // spf, (s % spf) * sb:(s % spf + 1) * sb].tobytes(), 6)]
 print(f"{sys.argv[2]}: total {total}, bad {len(bad)}: {bad[:40]}", flush=True)
+for b in bad[:6]:
+    g = o[b * slot:b * slot + sz[b]].tobytes()
+    w = zlib.compress(flat[b // spf, (b % spf) * sb:(b % spf + 1) * sb].tobytes(), 6)
+    d = next((i for i in range(min(len(g), len(w))) if g[i] != w[i]), None)
+    print(f"  strip {b}: gpu {len(g)} B, zlib {len(w)} B, first difference at byte {d}", flush=True)

@@ -39,9 +39,8 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kTile = 256;                   // blocks (= lanes) per workgroup
-constexpr int kSegBytes = kTile * 3;         // one (i, j) subband run of a full tile
-constexpr int kStageBytes = 64 * kSegBytes;  // 48 KiB LDS image
+constexpr int kTile = 256;                   // blocks (= lanes) per workgroup; a full tile's (i, j)
+                                             // subband run is kTile * 3 bytes, its LDS image 48 KiB
 
 struct Geom {
     int H, W, Hp, Wp, top, left, nbx, nby, tiles_per_row;
@@ -89,20 +88,20 @@ __device__ __forceinline__ uint32_t seg_base(const Geom &g, int seg)
     return (i * (uint32_t)g.nby * (uint32_t)g.Wp + j * (uint32_t)g.nbx) * 3u;
 }
 
-template <bool SUB, bool TO_GLOBAL>
+template <bool SUB, bool TO_GLOBAL, int T = kTile>
 __device__ __forceinline__ void move_runs_tab(const Geom &g, uint8_t *stage, const uint32_t *rowbase,
                                               uint8_t *frame, int nvalid)
 {
     constexpr int nseg = SUB ? 64 : 8;
     constexpr int bpb = SUB ? 3 : 24;                  // bytes per block in a run
-    constexpr int lds_stride = SUB ? kSegBytes : kTile * 24;
+    constexpr int lds_stride = SUB ? T * 3 : T * 24;
     const int tid = threadIdx.x;
     if (g.vec) {
         const int cps = (nvalid * bpb) >> 4;           // nvalid is a multiple of 16
         // stage bytes are the low bytes of k: XOR 0x80 == +128 mod 256 (2D-DCT.py:348,361)
         const int total = nseg * cps;
 #pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
-        for (int q = tid; q < total; q += kTile) {
+        for (int q = tid; q < total; q += T) {
             const int seg = q / cps;
             const int off = (q - seg * cps) << 4;
             const int blk = off / bpb;
@@ -115,7 +114,7 @@ __device__ __forceinline__ void move_runs_tab(const Geom &g, uint8_t *stage, con
     } else {
         const int seg_len = nvalid * bpb, total = nseg * seg_len;
 #pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
-        for (int q = tid; q < total; q += kTile) {
+        for (int q = tid; q < total; q += T) {
             const int seg = q / seg_len;
             const int off = q - seg * seg_len;
             const int blk = off / bpb;
@@ -137,28 +136,38 @@ __device__ __forceinline__ void move_runs_tab(const Geom &g, uint8_t *stage, con
 // multiply-shifts and the run bases come from two per-launch constants
 // (full-rate v_mul_u32_u24 instead of quarter-rate 32-bit multiplies and
 // 64-bit address arithmetic) whenever the frame's subband stride fits 24 bits.
-template <bool SUB>
+// multiply-shift division q / cps for q < 64 cps (tiles of T = 256, 384, 512 blocks)
+template <int T>
+struct DivCps;
+template <>
+struct DivCps<256> { static constexpr uint32_t m = 2731, s = 17; };   // / 48
+template <>
+struct DivCps<384> { static constexpr uint32_t m = 3641, s = 18; };   // / 72
+template <>
+struct DivCps<512> { static constexpr uint32_t m = 2731, s = 18; };   // / 96
+
+template <bool SUB, int T = kTile>
 __device__ __forceinline__ void move_runs_full(const Geom &g, const uint8_t *stage, const uint32_t *rowbase,
                                                uint8_t *frame)
 {
     constexpr int nseg = SUB ? 64 : 8;
     constexpr int bpb = SUB ? 3 : 24;
-    constexpr int lds_stride = SUB ? kSegBytes : kTile * 24;
-    constexpr int cps = (kTile * bpb) >> 4;
-    constexpr int per_lane = nseg * cps / kTile;
-    static_assert(nseg * cps % kTile == 0, "whole stores per lane");
+    constexpr int lds_stride = SUB ? T * 3 : T * 24;
+    constexpr int cps = (T * bpb) >> 4;
+    constexpr int per_lane = nseg * cps / T;
+    static_assert(nseg * cps % T == 0, "whole stores per lane");
     const int tid = threadIdx.x;
     u32x4 v[per_lane];
     uint32_t go[per_lane];
     const uint32_t segA = (uint32_t)g.nby * (uint32_t)g.Wp * 3u, segB = (uint32_t)g.nbx * 3u;
     if (SUB && segA < (1u << 24)) {
-        static_assert(!SUB || (cps == 48 && bpb == 3), "multiply-shift constants");
+        static_assert(!SUB || bpb == 3, "multiply-shift constants");
 #pragma unroll
         for (int r = 0; r < per_lane; ++r) {
-            const int q = tid + r * kTile;                                   // < 3072
-            const int seg = (int)(__umul24((uint32_t)q, 21846u) >> 20);      // q / 48
-            const int off = (q - seg * cps) << 4;                            // < 768
-            const int blk = (int)(__umul24((uint32_t)off, 43691u) >> 17);    // off / 3
+            const int q = tid + r * T;                                                  // < 64 cps
+            const int seg = (int)(__umul24((uint32_t)q, DivCps<T>::m) >> DivCps<T>::s);   // q / cps
+            const int off = (q - seg * cps) << 4;                                       // < 3 T
+            const int blk = (int)(__umul24((uint32_t)off, 683u) >> 11);                 // off / 3
             go[r] = rowbase[blk] + __umul24((uint32_t)(seg >> 3), segA) + __umul24((uint32_t)(seg & 7), segB) +
                     (uint32_t)(off - blk * bpb);
             v[r] = *reinterpret_cast<const u32x4 *>(stage + seg * lds_stride + off);
@@ -166,7 +175,7 @@ __device__ __forceinline__ void move_runs_full(const Geom &g, const uint8_t *sta
     } else {
 #pragma unroll
         for (int r = 0; r < per_lane; ++r) {
-            const int q = tid + r * kTile;
+            const int q = tid + r * T;
             const int seg = q / cps;
             const int off = (q - seg * cps) << 4;
             const int blk = off / bpb;
@@ -226,23 +235,23 @@ __device__ __forceinline__ void load_block(const Geom &g, const uint8_t *src, in
     }
 }
 
-template <bool POW2, bool SUB, bool PERC, bool PK>
+template <bool POW2, bool SUB, bool PERC, bool PK, int T = kTile>
 __device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncConsts &K, const FinalK &rowk,
                                              uint8_t *stage, int tid)
 {
     // each index byte goes from the low byte of its register straight into
     // the LDS image of the output (no conversion, no packing)
     auto s0 = [&](int i, int j, uint32_t w) {
-        if (SUB) stage[(i * 8 + j) * kSegBytes + tid * 3 + 0] = (uint8_t)w;
-        else stage[i * (kTile * 24) + tid * 24 + j * 3 + 0] = (uint8_t)w;
+        if (SUB) stage[(i * 8 + j) * (T * 3) + tid * 3 + 0] = (uint8_t)w;
+        else stage[i * (T * 24) + tid * 24 + j * 3 + 0] = (uint8_t)w;
     };
     auto s1 = [&](int i, int j, uint32_t w) {
-        if (SUB) stage[(i * 8 + j) * kSegBytes + tid * 3 + 1] = (uint8_t)w;
-        else stage[i * (kTile * 24) + tid * 24 + j * 3 + 1] = (uint8_t)w;
+        if (SUB) stage[(i * 8 + j) * (T * 3) + tid * 3 + 1] = (uint8_t)w;
+        else stage[i * (T * 24) + tid * 24 + j * 3 + 1] = (uint8_t)w;
     };
     auto s2 = [&](int i, int j, uint32_t w) {
-        if (SUB) stage[(i * 8 + j) * kSegBytes + tid * 3 + 2] = (uint8_t)w;
-        else stage[i * (kTile * 24) + tid * 24 + j * 3 + 2] = (uint8_t)w;
+        if (SUB) stage[(i * 8 + j) * (T * 3) + tid * 3 + 2] = (uint8_t)w;
+        else stage[i * (T * 24) + tid * 24 + j * 3 + 2] = (uint8_t)w;
     };
     if constexpr (PK && POW2 && !PERC) {
         encode_block_channel_pk<0>(raw, rowk, K.qd[0], s0);
@@ -264,13 +273,13 @@ __device__ __forceinline__ void encode_block(uint32_t (&raw)[8][6], const EncCon
 // the transforms: a workgroup entering or leaving its memory phase is not held
 // behind the resident workgroups' VALU streams (1-2.5 % faster than none over
 // three boxes, ABBA).
-template <bool POW2, bool SUB, bool PERC, bool PAD, bool PK>
-__global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
-                                                              uint8_t *__restrict__ kout, Geom g,
-                                                              EncConsts K, FinalK rowk)
+template <bool POW2, bool SUB, bool PERC, bool PAD, bool PK, int T = kTile>
+__global__ __launch_bounds__(T) void dct_dz_encode_kernel(const uint8_t *__restrict__ rgb,
+                                                          uint8_t *__restrict__ kout, Geom g,
+                                                          EncConsts K, FinalK rowk)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kStageBytes];
-    __shared__ uint32_t rowbase[kTile];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[64 * T * 3];
+    __shared__ uint32_t rowbase[T];
     const int tid = threadIdx.x;
     // each XCD takes a contiguous range of tiles (workgroups are dealt round
     // robin), so neighbouring tiles -- which share partial lines at run joins --
@@ -280,8 +289,8 @@ __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__r
     const unsigned t = xcd * q + min(xcd, r) + (gid >> 3);
     const long long frame = t / gridDim.x;
     const int tile = (int)(t - (unsigned)frame * gridDim.x);
-    const int n0 = tile * kTile;
-    const int nvalid = min(kTile, g.nblocks - n0);
+    const int n0 = tile * T;
+    const int nvalid = min(T, g.nblocks - n0);
     if (tid < nvalid) {
         int by, bx;
         tile_block(g, n0 + tid, by, bx);
@@ -290,12 +299,12 @@ __global__ __launch_bounds__(kTile) void dct_dz_encode_kernel(const uint8_t *__r
         __builtin_amdgcn_s_setprio(3);
         load_block<PAD>(g, rgb + frame * g.in_stride, by, bx, raw);
         __builtin_amdgcn_s_setprio(0);
-        encode_block<POW2, SUB, PERC, PK>(raw, K, rowk, stage, tid);
+        encode_block<POW2, SUB, PERC, PK, T>(raw, K, rowk, stage, tid);
     }
     __syncthreads();
     __builtin_amdgcn_s_setprio(3);
-    if (nvalid == kTile && g.vec) move_runs_full<SUB>(g, stage, rowbase, kout + frame * g.out_stride);
-    else move_runs_tab<SUB, true>(g, stage, rowbase, kout + frame * g.out_stride, nvalid);
+    if (nvalid == T && g.vec) move_runs_full<SUB, T>(g, stage, rowbase, kout + frame * g.out_stride);
+    else move_runs_tab<SUB, true, T>(g, stage, rowbase, kout + frame * g.out_stride, nvalid);
 }
 
 // ---------------------------------------------------------------------------

@@ -67,25 +67,29 @@ constexpr int64_t kRrOff = kRfOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSymOff = kRrOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;   // adler sums (2 x u64), worklist length (u32)
 constexpr int64_t kWsPerStrip = kSumOff + 32;
-// Rounds: at most kRound strips share one workspace slot; up to kZSlots rounds
-// are in flight at once on library streams (round r on stream r % kZSlots,
-// after round r - kZSlots, which used the same slot), so one round's
+// Rounds: the strips of a call are processed in rounds whose workspace slots
+// together stay under kWsBudget (about 3.9 GB); with kZSlots > 1, up to that
+// many rounds are in flight at once on library streams (round r on stream
+// r % slots, after round r - slots, which used the same slot), so one round's
 // latency-bound tail -- a few strips' serial parses -- overlaps the next
-// rounds' work.  Workspace: kZSlots x kRound x kWsPerStrip < 4 GB.
-constexpr int64_t kRound = 1200;
+// rounds' work.  Default 1 slot (rounds in series on the caller's stream):
+// concurrent rounds produced wrong strips on MI355X, so
+// VCF_ZLIB_SLOTS > 1 is a diagnostic setting only.
+constexpr int64_t kWsBudget = 3900000000LL;
 constexpr int kZSlots = 3;
 static_assert(kZSlots <= kAuxStreams, "one library stream per slot");
 struct ZRounds {
     int64_t rounds, per, slots;
     explicit ZRounds(int64_t total)
     {
-        rounds = std::max<int64_t>(1, (total + kRound - 1) / kRound);
-        per = (total + rounds - 1) / rounds;
-        static const int max_slots = [] {   // VCF_ZLIB_SLOTS (A/B diagnostics): 1 = rounds in series
+        static const int max_slots = [] {   // VCF_ZLIB_SLOTS (diagnostics): rounds in flight, default 1
             const char *e = getenv("VCF_ZLIB_SLOTS");
-            const int v = e ? atoi(e) : kZSlots;
+            const int v = e ? atoi(e) : 1;
             return v < 1 ? 1 : v > kZSlots ? kZSlots : v;
         }();
+        const int64_t round_max = std::max<int64_t>(1, kWsBudget / (max_slots * kWsPerStrip));
+        rounds = std::max<int64_t>(1, (total + round_max - 1) / round_max);
+        per = (total + rounds - 1) / rounds;
         slots = std::min<int64_t>(max_slots, rounds);
     }
 };
@@ -660,7 +664,7 @@ struct Wave {
     uint32_t ibase = 0x80000000u;
     uint4 iv;
 
-    __device__ Wave(ParseSmem &s, const uint8_t *in, uint32_t len, const uint8_t *w, uint32_t g, uint32_t *o,
+    __device__ __forceinline__ Wave(ParseSmem &s, const uint8_t *in, uint32_t len, const uint8_t *w, uint32_t g, uint32_t *o,
                     uint32_t ow)
         : sm(s), src(in), n(len), hd(reinterpret_cast<const uint16_t *>(w + kHdOff)),
           rf(reinterpret_cast<const uint32_t *>(w + kRfOff)), rr(reinterpret_cast<const uint32_t *>(w + kRrOff)),
@@ -675,7 +679,7 @@ struct Wave {
     }
 
     // ---- the windows ---------------------------------------------------
-    __device__ void window(uint32_t p)
+    __device__ __forceinline__ void window(uint32_t p)
     {
         if (p - base < 512u) return;
         base = p & ~7u;
@@ -692,19 +696,19 @@ struct Wave {
         bv0 = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
         bv1 = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
     }
-    __device__ static uint32_t pick4(const uint4 &v, uint32_t l, uint32_t e)   // dword e (0..3) of lane l
+    __device__ __forceinline__ static uint32_t pick4(const uint4 &v, uint32_t l, uint32_t e)   // dword e (0..3) of lane l
     {
         const uint32_t a = lane_val(v.x, l), b = lane_val(v.y, l), c = lane_val(v.z, l), d = lane_val(v.w, l);
         return e == 0 ? a : e == 1 ? b : e == 2 ? c : d;
     }
-    __device__ uint32_t u32_at(const uint4 &v0, const uint4 &v1, uint32_t p)
+    __device__ __forceinline__ uint32_t u32_at(const uint4 &v0, const uint4 &v1, uint32_t p)
     {
         const uint32_t off = p - base, l = off >> 3, e = off & 7;
         return e < 4 ? pick4(v0, l, e) : pick4(v1, l, e - 4);
     }
 
     // ---- bit output ----------------------------------------------------
-    __device__ void store_words(uint32_t first, uint32_t count)   // stg[0..count) -> out32[first..)
+    __device__ __forceinline__ void store_words(uint32_t first, uint32_t count)   // stg[0..count) -> out32[first..)
     {
         for (uint32_t i = lane_id(); i < count; i += 64) {
             if (first + i < out_words) out32[first + i] = sm.stg[i];
@@ -712,7 +716,7 @@ struct Wave {
         }
     }
     // every lane contributes nbits (<= 57) bits of val; lanes in order
-    __device__ void emit_par(uint64_t val, uint32_t nbits)
+    __device__ __forceinline__ void emit_par(uint64_t val, uint32_t nbits)
     {
         uint32_t tot;
         const uint32_t off = excl_scan(nbits, tot);
@@ -741,7 +745,7 @@ struct Wave {
         Wave &w;
         uint64_t acc;
         uint32_t accbits, word;
-        __device__ void operator()(uint32_t v, int nb)
+        __device__ __forceinline__ void operator()(uint32_t v, int nb)
         {
             acc |= (uint64_t)(v & ((1u << nb) - 1u)) << accbits;
             accbits += nb;
@@ -754,13 +758,13 @@ struct Wave {
             }
         }
     };
-    __device__ Serial serial_begin() { return Serial{*this, sm.stg[0], bitpos & 31, bitpos >> 5}; }
-    __device__ void serial_end(const Serial &s)   // lane 0 publishes; all lanes pick up bitpos
+    __device__ __forceinline__ Serial serial_begin() { return Serial{*this, sm.stg[0], bitpos & 31, bitpos >> 5}; }
+    __device__ __forceinline__ void serial_end(const Serial &s)   // lane 0 publishes; all lanes pick up bitpos
     {
         sm.stg[0] = (uint32_t)s.acc;
         sm.bcast[0] = s.word * 32 + s.accbits;
     }
-    __device__ void windup()   // bi_windup: to a byte boundary (the bits above are zero)
+    __device__ __forceinline__ void windup()   // bi_windup: to a byte boundary (the bits above are zero)
     {
         const uint32_t nb = (bitpos + 7) & ~7u;
         if ((nb >> 5) != (bitpos >> 5)) {   // the partial word became whole: store it, start a new one
@@ -773,7 +777,7 @@ struct Wave {
     }
 
     // ---- deflate_slow's Ops ----------------------------------------------
-    __device__ uint32_t byte(uint32_t p)
+    __device__ __forceinline__ uint32_t byte(uint32_t p)
     {
         if constexpr (LAZY) {
             ensure(p);
@@ -785,14 +789,14 @@ struct Wave {
         return (w >> ((e & 3) * 8)) & 0xffu;
     }
     // zlib's head[] as p is inserted (0 = NIL)
-    __device__ uint32_t head(uint32_t p)
+    __device__ __forceinline__ uint32_t head(uint32_t p)
     {
         window(p);
         const uint32_t off = p - base, l = off >> 3, e = off & 7;
         const uint32_t w = pick4(hv, l, e >> 1);
         return (w >> ((e & 1) * 16)) & 0xffffu;
     }
-    __device__ void slide()   // fill_window's slide: past the end, the stale copy WSIZE back
+    __device__ __forceinline__ void slide()   // fill_window's slide: past the end, the stale copy WSIZE back
     {
         if constexpr (LAZY) {
             wslid = true;
@@ -803,16 +807,16 @@ struct Wave {
     }
     // the byte zlib's window holds at input position P (P < wbase + kLazyWin):
     // the strip, then zeros (fill_window's high_water zeroing) or, once slid, the stale copy
-    __device__ uint32_t win_src(uint32_t P) const
+    __device__ __forceinline__ uint32_t win_src(uint32_t P) const
     {
         return P < n ? (uint32_t)src[P] : (wslid && P - WSIZE < n ? (uint32_t)src[P - WSIZE] : 0u);
     }
-    __device__ void fill(uint32_t from, uint32_t to)   // window bytes of input positions [from, to)
+    __device__ __forceinline__ void fill(uint32_t from, uint32_t to)   // window bytes of input positions [from, to)
     {
         for (uint32_t P = from + lane_id(); P < to; P += 64) lwin[P - wbase] = (uint8_t)win_src(P);
     }
     // keep [p - MAX_DIST, p + kLazyAhead) in the window: shift it forward when p runs ahead
-    __device__ void ensure(uint32_t p)
+    __device__ __forceinline__ void ensure(uint32_t p)
     {
         if (p + kLazyAhead <= wbase + kLazyWin) return;
         const uint32_t nb = (p > (uint32_t)MAX_DIST ? p - MAX_DIST : 0u) & ~255u;
@@ -827,14 +831,14 @@ struct Wave {
         fill(old_end, nb + kLazyWin);
         wave_sync();
     }
-    __device__ uint32_t ld4(uint32_t a)   // window offsets
+    __device__ __forceinline__ uint32_t ld4(uint32_t a)   // window offsets
     {
         const uint32_t *w32 = reinterpret_cast<const uint32_t *>(lwin);
         return __builtin_amdgcn_alignbyte(w32[(a >> 2) + 1], w32[a >> 2], a & 3);
     }
-    __device__ uint32_t hash_at(uint32_t q) { return hash3(lwin[q], lwin[q + 1], lwin[q + 2]); }   // window offset
+    __device__ __forceinline__ uint32_t hash_at(uint32_t q) { return hash3(lwin[q], lwin[q + 1], lwin[q + 2]); }   // window offset
     // common prefix of the strings at a and b, up to MAX_MATCH: one wave-wide compare
-    __device__ uint32_t wave_lcp(uint32_t a, uint32_t b)
+    __device__ __forceinline__ uint32_t wave_lcp(uint32_t a, uint32_t b)
     {
         const uint32_t x = ld4(a + 4 * lane_id()) ^ ld4(b + 4 * lane_id());
         const uint64_t m = __ballot(x != 0);
@@ -846,7 +850,7 @@ struct Wave {
         if (lwin[a + 256] == lwin[b + 256]) l = lwin[a + 257] == lwin[b + 257] ? 258 : 257;
         return l;
     }
-    __device__ uint32_t lane_lcp(uint32_t a, uint32_t b)   // one lane, 16 bytes per step
+    __device__ __forceinline__ uint32_t lane_lcp(uint32_t a, uint32_t b)   // one lane, 16 bytes per step
     {
         uint32_t l = 0;
         while (l < (uint32_t)MAX_MATCH) {
@@ -863,7 +867,7 @@ struct Wave {
     }
 #if VCF_ZLIB_PROF
     unsigned long long t_longest = 0, t_flush = 0, n_longest = 0, n_rounds = 0, n_shift = 0;
-    __device__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
+    __device__ __forceinline__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
                             uint32_t limit, uint32_t &len, uint32_t &pos)
     {
         const unsigned long long t0 = clock64();
@@ -872,24 +876,24 @@ struct Wave {
         ++n_longest;
         return r;
     }
-    __device__ void flush(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
+    __device__ __forceinline__ void flush(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
     {
         const unsigned long long t0 = clock64();
         flush_impl(stored_len, buf_ok, block_start, last);
         t_flush += clock64() - t0;
     }
 #else
-    __device__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
+    __device__ __forceinline__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
                             uint32_t limit, uint32_t &len, uint32_t &pos)
     {
         return longest_impl(p, hdp, prev_len, chain, nice, limit, len, pos);
     }
-    __device__ void flush(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
+    __device__ __forceinline__ void flush(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
     {
         flush_impl(stored_len, buf_ok, block_start, last);
     }
 #endif
-    __device__ bool longest_impl(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
+    __device__ __forceinline__ bool longest_impl(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
                                  uint32_t limit, uint32_t &len, uint32_t &pos)
     {
         if constexpr (LAZY) {
@@ -898,16 +902,6 @@ struct Wave {
             ensure(p);
             const uint32_t wp = p - wbase;   // window offsets from here on (every candidate is >= wbase)
             const uint32_t Tn = max(nice, prev_len + 1);
-            const uint32_t l1 = wave_lcp(hdp - wbase, wp);
-            if (l1 >= Tn) {
-                len = l1;
-                pos = hdp;
-                return true;
-            }
-            const uint32_t hp = hash_at(wp);
-            // only a candidate longer than F = max(prev_len, the head's length) can change the
-            // result, and such a one matches at bytes F-1 and F (longest_match's scan_end test)
-            const uint32_t F = max(prev_len, l1);
             uint32_t ip;
             {   // idx[p] from its window
                 if (p - ibase >= 512u) {
@@ -917,13 +911,29 @@ struct Wave {
                 const uint32_t off = p - ibase, e = off & 7;
                 ip = (pick4(iv, off >> 3, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
             }
+            // the first two chain rounds' candidates, requested before the head compare so
+            // their global latency overlaps it (volatile: the compiler keeps them here)
+            const volatile uint16_t *vs = sorted;
+            const uint32_t g0 = lane_id(), g1 = 64 + lane_id();
+            const uint32_t pre0 = vs[g0 < ip ? ip - 1 - g0 : 0u];
+            const uint32_t pre1 = chain > 64u ? (uint32_t)vs[g1 < ip ? ip - 1 - g1 : 0u] : 0u;
+            const uint32_t hp = hash_at(wp);
+            const uint32_t l1 = wave_lcp(hdp - wbase, wp);
+            if (l1 >= Tn) {
+                len = l1;
+                pos = hdp;
+                return true;
+            }
+            // only a candidate longer than F = max(prev_len, the head's length) can change the
+            // result, and such a one matches at bytes F-1 and F (longest_match's scan_end test)
+            const uint32_t F = max(prev_len, l1);
             uint32_t best = prev_len, bpos = 0;
             bool found = false;
             for (uint32_t b = 0; b < chain; b += 64) {
                 VCF_ZPROF_COUNT(n_rounds);
                 const uint32_t gk = b + lane_id();
                 bool v = gk < chain && gk < ip;
-                const uint32_t c = v ? (uint32_t)sorted[ip - 1 - gk] : 0u;
+                const uint32_t c = !v ? 0u : b == 0 ? pre0 : b == 64 ? pre1 : (uint32_t)sorted[ip - 1 - gk];
                 v = v && (gk == 0 || c > limit);
                 const uint32_t wc = v ? c - wbase : 0u;
                 v = v && hash_at(wc) == hp;
@@ -962,25 +972,25 @@ struct Wave {
         pos = p - (r & 0xffffu);
         return len > prev_len;
     }
-    __device__ bool tally(uint32_t dist, uint32_t lc)
+    __device__ __forceinline__ bool tally(uint32_t dist, uint32_t lc)
     {
         if (lane_id() == 0) syms[nsym] = dist << 8 | lc;   // counted at flush
         ++nsym;
         return nsym == (uint32_t)LIT_BUFSIZE - 1;
     }
-    __device__ void init_freqs()
+    __device__ __forceinline__ void init_freqs()
     {
         for (uint32_t i = lane_id(); i < (uint32_t)L_CODES; i += 64) sm.lfreq[i] = 0;
         if (lane_id() < (uint32_t)D_CODES) sm.dfreq[lane_id()] = 0;
         if (lane_id() < (uint32_t)BL_CODES) sm.bfreq[lane_id()] = 0;
         wave_sync();
     }
-    __device__ static void add16(uint16_t *a, uint32_t i)   // a[i]++ as a packed 32-bit LDS add (no carry: < 65536)
+    __device__ __forceinline__ static void add16(uint16_t *a, uint32_t i)   // a[i]++ as a packed 32-bit LDS add (no carry: < 65536)
     {
         atomicAdd(reinterpret_cast<uint32_t *>(a) + (i >> 1), 1u << ((i & 1) * 16));
     }
     // _tr_tally's counts for the whole block at once (LDS atomics), then init_block's END_BLOCK
-    __device__ void count_block()
+    __device__ __forceinline__ void count_block()
     {
         for (uint32_t i = lane_id(); i < nsym; i += 64) {
             const uint32_t sy = ld_l2(syms + i), dist = sy >> 8, lc = sy & 0xff;
@@ -995,7 +1005,7 @@ struct Wave {
         if (lane_id() == 0) sm.lfreq[END_BLOCK] += 1;   // init_block's END_BLOCK count
         wave_sync();
     }
-    __device__ void flush_impl(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
+    __device__ __forceinline__ void flush_impl(uint32_t stored_len, bool buf_ok, uint32_t block_start, bool last)
     {
         __threadfence();   // the block's symbols (lane 0's stores) before the other lanes read them
         wave_sync();
