@@ -133,3 +133,50 @@ def test_device_iii_tiff_equals_host_writer():
             want = imwrite_bytes(k[i])
             assert got[i] == want and sizes[i] == len(want), (n, i)
             assert np.array_equal(imread_bytes(bytes(got[i])), k[i])
+
+
+def _golden_tif_cases():
+    import glob
+    import os
+    from conftest import GOLDEN
+    return sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "dct_*.npz")))
+
+
+@pytest.mark.parametrize("name", _golden_tif_cases())
+def test_gpu_tiff_equals_reference_files(name):
+    """The GPU deflate pinned to the reference's own bytes: the
+    TIFF of every golden case's index array `k`, deflated on the GPU
+    (tiff_frames_device), equals the .tif the reference's 2D-DCT.py wrote
+    (tests/golden/dct_*.npz 'tif', tifffile 2021.7.2 + zlib, make_golden*.py)."""
+    import os
+    from conftest import GOLDEN
+    from vcf_amd.device import DeviceBuffer
+    from vcf_amd.zlib_gpu import covers, tiff_frames_device
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    k = np.ascontiguousarray(z["k"])
+    if k.dtype not in (np.uint8, np.uint16) or not covers(k.shape, k.dtype.itemsize):
+        pytest.skip(f"{k.dtype} {k.shape}: not a TIFF the GPU deflate covers")
+    files = tiff_frames_device(DeviceBuffer.from_array(k), 1, k.shape, k.dtype)
+    assert files[0] == z["tif"].tobytes()
+
+
+@pytest.mark.parametrize("name", ["smooth_512x512", "rand_512x512"])
+def test_gpu_tiff_512_matches_reference_sha256(manifest, name):
+    """The C1 cases by SHA-256 (tests/golden/manifest.json big_cases): the GPU
+    deflate of the indices gives the reference's .tif."""
+    import hashlib
+    import importlib.util
+    import os
+    from conftest import GOLDEN
+    from vcf_amd import dct
+    from vcf_amd.device import DeviceBuffer
+    from vcf_amd.zlib_gpu import tiff_frames_device
+    case = [c for c in manifest["big_cases"] if c["name"] == name][0]
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    rgb = m.synth(case["kind"], case["H"], case["W"], case["seed"])
+    k = dct.encode(rgb, Q=32)
+    tif = tiff_frames_device(DeviceBuffer.from_array(np.ascontiguousarray(k)), 1, k.shape, np.uint8)[0]
+    assert len(tif) == case["encode_bytes"]
+    assert hashlib.sha256(tif).hexdigest() == case["sha256"]["tif"]

@@ -42,7 +42,6 @@
 #include "vcf_amd.h"
 #include "vcf_deflate.h"
 #include "vcf_internal.h"
-#include "vcf_pipeline.h"
 
 namespace vcf {
 namespace {
@@ -67,30 +66,19 @@ constexpr int64_t kRrOff = kRfOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSymOff = kRrOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;   // adler sums (2 x u64), worklist length (u32)
 constexpr int64_t kWsPerStrip = kSumOff + 32;
-// Rounds: the strips of a call are processed in rounds whose workspace slots
-// together stay under kWsBudget (about 3.9 GB); with kZSlots > 1, up to that
-// many rounds are in flight at once on library streams (round r on stream
-// r % slots, after round r - slots, which used the same slot), so one round's
-// latency-bound tail -- a few strips' serial parses -- overlaps the next
-// rounds' work.  Default 1 slot (rounds in series on the caller's stream):
-// concurrent rounds produced wrong strips on MI355X, so
-// VCF_ZLIB_SLOTS > 1 is a diagnostic setting only.
+// Rounds: the strips of a call are processed in rounds whose workspace
+// stays under kWsBudget (about 3.9 GB), one round after the other on the
+// caller's stream.  (Rounds in flight on library streams, each with its own
+// workspace slot, measured slower -- 517 vs 453 ms for C4 -- and produced a
+// wrong strip now and then on MI355X)
 constexpr int64_t kWsBudget = 3900000000LL;
-constexpr int kZSlots = 3;
-static_assert(kZSlots <= kAuxStreams, "one library stream per slot");
 struct ZRounds {
-    int64_t rounds, per, slots;
+    int64_t rounds, per;
     explicit ZRounds(int64_t total)
     {
-        static const int max_slots = [] {   // VCF_ZLIB_SLOTS (diagnostics): rounds in flight, default 1
-            const char *e = getenv("VCF_ZLIB_SLOTS");
-            const int v = e ? atoi(e) : 1;
-            return v < 1 ? 1 : v > kZSlots ? kZSlots : v;
-        }();
-        const int64_t round_max = std::max<int64_t>(1, kWsBudget / (max_slots * kWsPerStrip));
+        const int64_t round_max = std::max<int64_t>(1, kWsBudget / kWsPerStrip);
         rounds = std::max<int64_t>(1, (total + round_max - 1) / round_max);
         per = (total + rounds - 1) / rounds;
-        slots = std::min<int64_t>(max_slots, rounds);
     }
 };
 constexpr int kK2bThreads = 1024;    // K2b: 16 waves per strip, one listed position per wave at a time
@@ -663,6 +651,10 @@ struct Wave {
     const uint16_t *idx = nullptr, *sorted = nullptr;
     uint32_t ibase = 0x80000000u;
     uint4 iv;
+    // the chain candidates of the positions the next call will most likely be at (p + 1,
+    // and p + the match length), requested at the end of a call: their global latency
+    // overlaps the parse step in between (~70 % of the calls are at one of the two)
+    uint32_t pfa_p = 0xffffffffu, pfa0 = 0, pfa1 = 0, pfb_p = 0xffffffffu, pfb0 = 0, pfb1 = 0;
 
     __device__ __forceinline__ Wave(ParseSmem &s, const uint8_t *in, uint32_t len, const uint8_t *w, uint32_t g, uint32_t *o,
                     uint32_t ow)
@@ -893,10 +885,48 @@ struct Wave {
         flush_impl(stored_len, buf_ok, block_start, last);
     }
 #endif
-    __device__ __forceinline__ bool longest_impl(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
-                                 uint32_t limit, uint32_t &len, uint32_t &pos)
+    __device__ __forceinline__ void fetch_cands(uint32_t ip, uint32_t chain, uint32_t &c0, uint32_t &c1)
+    {
+        const volatile uint16_t *vs = sorted;
+        const uint32_t g0 = lane_id(), g1 = 64 + lane_id();
+        c0 = vs[g0 < ip ? ip - 1 - g0 : 0u];
+        c1 = chain > 64u ? (uint32_t)vs[g1 < ip ? ip - 1 - g1 : 0u] : 0u;
+    }
+    __device__ __forceinline__ uint32_t idx_known(uint32_t q)   // idx[q] from the window, or ~0 if outside it
+    {
+        if (q - ibase >= 512u) return 0xffffffffu;
+        const uint32_t off = q - ibase, e = off & 7;
+        return (pick4(iv, off >> 3, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
+    }
+    __device__ __forceinline__ void prefetch_next(uint32_t p, uint32_t len, uint32_t chain)
+    {
+        const uint32_t qa = p + 1, qb = p + (len >= (uint32_t)MIN_MATCH ? len : 1u);
+        const uint32_t ia = idx_known(qa);
+        pfa_p = ia != 0xffffffffu && qa + MIN_MATCH <= n ? qa : 0xffffffffu;
+        if (pfa_p != 0xffffffffu) fetch_cands(ia, chain, pfa0, pfa1);
+        const uint32_t ib = qb != qa ? idx_known(qb) : 0xffffffffu;
+        pfb_p = ib != 0xffffffffu && qb + MIN_MATCH <= n ? qb : 0xffffffffu;
+        if (pfb_p != 0xffffffffu) fetch_cands(ib, chain, pfb0, pfb1);
+    }
+    __device__ __forceinline__ bool longest_impl(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain,
+                                                 uint32_t nice, uint32_t limit, uint32_t &len, uint32_t &pos)
     {
         if constexpr (LAZY) {
+            const bool r = lazy_longest(p, hdp, prev_len, chain, nice, limit, len, pos);
+            prefetch_next(p, r ? len : 0u, chain);
+            return r;
+        }
+        // the K2 results: the full chain's, or the reduced chain's once prev_len >= good
+        window(p);
+        const uint32_t r = prev_len >= good ? u32_at(rv0, rv1, p) : u32_at(fv0, fv1, p);
+        len = r >> 16;
+        pos = p - (r & 0xffffu);
+        return len > prev_len;
+    }
+    __device__ __forceinline__ bool lazy_longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain,
+                                                 uint32_t nice, uint32_t limit, uint32_t &len, uint32_t &pos)
+    {
+        {
             // the first candidate (chain order) reaching max(nice, prev_len+1), else the
             // first reaching the longest length found, if longer than prev_len
             ensure(p);
@@ -911,12 +941,19 @@ struct Wave {
                 const uint32_t off = p - ibase, e = off & 7;
                 ip = (pick4(iv, off >> 3, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
             }
-            // the first two chain rounds' candidates, requested before the head compare so
-            // their global latency overlaps it (volatile: the compiler keeps them here)
-            const volatile uint16_t *vs = sorted;
-            const uint32_t g0 = lane_id(), g1 = 64 + lane_id();
-            const uint32_t pre0 = vs[g0 < ip ? ip - 1 - g0 : 0u];
-            const uint32_t pre1 = chain > 64u ? (uint32_t)vs[g1 < ip ? ip - 1 - g1 : 0u] : 0u;
+            // the first two chain rounds' candidates: prefetched by the previous call, or
+            // requested here before the head compare so their latency overlaps it
+            // (volatile: the compiler keeps the loads where they are)
+            uint32_t pre0, pre1;
+            if (p == pfa_p) {
+                pre0 = pfa0;
+                pre1 = pfa1;
+            } else if (p == pfb_p) {
+                pre0 = pfb0;
+                pre1 = pfb1;
+            } else {
+                fetch_cands(ip, chain, pre0, pre1);
+            }
             const uint32_t hp = hash_at(wp);
             const uint32_t l1 = wave_lcp(hdp - wbase, wp);
             if (l1 >= Tn) {
@@ -965,12 +1002,6 @@ struct Wave {
             pos = bpos;
             return found;
         }
-        // the K2 results: the full chain's, or the reduced chain's once prev_len >= good
-        window(p);
-        const uint32_t r = prev_len >= good ? u32_at(rv0, rv1, p) : u32_at(fv0, fv1, p);
-        len = r >> 16;
-        pos = p - (r & 0xffffu);
-        return len > prev_len;
     }
     __device__ __forceinline__ bool tally(uint32_t dist, uint32_t lc)
     {
@@ -1172,8 +1203,7 @@ int vcf_zlib_prof_read(unsigned long long *host8, int reset)
 int64_t vcf_zlib_workspace(int64_t n_strips)
 {
     if (n_strips < 0) return -1;
-    const ZRounds zr(n_strips);
-    return zr.slots * zr.per * kWsPerStrip;
+    return ZRounds(n_strips).per * kWsPerStrip;
 }
 
 int64_t vcf_zlib_strip_count(int64_t frame_bytes, int32_t strip_bytes)
@@ -1232,29 +1262,9 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
         return hip_check(hipGetLastError(), "zlib_parse_kernel (lazy) launch");
     };
     const ZRounds zr(total);
-    uint8_t *ws = (uint8_t *)ws_dev;
-    if (zr.rounds == 1) return round(0, (unsigned)total, ws, st);
-    // rounds in flight on library streams, forked from the caller's stream and joined back to it
-    AuxStreams &ax = aux_for_current_device();
-    std::lock_guard<std::mutex> lock(ax.mu);
-    int rc = ax.init();
-    if (rc != VCF_OK) return rc;
-    if ((rc = hip_check(hipEventRecord(ax.fork, st), "hipEventRecord")) != VCF_OK) return rc;
-    for (int j = 0; j < zr.slots; ++j)
-        if ((rc = hip_check(hipStreamWaitEvent(ax.s[j], ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
-    for (int64_t r = 0; r < zr.rounds && rc == VCF_OK; ++r) {
-        const int64_t s0 = r * zr.per;
-        if (s0 >= total) break;
-        const int j = (int)(r % zr.slots);
-        rc = round(s0, (unsigned)std::min<int64_t>(zr.per, total - s0), ws + (int64_t)j * zr.per * kWsPerStrip,
-                   ax.s[j]);
-    }
-    // join every library stream even after an error, so the caller's stream never runs ahead
-    for (int j = 0; j < zr.slots; ++j) {
-        int r2 = hip_check(hipEventRecord(ax.join[j], ax.s[j]), "hipEventRecord");
-        if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(st, ax.join[j], 0), "hipStreamWaitEvent");
-        if (rc == VCF_OK) rc = r2;
-    }
+    int rc = VCF_OK;
+    for (int64_t s0 = 0; s0 < total && rc == VCF_OK; s0 += zr.per)
+        rc = round(s0, (unsigned)std::min<int64_t>(zr.per, total - s0), (uint8_t *)ws_dev, st);
     return rc;
 }
 
