@@ -434,6 +434,18 @@ int64_t vcf_zlib_strip_count(int64_t frame_bytes, int32_t strip_bytes);
 int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes, int32_t strip_bytes, int32_t level,
                     uint8_t *out_dev, int64_t slot_bytes, int32_t *sizes_dev, void *ws_dev, void *stream);
 
+/* ---- TIFF strip inflate on the GPU (TIFF.py:33-39, the decode side of -c TIFF)
+ * zlib.decompress for every strip of a batch: strip s is comp_len_dev[s] bytes
+ * of a zlib stream at comp_dev + comp_off_dev[s], inflated to
+ * out_dev + out_off_dev[s], which must come to exactly out_len_dev[s] bytes
+ * (the TIFF's rows per strip x row bytes).  status_dev[s] = 0, or < 0 when the
+ * stream is not one zlib accepts with that length (-1 header, -2 block, -3
+ * code, -4 distance, -5 length, -6 adler32, -7 input overrun).  Device
+ * arrays; RFC 1950/1951, stored, fixed and dynamic blocks. */
+int vcf_inflate_strips(const uint8_t *comp_dev, const int64_t *comp_off_dev, const int32_t *comp_len_dev,
+                       int64_t n_strips, uint8_t *out_dev, const int64_t *out_off_dev, const int32_t *out_len_dev,
+                       int32_t *status_dev, void *stream);
+
 /* ---- deadzone quantizer plug-in (deadzone.py:95-117, assumption A5) ---------- */
 
 /* k[i] = (int32)(x[i] / Q), truncation toward zero; the division is float32

@@ -71,10 +71,19 @@ def main():
         t0 = time.perf_counter()
         dcodec.decode_fns(dpairs, batch=a.batch, io_threads=a.threads)
         t_dec = time.perf_counter() - t0
+        # the same with the strips inflated on host threads (round 3's path)
+        from vcf_amd.codec.tiff import TIFFCodec
+        TIFFCodec.gpu_batches = False
+        t0 = time.perf_counter()
+        dcodec.decode_fns(dpairs, batch=a.batch, io_threads=a.threads)
+        t_dec_host = time.perf_counter() - t0
+        TIFFCodec.gpu_batches = True
         print(json.dumps({
             "metric": "Mpixels/s III decode end to end (.tif files -> PNG files), 1 GPU",
             "value": round(px / t_dec / 1e6, 1), "unit": "Mpixels/s", "frames": a.frames,
-            "frame": [a.H, a.W, 3], "threads": a.threads, "batch": a.batch}), flush=True)
+            "frame": [a.H, a.W, 3], "threads": a.threads, "batch": a.batch,
+            "tiff_inflate": "GPU (vcf_inflate_strips)",
+            "host_inflate_value": round(px / t_dec_host / 1e6, 1)}), flush=True)
         print(json.dumps({
             "metric": "Mpixels/s III encode end to end (PNG files -> .tif files), 1 GPU",
             "value": round(px / t_e2e / 1e6, 1), "unit": "Mpixels/s", "frames": a.frames,

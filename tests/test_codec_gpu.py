@@ -196,3 +196,33 @@ def test_staged_pipeline_wide_rows_keep_host_writer(tmp_path):
         ref = str(tmp_path / f"ref_{i}")
         assert sizes[i] == CoDec(_args("encode")).encode_fn(src, ref)
         assert open(out + ".tif", "rb").read() == open(ref + ".tif", "rb").read()
+
+
+@pytest.mark.parametrize("shape", [(61, 77), (1080, 1920), (9, 21850)])
+def test_decode_fns_gpu_inflate_equals_decode_fn(tmp_path, shape):
+    """decode_fns inflates -c TIFF strips on the GPU (zlib_gpu.StripInflater,
+    straight into the index frames the decode kernel reads): the PNGs equal
+    decode_fn's (host inflate) frame for frame, mixed with a file whose TIFF
+    the host writes (-x layout of another shape) in the same batch."""
+    from vcf_amd.codec.dct2d import CoDec
+    rng = np.random.default_rng(shape[0])
+    H, W = shape
+    pairs, dpairs = [], []
+    for i in range(4):
+        y = np.arange(H)[:, None, None]
+        x = np.arange(W)[None, :, None]
+        rgb = np.clip(128 + 60 * np.sin(x / (17.0 + i) + y / 29.0 + np.arange(3)) + rng.normal(0, 9, (H, W, 3)),
+                      0, 255).astype(np.uint8)
+        src = _png(tmp_path / f"in_{i}.png", rgb)
+        out = str(tmp_path / f"enc_{i}")
+        CoDec(_args("encode")).encode_fn(src, out)
+        pairs.append((out, str(tmp_path / f"dec_{i}.png")))
+    extra = _png(tmp_path / "odd.png", rng.integers(0, 256, (33, 35, 3), dtype=np.uint8))
+    CoDec(_args("encode")).encode_fn(extra, str(tmp_path / "enc_odd"))
+    pairs.append((str(tmp_path / "enc_odd"), str(tmp_path / "dec_odd.png")))
+    sizes = CoDec(_args("decode")).decode_fns(pairs, batch=3)
+    for i, (enc, dec) in enumerate(pairs):
+        ref = str(tmp_path / f"ref_{i}.png")
+        CoDec(_args("decode")).decode_fn(enc, ref)
+        assert np.array_equal(np.asarray(Image.open(dec)), np.asarray(Image.open(ref))), i
+        assert sizes[i] > 0

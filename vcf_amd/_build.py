@@ -22,7 +22,8 @@ AB_SOURCES = ["ab/vcf_dct_dz_ab.hip", "ab/vcf_dwt_ab.hip"]
 AB_LINK = ["vcf_runtime.hip", "vcf_dct_any.hip"]
 SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_dct_any.hip", "vcf_quant.hip", "vcf_dwt.hip", "vcf_cbaac.cpp",
            "vcf_cbahc.cpp", "vcf_ipp.hip", "vcf_ipp_rdo.hip",
-           "vcf_png.cpp", "vcf_comm.cpp", "vcf_cbaac_gpu.hip", "vcf_plugins.hip", "vcf_deflate.hip"]
+           "vcf_png.cpp", "vcf_comm.cpp", "vcf_cbaac_gpu.hip", "vcf_plugins.hip", "vcf_deflate.hip",
+           "vcf_inflate.hip"]
 HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h", "vcf_wavelets.h", "vcf_pocketfft.h", "vcf_pocketfft_tables.h",
            "vcf_pocketfft_rt.h", "vcf_pocketfft_blue.h", "vcf_sincos.h", "vcf_pipeline.h", "vcf_dwt_band.h", "vcf_idwt_line.h", "vcf_deflate.h"]
 OBJDIR = os.path.join(ROOT, "build", "obj")

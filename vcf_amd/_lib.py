@@ -135,6 +135,7 @@ SIGNATURES = {
     "vcf_zlib_bound": [_I64],
     "vcf_zlib_workspace": [_I64],
     "vcf_zlib_max_strip": [],
+    "vcf_inflate_strips": [_P, _P, _P, _I64, _P, _P, _P, _P, _P],
     "vcf_zlib_strip_count": [_I64, _I32],
     "vcf_zlib_strips": [_P, _I64, _I64, _I32, _I32, _P, _I64, _P, _P, _P],
     "vcf_deadzone_quantize": [_P, _I32, _I64, _I32, _P, _P],

@@ -93,6 +93,18 @@ def make_quantizer(args):
     raise NotImplementedError(f"quantizer {quant!r}: deadzone and LloydMax are on the HIP path")
 
 
+class _Zipped:
+    """A read TIFF whose strips the GPU inflates (decode_fns): the file bytes and
+    its strip table (codec/tiff.py tiff_strips)."""
+
+    def __init__(self, data: bytes, info):
+        self.data, self.info = data, info
+
+    def host(self) -> np.ndarray:
+        from .tiff import imread_bytes
+        return imread_bytes(self.data)
+
+
 def _flags(args) -> int:
     return D.flags_from(bool(getattr(args, "disable_subbands", False)),
                         bool(getattr(args, "perceptual_quantization", False)))
@@ -463,11 +475,21 @@ class CoDec(EICCoDec):
             return [self.decode_fn(i, o) for i, o in pairs]
         sizes = [0] * len(pairs)
         batches = [pairs[b0:b0 + batch] for b0 in range(0, len(pairs), batch)]
+        # -c TIFF (the default): a batch's strips are inflated on the GPU straight into
+        # the index frames the decode kernel reads (vcf_amd/zlib_gpu.py StripInflater,
+        # zlib.decompress's semantics); the host threads only read the files
+        gpu_tiff = isinstance(self.entropy, TIFFCodec) and TIFFCodec.gpu_batches and self.block_size == 8
 
         def _read(p):
             cs = self.decode_read_fn(p[0])
             with open(f"{p[0]}_shape.bin", "rb") as f:
                 shp = struct.unpack("iii", f.read(12))
+            if gpu_tiff:
+                from .tiff import tiff_strips
+                info = tiff_strips(cs)
+                Hp, Wp = D.padded_shape(shp[0], shp[1], self.block_size)
+                if info is not None and tuple(info[0]) == (Hp, Wp, 3) and info[1] == np.uint8:
+                    return _Zipped(cs, info), shp
             return self.decompress(cs), shp
 
         with ThreadPoolExecutor(max_workers=io_threads) as pool:
@@ -482,8 +504,12 @@ class CoDec(EICCoDec):
                     groups.setdefault(tuple(shp), []).append(i)
                 ys = [None] * len(chunk)
                 for shp, idx in groups.items():
-                    out = D.decode(np.stack([got[i][0] for i in idx]), shp[0], shp[1], self.QSS,
-                                   self.flags, self.block_size)
+                    if all(isinstance(got[i][0], _Zipped) for i in idx):
+                        out = self._decode_zipped([got[i][0] for i in idx], shp)
+                    else:
+                        ks = [got[i][0] if not isinstance(got[i][0], _Zipped) else got[i][0].host()
+                              for i in idx]
+                        out = D.decode(np.stack(ks), shp[0], shp[1], self.QSS, self.flags, self.block_size)
                     for j, i in enumerate(idx):
                         ys[i] = out[j]
                 self.original_shape = got[-1][1]
@@ -493,6 +519,36 @@ class CoDec(EICCoDec):
             for i, f in writes:
                 sizes[i] = f.result()
         return sizes
+
+    def _decode_zipped(self, zs, shp):
+        """n TIFFs of one shape -> n decoded frames: every strip inflated on the GPU
+        into the index frames, the DCT + deadzone decode there, one download."""
+        from ..device import Stream
+        from .. import zlib_gpu
+        H, W = shp[0], shp[1]
+        Hp, Wp = D.padded_shape(H, W, self.block_size)
+        fb, n = Hp * Wp * 3, len(zs)
+        comp = np.frombuffer(b"".join(z.data for z in zs), np.uint8)
+        base = np.concatenate([[0], np.cumsum([len(z.data) for z in zs])[:-1]]).astype(np.int64)
+        comp_off = np.concatenate([b + np.asarray(z.info[2], np.int64) for b, z in zip(base, zs)])
+        comp_len = np.concatenate([np.asarray(z.info[3], np.int32) for z in zs])
+        sb = zs[0].info[4]
+        ns = len(zs[0].info[2])
+        if any(len(z.info[2]) != ns or z.info[4] != sb for z in zs):
+            raise ValueError("TIFFs of one shape with different strip layouts")
+        out_off = (np.arange(n, dtype=np.int64)[:, None] * fb + np.arange(ns, dtype=np.int64)[None, :] * sb).ravel()
+        out_len = np.minimum(sb, fb - np.arange(ns, dtype=np.int64) * sb)
+        out_len = np.tile(out_len, n).astype(np.int32)
+        bufs = getattr(self, "_zdec", None)
+        if bufs is None or bufs[0].nbytes < n * fb or bufs[1].nbytes < n * H * W * 3:
+            bufs = self._zdec = (DeviceBuffer(n * fb), DeviceBuffer(n * H * W * 3), Stream())
+        dk, drgb, st = bufs
+        zlib_gpu.inflater().inflate_into(comp, comp_off, comp_len, dk, out_off, out_len, st)
+        D.decode_device(dk, n, H, W, self.QSS, self.flags, out=drgb, stream=st, block_size=self.block_size)
+        res = np.empty((n, H, W, 3), np.uint8)
+        drgb.download(res, st)
+        st.synchronize()
+        return res
 
     # ---- quantizer surface (deadzone.py:95-124) -----------------------------
     def quantize_decom(self, decom):

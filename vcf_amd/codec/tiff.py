@@ -200,6 +200,27 @@ def _read_ifd(buf: bytes):
     return bo, tags
 
 
+def tiff_strips(buf: bytes):
+    """The strip table of a deflate-compressed, chunky, little-endian u8/u16
+    TIFF (what tifffile writes for TIFF.py:29): (shape, dtype, strip offsets,
+    strip byte counts, uncompressed bytes per full strip), or None for any
+    other TIFF (imread_bytes reads those on the host)."""
+    bo, t = _read_ifd(bytes(buf[:65536]) if len(buf) > 65536 else bytes(buf))
+    if bo != "<" or t.get(259, (1,))[0] not in (8, 32946) or t.get(284, (1,))[0] != 1:
+        return None
+    if 273 not in t or 279 not in t:
+        return None
+    W, H = t[256][0], t[257][0]
+    C = t.get(277, (1,))[0]
+    bps = t.get(258, (8,))[0]
+    if bps not in (8, 16):
+        return None
+    isz = bps // 8
+    rps = t.get(278, (H,))[0]
+    shape = (H, W, C) if C > 1 else (H, W)
+    return shape, np.dtype("<u%d" % isz), list(t[273]), list(t[279]), min(rps, H) * W * C * isz
+
+
 def imread_bytes(buf: bytes) -> np.ndarray:
     """tifffile.imread(BytesIO(buf)) for the files TIFF.py writes."""
     bo, t = _read_ifd(bytes(buf))

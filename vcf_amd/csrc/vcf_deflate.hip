@@ -671,13 +671,40 @@ struct Wave {
     }
 
     // ---- the windows ---------------------------------------------------
+    // LAZY: 512-aligned windows of hd[] and idx[], each with the next window requested
+    // as soon as the current one is in use (the parse only moves forward, at most
+    // MAX_MATCH positions at a time, so it always enters the next window)
+    uint4 hv_n, iv_n;
+    __device__ __forceinline__ static uint4 vload4(const uint16_t *a)
+    {
+        const volatile uint32_t *v = reinterpret_cast<const volatile uint32_t *>(a);
+        return make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    __device__ __forceinline__ void lazy_windows(uint32_t p)
+    {
+        if (p - base < 512u) return;
+        const uint32_t nb = p & ~511u;
+        if (nb == base + 512u) {
+            hv = hv_n;
+            iv = iv_n;
+        } else {
+            hv = *reinterpret_cast<const uint4 *>(hd + nb + 8 * lane_id());
+            iv = *reinterpret_cast<const uint4 *>(idx + nb + 8 * lane_id());
+        }
+        base = ibase = nb;
+        hv_n = vload4(hd + nb + 512 + 8 * lane_id());
+        iv_n = vload4(idx + nb + 512 + 8 * lane_id());
+    }
     __device__ __forceinline__ void window(uint32_t p)
     {
+        if constexpr (LAZY) {
+            lazy_windows(p);
+            return;
+        }
         if (p - base < 512u) return;
         base = p & ~7u;
         const uint32_t q = base + 8 * lane_id();
         hv = *reinterpret_cast<const uint4 *>(hd + q);
-        if constexpr (LAZY) return;
         fv0 = *reinterpret_cast<const uint4 *>(rf + q);
         fv1 = *reinterpret_cast<const uint4 *>(rf + q + 4);
         rv0 = *reinterpret_cast<const uint4 *>(rr + q);
@@ -885,35 +912,39 @@ struct Wave {
         flush_impl(stored_len, buf_ok, block_start, last);
     }
 #endif
-    __device__ __forceinline__ void fetch_cands(uint32_t ip, uint32_t chain, uint32_t &c0, uint32_t &c1)
+    // candidates 0..127 of the chain of a position whose bucket slot is ip (both rounds,
+    // whatever chain limit the call will have: the reduced limit of one call may be the
+    // full limit of the next)
+    __device__ __forceinline__ void fetch_cands(uint32_t ip, uint32_t &c0, uint32_t &c1)
     {
         const volatile uint16_t *vs = sorted;
         const uint32_t g0 = lane_id(), g1 = 64 + lane_id();
         c0 = vs[g0 < ip ? ip - 1 - g0 : 0u];
-        c1 = chain > 64u ? (uint32_t)vs[g1 < ip ? ip - 1 - g1 : 0u] : 0u;
+        c1 = vs[g1 < ip ? ip - 1 - g1 : 0u];
     }
-    __device__ __forceinline__ uint32_t idx_known(uint32_t q)   // idx[q] from the window, or ~0 if outside it
+    __device__ __forceinline__ uint32_t idx_known(uint32_t q)   // idx[q] from the windows, or ~0 if outside them
     {
-        if (q - ibase >= 512u) return 0xffffffffu;
-        const uint32_t off = q - ibase, e = off & 7;
-        return (pick4(iv, off >> 3, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
+        const uint32_t off = q - ibase;
+        if (off >= 1024u) return 0xffffffffu;
+        const uint32_t o = off & 511u, e = o & 7;
+        return (pick4(off < 512u ? iv : iv_n, o >> 3, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
     }
-    __device__ __forceinline__ void prefetch_next(uint32_t p, uint32_t len, uint32_t chain)
+    __device__ __forceinline__ void prefetch_next(uint32_t p, uint32_t len)
     {
         const uint32_t qa = p + 1, qb = p + (len >= (uint32_t)MIN_MATCH ? len : 1u);
         const uint32_t ia = idx_known(qa);
         pfa_p = ia != 0xffffffffu && qa + MIN_MATCH <= n ? qa : 0xffffffffu;
-        if (pfa_p != 0xffffffffu) fetch_cands(ia, chain, pfa0, pfa1);
+        if (pfa_p != 0xffffffffu) fetch_cands(ia, pfa0, pfa1);
         const uint32_t ib = qb != qa ? idx_known(qb) : 0xffffffffu;
         pfb_p = ib != 0xffffffffu && qb + MIN_MATCH <= n ? qb : 0xffffffffu;
-        if (pfb_p != 0xffffffffu) fetch_cands(ib, chain, pfb0, pfb1);
+        if (pfb_p != 0xffffffffu) fetch_cands(ib, pfb0, pfb1);
     }
     __device__ __forceinline__ bool longest_impl(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain,
                                                  uint32_t nice, uint32_t limit, uint32_t &len, uint32_t &pos)
     {
         if constexpr (LAZY) {
             const bool r = lazy_longest(p, hdp, prev_len, chain, nice, limit, len, pos);
-            prefetch_next(p, r ? len : 0u, chain);
+            prefetch_next(p, r ? len : 0u);
             return r;
         }
         // the K2 results: the full chain's, or the reduced chain's once prev_len >= good
@@ -932,15 +963,8 @@ struct Wave {
             ensure(p);
             const uint32_t wp = p - wbase;   // window offsets from here on (every candidate is >= wbase)
             const uint32_t Tn = max(nice, prev_len + 1);
-            uint32_t ip;
-            {   // idx[p] from its window
-                if (p - ibase >= 512u) {
-                    ibase = p & ~7u;
-                    iv = *reinterpret_cast<const uint4 *>(idx + ibase + 8 * lane_id());
-                }
-                const uint32_t off = p - ibase, e = off & 7;
-                ip = (pick4(iv, off >> 3, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
-            }
+            lazy_windows(p);
+            const uint32_t ip = idx_known(p);
             // the first two chain rounds' candidates: prefetched by the previous call, or
             // requested here before the head compare so their latency overlaps it
             // (volatile: the compiler keeps the loads where they are)
@@ -952,7 +976,7 @@ struct Wave {
                 pre0 = pfb0;
                 pre1 = pfb1;
             } else {
-                fetch_cands(ip, chain, pre0, pre1);
+                fetch_cands(ip, pre0, pre1);
             }
             const uint32_t hp = hash_at(wp);
             const uint32_t l1 = wave_lcp(hdp - wbase, wp);

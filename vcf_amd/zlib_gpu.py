@@ -157,3 +157,63 @@ def tiff_frames_device(src: DeviceBuffer, n_frames: int, shape, dtype=np.uint8, 
     _, _, strip_bytes = strip_layout(shape if len(shape) == 3 else shape + (1,), dt.itemsize)
     strips = deflater().deflate_device(src, n_frames, frame_bytes, strip_bytes, LEVEL, offset, stream)
     return [container(shape, dt, s) for s in strips]
+
+
+class StripInflater:
+    """zlib.decompress of a batch of strips on the GPU (vcf_inflate_strips), the
+    decode side of TIFF.py:33-39: the compressed strips go up in one copy, the
+    inflated bytes land in a device buffer (e.g. the index frames the DCT
+    decode reads).  Buffers grow on demand and are reused."""
+
+    def __init__(self):
+        self._bufs = {}
+        self._lock = threading.Lock()
+
+    def _buf(self, name: str, nbytes: int) -> DeviceBuffer:
+        b = self._bufs.get(name)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                b.free()
+            b = self._bufs[name] = DeviceBuffer(max(int(nbytes), 16))
+        return b
+
+    def inflate_into(self, comp: np.ndarray, comp_off: np.ndarray, comp_len: np.ndarray, out: DeviceBuffer,
+                     out_off: np.ndarray, out_len: np.ndarray, stream: Stream) -> None:
+        """Strip s: comp[comp_off[s]:][:comp_len[s]] (host bytes) -> out at
+        out_off[s], exactly out_len[s] bytes.  Raises ValueError naming the
+        first strip zlib would reject (corrupt stream, wrong length, adler32)."""
+        n = int(len(comp_len))
+        if n == 0:
+            return
+        comp = np.ascontiguousarray(comp, np.uint8)
+        tab = np.concatenate([np.asarray(comp_off, np.int64), np.asarray(out_off, np.int64)])
+        lens = np.concatenate([np.asarray(comp_len, np.int32), np.asarray(out_len, np.int32)])
+        with self._lock:
+            dc, dt, dl, ds = (self._buf("comp", comp.nbytes), self._buf("tab", tab.nbytes),
+                              self._buf("lens", lens.nbytes), self._buf("status", 4 * n))
+            dc.upload(comp, stream)
+            dt.upload(tab, stream)
+            dl.upload(lens, stream)
+            L.call("vcf_inflate_strips", dc.ptr, dt.ptr, dl.ptr, n, out.ptr, dt.address(8 * n), dl.address(4 * n),
+                   ds.ptr, stream.handle)
+            st = np.empty(n, np.int32)
+            ds.download(st, stream)
+            stream.synchronize()
+        bad = np.nonzero(st)[0]
+        if bad.size:
+            raise ValueError(f"inflate: strip {int(bad[0])} is not a zlib stream of its length (status {int(st[bad[0]])})")
+
+    def close(self):
+        for b in self._bufs.values():
+            b.free()
+        self._bufs.clear()
+
+
+_inflater = None
+
+
+def inflater() -> StripInflater:
+    global _inflater
+    if _inflater is None:
+        _inflater = StripInflater()
+    return _inflater
