@@ -153,7 +153,7 @@ def test_decode_variants_batched():
     k = D.encode(frames, 32, 0)
     a = D.decode(k, 72, 4104, 32, 0, variant=1)
     b = D.decode(k, 72, 4104, 32, 0, variant=2)
-    for v in (0, 3, 4, 5, 6, 7, 8):   # the default and the A/B variants of 2
+    for v in (0, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13):   # the default and the A/B variants of 2
         assert np.array_equal(D.decode(k, 72, 4104, 32, 0, variant=v), b), v
     assert np.array_equal(a, b)
     assert np.array_equal(a[2], O.decode_frame(k[2], 72, 4104, 32, 0))

@@ -538,10 +538,10 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_encode_cols(const uint8_t *__re
 // its 8 truncated int16 samples; after the three channels each lane converts
 // its row to RGB and stores its 24 bytes.  ~60 VGPRs: 8 waves per SIMD.
 // ---------------------------------------------------------------------------
-template <int TB>
+template <int TB, bool TRH = false>
 struct DecColsSmem {
-    double tr[TB][8][9];   // per-block transpose tile, pitch 9
-    double lut[256];       // DQ 1: the dequantized int16 value of each index byte, / 16
+    double tr[TB][TRH ? 4 : 8][9];   // per-block transpose tile, pitch 9 (TRH: half of it, used twice)
+    double lut[256];                 // DQ 1: the dequantized int16 value of each index byte, / 16
     uint8_t stage[64 * TB * 3 + 8 * 32];
 };
 
@@ -555,16 +555,26 @@ struct DecColsSmem {
 // table of the 256 possible values, already divided by 16 -- a power of two
 // commutes with every rounding of the transform (no value comes near the
 // subnormal range), so the outputs are bit-identical and need no scaling.
+// 3: the 24-bit multiply with the 1/16 folded into the input (one multiply
+// per input instead of per output; no table, no LDS reads).
 // EPI 1 (aligned frames): to_RGB, += 128 and the clamp on pixel pairs in packed
 // int16 arithmetic (v_pk_add/sub/max/min_i16 wrap exactly as numpy's int16),
 // the 24 bytes formed with byte permutes; 0: one pixel at a time.
+// ACT: the DC-only wave test (round 3).  0: none; 1: the product's (the OR and
+// the AND of the AC index bytes); 2: the OR of the dequantized AC values' high
+// words (a double is +-0 iff its high word is 0 or 0x80000000, and every
+// nonzero input here is >= 1/16 in magnitude, so a zero high word means a zero
+// value: three v_or3 per column, no byte compares).  TRH: the transpose tile
+// halved (rows 0-3, then 4-7 through the same 4 rows): 9 KiB less LDS per
+// workgroup, more workgroups per CU.
 template <int TB, bool SUB, bool PERC, bool PAD, bool NTL = false, bool NTS = true, int PRIO = 3, int DQ = 0,
-          int EPI = 0>
+          int EPI = 0, int ACT = 0, bool TRH = false>
 __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__restrict__ kin,
                                                               uint8_t *__restrict__ rgb, Geom g, int Q,
                                                               int tiles_per_row)
 {
-    __shared__ __attribute__((aligned(16))) DecColsSmem<TB> sm;
+    constexpr bool PREF = (DQ == 1 || DQ == 3) && !PERC;   // inputs already divided by 16
+    __shared__ __attribute__((aligned(16))) DecColsSmem<TB, TRH> sm;
     const int tid = threadIdx.x;
     const int lb = tid >> 3, x = tid & 7;
     const int by = blockIdx.x / tiles_per_row;
@@ -632,10 +642,16 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
     for (int C = 0; C < 3; ++C) {
         // :399-411 astype(int16) - 128, Q*k in int16 (A5); -p de-weighting (:421-435)
         double col[8];
+        uint32_t acor = 0, acand = 0xFFu;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int kb = SUB ? sm.stage[cols_stage_off<TB, SUB>(i * 8 + x) + lb * 3 + C]
                                : sm.stage[cols_stage_off<TB, SUB>(i) + lb * 24 + x * 3 + C];
+            if constexpr (ACT == 1) {
+                const uint32_t ac = (i == 0 && x == 0) ? 128u : (uint32_t)kb;
+                acor |= ac;
+                acand &= ac;
+            }
             if constexpr (DQ == 1 && !PERC) {
                 col[i] = sm.lut[kb];
                 continue;
@@ -645,21 +661,56 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
                 const float f = (float)((double)(float)yv / pweight_rt(C, i * 8 + x));
                 yv = (int16_t)(int)f;
             }
-            col[i] = (double)yv;
+            col[i] = PREF ? (double)yv * 0.0625 : (double)yv;
+        }
+        bool dc_only = false;
+        if constexpr (ACT == 1) dc_only = __ballot(acor != 128u || acand != 128u) == 0;
+        if constexpr (ACT == 2) {
+            uint32_t h = x == 0 ? 0u : (uint32_t)__double2hiint(col[0]);
+            h = h | (uint32_t)__double2hiint(col[1]) | (uint32_t)__double2hiint(col[2]);
+            h = h | (uint32_t)__double2hiint(col[3]) | (uint32_t)__double2hiint(col[4]);
+            h = h | (uint32_t)__double2hiint(col[5]) | (uint32_t)__double2hiint(col[6]);
+            h |= (uint32_t)__double2hiint(col[7]);
+            dc_only = __ballot((h & 0x7FFFFFFFu) != 0u) == 0;
+        }
+        if (ACT && dc_only) {   // wave-uniform: every block of the wave DC-only in channel C
+            double v = __shfl(col[0], __lane_id() & ~7);
+            double r[8] = {v, 0, 0, 0, 0, 0, 0, 0};
+            dct3_8r_k<1>(r);
+            double q[8] = {r[0], 0, 0, 0, 0, 0, 0, 0};
+            dct3_8r_k<1>(q);
+            const int o = (int16_t)(int)(PREF ? q[0] : q[0] * 0.0625);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) out[C][j] = o;
+            continue;
         }
         // :440 synthesize_image (A2): axis 0 (this lane's column), then axis 1
         dct3_8r(col);
-#pragma unroll
-        for (int y = 0; y < 8; ++y) tr[y][x] = col[y];
-        wave_lds_fence();
         double row[8];
+        if constexpr (TRH) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) row[j] = tr[x][j];
-        wave_lds_fence();   // the tile is rewritten by the next channel
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int y = 0; y < 4; ++y) tr[y][x] = col[4 * h + y];
+                wave_lds_fence();
+                if ((x >> 2) == h) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) row[j] = tr[x & 3][j];
+                }
+                wave_lds_fence();
+            }
+        } else {
+#pragma unroll
+            for (int y = 0; y < 8; ++y) tr[y][x] = col[y];
+            wave_lds_fence();
+#pragma unroll
+            for (int j = 0; j < 8; ++j) row[j] = tr[x][j];
+            wave_lds_fence();   // the tile is rewritten by the next channel
+        }
         dct3_8r(row);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)   // fct 1/4 per pass (already in the inputs for DQ 1); int16
-            out[C][j] = (int16_t)(int)(DQ == 1 && !PERC ? row[j] : row[j] * 0.0625);
+        for (int j = 0; j < 8; ++j)   // fct 1/4 per pass (already in the inputs for DQ 1/3); int16
+            out[C][j] = (int16_t)(int)(PREF ? row[j] : row[j] * 0.0625);
     }
     // :444 remove_padding, :449 to_RGB (int16), :454 += 128, :466 clip, uint8
     if constexpr (EPI == 1 && !PAD) {
@@ -1098,7 +1149,7 @@ int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frame
         return dct_any_decode_u8(k_dev, n_frames, H, W, block_size, Q, flags, rgb_dev, stream);
     int rc = check_args(k_dev, rgb_dev, n_frames, H, W, block_size, Q, flags, true);
     if (rc != VCF_OK) return rc;
-    if (variant < 0 || variant > 8) return set_error(VCF_ERR_INVALID, "unknown decode variant %d", variant);
+    if (variant < 0 || variant > 13) return set_error(VCF_ERR_INVALID, "unknown decode variant %d", variant);
     if (n_frames == 0) return VCF_OK;
     Geom g;
     make_geom(H, W, g);
@@ -1125,9 +1176,24 @@ int vcf_dct_dz_decode_variant(int variant, const uint8_t *k_dev, int64_t n_frame
         else if (variant == 7)   // 24-bit multiply for the dequantization
             hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 2>), grid, dim3(256), 0,
                                (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
-        else   // the table and the packed int16 epilogue
+        else if (variant == 8)   // the table and the packed int16 epilogue
             hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 1, 1>), grid, dim3(256),
                                0, (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
+        else if (variant == 9)   // 8 + the product's DC-only test
+            hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 1, 1, 1>), grid,
+                               dim3(256), 0, (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
+        else if (variant == 10)   // 8 + the high-word DC-only test
+            hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 1, 1, 2>), grid,
+                               dim3(256), 0, (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
+        else if (variant == 11)   // arithmetic dequantization (1/16 folded in) + the high-word test
+            hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 3, 1, 2>), grid,
+                               dim3(256), 0, (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
+        else if (variant == 12)   // 10 with the half transpose tile
+            hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 1, 1, 2, true>), grid,
+                               dim3(256), 0, (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
+        else   // 11 with the half transpose tile
+            hipLaunchKernelGGL((dct_dz_decode_cols<32, true, false, false, false, true, 3, 3, 1, 2, true>), grid,
+                               dim3(256), 0, (hipStream_t)stream, k_dev, rgb_dev, g, (int)Q, tpr);
         return hip_check(hipGetLastError(), "decode variant 3/4 launch");
     }
     if (variant != 1)
