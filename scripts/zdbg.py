@@ -1,6 +1,7 @@
-"""Diagnostic: deflate the C4 workload once and dump every strip's size and a
-checksum of its bytes (compare runs with VCF_ZLIB_SLOTS=1 and =3)."""
-import sys, os, zlib
+"""Diagnostic: deflate the C4 workload once, dump every strip's size and a
+checksum of its bytes, and list the strips that differ from zlib.  ZLIB_SO:
+a diagnostic build (scripts/libvcf_zprof_NAME.so) instead of the product library."""
+import ctypes, sys, os, zlib
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -17,7 +18,14 @@ fb = flat.shape[1]; _, _, sb = strip_layout(frames.shape[1:], 1)
 spf = int(L.lib().vcf_zlib_strip_count(fb, sb)); total = spf * n; slot = int(L.lib().vcf_zlib_bound(sb))
 d = DeviceBuffer.from_array(flat); out = DeviceBuffer(total * slot); sizes = DeviceBuffer(total * 4)
 ws = DeviceBuffer(int(L.lib().vcf_zlib_workspace(total))); st = Stream()
-L.call("vcf_zlib_strips", d.ptr, n, fb, sb, 6, out.ptr, slot, sizes.ptr, ws.ptr, st.handle)
+so = os.environ.get("ZLIB_SO")
+if so:
+    P = ctypes.CDLL(os.path.join(ROOT, "scripts", so))
+    P.vcf_zlib_strips.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    assert P.vcf_zlib_strips(d.ptr, n, fb, sb, 6, out.ptr, slot, sizes.ptr, ws.ptr, st.handle) == 0
+else:
+    L.call("vcf_zlib_strips", d.ptr, n, fb, sb, 6, out.ptr, slot, sizes.ptr, ws.ptr, st.handle)
 st.synchronize()
 sz = sizes.download(np.empty(total, np.int32))
 o = out.download(np.empty(total * slot, np.uint8))
@@ -25,9 +33,31 @@ crc = np.array([zlib.crc32(o[s * slot:s * slot + sz[s]].tobytes()) for s in rang
 np.savez(sys.argv[2], sz=sz, crc=crc)
 bad = [s for s in range(total) if o[s * slot:s * slot + sz[s]].tobytes() !=
        zlib.compress(flat[s // spf, (s % spf) * sb:(s % spf + 1) * sb].tobytes(), 6)]
-print(f"{sys.argv[2]}: total {total}, bad {len(bad)}: {bad[:40]}", flush=True)
+print(f"{sys.argv[2]} ({so or 'product'}): total {total}, bad {len(bad)}: {bad[:40]}", flush=True)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+from ztokens import first_divergence
+
+
+def lazy_of(strip):   # K1's parse-order rule: distinct hashes per 64-position group
+    b = strip.astype(np.uint32)
+    h = ((b[:-2] << 10) ^ (b[1:-1] << 5) ^ b[2:]) & 0x7fff
+    d = sum(len(np.unique(h[i:i + 64])) for i in range(0, len(h), 64))
+    return d * 4 < len(h)
+
+
+dump = {}
 for b in bad[:6]:
     g = o[b * slot:b * slot + sz[b]].tobytes()
-    w = zlib.compress(flat[b // spf, (b % spf) * sb:(b % spf + 1) * sb].tobytes(), 6)
+    src = flat[b // spf, (b % spf) * sb:(b % spf + 1) * sb]
+    w = zlib.compress(src.tobytes(), 6)
     d = next((i for i in range(min(len(g), len(w))) if g[i] != w[i]), None)
-    print(f"  strip {b}: gpu {len(g)} B, zlib {len(w)} B, first difference at byte {d}", flush=True)
+    try:
+        fd = first_divergence(g, w)
+    except Exception as e:   # a corrupt stream
+        fd = f"gpu stream does not parse: {e!r}"
+    print(f"  strip {b}: gpu {len(g)} B, zlib {len(w)} B, first difference at byte {d}, lazy {lazy_of(src)}, "
+          f"{fd}", flush=True)
+    dump[f"src_{b}"] = src
+    dump[f"gpu_{b}"] = np.frombuffer(g, np.uint8)
+if dump:
+    np.savez(sys.argv[2].replace(".npz", "_bad.npz"), **dump)

@@ -1,0 +1,9 @@
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_deflate_gpu.py tests/test_inflate_gpu.py -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/zt.log 2>&1; rc=$?; echo "deflate tests rc=$rc"; tail -3 gpurun_out/zt.log; [ $rc -eq 0 ] || exit $rc
+for L in "" ""; do
+  ZLIB_SO=$L timeout -k 10 300 python -u scripts/zdbg.py 256 gpurun_out/zd_${L:-product}_$RANDOM.npz || exit $?
+done
+timeout -k 10 300 python -u scripts/bench_zlib.py --only dct_c4_1080p,dct_1080p,rgb_1080p --frames 256 --reps 3 > gpurun_out/bz.jsonl 2> gpurun_out/bz.err || exit $?
+cut -c1-400 gpurun_out/bz.jsonl; grep differ gpurun_out/bz.err
+timeout -k 10 200 python -u scripts/zprof_run.py 256 || exit $?

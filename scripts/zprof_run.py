@@ -9,7 +9,7 @@ from bench import synth_frame, c4_frame
 from vcf_amd import _lib as L, dct
 from vcf_amd.codec.tiff import strip_layout
 from vcf_amd.device import DeviceBuffer, Stream, Event
-P = ctypes.CDLL(os.path.join(ROOT, "scripts", "libvcf_zprof.so"))
+P = ctypes.CDLL(os.path.join(ROOT, "scripts", os.environ.get("ZPROF_LIB", "libvcf_zprof.so")))
 P.vcf_zlib_strips.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                               ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 P.vcf_zlib_workspace.restype = ctypes.c_int64
@@ -24,7 +24,7 @@ fb = flat.shape[1]; _, _, sb = strip_layout(frames.shape[1:], 1)
 spf = int(L.lib().vcf_zlib_strip_count(fb, sb)); total = spf * n; slot = int(L.lib().vcf_zlib_bound(sb))
 d = DeviceBuffer.from_array(flat); out = DeviceBuffer(total * slot); sizes = DeviceBuffer(total * 4)
 ws = DeviceBuffer(int(P.vcf_zlib_workspace(total))); st = Stream()
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 16)()
 for rep in range(2):
     P.vcf_zlib_prof_read(buf, 1)
     e0, e1 = Event(), Event()
@@ -39,4 +39,7 @@ print(json.dumps({"frames": n, "strips": total, "ms": round(e0.elapsed_ms(e1), 2
                   "flush_cycles_per_strip": v[2] // ns, "longest_calls_per_strip": v[3] / ns,
                   "chain_rounds_per_strip": v[4] / ns, "shifts_per_strip": v[5] / ns,
                   "cycles_per_longest": v[1] // max(1, v[3]),
-                  "k3_cycles_per_strip": v[7] // max(1, total - v[6])}), flush=True)
+                  "k3_cycles_per_strip": v[7] // max(1, total - v[6]),
+                  "head_cycles_per_longest": v[8] // max(1, v[3]), "lcp_steps_per_round": v[9] / max(1, v[4]),
+                  "scan_end_passes_per_round": v[10] / max(1, v[4]), "prefetch_served": v[11] / max(1, v[3]),
+                  "lib": os.environ.get("ZPROF_LIB", "libvcf_zprof.so")}), flush=True)

@@ -180,3 +180,30 @@ def test_gpu_tiff_512_matches_reference_sha256(manifest, name):
     tif = tiff_frames_device(DeviceBuffer.from_array(np.ascontiguousarray(k)), 1, k.shape, np.uint8)[0]
     assert len(tif) == case["encode_bytes"]
     assert hashlib.sha256(tif).hexdigest() == case["sha256"]["tif"]
+
+
+def test_c4_workload_every_strip_equals_zlib():
+    """bench.py's C4 content (256 1080p DCT index frames, 25 344 strips): several
+    workspace rounds, lazy and register-window strips side by side.  Every strip
+    against zlib.compress: a strip coded from stale workspace data (the previous
+    round's strip in the same slot) shows up here."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import bench
+    from vcf_amd import dct
+    from vcf_amd.codec.tiff import strip_layout
+    from vcf_amd.device import DeviceBuffer
+    from vcf_amd.zlib_gpu import StripDeflater
+    n, H, W = 256, 1080, 1920
+    bases = [bench.synth_frame(H, W, seed=100 + s) for s in range(4)]
+    k = np.concatenate([dct.encode(np.stack([bench.c4_frame(bases, i) for i in range(f, f + 16)]), Q=32)
+                        for f in range(0, n, 16)])
+    flat = np.ascontiguousarray(k.reshape(n, -1))
+    sb = strip_layout(k.shape[1:], 1)[2]
+    got = StripDeflater().deflate_device(DeviceBuffer.from_array(flat), n, flat.shape[1], sb, 6)
+    spf = len(got[0])
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda s: zlib.compress(flat[s // spf, (s % spf) * sb:(s % spf + 1) * sb].tobytes(), 6),
+                           range(n * spf)))
+    bad = [s for s in range(n * spf) if bytes(got[s // spf][s % spf]) != want[s]]
+    assert not bad, bad[:20]

@@ -692,11 +692,6 @@ struct LaneLds {
     uint4 M[16][2];        // M[i]: 1 in the u16 entries t > i
 };
 
-__device__ __forceinline__ uint32_t u16_of(const uint4 &v, int k)   // k compile-time
-{
-    const uint32_t d = k < 2 ? v.x : k < 4 ? v.y : k < 6 ? v.z : v.w;
-    return (k & 1) ? d >> 16 : d & 0xFFFFu;
-}
 __device__ __forceinline__ uint4 add4(const uint4 &a, const uint4 &b)
 {
     return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);

@@ -136,15 +136,12 @@ __device__ __forceinline__ void move_runs_tab(const Geom &g, uint8_t *stage, con
 // multiply-shifts and the run bases come from two per-launch constants
 // (full-rate v_mul_u32_u24 instead of quarter-rate 32-bit multiplies and
 // 64-bit address arithmetic) whenever the frame's subband stride fits 24 bits.
-// multiply-shift division q / cps for q < 64 cps (tiles of T = 256, 384, 512 blocks)
+// multiply-shift division q / cps for q < 64 cps (tiles of T = 256 blocks; 384- and
+// 512-block tiles, m/s = 3641/18 and 2731/18, measured slower: DESIGN.md §6)
 template <int T>
 struct DivCps;
 template <>
 struct DivCps<256> { static constexpr uint32_t m = 2731, s = 17; };   // / 48
-template <>
-struct DivCps<384> { static constexpr uint32_t m = 3641, s = 18; };   // / 72
-template <>
-struct DivCps<512> { static constexpr uint32_t m = 2731, s = 18; };   // / 96
 
 template <bool SUB, int T = kTile>
 __device__ __forceinline__ void move_runs_full(const Geom &g, const uint8_t *stage, const uint32_t *rowbase,

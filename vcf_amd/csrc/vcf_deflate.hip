@@ -42,6 +42,7 @@
 #include "vcf_amd.h"
 #include "vcf_deflate.h"
 #include "vcf_internal.h"
+#include "vcf_pipeline.h"
 
 namespace vcf {
 namespace {
@@ -49,7 +50,6 @@ namespace {
 using namespace dfl;
 
 constexpr int kStgWords = 128;       // bit staging for one 64-symbol step (<= 3072 + 31 bits)
-constexpr int kStage = 1024;         // K1: bytes staged per step
 constexpr int kK2Threads = 256;
 constexpr int kPer = 16;             // K2: consecutive positions per thread
 constexpr int kChunk = kK2Threads * kPer;                 // K2: positions per workgroup
@@ -94,11 +94,19 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 #ifndef VCF_ZLIB_PROF
 #define VCF_ZLIB_PROF 0
 #endif
+#ifndef VCF_ZX_NOCAP   // A/B (diagnostic builds): lane compares run on to MAX_MATCH
+#define VCF_ZX_NOCAP 0
+#endif
+#ifndef VCF_ZX_SERIAL   // A/B (diagnostic builds): every kernel of a round on the caller's stream
+#define VCF_ZX_SERIAL 0
+#endif
 #if VCF_ZLIB_PROF
 // diagnostic build only (scripts/zprof_build.sh): per-phase clock totals of the parse kernels
 // [0] lazy total, [1] lazy longest, [2] lazy flush, [3] longest calls, [4] chain rounds,
-// [5] window shifts, [6] lazy strips, [7] K3 (non-lazy) total
-__device__ unsigned long long g_zprof[8];
+// [5] window shifts, [6] lazy strips, [7] K3 (non-lazy) total, [8] lazy longest up to the end
+// of the head compare, [9] lane compare steps (the wave's maximum per round), [10] candidates
+// passing the scan_end test, [11] calls served by the prefetch
+__device__ unsigned long long g_zprof[16];
 #define VCF_ZPROF_COUNT(x) (++(x))
 #else
 #define VCF_ZPROF_COUNT(x) ((void)0)
@@ -124,10 +132,22 @@ __device__ __forceinline__ uint32_t excl_scan(uint32_t v, uint32_t &total)
     total = (uint32_t)__shfl(incl, 63, 64);
     return incl - v;
 }
+// Data a wave stores and later reads back in the same kernel (the parse's symbol
+// buffer) goes through agent-scope accesses on both sides.  An agent-scope load
+// must see other XCDs' writes, so on gfx950 it does not take this XCD's L2 copy,
+// and a plain store stays in that (write-back) L2: a plain store followed by an
+// agent-scope load can read what the address held before the store -- here, the
+// previous round's strip in the same workspace slot (seen as rare, run-dependent
+// wrong strips).  Both accesses at agent scope meet at the coherent level.
 template <class T>
-__device__ __forceinline__ T ld_l2(const T *p)   // coherent with the other lanes' earlier stores (not via L1)
+__device__ __forceinline__ T ld_l2(const T *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_l2(T *p, T v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct Strip {
@@ -156,52 +176,60 @@ __device__ __forceinline__ Strip strip_of(const uint8_t *in, int64_t frame_bytes
 // of p -- the earlier positions with p's hash, newest first -- is
 // sorted[idx[p]-1], sorted[idx[p]-2], ... while the hash stays p's; hd[p] is
 // its first element (zlib's head[] as p is inserted, 0 = NIL).
-struct OrderSmem {
-    uint32_t cnt[1 << 14];              // 32768 u16 counters / cursors, packed in pairs
-    uint8_t stage[kStage + 64];
-};
-
-__device__ __forceinline__ void stage_chunk(uint8_t *stage, const uint8_t *src, uint32_t n, uint32_t c0)
-{
-    for (uint32_t j = lane_id(); j < (uint32_t)kStage + 2; j += 64) {
-        const uint32_t p = c0 + j;
-        stage[j] = p < n ? src[p] : 0u;
-    }
-}
-
 __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c)   // zlib UPDATE_HASH x3
 {
     return (a << 10 ^ b << 5 ^ c) & 0x7fffu;
 }
 
-// One wave per strip.  Pass 1: the hash histogram (and the adler32 sums);
-// exclusive scan; pass 2: the ordered scatter, 256 positions (four 64-lane
-// sub-groups) per step: within a sub-group the same-hash lane masks give each
-// position its rank, the first lane of each hash (the leader) adds the
-// sub-group's count to the bucket cursor with one LDS atomic returning the old
-// cursor -- the four sub-groups' atomics issue back to back and execute in
-// order, so a later sub-group sees an earlier one's update -- and the other
-// lanes take the leader's old cursor by ds_bpermute.  hd[] (zlib's head[] as
-// p is inserted) is zlib_head_kernel's: every position in parallel from
+// kK1Waves waves per strip, sharing the 32768 bucket counters in LDS.  Pass 1:
+// the hash histogram (and the adler32 sums), all waves.  Scan: wave w owns the
+// buckets with hash >> 13 == w (a quarter of the hash space) and scans them
+// from the total of the lower quarters.  Pass 2, the ordered scatter: every
+// wave walks all positions (the chunk is staged once per workgroup) but acts on
+// its own quarter's only, so the waves never share a bucket and each keeps
+// zlib's order inside its buckets without any ordering between waves.  Per 256
+// positions (four 64-lane sub-groups): within a sub-group the same-hash lane
+// masks give each position its rank, the first lane of each hash (the leader)
+// adds the sub-group's count to the bucket cursor with one LDS atomic returning
+// the old cursor -- the four sub-groups' atomics issue back to back and execute
+// in order, so a later sub-group sees an earlier one's update -- and the other
+// lanes take the leader's old cursor by ds_bpermute.  hd[] (zlib's head[] as p
+// is inserted) is zlib_head_kernel's: every position in parallel from
 // sorted[idx[p]-1].
-__global__ __launch_bounds__(64) void zlib_order_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
-                                                       int32_t strip_bytes, int32_t spf, uint8_t *__restrict__ ws,
-                                                       int64_t s0)
+constexpr int kK1Waves = 4, kK1Stage = 2048;
+struct OrderSmem4 {
+    uint32_t cnt[1 << 14];              // 32768 u16 counters / cursors, packed in pairs
+    uint8_t stage[kK1Stage + 64];
+    uint32_t qtot[kK1Waves];
+    uint64_t sums[kK1Waves][2];
+    uint32_t distinct[kK1Waves];
+};
+
+__global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t *__restrict__ in,
+                                                                  int64_t frame_bytes, int32_t strip_bytes,
+                                                                  int32_t spf, uint8_t *__restrict__ ws, int64_t s0)
 {
-    __shared__ __attribute__((aligned(16))) OrderSmem sm;
+    __shared__ __attribute__((aligned(16))) OrderSmem4 sm;
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s0 + blockIdx.x);
     uint16_t *idx = reinterpret_cast<uint16_t *>(S.ws + kIdxOff);
     uint16_t *sorted = reinterpret_cast<uint16_t *>(S.ws + kSortOff);
-    const uint32_t lane = lane_id(), n = S.n;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6, n = S.n;
+    constexpr uint32_t NT = 64 * kK1Waves;
     const uint32_t np = n >= 3 ? n - 2 : 0;   // positions 0..n-3 are inserted
-    for (uint32_t i = lane; i < (1u << 14); i += 64) sm.cnt[i] = 0;
+    for (uint32_t i = tid; i < (1u << 14); i += NT) sm.cnt[i] = 0;
+    auto stage = [&](uint32_t c0) {
+        __syncthreads();
+        for (uint32_t j = tid; j < (uint32_t)kK1Stage + 2; j += NT) {
+            const uint32_t p = c0 + j;
+            sm.stage[j] = p < n ? S.src[p] : 0u;
+        }
+        __syncthreads();
+    };
     uint64_t sb = 0, swb = 0;
     // histogram of the hashes (and the adler32 sums)
-    for (uint32_t c0 = 0; c0 < n; c0 += kStage) {
-        wave_sync();
-        stage_chunk(sm.stage, S.src, n, c0);
-        wave_sync();
-        for (uint32_t j = lane; j < (uint32_t)kStage; j += 64) {
+    for (uint32_t c0 = 0; c0 < n; c0 += kK1Stage) {
+        stage(c0);
+        for (uint32_t j = tid; j < (uint32_t)kK1Stage; j += NT) {
             const uint32_t p = c0 + j, b = sm.stage[j];
             sb += b;
             swb += (uint64_t)(p < n ? n - p : 0u) * b;
@@ -211,38 +239,40 @@ __global__ __launch_bounds__(64) void zlib_order_kernel(const uint8_t *__restric
             }
         }
     }
-    wave_sync();
-    // exclusive scan of the 32768 counters (each total < 65536: u16 starts)
+    __syncthreads();
+    // exclusive scan: wave w's quarter (4096 words, 64 per lane), from the lower quarters' total
+    constexpr uint32_t kQW = (1u << 14) / kK1Waves, kLW = kQW / 64;
+    uint32_t *qc = sm.cnt + w * kQW + lane * kLW;
     uint32_t tsum = 0;
-    for (uint32_t i = 0; i < 256; ++i) {
-        const uint32_t w = sm.cnt[lane * 256 + i];
-        tsum += (w & 0xffffu) + (w >> 16);
+    for (uint32_t i = 0; i < kLW; ++i) {
+        const uint32_t x = qc[i];
+        tsum += (x & 0xffffu) + (x >> 16);
     }
     uint32_t tot;
     uint32_t run = excl_scan(tsum, tot);
-    for (uint32_t i = 0; i < 256; ++i) {
-        const uint32_t w = sm.cnt[lane * 256 + i];
-        const uint32_t c0 = w & 0xffffu, c1 = w >> 16;
-        const uint32_t st = run | ((run + c0) << 16);
-        sm.cnt[lane * 256 + i] = st;
+    if (lane == 0) sm.qtot[w] = tot;
+    __syncthreads();
+    for (uint32_t v = 0; v < w; ++v) run += sm.qtot[v];
+    for (uint32_t i = 0; i < kLW; ++i) {
+        const uint32_t x = qc[i];
+        const uint32_t c0 = x & 0xffffu, c1 = x >> 16;
+        qc[i] = run | ((run + c0) << 16);
         run += c0 + c1;
     }
-    // ordered scatter
-    uint32_t distinct = 0;   // sum over the 64-position groups of their distinct hashes
+    // ordered scatter of this wave's quarter
+    uint32_t distinct = 0;   // over the 64-position groups: their distinct hashes in this quarter
     const uint64_t lt = (1ull << lane) - 1;
-    for (uint32_t c0 = 0; c0 < np; c0 += kStage) {
-        wave_sync();
-        stage_chunk(sm.stage, S.src, n, c0);
-        wave_sync();
-        for (uint32_t g = 0; g < (uint32_t)kStage && c0 + g < np; g += 256) {
+    for (uint32_t c0 = 0; c0 < np; c0 += kK1Stage) {
+        stage(c0);
+        for (uint32_t g = 0; g < (uint32_t)kK1Stage && c0 + g < np; g += 256) {
             uint32_t h[4], rank[4], cntj[4], old[4];
             uint64_t mine[4];
             bool v[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint32_t j = g + 64 * q + lane;
-                v[q] = c0 + j < np && j < (uint32_t)kStage;
                 h[q] = hash3(sm.stage[j], sm.stage[j + 1], sm.stage[j + 2]);
+                v[q] = c0 + j < np && j < (uint32_t)kK1Stage && (h[q] >> 13) == w;
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -283,11 +313,24 @@ __global__ __launch_bounds__(64) void zlib_order_kernel(const uint8_t *__restric
         swb += __shfl_xor(swb, d, 64);
     }
     if (lane == 0) {
+        sm.sums[w][0] = sb;
+        sm.sums[w][1] = swb;
+        sm.distinct[w] = distinct;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t a = 0, b = 0;
+        uint32_t dsum = 0;
+        for (int v = 0; v < kK1Waves; ++v) {
+            a += sm.sums[v][0];
+            b += sm.sums[v][1];
+            dsum += sm.distinct[v];
+        }
         uint64_t *sums = reinterpret_cast<uint64_t *>(S.ws + kSumOff);
-        sums[0] = sb;
-        sums[1] = swb;
+        sums[0] = a;
+        sums[1] = b;
         *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 16) = 0;   // K2's worklist length
-        *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = distinct * kLazyDiv < np ? 1u : 0u;   // parse order
+        *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = dsum * kLazyDiv < np ? 1u : 0u;   // parse order
     }
 }
 
@@ -869,10 +912,15 @@ struct Wave {
         if (lwin[a + 256] == lwin[b + 256]) l = lwin[a + 257] == lwin[b + 257] ? 258 : 257;
         return l;
     }
-    __device__ __forceinline__ uint32_t lane_lcp(uint32_t a, uint32_t b)   // one lane, 16 bytes per step
+    // one lane, 16 bytes per step, until a difference or `cap` bytes (a result >= cap is
+    // not exact: the caller only needs to know it reached cap)
+    __device__ __forceinline__ uint32_t lane_lcp(uint32_t a, uint32_t b, uint32_t cap = MAX_MATCH, uint32_t from = 0)
     {
-        uint32_t l = 0;
-        while (l < (uint32_t)MAX_MATCH) {
+        uint32_t l = from;
+        while (l < cap) {
+#if VCF_ZLIB_PROF
+            ++lcp_steps;
+#endif
             const uint32_t x0 = ld4(a + l) ^ ld4(b + l), x1 = ld4(a + l + 4) ^ ld4(b + l + 4);
             const uint32_t x2 = ld4(a + l + 8) ^ ld4(b + l + 8), x3 = ld4(a + l + 12) ^ ld4(b + l + 12);
             if (x0 | x1 | x2 | x3) {
@@ -886,6 +934,7 @@ struct Wave {
     }
 #if VCF_ZLIB_PROF
     unsigned long long t_longest = 0, t_flush = 0, n_longest = 0, n_rounds = 0, n_shift = 0;
+    unsigned long long t_head = 0, n_lcp = 0, n_cand = 0, n_pf = 0;
     __device__ __forceinline__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
                             uint32_t limit, uint32_t &len, uint32_t &pos)
     {
@@ -954,9 +1003,16 @@ struct Wave {
         pos = p - (r & 0xffffu);
         return len > prev_len;
     }
+#if VCF_ZLIB_PROF
+    uint32_t lcp_steps = 0;
+#endif
     __device__ __forceinline__ bool lazy_longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain,
                                                  uint32_t nice, uint32_t limit, uint32_t &len, uint32_t &pos)
     {
+#if VCF_ZLIB_PROF
+        const unsigned long long th0 = clock64();
+        if (p == pfa_p || p == pfb_p) ++n_pf;
+#endif
         {
             // the first candidate (chain order) reaching max(nice, prev_len+1), else the
             // first reaching the longest length found, if longer than prev_len
@@ -980,6 +1036,9 @@ struct Wave {
             }
             const uint32_t hp = hash_at(wp);
             const uint32_t l1 = wave_lcp(hdp - wbase, wp);
+#if VCF_ZLIB_PROF
+            t_head += clock64() - th0;
+#endif
             if (l1 >= Tn) {
                 len = l1;
                 pos = hdp;
@@ -996,27 +1055,57 @@ struct Wave {
                 bool v = gk < chain && gk < ip;
                 const uint32_t c = !v ? 0u : b == 0 ? pre0 : b == 64 ? pre1 : (uint32_t)sorted[ip - 1 - gk];
                 v = v && (gk == 0 || c > limit);
-                const uint32_t wc = v ? c - wbase : 0u;
-                v = v && hash_at(wc) == hp;
+                // every LDS read of the round issued at once, on every lane (a lane off
+                // the chain reads p's own bytes): the candidate's first four bytes (its
+                // hash), the scan_end bytes, and the first 16 bytes of the compare
+                const uint32_t wc = v ? c - wbase : wp;
+                const uint32_t c4 = ld4(wc);
+                const bool se = lwin[wc + F] == lwin[wp + F] && lwin[wc + F - 1] == lwin[wp + F - 1];
+                uint32_t x16[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) x16[u] = ld4(wc + 4 * u) ^ ld4(wp + 4 * u);
+                v = v && hash3(c4 & 0xffu, (c4 >> 8) & 0xffu, (c4 >> 16) & 0xffu) == hp;
                 const uint64_t stop = __ballot(!v);
                 const uint32_t nv = stop ? (uint32_t)__ffsll((unsigned long long)stop) - 1 : 64u;
                 v = lane_id() < nv;
-                const bool cand = v && gk != 0 && lwin[wc + F] == lwin[wp + F] && lwin[wc + F - 1] == lwin[wp + F - 1];
-                const uint32_t l = v ? (gk == 0 ? l1 : cand ? lane_lcp(wc, wp) : 0u) : 0u;
+                const bool cand = v && gk != 0 && se;
+#if VCF_ZLIB_PROF
+                n_cand += (unsigned long long)__popcll(__ballot(cand));
+                lcp_steps = 0;
+#endif
+                // compared up to Tn only: a candidate reaching Tn ends the call, and its
+                // full length (zlib compares on to MAX_MATCH) comes from one wave compare
+                uint32_t l = 0;
+                if (v && gk == 0) l = l1;
+                if (cand) {
+                    const uint32_t x = x16[0] | x16[1] | x16[2] | x16[3];
+                    if (x) {
+                        const uint32_t q = x16[0] ? 0u : x16[1] ? 4u : x16[2] ? 8u : 12u;
+                        l = q + ((uint32_t)__builtin_ctz(x16[0] ? x16[0] : x16[1] ? x16[1] : x16[2] ? x16[2] : x16[3]) >> 3);
+                    } else {
+                        l = lane_lcp(wc, wp, VCF_ZX_NOCAP ? (uint32_t)MAX_MATCH : Tn, 16u);
+                    }
+                }
+#if VCF_ZLIB_PROF
+                {
+                    uint32_t ms = lcp_steps;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) ms = max(ms, (uint32_t)__shfl_xor(ms, d, 64));
+                    n_lcp += uni(ms);
+                }
+#endif
                 const uint64_t hit = __ballot(v && l >= Tn);
                 if (hit) {
                     const uint32_t k = (uint32_t)__ffsll((unsigned long long)hit) - 1;
-                    len = lane_val(l, k);
                     pos = lane_val(c, k);
+                    len = k == 0 && b == 0 ? l1 : wave_lcp(pos - wbase, wp);
                     return true;
                 }
-                uint32_t m = l;
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor(m, d, 64));
-                m = uni(m);
-                if (m > best) {
-                    const uint32_t k = (uint32_t)__ffsll((unsigned long long)__ballot(v && l == m)) - 1;
-                    best = m;
+                // the first lane with the longest length beyond best: step from improvement
+                // to improvement in lane order (few steps; no cross-lane max reduction)
+                for (uint64_t better = __ballot(v && l > best); better; better = __ballot(v && l > best)) {
+                    const uint32_t k = (uint32_t)__ffsll((unsigned long long)better) - 1;
+                    best = lane_val(l, k);
                     bpos = lane_val(c, k);
                     found = true;
                 }
@@ -1029,7 +1118,7 @@ struct Wave {
     }
     __device__ __forceinline__ bool tally(uint32_t dist, uint32_t lc)
     {
-        if (lane_id() == 0) syms[nsym] = dist << 8 | lc;   // counted at flush
+        if (lane_id() == 0) st_l2(syms + nsym, dist << 8 | lc);   // counted at flush
         ++nsym;
         return nsym == (uint32_t)LIT_BUFSIZE - 1;
     }
@@ -1181,6 +1270,10 @@ __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restric
             atomicAdd(&g_zprof[4], wv.n_rounds);
             atomicAdd(&g_zprof[5], wv.n_shift);
             atomicAdd(&g_zprof[6], 1ull);
+            atomicAdd(&g_zprof[8], wv.t_head);
+            atomicAdd(&g_zprof[9], wv.n_lcp);
+            atomicAdd(&g_zprof[10], wv.n_cand);
+            atomicAdd(&g_zprof[11], wv.n_pf);
         } else {
             atomicAdd(&g_zprof[7], tp);
         }
@@ -1213,11 +1306,11 @@ int64_t vcf_zlib_bound(int64_t strip_bytes)
 int32_t vcf_zlib_max_strip(void) { return dfl::MAX_STRIP; }
 
 #if VCF_ZLIB_PROF
-int vcf_zlib_prof_read(unsigned long long *host8, int reset)
+int vcf_zlib_prof_read(unsigned long long *host16, int reset)
 {
-    int rc = hip_check(hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_zprof), sizeof(g_zprof)), "hipMemcpyFromSymbol");
+    int rc = hip_check(hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_zprof), sizeof(g_zprof)), "hipMemcpyFromSymbol");
     if (rc == VCF_OK && reset) {
-        static const unsigned long long z[8] = {};
+        static const unsigned long long z[16] = {};
         rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_zprof), z, sizeof(z)), "hipMemcpyToSymbol");
     }
     return rc;
@@ -1260,35 +1353,59 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     const int chunks = (int)((std::min<int64_t>(strip_bytes, frame_bytes) + kChunk - 1) / kChunk);
     const unsigned hd_blocks = (unsigned)((std::min<int64_t>(strip_bytes, frame_bytes) + kHdThreads * kHdPer - 1) /
                                           (kHdThreads * kHdPer));
-    auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws, hipStream_t rs) -> int {
-        hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64), 0, rs, in_dev, frame_bytes, strip_bytes,
+    // A round: K1 and the head table on the caller's stream; then the two kinds of
+    // strips side by side -- the lazy parse of the repetitive strips on the caller's
+    // stream, K2a/K2b and the register-window parse of the others on a library
+    // stream (forked by an event, joined before the next round reuses the
+    // workspace).  The two sides touch disjoint strips: their own output slots,
+    // sizes and workspace regions; both only read K1's and the head kernel's tables.
+    AuxStreams &ax = aux_for_current_device();
+    std::lock_guard<std::mutex> lock(ax.mu);
+    int rc = ax.init();
+    if (rc != VCF_OK) return rc;
+    hipStream_t side = VCF_ZX_SERIAL ? st : ax.s[0];
+    auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws) -> int {
+        hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64 * kK1Waves), 0, st, in_dev, frame_bytes, strip_bytes,
                            (int32_t)spf, ws, s0);
         int rc = hip_check(hipGetLastError(), "zlib_order_kernel launch");
         if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_head_kernel, dim3(hd_blocks, cnt), dim3(kHdThreads), 0, rs, in_dev, frame_bytes,
+        hipLaunchKernelGGL(zlib_head_kernel, dim3(hd_blocks, cnt), dim3(kHdThreads), 0, st, in_dev, frame_bytes,
                            strip_bytes, (int32_t)spf, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_head_kernel launch");
         if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, rs, in_dev,
+        if (side != st) {
+            if ((rc = hip_check(hipEventRecord(ax.fork, st), "hipEventRecord")) != VCF_OK) return rc;
+            if ((rc = hip_check(hipStreamWaitEvent(side, ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
+        }
+        hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, side, in_dev,
                            frame_bytes, strip_bytes, (int32_t)spf, level, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_match_kernel launch");
-        if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt), dim3(kK2bThreads), 0, rs, in_dev, frame_bytes, strip_bytes,
-                           (int32_t)spf, level, ws, s0);
-        rc = hip_check(hipGetLastError(), "zlib_chain_kernel launch");
-        if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3(cnt), dim3(64), 0, rs, in_dev, frame_bytes, strip_bytes,
-                           (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
-        rc = hip_check(hipGetLastError(), "zlib_parse_kernel launch");
-        if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3(cnt), dim3(64), 0, rs, in_dev, frame_bytes, strip_bytes,
-                           (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
-        return hip_check(hipGetLastError(), "zlib_parse_kernel (lazy) launch");
+        if (rc == VCF_OK) {
+            hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt), dim3(kK2bThreads), 0, side, in_dev, frame_bytes,
+                               strip_bytes, (int32_t)spf, level, ws, s0);
+            rc = hip_check(hipGetLastError(), "zlib_chain_kernel launch");
+        }
+        if (rc == VCF_OK) {
+            hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3(cnt), dim3(64), 0, side, in_dev, frame_bytes,
+                               strip_bytes, (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
+            rc = hip_check(hipGetLastError(), "zlib_parse_kernel launch");
+        }
+        if (rc == VCF_OK) {
+            hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
+                               (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
+            rc = hip_check(hipGetLastError(), "zlib_parse_kernel (lazy) launch");
+        }
+        // join the side stream even after an error, so the caller's stream never runs ahead
+        if (side != st) {
+            int r2 = hip_check(hipEventRecord(ax.join[0], side), "hipEventRecord");
+            if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(st, ax.join[0], 0), "hipStreamWaitEvent");
+            if (rc == VCF_OK) rc = r2;
+        }
+        return rc;
     };
     const ZRounds zr(total);
-    int rc = VCF_OK;
     for (int64_t s0 = 0; s0 < total && rc == VCF_OK; s0 += zr.per)
-        rc = round(s0, (unsigned)std::min<int64_t>(zr.per, total - s0), (uint8_t *)ws_dev, st);
+        rc = round(s0, (unsigned)std::min<int64_t>(zr.per, total - s0), (uint8_t *)ws_dev);
     return rc;
 }
 
