@@ -18,12 +18,20 @@ fb = flat.shape[1]; _, _, sb = strip_layout(frames.shape[1:], 1)
 spf = int(L.lib().vcf_zlib_strip_count(fb, sb)); total = spf * n; slot = int(L.lib().vcf_zlib_bound(sb))
 d = DeviceBuffer.from_array(flat); out = DeviceBuffer(total * slot); sizes = DeviceBuffer(total * 4)
 ws = DeviceBuffer(int(L.lib().vcf_zlib_workspace(total))); st = Stream()
+if "ZFILL" in os.environ:   # the workspace's contents before the call (uninitialised-read probe)
+    ws.fill(int(os.environ["ZFILL"]), st)
+    st.synchronize()
 so = os.environ.get("ZLIB_SO")
 if so:
     P = ctypes.CDLL(os.path.join(ROOT, "scripts", so))
     P.vcf_zlib_strips.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     assert P.vcf_zlib_strips(d.ptr, n, fb, sb, 6, out.ptr, slot, sizes.ptr, ws.ptr, st.handle) == 0
+    if hasattr(P, "vcf_zlib_dbg_read"):
+        st.synchronize()
+        dbg = (ctypes.c_uint * 8)()
+        P.vcf_zlib_dbg_read(dbg)
+        print("window check:", list(dbg), flush=True)
 else:
     L.call("vcf_zlib_strips", d.ptr, n, fb, sb, 6, out.ptr, slot, sizes.ptr, ws.ptr, st.handle)
 st.synchronize()

@@ -42,4 +42,7 @@ print(json.dumps({"frames": n, "strips": total, "ms": round(e0.elapsed_ms(e1), 2
                   "k3_cycles_per_strip": v[7] // max(1, total - v[6]),
                   "head_cycles_per_longest": v[8] // max(1, v[3]), "lcp_steps_per_round": v[9] / max(1, v[4]),
                   "scan_end_passes_per_round": v[10] / max(1, v[4]), "prefetch_served": v[11] / max(1, v[3]),
+                  "cand_wait_cycles_per_longest": v[12] // max(1, v[3]),
+                  "round_cycles_to_chain_ballot": v[13] // max(1, v[4]), "round_cycles_to_lengths": v[14] // max(1, v[4]),
+                  "round_cycles_rest": v[15] // max(1, v[4]),
                   "lib": os.environ.get("ZPROF_LIB", "libvcf_zprof.so")}), flush=True)

@@ -10,6 +10,15 @@
 
 using namespace vcf::dfl;
 
+#ifdef DH_STATS
+#include <algorithm>
+// diagnostic build only: [0] longest_match calls, [1] candidates visited, [2..5] calls whose
+// farthest candidate is beyond 8 / 12 / 16 / 24 KiB, [8..23] candidates by distance (2 KiB bins)
+extern "C" {
+unsigned long long dh_stats[32];
+}
+#endif
+
 namespace {
 
 struct BitOut {
@@ -90,7 +99,16 @@ struct HostOps {
                  uint32_t &len, uint32_t &pos)
     {
         bool found = false;
+#ifdef DH_STATS
+        uint32_t far = 0;
+        ++dh_stats[0];
+#endif
         do {
+#ifdef DH_STATS
+            far = p - cur > far ? p - cur : far;
+            ++dh_stats[1];
+            ++dh_stats[8 + std::min<uint32_t>((p - cur) >> 11, 15)];
+#endif
             const uint32_t l = lcp(cur, p);
             if (l > best) {
                 pos = cur;
@@ -99,6 +117,12 @@ struct HostOps {
                 if (l >= nice) break;
             }
         } while ((cur = prevpos[cur]) > limit && --chain != 0);
+#ifdef DH_STATS
+        dh_stats[2] += far > 8192;
+        dh_stats[3] += far > 12288;
+        dh_stats[4] += far > 16384;
+        dh_stats[5] += far > 24576;
+#endif
         len = best;
         return found;
     }

@@ -97,6 +97,23 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 #ifndef VCF_ZX_NOCAP   // A/B (diagnostic builds): lane compares run on to MAX_MATCH
 #define VCF_ZX_NOCAP 0
 #endif
+#ifndef VCF_ZX_NOPRIO   // A/B (diagnostic builds): the side stream at normal priority
+#define VCF_ZX_NOPRIO 0
+#endif
+#ifndef VCF_ZX_COHERENT   // A/B (diagnostic builds): agent-scope loads of the K1 / head tables in the lazy parse
+#define VCF_ZX_COHERENT 0
+#endif
+#ifndef VCF_ZX_WINCHECK   // (diagnostic) the lazy window checked against the strip at every call
+#define VCF_ZX_WINCHECK 0
+#endif
+#if VCF_ZX_WINCHECK
+// first failure: [0] 1 + kind (1: window at p, 2: window at a candidate), [1] strip, [2] p,
+// [3] position, [4] window byte, [5] strip byte, [6] wbase, [7] count of failures
+__device__ unsigned int g_zdbg[8];
+#endif
+#ifndef VCF_ZX_LDSZERO
+#define VCF_ZX_LDSZERO 0
+#endif
 #ifndef VCF_ZX_SERIAL   // A/B (diagnostic builds): every kernel of a round on the caller's stream
 #define VCF_ZX_SERIAL 0
 #endif
@@ -105,7 +122,9 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 // [0] lazy total, [1] lazy longest, [2] lazy flush, [3] longest calls, [4] chain rounds,
 // [5] window shifts, [6] lazy strips, [7] K3 (non-lazy) total, [8] lazy longest up to the end
 // of the head compare, [9] lane compare steps (the wave's maximum per round), [10] candidates
-// passing the scan_end test, [11] calls served by the prefetch
+// passing the scan_end test, [11] calls served by the prefetch, [12] cycles then waiting for
+// the first two rounds' candidates, [13..15] chain-round cycles: to the chain ballot, to the
+// lengths, the rest (rounds that end the call with a hit excluded from [15])
 __device__ unsigned long long g_zprof[16];
 #define VCF_ZPROF_COUNT(x) (++(x))
 #else
@@ -698,6 +717,23 @@ struct Wave {
     // and p + the match length), requested at the end of a call: their global latency
     // overlaps the parse step in between (~70 % of the calls are at one of the two)
     uint32_t pfa_p = 0xffffffffu, pfa0 = 0, pfa1 = 0, pfb_p = 0xffffffffu, pfb0 = 0, pfb1 = 0;
+#if VCF_ZX_WINCHECK
+    uint32_t dbg_strip = 0;
+    __device__ __forceinline__ void wincheck(uint32_t kind, uint32_t P, bool bad, uint32_t got, uint32_t want)
+    {
+        const uint64_t m = __ballot(bad);
+        if (!m) return;
+        const uint32_t k = (uint32_t)__ffsll((unsigned long long)m) - 1;
+        if (lane_id() == k) {
+            atomicAdd(&g_zdbg[7], 1u);
+            if (atomicCAS(&g_zdbg[0], 0u, kind) == 0u) {
+                g_zdbg[1] = dbg_strip; g_zdbg[2] = cur_p; g_zdbg[3] = P; g_zdbg[4] = got; g_zdbg[5] = want;
+                g_zdbg[6] = wbase;
+            }
+        }
+    }
+    uint32_t cur_p = 0;
+#endif
 
     __device__ __forceinline__ Wave(ParseSmem &s, const uint8_t *in, uint32_t len, const uint8_t *w, uint32_t g, uint32_t *o,
                     uint32_t ow)
@@ -718,10 +754,23 @@ struct Wave {
     // as soon as the current one is in use (the parse only moves forward, at most
     // MAX_MATCH positions at a time, so it always enters the next window)
     uint4 hv_n, iv_n;
-    __device__ __forceinline__ static uint4 vload4(const uint16_t *a)
+    // VCF_ZX_COHERENT (A/B): the workspace tables K1 and the head kernel wrote, read at agent scope
+    __device__ __forceinline__ static uint4 wload4(const uint16_t *a)
     {
-        const volatile uint32_t *v = reinterpret_cast<const volatile uint32_t *>(a);
-        return make_uint4(v[0], v[1], v[2], v[3]);
+#if VCF_ZX_COHERENT
+        const uint32_t *v = reinterpret_cast<const uint32_t *>(a);
+        return make_uint4(ld_l2(v), ld_l2(v + 1), ld_l2(v + 2), ld_l2(v + 3));
+#else
+        return *reinterpret_cast<const uint4 *>(a);
+#endif
+    }
+    __device__ __forceinline__ static uint32_t wload16(const uint16_t *a)
+    {
+#if VCF_ZX_COHERENT
+        return ld_l2(a);
+#else
+        return *a;
+#endif
     }
     __device__ __forceinline__ void lazy_windows(uint32_t p)
     {
@@ -731,12 +780,12 @@ struct Wave {
             hv = hv_n;
             iv = iv_n;
         } else {
-            hv = *reinterpret_cast<const uint4 *>(hd + nb + 8 * lane_id());
-            iv = *reinterpret_cast<const uint4 *>(idx + nb + 8 * lane_id());
+            hv = wload4(hd + nb + 8 * lane_id());
+            iv = wload4(idx + nb + 8 * lane_id());
         }
         base = ibase = nb;
-        hv_n = vload4(hd + nb + 512 + 8 * lane_id());
-        iv_n = vload4(idx + nb + 512 + 8 * lane_id());
+        hv_n = wload4(hd + nb + 512 + 8 * lane_id());
+        iv_n = wload4(idx + nb + 512 + 8 * lane_id());
     }
     __device__ __forceinline__ void window(uint32_t p)
     {
@@ -934,7 +983,7 @@ struct Wave {
     }
 #if VCF_ZLIB_PROF
     unsigned long long t_longest = 0, t_flush = 0, n_longest = 0, n_rounds = 0, n_shift = 0;
-    unsigned long long t_head = 0, n_lcp = 0, n_cand = 0, n_pf = 0;
+    unsigned long long t_head = 0, n_lcp = 0, n_cand = 0, n_pf = 0, t_wait = 0, t_r0 = 0, t_r1 = 0, t_r2 = 0;
     __device__ __forceinline__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
                             uint32_t limit, uint32_t &len, uint32_t &pos)
     {
@@ -966,10 +1015,10 @@ struct Wave {
     // full limit of the next)
     __device__ __forceinline__ void fetch_cands(uint32_t ip, uint32_t &c0, uint32_t &c1)
     {
-        const volatile uint16_t *vs = sorted;
+        const uint16_t *vs = sorted;
         const uint32_t g0 = lane_id(), g1 = 64 + lane_id();
-        c0 = vs[g0 < ip ? ip - 1 - g0 : 0u];
-        c1 = vs[g1 < ip ? ip - 1 - g1 : 0u];
+        c0 = wload16(vs + (g0 < ip ? ip - 1 - g0 : 0u));
+        c1 = wload16(vs + (g1 < ip ? ip - 1 - g1 : 0u));
     }
     __device__ __forceinline__ uint32_t idx_known(uint32_t q)   // idx[q] from the windows, or ~0 if outside them
     {
@@ -1018,12 +1067,19 @@ struct Wave {
             // first reaching the longest length found, if longer than prev_len
             ensure(p);
             const uint32_t wp = p - wbase;   // window offsets from here on (every candidate is >= wbase)
+#if VCF_ZX_WINCHECK
+            cur_p = p;
+            for (uint32_t P0 = (p > 128u + wbase ? p - 128u : wbase); P0 < p + 256u; P0 += 64) {
+                const uint32_t P = P0 + lane_id();
+                const uint32_t got = lwin[P - wbase], want = win_src(P);
+                wincheck(2u, P, P < wbase + kLazyWin && got != want, got, want);
+            }
+#endif
             const uint32_t Tn = max(nice, prev_len + 1);
             lazy_windows(p);
             const uint32_t ip = idx_known(p);
             // the first two chain rounds' candidates: prefetched by the previous call, or
             // requested here before the head compare so their latency overlaps it
-            // (volatile: the compiler keeps the loads where they are)
             uint32_t pre0, pre1;
             if (p == pfa_p) {
                 pre0 = pfa0;
@@ -1037,7 +1093,12 @@ struct Wave {
             const uint32_t hp = hash_at(wp);
             const uint32_t l1 = wave_lcp(hdp - wbase, wp);
 #if VCF_ZLIB_PROF
-            t_head += clock64() - th0;
+            {
+                const unsigned long long th1 = clock64();
+                t_head += th1 - th0;
+                asm volatile("" ::"v"(pre0), "v"(pre1));   // (diagnostic) wait for the candidates here
+                t_wait += clock64() - th1;
+            }
 #endif
             if (l1 >= Tn) {
                 len = l1;
@@ -1051,10 +1112,18 @@ struct Wave {
             bool found = false;
             for (uint32_t b = 0; b < chain; b += 64) {
                 VCF_ZPROF_COUNT(n_rounds);
+#if VCF_ZLIB_PROF
+                const unsigned long long tr0 = clock64();
+#endif
                 const uint32_t gk = b + lane_id();
                 bool v = gk < chain && gk < ip;
-                const uint32_t c = !v ? 0u : b == 0 ? pre0 : b == 64 ? pre1 : (uint32_t)sorted[ip - 1 - gk];
-                v = v && (gk == 0 || c > limit);
+                const uint32_t c = !v ? 0u : b == 0 ? pre0 : b == 64 ? pre1 : wload16(sorted + ip - 1 - gk);
+                // sorted[] runs on past the bucket: a candidate of another bucket can be any
+                // position, also one outside the window (round 3 held the whole strip in LDS),
+                // so the bucket end must not be judged from window bytes there.  p's own
+                // bucket holds only earlier positions, and those past `limit` are in the
+                // window: c < p first, then the hash from the window.
+                v = v && c < p && (gk == 0 || c > limit);
                 // every LDS read of the round issued at once, on every lane (a lane off
                 // the chain reads p's own bytes): the candidate's first four bytes (its
                 // hash), the scan_end bytes, and the first 16 bytes of the compare
@@ -1064,8 +1133,18 @@ struct Wave {
                 uint32_t x16[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) x16[u] = ld4(wc + 4 * u) ^ ld4(wp + 4 * u);
+#if VCF_ZX_WINCHECK
+                {
+                    const uint32_t want = v ? win_src(c) | win_src(c + 1) << 8 | win_src(c + 2) << 16 | win_src(c + 3) << 24 : c4;
+                    wincheck(3u, c, v && c4 != want, c4, want);
+                }
+#endif
                 v = v && hash3(c4 & 0xffu, (c4 >> 8) & 0xffu, (c4 >> 16) & 0xffu) == hp;
                 const uint64_t stop = __ballot(!v);
+#if VCF_ZLIB_PROF
+                const unsigned long long tr1 = clock64();
+                t_r0 += tr1 - tr0;
+#endif
                 const uint32_t nv = stop ? (uint32_t)__ffsll((unsigned long long)stop) - 1 : 64u;
                 v = lane_id() < nv;
                 const bool cand = v && gk != 0 && se;
@@ -1095,6 +1174,10 @@ struct Wave {
                 }
 #endif
                 const uint64_t hit = __ballot(v && l >= Tn);
+#if VCF_ZLIB_PROF
+                const unsigned long long tr2 = clock64();
+                t_r1 += tr2 - tr1;
+#endif
                 if (hit) {
                     const uint32_t k = (uint32_t)__ffsll((unsigned long long)hit) - 1;
                     pos = lane_val(c, k);
@@ -1109,6 +1192,9 @@ struct Wave {
                     bpos = lane_val(c, k);
                     found = true;
                 }
+#if VCF_ZLIB_PROF
+                t_r2 += clock64() - tr2;
+#endif
                 if (nv < 64) break;
             }
             len = best;
@@ -1231,6 +1317,10 @@ __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restric
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s);
     if (strip_lazy(S) != LAZY) return;   // the other kernel codes this strip
     const uint32_t lane = lane_id();
+#if VCF_ZX_LDSZERO   // (diagnostic) LDS cleared first: a read of never-written LDS becomes deterministic
+    for (uint32_t i = lane; i < sizeof(sh) / 4; i += 64) reinterpret_cast<uint32_t *>(&sh)[i] = 0;
+    wave_sync();
+#endif
     Config cfg;
     level_config(level, cfg);
     for (uint32_t i = lane; i < (uint32_t)kStgWords; i += 64) sm.stg[i] = 0;
@@ -1248,6 +1338,9 @@ __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restric
             for (uint32_t p = lane; p < kLazyWin; p += 64) win[p] = p < S.n ? S.src[p] : 0u;
         }
         wv.lwin = win;
+#if VCF_ZX_WINCHECK
+        wv.dbg_strip = (uint32_t)s;
+#endif
         wv.idx = reinterpret_cast<const uint16_t *>(S.ws + kIdxOff);
         wv.sorted = reinterpret_cast<const uint16_t *>(S.ws + kSortOff);
     }
@@ -1274,6 +1367,10 @@ __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restric
             atomicAdd(&g_zprof[9], wv.n_lcp);
             atomicAdd(&g_zprof[10], wv.n_cand);
             atomicAdd(&g_zprof[11], wv.n_pf);
+            atomicAdd(&g_zprof[12], wv.t_wait);
+            atomicAdd(&g_zprof[13], wv.t_r0);
+            atomicAdd(&g_zprof[14], wv.t_r1);
+            atomicAdd(&g_zprof[15], wv.t_r2);
         } else {
             atomicAdd(&g_zprof[7], tp);
         }
@@ -1305,6 +1402,12 @@ int64_t vcf_zlib_bound(int64_t strip_bytes)
 
 int32_t vcf_zlib_max_strip(void) { return dfl::MAX_STRIP; }
 
+#if VCF_ZX_WINCHECK
+int vcf_zlib_dbg_read(unsigned int *host8)
+{
+    return hip_check(hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_zdbg), sizeof(g_zdbg)), "hipMemcpyFromSymbol");
+}
+#endif
 #if VCF_ZLIB_PROF
 int vcf_zlib_prof_read(unsigned long long *host16, int reset)
 {
@@ -1363,7 +1466,21 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     std::lock_guard<std::mutex> lock(ax.mu);
     int rc = ax.init();
     if (rc != VCF_OK) return rc;
-    hipStream_t side = VCF_ZX_SERIAL ? st : ax.s[0];
+    // the side stream at the highest priority: its strips are fewer but each takes
+    // longer (K2b walks every listed position's chain), and as a normal-priority
+    // queue its workgroups only got a CU when the lazy parse left one
+    static hipStream_t side_hi[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!side_hi[dev] && !VCF_ZX_NOPRIO) {
+        int least = 0, greatest = 0;
+        rc = hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+        if (rc == VCF_OK)
+            rc = hip_check(hipStreamCreateWithPriority(&side_hi[dev], hipStreamNonBlocking, greatest),
+                           "hipStreamCreateWithPriority");
+        if (rc != VCF_OK) return rc;
+    }
+    hipStream_t side = VCF_ZX_SERIAL ? st : VCF_ZX_NOPRIO ? ax.s[0] : side_hi[dev];
     auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws) -> int {
         hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64 * kK1Waves), 0, st, in_dev, frame_bytes, strip_bytes,
                            (int32_t)spf, ws, s0);
