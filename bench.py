@@ -452,10 +452,14 @@ def c5_check(info, Q: int) -> None:
     ref = O.decode_frame(k0, H, W, Q)
     mv = O.ipp_block_matching(ref, f1, 16, 8, False)
     k1 = O.encode_frame(O.ipp_residual(f1, O.ipp_motion_compensate(ref, mv, 16)), Q)
-    ok = (bytes(got[0]) == imwrite_bytes(k0) and bytes(got[1]) == imwrite_bytes(k1) and
-          np.array_equal(np.asarray(mvs[0]), np.asarray(mv)))
+    w0, w1 = imwrite_bytes(k0), imwrite_bytes(k1)
+    parts = {"file0": bytes(got[0]) == w0, "file1": bytes(got[1]) == w1,
+             "motion1": np.array_equal(np.asarray(mvs[0]), np.asarray(mv))}
+    ok = all(parts.values())
     info["verified"] = ("ok: frames 0 (I) and 1 (P) equal the host TIFF writer's files of the reference GOP "
-                        "loop's indices (C oracle), frame 1's motion field equal" if ok else "MISMATCH")
+                        "loop's indices (C oracle), frame 1's motion field equal" if ok else
+                        "MISMATCH: " + ", ".join(f"{k} {'ok' if v else 'differs'}" for k, v in parts.items()) +
+                        f" (file sizes {len(got[0])}/{len(w0)}, {len(got[1])}/{len(w1)})")
 
 
 def load_traffic(workload: str):
