@@ -148,7 +148,17 @@ class HostBuffer:
         p = ctypes.c_void_p()
         call("vcf_host_alloc", ctypes.byref(p), max(1, self.nbytes))
         self.ptr = p
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, self.nbytes)).from_address(p.value))[:self.nbytes]
+
+    @property
+    def array(self) -> np.ndarray:
+        """A uint8 view of the buffer.  Every view (and its slices and memoryviews)
+        keeps this HostBuffer alive through its ctypes base, so the page-locked memory
+        is freed only after the last view is gone -- a view that outlived its buffer
+        read freed memory (bench.py's C5 check after the block had returned).  The
+        buffer holds no view itself, so there is no reference cycle."""
+        cbuf = (ctypes.c_uint8 * max(1, self.nbytes)).from_address(self.ptr.value)
+        cbuf._owner = self
+        return np.ctypeslib.as_array(cbuf)[:self.nbytes]
 
     def free(self) -> None:
         if self.ptr is not None and self.ptr.value:

@@ -24,16 +24,23 @@ class PinnedArray:
     """A page-locked host allocation (hipHostMalloc) viewed as a numpy array."""
 
     def __init__(self, shape, dtype=np.uint8):
-        self.nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        self.shape, self.dtype = tuple(shape), np.dtype(dtype)
+        self.nbytes = int(np.prod(shape)) * self.dtype.itemsize
         p = ctypes.c_void_p()
         _lib.call("vcf_host_alloc", ctypes.byref(p), max(1, self.nbytes))
         self.ptr = p
-        buf = (ctypes.c_uint8 * max(1, self.nbytes)).from_address(p.value)
-        self.array = np.frombuffer(buf, np.uint8, count=self.nbytes).view(dtype).reshape(shape)
+
+    @property
+    def array(self) -> np.ndarray:
+        """The allocation as an array; every view keeps this object (and so the
+        page-locked memory) alive through its ctypes base, with no reference cycle
+        (device.HostBuffer.array)."""
+        buf = (ctypes.c_uint8 * max(1, self.nbytes)).from_address(self.ptr.value)
+        buf._owner = self
+        return np.frombuffer(buf, np.uint8, count=self.nbytes).view(self.dtype).reshape(self.shape)
 
     def free(self):
         if self.ptr is not None and self.ptr.value:
-            self.array = None
             _lib.lib().vcf_host_free(self.ptr)
         self.ptr = None
 
