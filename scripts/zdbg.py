@@ -22,11 +22,18 @@ if "ZFILL" in os.environ:   # the workspace's contents before the call (uninitia
     ws.fill(int(os.environ["ZFILL"]), st)
     st.synchronize()
 so = os.environ.get("ZLIB_SO")
+from vcf_amd.device import Event
 if so:
     P = ctypes.CDLL(os.path.join(ROOT, "scripts", so))
     P.vcf_zlib_strips.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-    assert P.vcf_zlib_strips(d.ptr, n, fb, sb, 6, out.ptr, slot, sizes.ptr, ws.ptr, st.handle) == 0
+    for rep in range(2):   # the second call timed
+        e0, e1 = Event(), Event()
+        e0.record(st)
+        assert P.vcf_zlib_strips(d.ptr, n, fb, sb, 6, out.ptr, slot, sizes.ptr, ws.ptr, st.handle) == 0
+        e1.record(st)
+        st.synchronize()
+    print(f"{so}: {e0.elapsed_ms(e1):.1f} ms", flush=True)
     if hasattr(P, "vcf_zlib_dbg_read"):
         st.synchronize()
         dbg = (ctypes.c_uint * 8)()

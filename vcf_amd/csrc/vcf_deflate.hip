@@ -82,6 +82,10 @@ struct ZRounds {
     }
 };
 constexpr int kK2bThreads = 1024;    // K2b: 16 waves per strip, one listed position per wave at a time
+#ifndef VCF_ZX_K2BSPLIT   // A/B (diagnostic builds): K2b workgroups per strip
+#define VCF_ZX_K2BSPLIT 4
+#endif
+constexpr int kK2bSplit = VCF_ZX_K2BSPLIT;   // K2b: workgroups per strip, the listed positions split between them
 // A strip is parsed LAZY (on demand, zlib's order of work) when K1 finds fewer than
 // one distinct hash per kLazyDiv positions among its 64-position groups: such
 // repetitive content leaves most positions inside long matches, which zlib -- and
@@ -200,12 +204,13 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c)   
     return (a << 10 ^ b << 5 ^ c) & 0x7fffu;
 }
 
-// kK1Waves waves per strip, sharing the 32768 bucket counters in LDS.  Pass 1:
-// the hash histogram (and the adler32 sums), all waves.  Scan: wave w owns the
-// buckets with hash >> 13 == w (a quarter of the hash space) and scans them
-// from the total of the lower quarters.  Pass 2, the ordered scatter: every
+// kK1Waves waves per strip, sharing the 32768 bucket counters in LDS; each
+// staged chunk's hashes are computed once into LDS.  Pass 1: the hash histogram
+// (and the adler32 sums), all waves.  Scan: wave w owns the buckets with
+// hash >> 12 == w (an eighth of the hash space) and scans them
+// from the total of the lower parts.  Pass 2, the ordered scatter: every
 // wave walks all positions (the chunk is staged once per workgroup) but acts on
-// its own quarter's only, so the waves never share a bucket and each keeps
+// its own part's only, so the waves never share a bucket and each keeps
 // zlib's order inside its buckets without any ordering between waves.  Per 256
 // positions (four 64-lane sub-groups): within a sub-group the same-hash lane
 // masks give each position its rank, the first lane of each hash (the leader)
@@ -215,10 +220,14 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c)   
 // lanes take the leader's old cursor by ds_bpermute.  hd[] (zlib's head[] as p
 // is inserted) is zlib_head_kernel's: every position in parallel from
 // sorted[idx[p]-1].
-constexpr int kK1Waves = 4, kK1Stage = 2048;
+#ifndef VCF_ZX_K1WAVES   // A/B (diagnostic builds): K1's waves per strip
+#define VCF_ZX_K1WAVES 8
+#endif
+constexpr int kK1Waves = VCF_ZX_K1WAVES, kK1Stage = 2048;
 struct OrderSmem4 {
     uint32_t cnt[1 << 14];              // 32768 u16 counters / cursors, packed in pairs
     uint8_t stage[kK1Stage + 64];
+    uint16_t hsh[kK1Stage];             // the chunk's hashes, computed once per chunk
     uint32_t qtot[kK1Waves];
     uint64_t sums[kK1Waves][2];
     uint32_t distinct[kK1Waves];
@@ -234,6 +243,8 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
     uint16_t *sorted = reinterpret_cast<uint16_t *>(S.ws + kSortOff);
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6, n = S.n;
     constexpr uint32_t NT = 64 * kK1Waves;
+    constexpr uint32_t kHashShiftW = kK1Waves == 8 ? 12 : kK1Waves == 4 ? 13 : 14;   // wave w: hash >> shift == w
+    static_assert(kK1Waves == 2 || kK1Waves == 4 || kK1Waves == 8, "hash space split in powers of two");
     const uint32_t np = n >= 3 ? n - 2 : 0;   // positions 0..n-3 are inserted
     for (uint32_t i = tid; i < (1u << 14); i += NT) sm.cnt[i] = 0;
     auto stage = [&](uint32_t c0) {
@@ -242,6 +253,9 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
             const uint32_t p = c0 + j;
             sm.stage[j] = p < n ? S.src[p] : 0u;
         }
+        __syncthreads();
+        for (uint32_t j = tid; j < (uint32_t)kK1Stage; j += NT)
+            sm.hsh[j] = (uint16_t)hash3(sm.stage[j], sm.stage[j + 1], sm.stage[j + 2]);
         __syncthreads();
     };
     uint64_t sb = 0, swb = 0;
@@ -253,13 +267,13 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
             sb += b;
             swb += (uint64_t)(p < n ? n - p : 0u) * b;
             if (p < np) {
-                const uint32_t h = hash3(b, sm.stage[j + 1], sm.stage[j + 2]);
+                const uint32_t h = sm.hsh[j];
                 atomicAdd(&sm.cnt[h >> 1], 1u << ((h & 1) * 16));
             }
         }
     }
     __syncthreads();
-    // exclusive scan: wave w's quarter (4096 words, 64 per lane), from the lower quarters' total
+    // exclusive scan: wave w's part of the hash space (kQW words, kLW per lane), from the lower parts' total
     constexpr uint32_t kQW = (1u << 14) / kK1Waves, kLW = kQW / 64;
     uint32_t *qc = sm.cnt + w * kQW + lane * kLW;
     uint32_t tsum = 0;
@@ -278,8 +292,8 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
         qc[i] = run | ((run + c0) << 16);
         run += c0 + c1;
     }
-    // ordered scatter of this wave's quarter
-    uint32_t distinct = 0;   // over the 64-position groups: their distinct hashes in this quarter
+    // ordered scatter of this wave's part
+    uint32_t distinct = 0;   // over the 64-position groups: their distinct hashes in this part
     const uint64_t lt = (1ull << lane) - 1;
     for (uint32_t c0 = 0; c0 < np; c0 += kK1Stage) {
         stage(c0);
@@ -290,8 +304,8 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint32_t j = g + 64 * q + lane;
-                h[q] = hash3(sm.stage[j], sm.stage[j + 1], sm.stage[j + 2]);
-                v[q] = c0 + j < np && j < (uint32_t)kK1Stage && (h[q] >> 13) == w;
+                h[q] = sm.hsh[j];
+                v[q] = c0 + j < np && (h[q] >> kHashShiftW) == w;
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -556,7 +570,10 @@ __global__ __launch_bounds__(kK2bThreads) void zlib_chain_kernel(const uint8_t *
     const uint32_t slide_at = n == (uint32_t)MAX_STRIP ? WSIZE + MAX_DIST + 1 : WSIZE + MAX_DIST;
     const uint32_t cfull = (uint32_t)cfg.chain, cred = (uint32_t)cfg.chain >> 2;
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-    for (uint32_t i = wave; i < cnt; i += kK2bThreads / 64) {
+    // the strip's list is split over gridDim.y workgroups (each with its own copy of
+    // the strip in LDS): a round has few such strips, one workgroup each left most CUs idle
+    constexpr uint32_t kWaves = kK2bThreads / 64;
+    for (uint32_t i = blockIdx.y * kWaves + wave; i < cnt; i += kWaves * gridDim.y) {
         const uint32_t p = list[i];
         const uint32_t ip = idx[p];
         const uint32_t hp = ((uint32_t)win[p] << 10 ^ (uint32_t)win[p + 1] << 5 ^ win[p + 2]) & 0x7fffu;
@@ -1498,7 +1515,7 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
                            frame_bytes, strip_bytes, (int32_t)spf, level, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_match_kernel launch");
         if (rc == VCF_OK) {
-            hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt), dim3(kK2bThreads), 0, side, in_dev, frame_bytes,
+            hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt, kK2bSplit), dim3(kK2bThreads), 0, side, in_dev, frame_bytes,
                                strip_bytes, (int32_t)spf, level, ws, s0);
             rc = hip_check(hipGetLastError(), "zlib_chain_kernel launch");
         }
