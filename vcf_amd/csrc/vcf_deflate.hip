@@ -72,13 +72,22 @@ constexpr int64_t kWsPerStrip = kSumOff + 32;
 // workspace slot, measured slower -- 517 vs 453 ms for C4 -- and produced a
 // wrong strip now and then on MI355X)
 constexpr int64_t kWsBudget = 3900000000LL;
+#ifndef VCF_ZX_SLOTS   // A/B (diagnostic builds): workspace slots (rounds in flight)
+#define VCF_ZX_SLOTS 1
+#endif
+// A call's strips in rounds: `slots` workspace slots of `per` strips each (within
+// the budget together); round r uses slot r % slots, so with two slots one round's
+// K1 and head kernel run while the other's parse finishes (the tails overlap).
 struct ZRounds {
-    int64_t rounds, per;
+    int64_t rounds, per, slots;
     explicit ZRounds(int64_t total)
     {
-        const int64_t round_max = std::max<int64_t>(1, kWsBudget / kWsPerStrip);
-        rounds = std::max<int64_t>(1, (total + round_max - 1) / round_max);
-        per = (total + rounds - 1) / rounds;
+        const int64_t one = std::max<int64_t>(1, kWsBudget / kWsPerStrip);
+        slots = total > 1024 ? VCF_ZX_SLOTS : 1;   // a few strips: one round on the caller's stream
+        const int64_t round_max = std::max<int64_t>(1, one / slots);
+        rounds = std::max<int64_t>(slots, (total + round_max - 1) / round_max);
+        per = std::max<int64_t>(1, (total + rounds - 1) / rounds);
+        if (rounds < slots) slots = rounds;
     }
 };
 constexpr int kK2bThreads = 1024;    // K2b: 16 waves per strip, one listed position per wave at a time
@@ -1440,7 +1449,8 @@ int vcf_zlib_prof_read(unsigned long long *host16, int reset)
 int64_t vcf_zlib_workspace(int64_t n_strips)
 {
     if (n_strips < 0) return -1;
-    return ZRounds(n_strips).per * kWsPerStrip;
+    const ZRounds zr(n_strips);
+    return zr.slots * zr.per * kWsPerStrip;
 }
 
 int64_t vcf_zlib_strip_count(int64_t frame_bytes, int32_t strip_bytes)
@@ -1473,73 +1483,93 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     const int chunks = (int)((std::min<int64_t>(strip_bytes, frame_bytes) + kChunk - 1) / kChunk);
     const unsigned hd_blocks = (unsigned)((std::min<int64_t>(strip_bytes, frame_bytes) + kHdThreads * kHdPer - 1) /
                                           (kHdThreads * kHdPer));
-    // A round: K1 and the head table on the caller's stream; then the two kinds of
-    // strips side by side -- the lazy parse of the repetitive strips on the caller's
-    // stream, K2a/K2b and the register-window parse of the others on a library
-    // stream (forked by an event, joined before the next round reuses the
-    // workspace).  The two sides touch disjoint strips: their own output slots,
+    // A round: K1 and the head table on the slot's main stream; then the two kinds
+    // of strips side by side -- the lazy parse of the repetitive strips on the main
+    // stream, K2a/K2b and the register-window parse of the others on the slot's side
+    // stream (forked by an event, joined back before the slot's next round reuses
+    // its workspace).  The two sides touch disjoint strips: their own output slots,
     // sizes and workspace regions; both only read K1's and the head kernel's tables.
+    // Slot 0's main stream is the caller's; slot 1's is a library stream forked from
+    // it at the start and joined back at the end, so the call keeps stream semantics.
     AuxStreams &ax = aux_for_current_device();
     std::lock_guard<std::mutex> lock(ax.mu);
     int rc = ax.init();
     if (rc != VCF_OK) return rc;
-    // the side stream at the highest priority: its strips are fewer but each takes
-    // longer (K2b walks every listed position's chain), and as a normal-priority
-    // queue its workgroups only got a CU when the lazy parse left one
-    static hipStream_t side_hi[64] = {};
+    // the side streams at the highest priority: their strips are fewer but each takes
+    // longer (K2b walks every listed position's chain), and as normal-priority queues
+    // their workgroups only got a CU when a lazy parse left one
+    static hipStream_t side_hi[64][2] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (!side_hi[dev] && !VCF_ZX_NOPRIO) {
-        int least = 0, greatest = 0;
-        rc = hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-        if (rc == VCF_OK)
-            rc = hip_check(hipStreamCreateWithPriority(&side_hi[dev], hipStreamNonBlocking, greatest),
-                           "hipStreamCreateWithPriority");
-        if (rc != VCF_OK) return rc;
+    for (int j = 0; j < 2 && !VCF_ZX_NOPRIO; ++j)
+        if (!side_hi[dev][j]) {
+            int least = 0, greatest = 0;
+            rc = hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+            if (rc == VCF_OK)
+                rc = hip_check(hipStreamCreateWithPriority(&side_hi[dev][j], hipStreamNonBlocking, greatest),
+                               "hipStreamCreateWithPriority");
+            if (rc != VCF_OK) return rc;
+        }
+    const ZRounds zr(total);
+    const int nslots = VCF_ZX_SERIAL ? 1 : (int)zr.slots;
+    hipStream_t main_s[2] = {st, ax.s[1]}, side_s[2];
+    for (int j = 0; j < 2; ++j) side_s[j] = VCF_ZX_SERIAL ? st : VCF_ZX_NOPRIO ? ax.s[2 + j] : side_hi[dev][j];
+    hipEvent_t fork_ev[2] = {ax.big[0], ax.big[1]}, join_ev[2] = {ax.join[0], ax.join[1]};
+    if (nslots > 1) {
+        if ((rc = hip_check(hipEventRecord(ax.fork, st), "hipEventRecord")) != VCF_OK) return rc;
+        if ((rc = hip_check(hipStreamWaitEvent(main_s[1], ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
     }
-    hipStream_t side = VCF_ZX_SERIAL ? st : VCF_ZX_NOPRIO ? ax.s[0] : side_hi[dev];
-    auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws) -> int {
-        hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64 * kK1Waves), 0, st, in_dev, frame_bytes, strip_bytes,
+    auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws, int j) -> int {
+        hipStream_t ms = main_s[j], ss = side_s[j];
+        hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64 * kK1Waves), 0, ms, in_dev, frame_bytes, strip_bytes,
                            (int32_t)spf, ws, s0);
         int rc = hip_check(hipGetLastError(), "zlib_order_kernel launch");
         if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_head_kernel, dim3(hd_blocks, cnt), dim3(kHdThreads), 0, st, in_dev, frame_bytes,
+        hipLaunchKernelGGL(zlib_head_kernel, dim3(hd_blocks, cnt), dim3(kHdThreads), 0, ms, in_dev, frame_bytes,
                            strip_bytes, (int32_t)spf, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_head_kernel launch");
         if (rc != VCF_OK) return rc;
-        if (side != st) {
-            if ((rc = hip_check(hipEventRecord(ax.fork, st), "hipEventRecord")) != VCF_OK) return rc;
-            if ((rc = hip_check(hipStreamWaitEvent(side, ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
+        if (ss != ms) {
+            if ((rc = hip_check(hipEventRecord(fork_ev[j], ms), "hipEventRecord")) != VCF_OK) return rc;
+            if ((rc = hip_check(hipStreamWaitEvent(ss, fork_ev[j], 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
         }
-        hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, side, in_dev,
+        hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, ss, in_dev,
                            frame_bytes, strip_bytes, (int32_t)spf, level, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_match_kernel launch");
         if (rc == VCF_OK) {
-            hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt, kK2bSplit), dim3(kK2bThreads), 0, side, in_dev, frame_bytes,
+            hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt, kK2bSplit), dim3(kK2bThreads), 0, ss, in_dev, frame_bytes,
                                strip_bytes, (int32_t)spf, level, ws, s0);
             rc = hip_check(hipGetLastError(), "zlib_chain_kernel launch");
         }
         if (rc == VCF_OK) {
-            hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3(cnt), dim3(64), 0, side, in_dev, frame_bytes,
+            hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3(cnt), dim3(64), 0, ss, in_dev, frame_bytes,
                                strip_bytes, (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
             rc = hip_check(hipGetLastError(), "zlib_parse_kernel launch");
         }
         if (rc == VCF_OK) {
-            hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3(cnt), dim3(64), 0, st, in_dev, frame_bytes, strip_bytes,
+            hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3(cnt), dim3(64), 0, ms, in_dev, frame_bytes, strip_bytes,
                                (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
             rc = hip_check(hipGetLastError(), "zlib_parse_kernel (lazy) launch");
         }
-        // join the side stream even after an error, so the caller's stream never runs ahead
-        if (side != st) {
-            int r2 = hip_check(hipEventRecord(ax.join[0], side), "hipEventRecord");
-            if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(st, ax.join[0], 0), "hipStreamWaitEvent");
+        // join the side stream even after an error, so the main stream never runs ahead
+        if (ss != ms) {
+            int r2 = hip_check(hipEventRecord(join_ev[j], ss), "hipEventRecord");
+            if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(ms, join_ev[j], 0), "hipStreamWaitEvent");
             if (rc == VCF_OK) rc = r2;
         }
         return rc;
     };
-    const ZRounds zr(total);
-    for (int64_t s0 = 0; s0 < total && rc == VCF_OK; s0 += zr.per)
-        rc = round(s0, (unsigned)std::min<int64_t>(zr.per, total - s0), (uint8_t *)ws_dev);
+    int r = 0;
+    for (int64_t s0 = 0; s0 < total && rc == VCF_OK; s0 += zr.per, ++r) {
+        const int j = r % nslots;
+        rc = round(s0, (unsigned)std::min<int64_t>(zr.per, total - s0),
+                   (uint8_t *)ws_dev + (int64_t)j * zr.per * kWsPerStrip, j);
+    }
+    if (nslots > 1) {   // slot 1's stream joins the caller's, also after an error
+        int r2 = hip_check(hipEventRecord(ax.join[2], main_s[1]), "hipEventRecord");
+        if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(st, ax.join[2], 0), "hipStreamWaitEvent");
+        if (rc == VCF_OK) rc = r2;
+    }
     return rc;
 }
 
