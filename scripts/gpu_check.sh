@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session: parity tests, smoke, bench, rocprofv3 kernel stats.
 # Stops at the first fault/abort/timeout (exit codes other than 0/1 from pytest).
-set -u
+set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
@@ -26,5 +26,5 @@ if [ "${NO_PROF:-0}" != "1" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
       -- python3 "$ROOT/bench.py" --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/prof_bench.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -2 "$OUT/prof_bench.log"
-  find "$OUT/prof" -name "*stats*" | head
+  ls "$OUT/prof"
 fi

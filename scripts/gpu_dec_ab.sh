@@ -1,4 +1,4 @@
-set -u
+set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_dct_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "decode_variants" > gpurun_out/dec_t.log 2>&1; rc=$?; echo "decode tests rc=$rc"; tail -3 gpurun_out/dec_t.log; [ $rc -eq 0 ] || exit $rc
 DECODE=1 DENSE=1 timeout -k 10 200 python -u scripts/bench_variants.py 0,8,9,10,11,12,13 > gpurun_out/dec_ab_dense.log 2>&1 || exit $?

@@ -1,6 +1,6 @@
 #!/bin/bash
 # 2D-DWT frame pipeline: DWT GPU tests, then ABBA encode/decode A/B of the stream counts.
-set -u
+set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$(pwd)/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -m gpu -x -q --timeout 120 --timeout-method thread tests/test_dwt_gpu.py > "$OUT/pytest_dwt.log" 2>&1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Strip-kernel DWT: parity vs oracle, A/B against the fused kernels, f64 issue rate.
-set -u
+set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 60 ./scripts/micro/f64_rate > "$OUT/f64_rate.log" 2>&1; echo "f64 rc=$?"; cat "$OUT/f64_rate.log"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU deflate: parity tests, the throughput comparison, and rocprofv3 kernel
 # stats of the C4 workload (256 x 1080p shifted frames), each step bounded.
-set -u
+set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
 TAG=${TAG:-z}

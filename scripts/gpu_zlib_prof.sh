@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel stats of the GPU deflate bench (per-kernel times of K1/K2/K3)
-set -u
+set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
 cd /tmp

@@ -17,14 +17,20 @@ flat = np.ascontiguousarray(frames.reshape(n, -1))
 fb = flat.shape[1]; _, _, sb = strip_layout(frames.shape[1:], 1)
 spf = int(L.lib().vcf_zlib_strip_count(fb, sb)); total = spf * n; slot = int(L.lib().vcf_zlib_bound(sb))
 d = DeviceBuffer.from_array(flat); out = DeviceBuffer(total * slot); sizes = DeviceBuffer(total * 4)
-ws = DeviceBuffer(int(L.lib().vcf_zlib_workspace(total))); st = Stream()
+so = os.environ.get("ZLIB_SO")
+if so:   # the workspace as the library under test sizes it
+    P = ctypes.CDLL(os.path.join(ROOT, "scripts", so))
+    P.vcf_zlib_workspace.restype = ctypes.c_int64
+    P.vcf_zlib_workspace.argtypes = [ctypes.c_int64]
+    ws = DeviceBuffer(int(P.vcf_zlib_workspace(total)))
+else:
+    ws = DeviceBuffer(int(L.lib().vcf_zlib_workspace(total)))
+st = Stream()
 if "ZFILL" in os.environ:   # the workspace's contents before the call (uninitialised-read probe)
     ws.fill(int(os.environ["ZFILL"]), st)
     st.synchronize()
-so = os.environ.get("ZLIB_SO")
 from vcf_amd.device import Event
 if so:
-    P = ctypes.CDLL(os.path.join(ROOT, "scripts", so))
     P.vcf_zlib_strips.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     for rep in range(2):   # the second call timed

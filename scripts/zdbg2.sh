@@ -1,4 +1,4 @@
-set -u
+set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_deflate_gpu.py tests/test_inflate_gpu.py -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/zt.log 2>&1; rc=$?; echo "deflate tests rc=$rc"; tail -3 gpurun_out/zt.log; [ $rc -eq 0 ] || exit $rc
 for L in "" ""; do

@@ -1,4 +1,4 @@
-set -u
+set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 for L in libvcf_zprof.so libvcf_zprof_noprio.so libvcf_zprof_serial.so libvcf_zprof.so libvcf_zprof_noprio.so libvcf_zprof_serial.so; do
   ZPROF_LIB=$L timeout -k 10 200 python -u scripts/zprof_run.py 256 || exit $?

@@ -1,4 +1,4 @@
-set -u
+set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 for r in 1 2; do
   ZLIB_SO=libvcf_zvar_wcheck.so timeout -k 10 300 python -u scripts/zdbg.py 256 gpurun_out/zw_$r.npz 2>&1 | grep -v "^  strip" | cut -c1-200 || exit $?
