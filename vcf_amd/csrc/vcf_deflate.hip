@@ -127,6 +127,9 @@ __device__ unsigned int g_zdbg[8];
 #ifndef VCF_ZX_LDSZERO
 #define VCF_ZX_LDSZERO 0
 #endif
+#ifndef VCF_ZX_EARLY0   // A/B (diagnostic builds): round 0's candidate reads before the head compare
+#define VCF_ZX_EARLY0 1
+#endif
 #ifndef VCF_ZX_SERIAL   // A/B (diagnostic builds): every kernel of a round on the caller's stream
 #define VCF_ZX_SERIAL 0
 #endif
@@ -1116,6 +1119,33 @@ struct Wave {
             } else {
                 fetch_cands(ip, pre0, pre1);
             }
+            // a chain round's LDS reads that do not depend on the head's length: the
+            // candidate's first four bytes (its hash) and the first 16 bytes of the
+            // compare, on every lane (a lane off the chain reads p's own bytes)
+            struct RoundRd {
+                uint32_t c, wc, c4, x16[4];
+                bool v;
+            };
+            auto rd = [&](uint32_t b) -> RoundRd {
+                RoundRd r;
+                const uint32_t gk = b + lane_id();
+                r.v = gk < chain && gk < ip;
+                r.c = !r.v ? 0u : b == 0 ? pre0 : b == 64 ? pre1 : wload16(sorted + ip - 1 - gk);
+                // sorted[] runs on past the bucket: a candidate of another bucket can be any
+                // position, also one outside the window (round 3 held the whole strip in LDS),
+                // so the bucket end must not be judged from window bytes there.  p's own
+                // bucket holds only earlier positions, and those past `limit` are in the
+                // window: c < p first, then the hash from the window.
+                r.v = r.v && r.c < p && (gk == 0 || r.c > limit);
+                r.wc = r.v ? r.c - wbase : wp;
+                r.c4 = ld4(r.wc);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) r.x16[u] = ld4(r.wc + 4 * u) ^ ld4(wp + 4 * u);
+                return r;
+            };
+            // round 0's reads issued with the head compare's (VCF_ZX_EARLY0; 0: in the round)
+            RoundRd r0;
+            if (VCF_ZX_EARLY0) r0 = rd(0);
             const uint32_t hp = hash_at(wp);
             const uint32_t l1 = wave_lcp(hdp - wbase, wp);
 #if VCF_ZLIB_PROF
@@ -1142,23 +1172,12 @@ struct Wave {
                 const unsigned long long tr0 = clock64();
 #endif
                 const uint32_t gk = b + lane_id();
-                bool v = gk < chain && gk < ip;
-                const uint32_t c = !v ? 0u : b == 0 ? pre0 : b == 64 ? pre1 : wload16(sorted + ip - 1 - gk);
-                // sorted[] runs on past the bucket: a candidate of another bucket can be any
-                // position, also one outside the window (round 3 held the whole strip in LDS),
-                // so the bucket end must not be judged from window bytes there.  p's own
-                // bucket holds only earlier positions, and those past `limit` are in the
-                // window: c < p first, then the hash from the window.
-                v = v && c < p && (gk == 0 || c > limit);
-                // every LDS read of the round issued at once, on every lane (a lane off
-                // the chain reads p's own bytes): the candidate's first four bytes (its
-                // hash), the scan_end bytes, and the first 16 bytes of the compare
-                const uint32_t wc = v ? c - wbase : wp;
-                const uint32_t c4 = ld4(wc);
+                const RoundRd rr = VCF_ZX_EARLY0 && b == 0 ? r0 : rd(b);
+                bool v = rr.v;
+                const uint32_t c = rr.c, wc = rr.wc, c4 = rr.c4;
+                const uint32_t *x16 = rr.x16;
+                // zlib's scan_end bytes at F (known only after the head compare)
                 const bool se = lwin[wc + F] == lwin[wp + F] && lwin[wc + F - 1] == lwin[wp + F - 1];
-                uint32_t x16[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) x16[u] = ld4(wc + 4 * u) ^ ld4(wp + 4 * u);
 #if VCF_ZX_WINCHECK
                 {
                     const uint32_t want = v ? win_src(c) | win_src(c + 1) << 8 | win_src(c + 2) << 16 | win_src(c + 3) << 24 : c4;
