@@ -83,6 +83,34 @@ def main():
             comp = list(ex.map(lambda c: zlib.compress(c, 6), strips))
             host_s = time.perf_counter() - t
         gms = float(np.median(ms))
+        # the decode side: the GPU's own streams inflated on the GPU (vcf_inflate_strips),
+        # straight from their slots into a frame buffer, against zlib.decompress on the pool
+        k_of = np.arange(total) % spf
+        out_len = np.minimum(sb, fb - k_of * sb).astype(np.int32)
+        out_off = ((np.arange(total) // spf) * fb + k_of * sb).astype(np.int64)
+        comp_off = (np.arange(total, dtype=np.int64) * slot)
+        dco, dcl = DeviceBuffer.from_array(comp_off), DeviceBuffer.from_array(sz.astype(np.int32))
+        doo, dol = DeviceBuffer.from_array(out_off), DeviceBuffer.from_array(out_len)
+        dst, dimg = DeviceBuffer(4 * total), DeviceBuffer(flat.nbytes)
+        ims = []
+        for r in range(args.reps + 1):
+            e0.record(st)
+            L.call("vcf_inflate_strips", out.ptr, dco.ptr, dcl.ptr, total, dimg.ptr, doo.ptr, dol.ptr, dst.ptr,
+                   st.handle)
+            e1.record(st)
+            st.synchronize()
+            if r:
+                ims.append(e0.elapsed_ms(e1))
+        status = dst.download(np.empty(total, np.int32))
+        inflate_ok = bool((status == 0).all() and np.array_equal(dimg.download(np.empty_like(flat)), flat))
+        comp_strips = [slots[s * slot:s * slot + sz[s]].tobytes() for s in range(total)]
+        with ThreadPoolExecutor(args.threads) as ex:
+            t = time.perf_counter()
+            list(ex.map(zlib.decompress, comp_strips))
+            host_inf_s = time.perf_counter() - t
+        ims_med = float(np.median(ims))
+        for b in (dco, dcl, doo, dol, dst, dimg):
+            b.free()
         print(json.dumps({"workload": f"{name}: {n} frames, {total} strips of {sb} B, zlib level 6",
                           "gpu_ms": round(gms, 3), "gpu_GBps": round(flat.nbytes / gms / 1e6, 2),
                           "host_ms": round(host_s * 1e3, 2), "host_threads": args.threads,
@@ -90,7 +118,10 @@ def main():
                           "speedup": round(host_s * 1e3 / gms, 2),
                           "ratio": round(flat.nbytes / max(1, int(sz.sum())), 2),
                           "bytes_equal_zlib": bool(ok and sum(map(len, comp)) == int(sz.sum())),
-                          "strips_checked": len(chk)}), flush=True)
+                          "strips_checked": len(chk),
+                          "inflate_gpu_ms": round(ims_med, 3), "inflate_gpu_GBps": round(flat.nbytes / ims_med / 1e6, 2),
+                          "inflate_host_ms": round(host_inf_s * 1e3, 2),
+                          "inflate_equal_input": inflate_ok}), flush=True)
         for b in (d, out, sizes, ws):
             b.free()
 
