@@ -1,0 +1,21 @@
+#!/bin/bash
+# SQ counters of the GPU deflate's kernels (C4 content, 64 frames): two --pmc passes
+set -u -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd); OUT=$ROOT/gpurun_out/pmc_zlib; mkdir -p "$OUT"; export TMPDIR=/tmp; cd /tmp
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES" \
+           "SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o pmc \
+      -- python3 "$ROOT/scripts/zdbg.py" 64 "$OUT/zd_$i.npz" > "$OUT/p$i.log" 2>&1
+  rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+python3 "$ROOT/scripts/pmc_summary.py" "$OUT" > "$OUT/summary.json"
+python3 - "$OUT/summary.json" <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1]))
+for k, v in d.items():
+    if "zlib" in k:
+        print(k, {c: round(x) for c, x in v.items() if not c.startswith("_")})
+PY
