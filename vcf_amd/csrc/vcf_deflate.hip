@@ -1343,11 +1343,17 @@ struct ParseShared {
     ParseSmem sm;
 };
 template <>
+#ifndef VCF_ZX_LDSPAD   // (diagnostic) extra LDS per lazy-parse workgroup: fewer strips per CU
+#define VCF_ZX_LDSPAD 0
+#endif
 struct ParseShared<true> {
     ParseSmem sm;
     uint32_t win32[kLazyWin / 4];   // the sliding window of the strip (Wave::ensure)
+#if VCF_ZX_LDSPAD
+    uint32_t pad[VCF_ZX_LDSPAD / 4];
+#endif
 };
-static_assert(sizeof(ParseShared<true>) <= 40960, "four lazy-parse workgroups per CU");
+static_assert(VCF_ZX_LDSPAD || sizeof(ParseShared<true>) <= 40960, "four lazy-parse workgroups per CU");
 
 template <bool LAZY>
 __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
