@@ -425,16 +425,10 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
     for (int C = 0; C < 3; ++C) {
         // :399-411 astype(int16) - 128, Q*k in int16 (A5); -p de-weighting (:421-435)
         double col[8];
-        // AC index bytes of the column: all 128 (coefficient 0) iff their OR
-        // and their AND are both 128 (the lane x = 0 skips its DC byte)
-        uint32_t acor = 0, acand = 0xFFu;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int kb = SUB ? sm.stage[cols_stage_off<TB, SUB>(i * 8 + x) + lb * 3 + C]
                                : sm.stage[cols_stage_off<TB, SUB>(i) + lb * 24 + x * 3 + C];
-            const uint32_t ac = (i == 0 && x == 0) ? 128u : (uint32_t)kb;
-            acor |= ac;
-            acand &= ac;
             if constexpr (DQ == 1 && !PERC) {
                 col[i] = sm.lut[kb];
                 continue;
@@ -452,8 +446,18 @@ __global__ __launch_bounds__(TB * 8) void dct_dz_decode_cols(const uint8_t *__re
         // not known zeros (vcf_dct8.h; bit-identical int16 outputs).  The
         // branch is wave-uniform.  (64 x 4K S-smooth frames: 1.01 -> 0.756 ms;
         // uniform-random frames, no DC-only wave: 1.187 -> 1.262 ms, the AC
-        // test; profiles/r03_dct_decode_dc_ab.log)
-        if (__ballot(acor != 128u || acand != 128u) == 0) {
+        // test; profiles/r03_dct_decode_dc_ab.log.)  The test: the OR of the
+        // dequantized AC values' high words -- a double is +-0 iff its high
+        // word is 0 or 0x80000000, and every nonzero input here is >= 1/16 in
+        // magnitude, so a zero high word means a zero value; three v_or3 per
+        // column instead of byte compares (round 4, decode A/B variant 10:
+        // -1 % on both contents, profiles/r04_dct_decode_*_ab.log)
+        uint32_t hw = x == 0 ? 0u : (uint32_t)__double2hiint(col[0]);
+        hw = hw | (uint32_t)__double2hiint(col[1]) | (uint32_t)__double2hiint(col[2]);
+        hw = hw | (uint32_t)__double2hiint(col[3]) | (uint32_t)__double2hiint(col[4]);
+        hw = hw | (uint32_t)__double2hiint(col[5]) | (uint32_t)__double2hiint(col[6]);
+        hw |= (uint32_t)__double2hiint(col[7]);
+        if (__ballot((hw & 0x7FFFFFFFu) != 0u) == 0) {
             const int kb = sm.stage[cols_stage_off<TB, SUB>(0) + lb * (SUB ? 3 : 24) + C];
             double v;
             if constexpr (DQ == 1 && !PERC) {
