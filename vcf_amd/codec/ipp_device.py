@@ -10,8 +10,9 @@ comp + rec - 128 clipped (:559-561).  GOPs are independent, frames inside a
 GOP are serial.  Here a rank's GOPs (GOP g on rank floor(g*P/G),
 shard.frame_range over GOPs) advance in lock step: at step p every GOP's
 frame p is processed, the per-frame tools on each GOP's frame and the DCT +
-deadzone encode, the GPU TIFF deflate (vcf_zlib_strips, byte-exact with
-zlib) and the DCT decode as one batched launch each over the step's frames.
+deadzone encode and the DCT decode as one batched launch each over the step's
+frames; every frame's indices stay in HBM, and after the loop all their TIFF
+strips are deflated in one call (vcf_zlib_strips, byte-exact with zlib).
 Nothing but the strip sizes and the motion fields leaves the GPU until the
 end: then every frame's TIFF file (the host writer's prefix + the deflated
 strips) is packed on the device and gathered to rank 0 over RCCL
@@ -79,12 +80,12 @@ class DeviceIPP:
         self.comp = DeviceBuffer(ng * self.fb)
         self.res = DeviceBuffer(ng * self.fb)
         self.rec = DeviceBuffer(ng * self.fb)
-        self.k = DeviceBuffer(ng * self.kb)
+        self.k = DeviceBuffer(max(1, self.n_local) * self.kb)   # every frame's indices, in deflate order
         self.mv = DeviceBuffer(max(1, ng * self.hb * self.wb * 8))
         self.gray = DeviceBuffer(2 * self.H * self.W)
         self.out = DeviceBuffer(max(1, self.n_local * self.spf * self.slot))
         self.sizes = DeviceBuffer(max(4, self.n_local * self.spf * 4))
-        self.ws = DeviceBuffer(max(16, Z.workspace(ng * self.spf)))
+        self.ws = DeviceBuffer(max(16, Z.workspace(max(1, self.n_local) * self.spf)))
         self.exchange = Exchange(comm, self.rank, self.world, self.N, ranges, self.stream)
 
     def _frames_of_step(self, p: int):
@@ -132,13 +133,10 @@ class DeviceIPP:
                     call("vcf_memcpy_dtoh", m.ctypes.data_as(ctypes.c_void_p), mv.ptr, m.nbytes, sh)
                 mv_of[f] = m
             n = len(gs)
-            D.encode_device(self.res, n, self.H, self.W, self.Q, 0, out=self.k, stream=self.stream)
-            # the step's files: strips of frames [len(order), len(order) + n) of the deflate order
-            base = len(order)
-            call("vcf_zlib_strips", self.k.ptr, n, kb, self.strip_bytes, Z.LEVEL,
-                 self.out.address(base * self.spf * self.slot), self.slot,
-                 self.sizes.address(base * self.spf * 4), self.ws.ptr, sh)
-            D.decode_device(self.k, n, self.H, self.W, self.Q, 0, out=self.rec, stream=self.stream)
+            # the step's indices stay in HBM at their deflate positions [len(order), len(order) + n)
+            kstep = _At(self.k, len(order) * kb, n * kb)
+            D.encode_device(self.res, n, self.H, self.W, self.Q, 0, out=kstep, stream=self.stream)
+            D.decode_device(kstep, n, self.H, self.W, self.Q, 0, out=self.rec, stream=self.stream)
             for j, g in enumerate(gs):
                 rec = self.rec.address(j * fb)
                 if p == 0:
@@ -146,6 +144,11 @@ class DeviceIPP:
                 else:
                     call("vcf_ipp_reconstruct", self.comp.address(g * fb), rec, fb, self.ref.address(g * fb), sh)
                 order.append((self.g_lo + g) * self.gop + p - self.lo)
+        # every frame's TIFF strips in one call (one set of rounds instead of one partial
+        # round per step: 10 calls of ~3 000 strips left the GPU half idle in each tail)
+        if self.n_local:
+            call("vcf_zlib_strips", self.k.ptr, self.n_local, kb, self.strip_bytes, Z.LEVEL, self.out.ptr, self.slot,
+                 self.sizes.ptr, self.ws.ptr, sh)
         t = mark("gop_loop", t)
         # every frame's TIFF prefix from the strip sizes, the strips in frame order
         sz = np.empty(max(1, self.n_local * self.spf), np.int32)
