@@ -424,7 +424,10 @@ int64_t vcf_png_encode_bound(int32_t H, int32_t W);
  * strip_bytes <= 65536 (tifffile's strips for rows up to 64 KB);
  * slot_bytes a multiple of 4 >= vcf_zlib_bound(strip_bytes); ws_dev holds
  * vcf_zlib_workspace(total strips) bytes (16-byte aligned; out_dev and
- * sizes_dev 4-byte aligned). */
+ * sizes_dev 4-byte aligned) -- at most ~3.9 GB whatever the batch: the strips
+ * are coded in rounds that reuse it.  The call is asynchronous on `stream`;
+ * internally part of each round runs on library streams forked from and
+ * joined back to it, so the caller sees ordinary stream semantics. */
 int64_t vcf_zlib_bound(int64_t strip_bytes);
 int64_t vcf_zlib_workspace(int64_t n_strips);
 /* the largest strip_bytes vcf_zlib_strips takes (65536: frames with rows of
