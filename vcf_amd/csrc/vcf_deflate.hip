@@ -1368,6 +1368,10 @@ __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restric
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s);
     if (strip_lazy(S) != LAZY) return;   // the other kernel codes this strip
     const uint32_t lane = lane_id();
+#ifndef VCF_ZX_PARSEPRIO   // the lazy parse at wave priority 3: beside the side stream's K2b waves on a CU it wins issue (-0.7 %)
+#define VCF_ZX_PARSEPRIO 3
+#endif
+    if (LAZY && VCF_ZX_PARSEPRIO) __builtin_amdgcn_s_setprio(VCF_ZX_PARSEPRIO);
 #if VCF_ZX_LDSZERO   // (diagnostic) LDS cleared first: a read of never-written LDS becomes deterministic
     for (uint32_t i = lane; i < sizeof(sh) / 4; i += 64) reinterpret_cast<uint32_t *>(&sh)[i] = 0;
     wave_sync();
