@@ -3,7 +3,7 @@ checksum of its bytes, and list the strips that differ from zlib.  ZLIB_SO:
 a diagnostic build (scripts/libvcf_zprof_NAME.so) instead of the product library."""
 import ctypes, sys, os, zlib
 import numpy as np
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from bench import synth_frame, c4_frame
 from vcf_amd import _lib as L, dct
@@ -19,7 +19,7 @@ spf = int(L.lib().vcf_zlib_strip_count(fb, sb)); total = spf * n; slot = int(L.l
 d = DeviceBuffer.from_array(flat); out = DeviceBuffer(total * slot); sizes = DeviceBuffer(total * 4)
 so = os.environ.get("ZLIB_SO")
 if so:   # the workspace as the library under test sizes it
-    P = ctypes.CDLL(os.path.join(ROOT, "scripts", so))
+    P = ctypes.CDLL(os.path.join(ROOT, "scripts", "debug", so))
     P.vcf_zlib_workspace.restype = ctypes.c_int64
     P.vcf_zlib_workspace.argtypes = [ctypes.c_int64]
     ws = DeviceBuffer(int(P.vcf_zlib_workspace(total)))
@@ -55,7 +55,7 @@ np.savez(sys.argv[2], sz=sz, crc=crc)
 bad = [s for s in range(total) if o[s * slot:s * slot + sz[s]].tobytes() !=
        zlib.compress(flat[s // spf, (s % spf) * sb:(s % spf + 1) * sb].tobytes(), 6)]
 print(f"{sys.argv[2]} ({so or 'product'}): total {total}, bad {len(bad)}: {bad[:40]}", flush=True)
-sys.path.insert(0, os.path.join(ROOT, "scripts"))
+sys.path.insert(0, os.path.join(ROOT, "scripts", "debug"))
 from ztokens import first_divergence
 
 

@@ -3,13 +3,13 @@ scripts/libvcf_zprof.so, VCF_ZLIB_PROF): one vcf_zlib_strips call over the C4
 workload, then the counters.  Prints one JSON line."""
 import ctypes, json, os, sys
 import numpy as np
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from bench import synth_frame, c4_frame
 from vcf_amd import _lib as L, dct
 from vcf_amd.codec.tiff import strip_layout
 from vcf_amd.device import DeviceBuffer, Stream, Event
-P = ctypes.CDLL(os.path.join(ROOT, "scripts", os.environ.get("ZPROF_LIB", "libvcf_zprof.so")))
+P = ctypes.CDLL(os.path.join(ROOT, "scripts", "debug", os.environ.get("ZPROF_LIB", "libvcf_zprof.so")))
 P.vcf_zlib_strips.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                               ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 P.vcf_zlib_workspace.restype = ctypes.c_int64

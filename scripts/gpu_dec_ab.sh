@@ -7,7 +7,7 @@ DECODE=1 timeout -k 10 200 python -u scripts/bench_variants.py 0,8,9,10,11,12,13
 cat gpurun_out/dec_ab_smooth.log
 timeout -k 10 400 python -u -m pytest tests/test_deflate_gpu.py -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/zt.log 2>&1; rc=$?; echo "deflate tests rc=$rc"; tail -2 gpurun_out/zt.log; [ $rc -eq 0 ] || exit $rc
 for L in libvcf_zprof.so libvcf_zprof_nocap.so libvcf_zprof_serial.so libvcf_zprof.so libvcf_zprof_nocap.so libvcf_zprof_serial.so; do
-  ZPROF_LIB=$L timeout -k 10 200 python -u scripts/zprof_run.py 256 || exit $?
+  ZPROF_LIB=$L timeout -k 10 200 python -u scripts/debug/zprof_run.py 256 || exit $?
 done
 timeout -k 10 300 python -u scripts/bench_zlib.py --only dct_c4_1080p --frames 256 --reps 3 > gpurun_out/bz.jsonl 2>/dev/null || exit $?
 cut -c1-300 gpurun_out/bz.jsonl

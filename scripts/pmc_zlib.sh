@@ -8,7 +8,7 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_AC
            "SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o pmc \
-      -- python3 "$ROOT/scripts/zdbg.py" 64 "$OUT/zd_$i.npz" > "$OUT/p$i.log" 2>&1
+      -- python3 "$ROOT/scripts/debug/zdbg.py" 64 "$OUT/zd_$i.npz" > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python3 "$ROOT/scripts/pmc_summary.py" "$OUT" > "$OUT/summary.json"

@@ -91,3 +91,13 @@ def test_harness_equals_zlib_fuzz(dh):
             b = np.repeat(rng.integers(0, 256, n // 50 + 1, dtype=np.uint8), 50)[:n].tobytes()
         level = int(rng.choice([6, 6, 4, 5, 7, 8, 9]))
         assert dh(b, level) == zlib.compress(b, level), (it, n, level)
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_zlib_rejects_corrupt_code_lengths(case):
+    """The oracle side of tests/test_inflate_gpu.py::test_rejects_corrupt_code_lengths:
+    zlib.decompress rejects each hand-built stream with the named message."""
+    from deflate_corrupt import CASES
+    name, stream, msg, _ = CASES[case]
+    with pytest.raises(zlib.error, match=msg):
+        zlib.decompress(stream)

@@ -200,8 +200,11 @@ def test_device_iii_single_rank_rccl():
         want = codec.compress(k).getvalue()
         assert got[i] == want and sizes[i] == len(want), i
         assert np.array_equal(codec.decompress(bytes(got[i])), k), i
-    sizes2, got2 = job.run(rgb)                  # reusable: same bytes again
-    assert got2 == got and list(sizes2) == list(sizes)
+    # reusable: same bytes again.  run() returns memoryviews into one reused
+    # page-locked buffer (valid until the next run), so copy before re-running
+    first = [bytes(g) for g in got]
+    sizes2, got2 = job.run(rgb)
+    assert [bytes(g) for g in got2] == first and list(sizes2) == list(sizes)
     comm.close()
 
 

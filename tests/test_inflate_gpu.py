@@ -10,7 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _inflate(streams, lengths):
+def _inflate(streams, lengths, violations=None):
     from vcf_amd.device import DeviceBuffer, Stream
     from vcf_amd.zlib_gpu import StripInflater
     comp = np.frombuffer(b"".join(streams), np.uint8) if streams else np.zeros(0, np.uint8)
@@ -20,7 +20,7 @@ def _inflate(streams, lengths):
     out_off = np.concatenate([[0], np.cumsum(out_len)[:-1]]).astype(np.int64)
     out = DeviceBuffer(max(16, int(out_len.sum())))
     st = Stream()
-    StripInflater().inflate_into(comp, comp_off, comp_len, out, out_off, out_len, st)
+    StripInflater().inflate_into(comp, comp_off, comp_len, out, out_off, out_len, st, violations=violations)
     host = np.empty(int(out_len.sum()), np.uint8)
     if host.size:
         out.download(host)
@@ -104,3 +104,62 @@ def test_reference_tiff_strips():
             want.append(k[j * strip_bytes:(j + 1) * strip_bytes])
     got = _inflate(streams, [len(w) for w in want])
     assert got == want and len(got) > 20
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_rejects_corrupt_code_lengths(case):
+    """inflate_table's checks (zlib inftrees.c): over-subscribed and incomplete
+    code-length sets, and inflate's missing end-of-block code, each rejected
+    with its own status (tests/deflate_corrupt.py; zlib rejects the same
+    streams, tests/test_deflate.py::test_zlib_rejects_corrupt_code_lengths)."""
+    from deflate_corrupt import CASES
+    name, stream, _, status = CASES[case]
+    with pytest.raises(ValueError, match=rf"\(status {status}\)"):
+        _inflate([stream], [1000])
+
+
+def test_rejects_bad_strip_tables():
+    """A strip table that does not fit its buffers is refused on the host,
+    before the kernel runs (no out-of-bounds device reads or writes)."""
+    from vcf_amd.device import DeviceBuffer, Stream
+    from vcf_amd.zlib_gpu import StripInflater
+    b = _data("image", 3000, np.random.default_rng(2))
+    c = np.frombuffer(zlib.compress(b, 6), np.uint8)
+    out, st, inf = DeviceBuffer(4096), Stream(), StripInflater()
+    one = lambda v: np.array([v], np.int64)   # noqa: E731
+    for args in ((one(0), one(len(c)), one(0), one(-1)),        # negative output length
+                 (one(0), one(-5), one(0), one(3000)),           # negative compressed length
+                 (one(10), one(len(c)), one(0), one(3000)),      # strip past the compressed bytes
+                 (one(0), one(len(c)), one(2000), one(3000))):   # strip past the output buffer
+        with pytest.raises(ValueError):
+            inf.inflate_into(c, args[0], args[1], out, args[2], args[3], st)
+    inf.inflate_into(c, one(0), one(len(c)), out, one(1000), one(3000), st)   # the same strip, fitting
+    got = np.empty(3000, np.uint8)
+    out.download(got, offset=1000)
+    assert got.tobytes() == b
+
+
+def test_window_check_reports_no_violations():
+    """The window-check build (A/B library, vcf_inflate_strips_wincheck):
+    every back-reference and flush read of the 32 KiB output ring lies in its
+    valid span -- zero violations -- on streams with matches at every
+    distance up to 32 768 (zlib levels 1-9, all strategies, 64 KiB strips,
+    long-distance repeats), and the outputs equal the product kernel's."""
+    rng = np.random.default_rng(77)
+    raw, streams = [], []
+    for level in (1, 4, 6, 9):
+        for strategy in (zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_RLE, zlib.Z_FIXED):
+            for kind in ("random", "sparse", "text", "image"):
+                b = _data(kind, int(rng.integers(30000, 65537)), rng)
+                raw.append(b)
+                streams.append(_compress(b, level, strategy))
+    for d in (1, 2, 257, 4096, 32767, 32768):   # a block repeated at distance d, then again
+        blk = rng.integers(0, 256, d if d < 32768 else 32768, dtype=np.uint8).tobytes()
+        b = (blk * (65536 // len(blk) + 2))[:65536]
+        raw.append(b)
+        streams.append(zlib.compress(b, 9))
+    viol = np.full(len(streams), 0xFFFFFFFF, np.uint32)
+    got = _inflate(streams, [len(b) for b in raw], violations=viol)
+    assert got == raw
+    assert not viol.any(), np.nonzero(viol)[0]
+    assert got == _inflate(streams, [len(b) for b in raw])

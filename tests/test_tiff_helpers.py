@@ -60,3 +60,57 @@ def test_tiff_strips_of_reference_files():
         assert np.array_equal(imread_bytes(tif), k), fn
         n += 1
     assert n > 0
+
+
+def test_tiff_strips_rejects_inconsistent_tables():
+    """tiff_strips returns None (host reader) for a strip table the GPU inflate
+    could not trust: an extra strip, a strip past the end of the file, and
+    parses an IFD that lies beyond the first 64 KiB."""
+    import struct
+
+    import numpy as np
+
+    from vcf_amd.codec.tiff import imwrite_bytes, tiff_strips
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (300, 300, 3), dtype=np.uint8)
+    buf = imwrite_bytes(img)
+    shape, dt, offs, counts, sb = tiff_strips(buf)
+    assert shape == (300, 300, 3) and len(offs) == -(-img.nbytes // sb)
+
+    def patched(new_offs, new_counts):
+        # rebuild a minimal little-endian TIFF around the same strips with the given table
+        n = len(new_offs)
+        entries = [(256, 3, 1, 300), (257, 3, 1, 300), (258, 3, 1, 8), (259, 3, 1, 8), (262, 3, 1, 2),
+                   (277, 3, 1, 3), (278, 3, 1, sb // 900), (284, 3, 1, 1)]
+        data = bytearray(buf)
+        arr_off = len(data)
+        data += struct.pack("<%dI" % n, *new_offs)
+        cnt_off = len(data)
+        data += struct.pack("<%dI" % n, *new_counts)
+        ifd_off = len(data)
+        tags = sorted(entries + [(273, 4, n, arr_off if n > 1 else new_offs[0]),
+                                 (279, 4, n, cnt_off if n > 1 else new_counts[0])])
+        data += struct.pack("<H", len(tags))
+        for code, typ, count, val in tags:
+            data += struct.pack("<HHI", code, typ, count) + (struct.pack("<HH", val, 0) if typ == 3 and count == 1
+                                                              else struct.pack("<I", val))
+        data += struct.pack("<I", 0)
+        data[4:8] = struct.pack("<I", ifd_off)
+        return bytes(data)
+
+    # the same table, IFD written at the end (past 64 KiB): parsed, same strips
+    big = patched(offs, counts)
+    assert ifd_beyond_small(big)
+    got = tiff_strips(big)
+    assert got is not None and got[2] == offs and got[3] == counts
+    assert tiff_strips(patched(offs + [offs[-1]], counts + [counts[-1]])) is None   # an extra strip
+    assert tiff_strips(patched(offs[:-1], counts[:-1])) is None                     # a missing strip
+    bad = list(counts)
+    bad[-1] = len(big) + 10
+    assert tiff_strips(patched(offs, bad)) is None                                  # past the end of the file
+    assert tiff_strips(b"II*\x00\xff\xff\x00\x00") is None                          # IFD offset out of range
+
+
+def ifd_beyond_small(b):
+    import struct
+    return struct.unpack("<I", b[4:8])[0] >= 65536

@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libvcf_amd.so")
 AB_LIB = os.path.join(PKG, "libvcf_amd_ab.so")
 # the A/B archive's own sources, linked with these product objects
-AB_SOURCES = ["ab/vcf_dct_dz_ab.hip", "ab/vcf_dwt_ab.hip"]
+AB_SOURCES = ["ab/vcf_dct_dz_ab.hip", "ab/vcf_dwt_ab.hip", "ab/vcf_inflate_wincheck.hip"]
 AB_LINK = ["vcf_runtime.hip", "vcf_dct_any.hip"]
 SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_dct_any.hip", "vcf_quant.hip", "vcf_dwt.hip", "vcf_cbaac.cpp",
            "vcf_cbahc.cpp", "vcf_ipp.hip", "vcf_ipp_rdo.hip",

@@ -179,6 +179,7 @@ AB_SIGNATURES = {
     "vcf_dct_dz_decode_variant": [ctypes.c_int, _P, _I64, _I32, _I32, _I32, _I32, _U32, _P, _P],
     "vcf_dwt_dz_encode_variant": [_I32, _P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
     "vcf_dwt_dz_decode_variant": [_I32, _P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
+    "vcf_inflate_strips_wincheck": [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
 }
 
 _lib = None

@@ -204,21 +204,42 @@ def tiff_strips(buf: bytes):
     """The strip table of a deflate-compressed, chunky, little-endian u8/u16
     TIFF (what tifffile writes for TIFF.py:29): (shape, dtype, strip offsets,
     strip byte counts, uncompressed bytes per full strip), or None for any
-    other TIFF (imread_bytes reads those on the host)."""
-    bo, t = _read_ifd(bytes(buf[:65536]) if len(buf) > 65536 else bytes(buf))
+    other TIFF (imread_bytes reads those on the host) -- including one whose
+    strip table does not describe the image: a strip count other than
+    ceil(frame bytes / strip bytes), or a strip past the end of the file.
+    The GPU inflate trusts the table it is given, so only a consistent one
+    goes there; the host reader reports the others as zlib/tifffile would."""
+    try:
+        # the IFD of a tifffile-written file sits in the first 64 KiB; parse
+        # the whole buffer when it does not (other writers put it at the end)
+        try:
+            bo, t = _read_ifd(bytes(buf[:65536]) if len(buf) > 65536 else bytes(buf))
+        except (struct.error, ValueError, KeyError):
+            if len(buf) <= 65536:
+                raise
+            bo, t = _read_ifd(bytes(buf))
+    except (struct.error, ValueError, KeyError):
+        return None
     if bo != "<" or t.get(259, (1,))[0] not in (8, 32946) or t.get(284, (1,))[0] != 1:
         return None
-    if 273 not in t or 279 not in t:
+    if 273 not in t or 279 not in t or 256 not in t or 257 not in t:
         return None
     W, H = t[256][0], t[257][0]
     C = t.get(277, (1,))[0]
     bps = t.get(258, (8,))[0]
-    if bps not in (8, 16):
+    if bps not in (8, 16) or W <= 0 or H <= 0 or C <= 0:
         return None
     isz = bps // 8
     rps = t.get(278, (H,))[0]
     shape = (H, W, C) if C > 1 else (H, W)
-    return shape, np.dtype("<u%d" % isz), list(t[273]), list(t[279]), min(rps, H) * W * C * isz
+    strip_bytes = min(max(rps, 1), H) * W * C * isz
+    offs, counts = list(t[273]), list(t[279])
+    frame_bytes = H * W * C * isz
+    if len(offs) != len(counts) or len(offs) != -(-frame_bytes // strip_bytes):
+        return None
+    if any(o < 0 or c < 0 or o + c > len(buf) for o, c in zip(offs, counts)):
+        return None
+    return shape, np.dtype("<u%d" % isz), offs, counts, strip_bytes
 
 
 def imread_bytes(buf: bytes) -> np.ndarray:

@@ -20,7 +20,15 @@
 //   * the adler32 trailer is checked (sums over the flushed bytes, reduced at
 //     the end), and the output length against the strip's expected length.
 // status[s] = 0, or a negative code for a stream that is not what zlib would
-// accept (corrupt data, wrong length, adler mismatch).
+// accept (corrupt data, wrong length, adler mismatch, an over-subscribed or
+// incomplete code-length set as inflate_table rejects it, a dynamic block
+// without an end-of-block code, a negative strip length).
+//
+// Window-check diagnostic (VCF_INFLATE_WINCHECK_BUILD, compiled into the A/B
+// library as vcf_inflate_strips_wincheck): every back-reference read and
+// every flush read of the 32 KiB output ring is checked against the ring's
+// valid span -- the byte was written (q < p + i) and not yet overwritten
+// (p + i - q <= 32 KiB) -- and the violations are counted per strip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,6 +62,9 @@ enum : int32_t {
     kErrLength = -5,
     kErrAdler = -6,
     kErrInput = -7,
+    kErrTree = -8,   // over-subscribed / incomplete code lengths (zlib: "invalid code lengths set" etc.)
+    kErrEob = -9,    // dynamic block without a code for symbol 256 ("invalid code -- missing end-of-block")
+    kErrArgs = -10,  // negative compressed or output length
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -79,7 +90,15 @@ struct InflateSmem {
 struct Tree {
     uint32_t first, count, offs;   // this lane's length
     uint16_t *sorted;
+    bool ok;                       // inflate_table would accept the lengths
 };
+
+// inflate_table's checks (zlib inftrees.c): left = 1; left = 2 left - count[L]
+// for L = 1..15, over-subscribed if it ever goes negative; an incomplete set
+// (left > 0 at the end) is accepted only for the literal/length and distance
+// trees with a single code of length 1 (max == 1), never for the code-length
+// tree.  No code at all (max == 0) is accepted: decoding then fails on use.
+enum TreeKind { kCodes, kLensOrDists };
 
 struct Inflater {
     InflateSmem &sm;
@@ -148,7 +167,7 @@ struct Inflater {
     __device__ __forceinline__ uint32_t byte_pos() const { return rpos - nb / 8; }
 
     // build a tree from code lengths lens[0..n) (LDS, uniform n <= 288)
-    __device__ __forceinline__ Tree build(const uint8_t *lens, uint32_t n, uint16_t *sorted)
+    __device__ __forceinline__ Tree build(const uint8_t *lens, uint32_t n, uint16_t *sorted, TreeKind kind)
     {
         const uint32_t lane = lane_id();
         if (lane < 16) sm.cursor[lane] = 0;
@@ -167,14 +186,20 @@ struct Inflater {
         }
         off -= cnt;
         // first[L] = (first[L-1] + count[L-1]) << 1, first[1] = 0: serial over 15 lengths
-        uint32_t fl = 0, f = 0, c_prev = 0;
+        uint32_t fl = 0, f = 0, c_prev = 0, maxlen = 0;
+        int32_t left = 1;
+        bool over = false;
         for (uint32_t L = 1; L <= 15; ++L) {
             const uint32_t cL = (uint32_t)__shfl((int)cnt, (int)L, 64);
             f = (f + c_prev) << 1;
             if (lane == L) fl = f;
             c_prev = cL;
+            left = 2 * left - (int32_t)cL;
+            over = over || left < 0;
+            if (cL) maxlen = L;
         }
-        Tree t{fl, cnt, off, sorted};
+        const bool incomplete = maxlen != 0 && left > 0 && (kind == kCodes || maxlen != 1);
+        Tree t{fl, cnt, off, sorted, !over && !incomplete};
         wave_sync();
         if (lane >= 1 && lane <= 15) sm.cursor[lane] = off;
         wave_sync();
@@ -217,21 +242,31 @@ struct Inflater {
     }
 };
 
+template <bool WC>
 __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__ comp, const int64_t *__restrict__ comp_off,
                                                     const int32_t *__restrict__ comp_len, uint8_t *__restrict__ out,
                                                     const int64_t *__restrict__ out_off,
-                                                    const int32_t *__restrict__ out_len, int32_t *__restrict__ status)
+                                                    const int32_t *__restrict__ out_len, int32_t *__restrict__ status,
+                                                    uint32_t *__restrict__ viol)
 {
     __shared__ __attribute__((aligned(16))) InflateSmem sm;
     const uint32_t s = blockIdx.x, lane = lane_id();
+    if (comp_len[s] < 0 || out_len[s] < 0) {   // nothing is read or written for such a strip
+        if (lane == 0) status[s] = kErrArgs;
+        if (WC && lane == 0) viol[s] = 0;
+        return;
+    }
     const uint32_t n_in = (uint32_t)comp_len[s], n_out = (uint32_t)out_len[s];
     uint8_t *dst = out + out_off[s];
     Inflater in(sm, comp + comp_off[s], n_in);
     int32_t err = kOk;
     uint32_t p = 0, flushed = 0;
+    uint32_t nviol = 0;        // WC: ring reads outside the valid span (this lane's count)
     uint64_t s1 = 0, s2 = 0;   // this lane's adler terms: sum b, sum i*b over flushed bytes
     auto flush = [&](uint32_t upto) {   // output [flushed, upto) from the ring to HBM (upto - flushed <= 32 KiB)
         upto = min(upto, n_out);
+        // WC: every byte still to flush must be in the ring (written, not overwritten)
+        if (WC && (upto > p || p - flushed > kOutRing)) ++nviol;
         while (flushed < upto) {
             const uint32_t end = min(upto, (flushed & ~(kInChunk - 1)) + kInChunk);
             const uint32_t o = flushed + 16 * lane;
@@ -290,8 +325,8 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
                 for (uint32_t i = lane; i < 318; i += 64)
                     sm.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
                 wave_sync();
-                tl = in.build(sm.lens, 288, sm.sorted_ll);
-                td = in.build(sm.lens + 288, 30, sm.sorted_d);
+                tl = in.build(sm.lens, 288, sm.sorted_ll, kLensOrDists);
+                td = in.build(sm.lens + 288, 30, sm.sorted_d, kLensOrDists);
             } else {   // dynamic trees (3.2.7)
                 const uint32_t hlit = in.bits(5) + 257, hdist = in.bits(5) + 1, hclen = in.bits(4) + 4;
                 if (hlit > 286 || hdist > 30) {
@@ -305,7 +340,11 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
                     if (lane == 0) sm.lens[c_clen_order[i]] = (uint8_t)v;
                 }
                 wave_sync();
-                const Tree tc = in.build(sm.lens, 19, sm.sorted_cl);
+                const Tree tc = in.build(sm.lens, 19, sm.sorted_cl, kCodes);
+                if (!tc.ok) {
+                    err = kErrTree;
+                    break;
+                }
                 uint32_t k = 0, prev = 0;
                 uint8_t *ln = sm.lens + 19;   // the decoded lengths land after the 19 code-length lengths
                 while (k < hlit + hdist) {
@@ -339,8 +378,16 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
                     wave_sync();
                 }
                 if (err != kOk) break;
-                tl = in.build(ln, hlit, sm.sorted_ll);
-                td = in.build(ln + hlit, hdist, sm.sorted_d);
+                if (ln[256] == 0) {
+                    err = kErrEob;
+                    break;
+                }
+                tl = in.build(ln, hlit, sm.sorted_ll, kLensOrDists);
+                td = in.build(ln + hlit, hdist, sm.sorted_d, kLensOrDists);
+                if (!tl.ok || !td.ok) {
+                    err = kErrTree;
+                    break;
+                }
             }
             // the block's symbols
             for (;;) {
@@ -367,7 +414,12 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
                     for (uint32_t r = 0; r < len; r += 64) {
                         const uint32_t i = r + lane;
                         uint8_t v = 0;
-                        if (i < len) v = sm.out[(p - dist + (i % dist)) & kOutMask];
+                        if (i < len) {
+                            const uint32_t q = p - dist + (i % dist);
+                            // WC: q was written (q < p + i) and its slot not yet reused (p + i - q <= 32 KiB)
+                            if (WC && (q >= p + i || p + i - q > kOutRing)) ++nviol;
+                            v = sm.out[q & kOutMask];
+                        }
                         if (i < len) sm.out[(p + i) & kOutMask] = v;
                     }
                     p += len;
@@ -413,6 +465,30 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
         if (in.byte_pos() > n_in) err = kErrInput;
     }
     if (lane == 0) status[s] = err;
+    if (WC) {
+        for (int d = 32; d >= 1; d >>= 1) nviol += __shfl_xor(nviol, d, 64);
+        if (lane == 0) viol[s] = nviol;
+    }
+}
+
+template <bool WC>
+int launch_inflate(const uint8_t *comp_dev, const int64_t *comp_off_dev, const int32_t *comp_len_dev, int64_t n_strips,
+                   uint8_t *out_dev, const int64_t *out_off_dev, const int32_t *out_len_dev, int32_t *status_dev,
+                   uint32_t *viol_dev, void *stream)
+{
+    if (n_strips < 0) return set_error(VCF_ERR_INVALID, "n_strips < 0");
+    if (n_strips == 0) return VCF_OK;
+    if (!comp_dev || !comp_off_dev || !comp_len_dev || !out_dev || !out_off_dev || !out_len_dev || !status_dev)
+        return set_error(VCF_ERR_INVALID, "null buffer");
+    for (int64_t s0 = 0; s0 < n_strips; s0 += 65535) {
+        const unsigned cnt = (unsigned)std::min<int64_t>(65535, n_strips - s0);
+        hipLaunchKernelGGL(inflate_kernel<WC>, dim3(cnt), dim3(64), 0, (hipStream_t)stream, comp_dev,
+                           comp_off_dev + s0, comp_len_dev + s0, out_dev, out_off_dev + s0, out_len_dev + s0,
+                           status_dev + s0, WC ? viol_dev + s0 : nullptr);
+        const int rc = hip_check(hipGetLastError(), "inflate_kernel launch");
+        if (rc != VCF_OK) return rc;
+    }
+    return VCF_OK;
 }
 
 }  // namespace
@@ -422,22 +498,24 @@ using namespace vcf;
 
 extern "C" {
 
+#ifndef VCF_INFLATE_WINCHECK_BUILD
 int vcf_inflate_strips(const uint8_t *comp_dev, const int64_t *comp_off_dev, const int32_t *comp_len_dev,
                        int64_t n_strips, uint8_t *out_dev, const int64_t *out_off_dev, const int32_t *out_len_dev,
                        int32_t *status_dev, void *stream)
 {
-    if (n_strips < 0) return set_error(VCF_ERR_INVALID, "n_strips < 0");
-    if (n_strips == 0) return VCF_OK;
-    if (!comp_dev || !comp_off_dev || !comp_len_dev || !out_dev || !out_off_dev || !out_len_dev || !status_dev)
-        return set_error(VCF_ERR_INVALID, "null buffer");
-    for (int64_t s0 = 0; s0 < n_strips; s0 += 65535) {
-        const unsigned cnt = (unsigned)std::min<int64_t>(65535, n_strips - s0);
-        hipLaunchKernelGGL(inflate_kernel, dim3(cnt), dim3(64), 0, (hipStream_t)stream, comp_dev, comp_off_dev + s0,
-                           comp_len_dev + s0, out_dev, out_off_dev + s0, out_len_dev + s0, status_dev + s0);
-        const int rc = hip_check(hipGetLastError(), "inflate_kernel launch");
-        if (rc != VCF_OK) return rc;
-    }
-    return VCF_OK;
+    return launch_inflate<false>(comp_dev, comp_off_dev, comp_len_dev, n_strips, out_dev, out_off_dev, out_len_dev,
+                                 status_dev, nullptr, stream);
 }
+#else
+// the diagnostic build (csrc/ab/vcf_inflate_wincheck.hip, include/vcf_amd_ab.h)
+int vcf_inflate_strips_wincheck(const uint8_t *comp_dev, const int64_t *comp_off_dev, const int32_t *comp_len_dev,
+                                int64_t n_strips, uint8_t *out_dev, const int64_t *out_off_dev,
+                                const int32_t *out_len_dev, int32_t *status_dev, uint32_t *viol_dev, void *stream)
+{
+    if (!viol_dev) return set_error(VCF_ERR_INVALID, "null violation counter buffer");
+    return launch_inflate<true>(comp_dev, comp_off_dev, comp_len_dev, n_strips, out_dev, out_off_dev, out_len_dev,
+                                status_dev, viol_dev, stream);
+}
+#endif
 
 }  // extern "C"

@@ -178,24 +178,46 @@ class StripInflater:
         return b
 
     def inflate_into(self, comp: np.ndarray, comp_off: np.ndarray, comp_len: np.ndarray, out: DeviceBuffer,
-                     out_off: np.ndarray, out_len: np.ndarray, stream: Stream) -> None:
+                     out_off: np.ndarray, out_len: np.ndarray, stream: Stream, violations: np.ndarray = None) -> None:
         """Strip s: comp[comp_off[s]:][:comp_len[s]] (host bytes) -> out at
         out_off[s], exactly out_len[s] bytes.  Raises ValueError naming the
-        first strip zlib would reject (corrupt stream, wrong length, adler32)."""
+        first strip zlib would reject (corrupt stream, wrong length, adler32),
+        and before anything runs on the device for a strip table that does not
+        fit its buffers (a negative length, a strip past the end of `comp` or
+        of `out`).  With `violations` (a uint32 array of one entry per strip)
+        the strips run through the A/B library's window-check diagnostic
+        (vcf_inflate_strips_wincheck), which fills it; test use only."""
         n = int(len(comp_len))
+        comp = np.ascontiguousarray(comp, np.uint8)
+        comp_off, out_off = np.asarray(comp_off, np.int64), np.asarray(out_off, np.int64)
+        comp_len, out_len = np.asarray(comp_len, np.int64), np.asarray(out_len, np.int64)
+        if not (len(comp_off) == len(out_off) == len(out_len) == n):
+            raise ValueError("inflate: strip table arrays of different lengths")
         if n == 0:
             return
-        comp = np.ascontiguousarray(comp, np.uint8)
-        tab = np.concatenate([np.asarray(comp_off, np.int64), np.asarray(out_off, np.int64)])
-        lens = np.concatenate([np.asarray(comp_len, np.int32), np.asarray(out_len, np.int32)])
+        if (comp_len < 0).any() or (out_len < 0).any() or (comp_off < 0).any() or (out_off < 0).any():
+            raise ValueError("inflate: negative strip offset or length")
+        if (comp_off + comp_len > comp.nbytes).any():
+            raise ValueError(f"inflate: strip {int(np.argmax(comp_off + comp_len > comp.nbytes))} reads past the "
+                             f"{comp.nbytes} compressed bytes")
+        if (out_off + out_len > out.nbytes).any() or (out_len > 0x7FFFFFFF).any() or (comp_len > 0x7FFFFFFF).any():
+            raise ValueError(f"inflate: a strip writes past the {out.nbytes}-byte output buffer")
+        tab = np.concatenate([comp_off, out_off])
+        lens = np.concatenate([comp_len, out_len]).astype(np.int32)
         with self._lock:
             dc, dt, dl, ds = (self._buf("comp", comp.nbytes), self._buf("tab", tab.nbytes),
                               self._buf("lens", lens.nbytes), self._buf("status", 4 * n))
             dc.upload(comp, stream)
             dt.upload(tab, stream)
             dl.upload(lens, stream)
-            L.call("vcf_inflate_strips", dc.ptr, dt.ptr, dl.ptr, n, out.ptr, dt.address(8 * n), dl.address(4 * n),
-                   ds.ptr, stream.handle)
+            if violations is None:
+                L.call("vcf_inflate_strips", dc.ptr, dt.ptr, dl.ptr, n, out.ptr, dt.address(8 * n),
+                       dl.address(4 * n), ds.ptr, stream.handle)
+            else:
+                dv = self._buf("viol", 4 * n)
+                L.call_ab("vcf_inflate_strips_wincheck", dc.ptr, dt.ptr, dl.ptr, n, out.ptr, dt.address(8 * n),
+                          dl.address(4 * n), ds.ptr, dv.ptr, stream.handle)
+                dv.download(violations[:n], stream)
             st = np.empty(n, np.int32)
             ds.download(st, stream)
             stream.synchronize()
