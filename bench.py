@@ -462,6 +462,222 @@ def c5_check(info, Q: int) -> None:
                         f" (file sizes {len(got[0])}/{len(w0)}, {len(got[1])}/{len(w1)})")
 
 
+# config C3 (BASELINE.json configs[2]): 2D-DWT l=5 CDF-9/7 (pywt's bior4.4) + deadzone at 4K
+C3_FRAMES, C3_LEVELS, C3_WAVELET = 8, 5, "bior4.4"
+# bior4.4's nonzero taps: decomposition low/high 9 / 7 of 10, reconstruction 7 / 9 of 10
+# (pywt 1.1.1's filter bank, vcf_amd/csrc/vcf_wavelets.h; zero taps are skipped bit-exactly,
+# DESIGN.md §4.5)
+C3_TAPS_NZ = (9, 7)
+FP64_ISSUE_TOPS = 34.0   # measured fp64 VALU lane-ops/s of gfx950 (scripts/micro/f64_rate.hip)
+
+
+def c3_fp64_ops_per_pixel(levels: int = C3_LEVELS, taps=C3_TAPS_NZ) -> float:
+    """Float64 multiplies + adds per RGB pixel of the C3 encode (the decode is
+    the same count with the reconstruction filters): per level and channel
+    each of the two separable passes makes one low and one high output per
+    input pair, with nz multiplies and nz - 1 adds each (pywt's sums start at
+    the first product), over a plane 1/4 the previous level's."""
+    per_pair = sum(2 * nz - 1 for nz in taps)           # 30 for bior4.4
+    per_plane_px = 2 * per_pair / 2                      # two passes, one output pair per 2 inputs
+    return 3 * per_plane_px * sum(0.25 ** l for l in range(levels))
+
+
+def c3_block(args, world: int, rank: int, group, frames):
+    """Config C3 of BASELINE.json: 2D-DWT l=5 (CDF-9/7 = pywt bior4.4, 'per'
+    mode, float64 in pywt's own tap order) + per-subband deadzone Q=32, 8 x 4K
+    frames resident in HBM per rank (weak scaling, no exchange):
+    vcf_dwt_dz_encode (2D-DWT.py:57-78 + quantize_decom_fn :113-136 + the
+    subband files' +128/dtype :162-200) and vcf_dwt_dz_decode (:80-101,
+    :138-160, :202-228), each timed like the headline (settle, barrier + sync
+    on both sides, max over ranks; HIP events on the launch stream for the
+    per-launch figure).  Roofline: HBM (RGB in + subband bytes out) and the
+    float64 issue rate the transforms are actually bound by.  Never raises."""
+    import vcf_amd.dwt as DW
+    from vcf_amd.device import DeviceBuffer, Event, Stream, synchronize
+    H, W, F, Lv, Q = 2160, 3840, C3_FRAMES, C3_LEVELS, args.QSS
+    info = {"workload": (f"2D-DWT C3: {F} x 4K frames per rank resident in HBM, l={Lv} {C3_WAVELET} (CDF-9/7, "
+                         f"pywt 'per' mode, float64), per-subband deadzone Q={Q}, packed 3l+1 subbands"),
+            "frames": F, "frame": [H, W, 3], "levels": Lv, "wavelet": C3_WAVELET, "n_ranks": world}
+    try:
+        w = DW.wavelet_index(C3_WAVELET)
+        shapes, pb, wb = DW.layout(H, W, Lv)
+        Ho, Wo = 2 * shapes[0][0], 2 * shapes[0][1]
+        din = DeviceBuffer(F * H * W * 3)
+        for f in range(F):
+            din.upload(frames[f % len(frames)], offset=f * H * W * 3)
+        dpk, dws, dout = DeviceBuffer(F * pb), DeviceBuffer(F * wb), DeviceBuffer(F * Ho * Wo * 3)
+        st = Stream()
+        enc = lambda: DW.encode_device(din, F, H, W, w, Lv, Q, dpk, dws, st)   # noqa: E731
+        dec = lambda: DW.decode_device(dpk, F, H, W, w, Lv, Q, dout, dws, st)  # noqa: E731
+        res = {}
+        for name, fn in (("encode", enc), ("decode", dec)):
+            for _ in range(3):
+                fn()
+            settle(fn, st, Event, 0.5, 3.0, chunk=8)
+            e0, e1 = Event(), Event()
+            group.barrier()
+            synchronize()
+            t0 = time.perf_counter()
+            e0.record(st)
+            for _ in range(args.c3_steps):
+                fn()
+            e1.record(st)
+            st.synchronize()
+            wall = (time.perf_counter() - t0) / args.c3_steps
+            res[name] = (group.allreduce_max(wall) if world > 1 else wall, e0.elapsed_ms(e1) / args.c3_steps)
+        ops = c3_fp64_ops_per_pixel() * F * H * W
+        for name, alg in (("encode", F * (H * W * 3 + pb)), ("decode", F * (pb + Ho * Wo * 3))):
+            wall, kms = res[name]
+            info[name] = {
+                "ms": round(wall * 1e3, 4), "value": round(world * F * H * W / wall / 1e6, 1), "unit": "Mpixels/s",
+                "launch_ms_events": round(kms, 4), "steps": args.c3_steps,
+                "roofline_hbm": {"achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "alg_bytes_per_launch": int(alg)},
+                "roofline_fp64_issue": {"achieved": round(ops / (kms * 1e-3) / 1e12, 2), "peak": FP64_ISSUE_TOPS,
+                                        "unit": "T fp64 lane-ops/s",
+                                        "frac": round(ops / (kms * 1e-3) / 1e12 / FP64_ISSUE_TOPS, 4),
+                                        "fp64_ops_per_launch": int(ops),
+                                        "ops_per_pixel": round(c3_fp64_ops_per_pixel(), 2)}}
+        if rank == 0:
+            info["_check"] = (dpk, dout, pb, Ho, Wo)
+    except Exception as e:   # reported in the block; the headline line still prints
+        info["error"] = f"{type(e).__name__}: {e}"
+    return info
+
+
+def c3_check(info, frames, Q: int) -> None:
+    """The checker leg (rank 0, N = 1): frame 0's packed subbands and its
+    reconstruction against the oracle (oracle/vcf_dwt_oracle.cpp: pywt 1.1.1's
+    'per' dwt/idwt restated with 2D-DWT.py's glue), and the oracle timed on
+    one frame, 1 thread, as the block's cpu_baseline."""
+    chk = info.pop("_check", None) if info else None
+    if chk is None:
+        return
+    import vcf_amd.dwt as DW
+    from oracle import oracle as O
+    dpk, dout, pb, Ho, Wo = chk
+    H, W = info["frame"][:2]
+    pk = np.empty(pb, np.uint8)
+    dpk.download(pk)
+    rec = np.empty((Ho, Wo, 3), np.uint8)
+    dout.download(rec)
+    t0 = time.perf_counter()
+    sb = O.dwt_encode_frame(frames[0], C3_WAVELET, C3_LEVELS, Q)
+    t_enc = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    want_rec = O.dwt_decode_frame(sb, H, W, C3_WAVELET, C3_LEVELS, Q)
+    t_dec = time.perf_counter() - t0
+    ok_enc = np.array_equal(pk, DW.pack(sb, H, W, C3_LEVELS))
+    ok_dec = np.array_equal(rec, want_rec)
+    info["verified"] = ("ok: frame 0's subbands and reconstruction bit-exact vs the oracle" if ok_enc and ok_dec else
+                        f"MISMATCH: subbands {'ok' if ok_enc else 'differ'}, reconstruction "
+                        f"{'ok' if ok_dec else 'differs'}")
+    info["cpu_baseline"] = {
+        "encode": {"value": round(H * W / t_enc / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+                   "sample": f"one 4K frame, oracle/vcf_dwt_oracle.cpp (pywt 1.1.1 'per' restated), {t_enc:.2f} s"},
+        "decode": {"value": round(H * W / t_dec / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+                   "sample": f"one 4K frame's subbands, oracle/vcf_dwt_oracle.cpp, {t_dec:.2f} s"}}
+
+
+def c2_block(args, world: int, rank: int, group):
+    """Config C2 of BASELINE.json: one 1080p frame, YCoCg + 2D-DCT B=8 +
+    deadzone + CBAAC, through the drop-in CoDec's own encode_fn / decode_fn
+    (files on disk: PNG in, code-stream + _shape.bin out, and back to PNG;
+    2D-DCT.py:268-468 with -c CBAAC, CBAAC.py:81-150).  Two entropy stages:
+    -c CBAAC, the reference's own .adpt_arith format (its serial adaptive
+    arithmetic coder, on the host), and -c TCBAACP (the tiled, prior-seeded
+    coder on the GPU: the indices never leave HBM).  Every rank codes its own
+    frame (replicas); per-call medians, max over ranks.  Never raises."""
+    import tempfile
+
+    from PIL import Image
+
+    from vcf_amd.codec import parser as P
+    from vcf_amd.codec.dct2d import CoDec
+    H, W = 1080, 1920
+    info = {"workload": ("C2: one 1080p PNG per rank through dct2d.CoDec.encode_fn / decode_fn (files), YCoCg + "
+                         f"2D-DCT B=8 + deadzone Q={args.QSS} + CBAAC (-c CBAAC: the reference's .adpt_arith, serial "
+                         "host coder; -c TCBAACP: tiled prior-seeded coder on the GPU)"),
+            "frame": [H, W, 3], "n_ranks": world, "reps": args.c2_reps}
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            src = os.path.join(d, "f.png")
+            img = synth_frame(H, W, seed=7 + rank)
+            Image.fromarray(img).save(src)
+            for ec in ("CBAAC", "TCBAACP"):
+                enc = CoDec(P.parse(P.dct_parser(), ["encode", "-c", ec, "-q", str(args.QSS)]))
+                dec = CoDec(P.parse(P.dct_parser(), ["decode", "-c", ec, "-q", str(args.QSS)]))
+                out, rec = os.path.join(d, "e_" + ec), os.path.join(d, "d_" + ec + ".png")
+                te, td = [], []
+                nbytes = enc.encode_fn(src, out)
+                dec.decode_fn(out, rec)
+                group.barrier()
+                for _ in range(args.c2_reps):
+                    t0 = time.perf_counter()
+                    nbytes = enc.encode_fn(src, out)
+                    t1 = time.perf_counter()
+                    dec.decode_fn(out, rec)
+                    t2 = time.perf_counter()
+                    te.append(t1 - t0)
+                    td.append(t2 - t1)
+                e_ms, d_ms = float(np.median(te)), float(np.median(td))
+                if world > 1:
+                    e_ms, d_ms = group.allreduce_max(e_ms), group.allreduce_max(d_ms)
+                blk = {"encode_fn_ms": round(e_ms * 1e3, 3), "decode_fn_ms": round(d_ms * 1e3, 3),
+                       "encode_value": round(world * H * W / e_ms / 1e6, 2),
+                       "decode_value": round(world * H * W / d_ms / 1e6, 2), "unit": "Mpixels/s",
+                       "code_bytes": int(nbytes), "bits_per_pixel": round(8 * nbytes / (H * W), 4)}
+                if rank == 0:
+                    with open(out + enc.file_extension, "rb") as f:
+                        cs = f.read()
+                    blk["_check"] = (img, dec.decompress(cs), np.asarray(Image.open(rec)))
+                info[ec] = blk
+            enc.bye()
+    except Exception as e:   # reported in the block; the headline line still prints
+        info["error"] = f"{type(e).__name__}: {e}"
+    return info
+
+
+def c2_check(info, Q: int) -> None:
+    """Checker leg (rank 0, N = 1): each codec's file decodes to the oracle's
+    indices of the frame and decode_fn's PNG equals the oracle's reconstruction;
+    the CPU baseline is the same C2 encode on one host core: the oracle's C DCT
+    (oracle/vcf_oracle.c) then the serial CBAAC coder restated in C++
+    (vcf_cbaac_encode, the reference's AdaptiveModel + A8 coder)."""
+    if not info or "error" in info:
+        return
+    from oracle import oracle as O
+    from vcf_amd import cbaac as CB
+    img = None
+    for ec in ("CBAAC", "TCBAACP"):
+        blk = info.get(ec)
+        if not blk or "_check" not in blk:
+            continue
+        img, k_got, rec = blk.pop("_check")
+        k_ref = O.encode_frame(img, Q)
+        ok_k = np.array_equal(np.asarray(k_got).reshape(k_ref.shape), k_ref)
+        ok_r = np.array_equal(rec, O.decode_frame(k_ref, img.shape[0], img.shape[1], Q))
+        blk["verified"] = ("ok: the file decodes to the oracle's indices, decode_fn's PNG equals the oracle's "
+                           "reconstruction" if ok_k and ok_r else
+                           f"MISMATCH: indices {'ok' if ok_k else 'differ'}, PNG {'ok' if ok_r else 'differs'}")
+    if img is None:
+        return
+    n, t0 = 0, time.perf_counter()
+    while True:
+        k = O.encode_frame(img, Q)
+        CB.CBAACCodec(order=0).compress(k)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= 3.0:
+            break
+    info["cpu_baseline"] = {"value": round(n * img.shape[0] * img.shape[1] / el / 1e6, 3), "unit": "Mpixels/s",
+                            "cores": 1, "kind": "port",
+                            "sample": (f"{n} x the 1080p frame: oracle/vcf_oracle.c DCT+deadzone, then the serial "
+                                       f"CBAAC coder (C++ restatement of CBAAC.py's model + coder), 1 thread, "
+                                       f"{el:.1f} s; no file I/O")}
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc pass (if it matches)."""
     p = os.path.join(ROOT, "profiles", "pmc_encode_4k.json")
@@ -499,6 +715,9 @@ def main():
     ap.add_argument("--c5-frames", type=int, default=64, help="4K frames of the C5 block (0 disables it)")
     ap.add_argument("--c5-steps", type=int, default=2)
     ap.add_argument("--c5-warmup", type=int, default=1)
+    ap.add_argument("--c3-steps", type=int, default=20, help="timed launches of the C3 block (0 disables it)")
+    ap.add_argument("--c2-reps", type=int, default=5, help="encode_fn/decode_fn calls per codec of the C2 block "
+                                                        "(0 disables it)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -559,6 +778,10 @@ def main():
     c4t = c4_block(args, world, rank, group, "TIFF") if args.c4_frames > 0 and not args.no_c4_tiff else None
     # C5 (IPP_DCT, 64 x 4K, GOP 10, full search, -c TIFF on the GPU deflate, GOP-sharded)
     c5 = c5_block(args, world, rank, group) if args.c5_frames > 0 else None
+    # C3 (2D-DWT l=5 bior4.4 + deadzone, 8 x 4K per rank, HBM-resident) and C2
+    # (one 1080p PNG through encode_fn/decode_fn with -c CBAAC and -c TCBAACP)
+    c3 = c3_block(args, world, rank, group, distinct) if args.c3_steps > 0 else None
+    c2 = c2_block(args, world, rank, group) if args.c2_reps > 0 else None
 
     # after the timed region (an idle GPU during seconds of CPU work would start
     # the timed steps at low clocks): parity spot check of the timed kernel's
@@ -570,8 +793,15 @@ def main():
         k_gpu = dout.download(np.empty((Hp, Wp, 3), np.uint8))
         parity = "bit-exact vs oracle (frame 0)" if np.array_equal(k_gpu, k_ref) else "MISMATCH"
         c5_check(c5, Q)
-    elif c5 is not None:
-        c5.pop("_check", None)
+        c3_check(c3, distinct, Q)
+        c2_check(c2, Q)
+    else:
+        for blk in (c5, c3):
+            if blk is not None:
+                blk.pop("_check", None)
+        for ec in ("CBAAC", "TCBAACP"):
+            if c2 is not None and isinstance(c2.get(ec), dict):
+                c2[ec].pop("_check", None)
 
     workload = (f"dct_dz_encode {H}x{W}x3 u8 RGB frames (4K), B=8, YCoCg, deadzone Q={Q}, "
                 f"subband layout, {F} frames/step/GPU resident in HBM")
@@ -613,6 +843,8 @@ def main():
             "c4_e2e_with_gather": c4,
             "c4_tiff_e2e_with_gather": c4t,
             "c5_e2e_with_gather": c5,
+            "c3_dwt": c3,
+            "c2_encode_decode_fn": c2,
         }
         print(json.dumps(out), flush=True)
     group.close()

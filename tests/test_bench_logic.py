@@ -26,3 +26,12 @@ def test_stage_table_skips_missing_ranks():
     t = c4_stage_table(rows, [3, 3, 2])
     assert t["stages_ms_max"] == {C4_STAGES[0]: 3.0} and t["slowest_rank"] == {C4_STAGES[0]: 2}
     assert t["stages_ms_rank0"] == {}
+
+
+def test_c3_fp64_op_count():
+    """C3's float64 work per pixel: bior4.4 (9 + 7 nonzero decomposition taps)
+    gives 30 multiplies + adds per output pair, two passes per level, three
+    channels, five levels of planes a quarter the size: 90 * (1 + 1/4 + ... + 1/256)."""
+    import bench
+    assert abs(bench.c3_fp64_ops_per_pixel() - 90 * sum(0.25 ** l for l in range(5))) < 1e-9
+    assert abs(bench.c3_fp64_ops_per_pixel(levels=1) - 90.0) < 1e-9

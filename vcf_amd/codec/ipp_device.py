@@ -81,7 +81,10 @@ class DeviceIPP:
         self.res = DeviceBuffer(ng * self.fb)
         self.rec = DeviceBuffer(ng * self.fb)
         self.k = DeviceBuffer(max(1, self.n_local) * self.kb)   # every frame's indices, in deflate order
-        self.mv = DeviceBuffer(max(1, ng * self.hb * self.wb * 8))
+        # every local frame's motion field at its frame slot (the I-frames' slots unused): the
+        # fields stay in HBM through the GOP loop and come back in one copy after it
+        self.mvb = self.hb * self.wb * 8
+        self.mv = DeviceBuffer(max(1, max(1, self.n_local) * self.mvb))
         self.gray = DeviceBuffer(2 * self.H * self.W)
         self.out = DeviceBuffer(max(1, self.n_local * self.spf * self.slot))
         self.sizes = DeviceBuffer(max(4, self.n_local * self.spf * 4))
@@ -111,7 +114,7 @@ class DeviceIPP:
 
         t = time.perf_counter()
         order = []   # local frame index (frame - lo) of each deflated frame, in deflate order
-        mv_of = {}
+        p_frames = []   # local indices of the P-frames, whose motion fields come back
         for p in range(self.gop):
             gs = self._frames_of_step(p)
             if not gs:
@@ -123,15 +126,12 @@ class DeviceIPP:
                     copy_dtod(self.res, j * fb, frames, f * fb, fb, self.stream)
                     continue
                 ref, comp = _At(self.ref, g * fb, fb), _At(self.comp, g * fb, fb)
-                mv = _At(self.mv, g * self.hb * self.wb * 8, self.hb * self.wb * 8)
+                mv = _At(self.mv, f * self.mvb, self.mvb)
                 call("vcf_ipp_block_match", ref.ptr, cur.ptr, self.H, self.W, self.bs, self.sr, int(self.fast),
                      mv.ptr, self.gray.ptr, sh)
                 call("vcf_ipp_motion_compensate", ref.ptr, mv.ptr, self.H, self.W, self.bs, comp.ptr, sh)
                 call("vcf_ipp_residual", cur.ptr, comp.ptr, fb, self.res.address(j * fb), sh)
-                m = np.empty((self.hb, self.wb, 2), np.float32)
-                if m.size:
-                    call("vcf_memcpy_dtoh", m.ctypes.data_as(ctypes.c_void_p), mv.ptr, m.nbytes, sh)
-                mv_of[f] = m
+                p_frames.append(f)
             n = len(gs)
             # the step's indices stay in HBM at their deflate positions [len(order), len(order) + n)
             kstep = _At(self.k, len(order) * kb, n * kb)
@@ -150,10 +150,14 @@ class DeviceIPP:
             call("vcf_zlib_strips", self.k.ptr, self.n_local, kb, self.strip_bytes, Z.LEVEL, self.out.ptr, self.slot,
                  self.sizes.ptr, self.ws.ptr, sh)
         t = mark("gop_loop", t)
-        # every frame's TIFF prefix from the strip sizes, the strips in frame order
+        # every frame's TIFF prefix from the strip sizes, the strips in frame order; the motion
+        # fields of the whole loop in the same synchronisation
         sz = np.empty(max(1, self.n_local * self.spf), np.int32)
         if self.n_local:
             self.sizes.download(sz[:self.n_local * self.spf], self.stream)
+        mv_all = np.empty((max(1, self.n_local), self.hb, self.wb, 2), np.float32)
+        if self.n_local and self.mvb:
+            call("vcf_memcpy_dtoh", mv_all.ctypes.data_as(ctypes.c_void_p), self.mv.ptr, self.n_local * self.mvb, sh)
         self.stream.synchronize()
         if (sz[:self.n_local * self.spf] < 0).any():
             raise RuntimeError("vcf_zlib_strips: a strip overflowed its slot")
@@ -165,5 +169,5 @@ class DeviceIPP:
         hlen = np.full(self.n_local, hdr.shape[1], np.int64)
         pay_src = (pos[:, None] * self.spf + np.arange(self.spf)[None, :]) * self.slot
         sizes, out = self.exchange.run(hdr.reshape(-1), hlen, self.out, pay_src, szf, mark, t)
-        mvs = [mv_of[f] for f in sorted(mv_of)]
+        mvs = [mv_all[f] for f in sorted(p_frames)]
         return sizes, out, mvs

@@ -4,6 +4,7 @@ libvcf_amd.so (vcf_dwt_dz_encode / vcf_dwt_dz_decode).  No CPU path."""
 from __future__ import annotations
 
 import ctypes
+import functools
 
 import numpy as np
 
@@ -17,6 +18,7 @@ def wavelet_index(name: str) -> int:
     return i.value
 
 
+@functools.lru_cache(maxsize=64)
 def layout(H: int, W: int, levels: int):
     """([(h_l, w_l) for l = 1..levels], packed bytes per frame, workspace bytes per frame)."""
     hs = (ctypes.c_int32 * levels)()
@@ -60,6 +62,27 @@ def _frames(a, what):
     if a.ndim != 4 or a.shape[-1] != 3 or a.dtype != np.uint8:
         raise ValueError(f"{what}: expected (N,) H x W x 3 uint8")
     return np.ascontiguousarray(a)
+
+
+def encode_device(din: DeviceBuffer, n: int, H: int, W: int, wavelet: int, levels: int, Q: int,
+                  packed: DeviceBuffer, workspace: DeviceBuffer, stream=None) -> None:
+    """n HBM-resident H x W x 3 u8 frames -> their packed subbands (layout()'s
+    bytes per frame), enqueued on `stream`; `wavelet` is wavelet_index()'s."""
+    _, pb, wb = layout(H, W, levels)
+    if din.nbytes < n * H * W * 3 or packed.nbytes < n * pb or workspace.nbytes < n * wb:
+        raise ValueError("dwt encode_device: buffer smaller than n frames need")
+    L.call("vcf_dwt_dz_encode", din.ptr, n, H, W, int(wavelet), levels, int(Q), packed.ptr, workspace.ptr,
+           None if stream is None else stream.handle)
+
+
+def decode_device(packed: DeviceBuffer, n: int, H: int, W: int, wavelet: int, levels: int, Q: int,
+                  out: DeviceBuffer, workspace: DeviceBuffer, stream=None) -> None:
+    """n frames' packed subbands in HBM -> u8 RGB (2*ceil(H/2) x 2*ceil(W/2) x 3 each)."""
+    shapes, pb, wb = layout(H, W, levels)
+    if packed.nbytes < n * pb or out.nbytes < n * 4 * shapes[0][0] * shapes[0][1] * 3 or workspace.nbytes < n * wb:
+        raise ValueError("dwt decode_device: buffer smaller than n frames need")
+    L.call("vcf_dwt_dz_decode", packed.ptr, n, H, W, int(wavelet), levels, int(Q), out.ptr, workspace.ptr,
+           None if stream is None else stream.handle)
 
 
 def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32, variant: int = 0):
