@@ -424,8 +424,9 @@ int64_t vcf_png_encode_bound(int32_t H, int32_t W);
  * strip_bytes <= 65536 (tifffile's strips for rows up to 64 KB);
  * slot_bytes a multiple of 4 >= vcf_zlib_bound(strip_bytes); ws_dev holds
  * vcf_zlib_workspace(total strips) bytes (16-byte aligned; out_dev and
- * sizes_dev 4-byte aligned) -- at most ~3.9 GB whatever the batch: the strips
- * are coded in rounds that reuse it.  The call is asynchronous on `stream`;
+ * sizes_dev 4-byte aligned) -- ~1.15 MB per strip, at most an eighth of the
+ * device's memory (3.9 to 40 GB) whatever the batch: past that the strips are
+ * coded in rounds that reuse it.  The call is asynchronous on `stream`;
  * internally part of each round runs on library streams forked from and
  * joined back to it, so the caller sees ordinary stream semantics. */
 int64_t vcf_zlib_bound(int64_t strip_bytes);
@@ -443,8 +444,12 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
  * out_dev + out_off_dev[s], which must come to exactly out_len_dev[s] bytes
  * (the TIFF's rows per strip x row bytes).  status_dev[s] = 0, or < 0 when the
  * stream is not one zlib accepts with that length (-1 header, -2 block, -3
- * code, -4 distance, -5 length, -6 adler32, -7 input overrun).  Device
- * arrays; RFC 1950/1951, stored, fixed and dynamic blocks. */
+ * code, -4 distance, -5 length, -6 adler32, -7 input overrun, -8 an
+ * over-subscribed or incomplete code-length set, -9 no end-of-block code,
+ * -10 a negative length: nothing read or written).  Device arrays, which the
+ * kernel trusts: offsets and lengths must lie inside comp_dev and out_dev
+ * (vcf_amd/zlib_gpu.py checks them on the host first); RFC 1950/1951,
+ * stored, fixed and dynamic blocks. */
 int vcf_inflate_strips(const uint8_t *comp_dev, const int64_t *comp_off_dev, const int32_t *comp_len_dev,
                        int64_t n_strips, uint8_t *out_dev, const int64_t *out_off_dev, const int32_t *out_len_dev,
                        int32_t *status_dev, void *stream);

@@ -207,3 +207,46 @@ def test_c4_workload_every_strip_equals_zlib():
                            range(n * spf)))
     bad = [s for s in range(n * spf) if bytes(got[s // spf][s % spf]) != want[s]]
     assert not bad, bad[:20]
+
+
+_MULTI_ROUND = r'''
+import sys, zlib
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import bench
+from vcf_amd import dct
+from vcf_amd import _lib as L
+from vcf_amd.codec.tiff import strip_layout
+from vcf_amd.device import DeviceBuffer
+from vcf_amd.zlib_gpu import StripDeflater
+n, H, W = 24, 1080, 1920
+bases = [bench.synth_frame(H, W, seed=100 + s) for s in range(4)]
+k = np.concatenate([dct.encode(np.stack([bench.c4_frame(bases, i) for i in range(f, f + 8)]), Q=32)
+                    for f in range(0, n, 8)])
+flat = np.ascontiguousarray(k.reshape(n, -1))
+sb = strip_layout(k.shape[1:], 1)[2]
+total = n * int(L.lib().vcf_zlib_strip_count(flat.shape[1], sb))
+per = int(L.lib().vcf_zlib_workspace(total)) // (int(L.lib().vcf_zlib_workspace(1)))
+got = StripDeflater().deflate_device(DeviceBuffer.from_array(flat), n, flat.shape[1], sb, 6)
+spf = len(got[0])
+bad = [s for s in range(n * spf)
+       if bytes(got[s // spf][s % spf]) != zlib.compress(flat[s // spf, (s % spf) * sb:(s % spf + 1) * sb].tobytes(), 6)]
+print("strips", total, "per_round", per, "bad", len(bad))
+assert per < total and not bad, bad[:20]
+'''
+
+
+def test_many_rounds_every_strip_equals_zlib():
+    """Deterministic multi-round run: the workspace budget forced down to ~50 MB
+    (VCF_ZX_BUDGET, read once per process, so a child process) cuts 2 376 C4
+    strips into rounds of 43 that reuse one workspace; every strip against
+    zlib.compress (a strip coded from the previous round's tables shows here)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, VCF_ZX_BUDGET="50000000")
+    p = subprocess.run([sys.executable, "-c", _MULTI_ROUND, root], env=env, capture_output=True, text=True,
+                       timeout=280)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    assert "bad 0" in p.stdout

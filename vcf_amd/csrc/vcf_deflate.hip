@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "vcf_amd.h"
 #include "vcf_deflate.h"
@@ -66,28 +67,41 @@ constexpr int64_t kRrOff = kRfOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSymOff = kRrOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;   // adler sums (2 x u64), worklist length (u32)
 constexpr int64_t kWsPerStrip = kSumOff + 32;
-// Rounds: the strips of a call are processed in rounds whose workspace
-// stays under kWsBudget (about 3.9 GB), one round after the other on the
-// caller's stream.  (Rounds in flight on library streams, each with its own
-// workspace slot, measured slower -- 517 vs 453 ms for C4 -- and produced a
-// wrong strip now and then on MI355X)
-constexpr int64_t kWsBudget = 3900000000LL;
-#ifndef VCF_ZX_SLOTS   // A/B (diagnostic builds): workspace slots (rounds in flight)
-#define VCF_ZX_SLOTS 1
-#endif
-// A call's strips in rounds: `slots` workspace slots of `per` strips each (within
-// the budget together); round r uses slot r % slots, so with two slots one round's
-// K1 and head kernel run while the other's parse finishes (the tails overlap).
+// Rounds: the strips of a call are processed in rounds whose workspace stays
+// under the budget, one round after the other on the caller's stream.  Every
+// round ends in a tail (the last strips' serial parses on a draining GPU), so
+// fewer, larger rounds are faster: the budget is an eighth of the device's HBM
+// (36 GB on MI355X: C4's 25 344 strips in one round, 317 -> 245 ms against
+// round 4's fixed 3.9 GB), at least 3.9 GB and at most 40 GB.  It depends only
+// on the device, so vcf_zlib_workspace and vcf_zlib_strips agree.  (Rounds in
+// flight on library streams, each with its own workspace slot, measured
+// slower -- 517 vs 453 ms for C4 -- and produced a wrong strip now and then on
+// MI355X)
+constexpr int64_t kWsBudget = 3900000000LL, kWsBudgetMax = 40000000000LL;
+// the budget in effect (VCF_ZX_BUDGET bytes overrides it: A/B of the round size)
+inline int64_t ws_budget()
+{
+    static int64_t b = 0;
+    if (!b) {
+        int64_t v = kWsBudget;
+        int dev = 0;
+        size_t total = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceTotalMem(&total, dev) == hipSuccess)
+            v = std::min(kWsBudgetMax, std::max(kWsBudget, (int64_t)(total / 8)));
+        const char *e = getenv("VCF_ZX_BUDGET");
+        b = e && atoll(e) > 0 ? atoll(e) : v;
+    }
+    return b;
+}
+// A call's strips in rounds of `per` strips (at most 65535: the y grid dimension of
+// the head and K2a launches), the workspace of one round within the budget.
 struct ZRounds {
-    int64_t rounds, per, slots;
+    int64_t rounds, per;
     explicit ZRounds(int64_t total)
     {
-        const int64_t one = std::max<int64_t>(1, kWsBudget / kWsPerStrip);
-        slots = total > 1024 ? VCF_ZX_SLOTS : 1;   // a few strips: one round on the caller's stream
-        const int64_t round_max = std::max<int64_t>(1, one / slots);
-        rounds = std::max<int64_t>(slots, (total + round_max - 1) / round_max);
+        const int64_t round_max = std::min<int64_t>(65535, std::max<int64_t>(1, ws_budget() / kWsPerStrip));
+        rounds = std::max<int64_t>(1, (total + round_max - 1) / round_max);
         per = std::max<int64_t>(1, (total + rounds - 1) / rounds);
-        if (rounds < slots) slots = rounds;
     }
 };
 constexpr int kK2bThreads = 1024;    // K2b: 16 waves per strip, one listed position per wave at a time
@@ -259,28 +273,57 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
     static_assert(kK1Waves == 2 || kK1Waves == 4 || kK1Waves == 8, "hash space split in powers of two");
     const uint32_t np = n >= 3 ? n - 2 : 0;   // positions 0..n-3 are inserted
     for (uint32_t i = tid; i < (1u << 14); i += NT) sm.cnt[i] = 0;
-    auto stage = [&](uint32_t c0) {
+    // chunk staging: thread t holds the 4 bytes at c0 + 4t of the chunk (thread 0
+    // also the 4 after the chunk, for the last hashes) in registers, loaded while
+    // the previous chunk was processed -- the global latency of the 64 stagings
+    // per strip overlaps the work instead of sitting between two barriers
+    static_assert(kK1Stage == 4 * NT, "one dword of the chunk per thread");
+    const bool al4 = (((uintptr_t)S.src) & 3) == 0;
+    auto fetch = [&](uint32_t c0, uint32_t &a, uint32_t &x) {
+        const uint32_t q = c0 + 4 * tid;
+        auto dw = [&](uint32_t P) -> uint32_t {
+            if (al4 && P + 4 <= n) return *reinterpret_cast<const uint32_t *>(S.src + P);
+            uint32_t v = 0;
+            for (uint32_t i = 0; i < 4; ++i) v |= (P + i < n ? (uint32_t)S.src[P + i] : 0u) << (8 * i);
+            return v;
+        };
+        a = q < n ? dw(q) : 0u;
+        x = tid == 0 && c0 + kK1Stage < n ? dw(c0 + kK1Stage) : 0u;
+    };
+    uint32_t pa = 0, px = 0;
+    auto stage = [&](uint32_t c0, uint32_t next) {
         __syncthreads();
-        for (uint32_t j = tid; j < (uint32_t)kK1Stage + 2; j += NT) {
-            const uint32_t p = c0 + j;
-            sm.stage[j] = p < n ? S.src[p] : 0u;
-        }
+        reinterpret_cast<uint32_t *>(sm.stage)[tid] = pa;
+        if (tid == 0) reinterpret_cast<uint32_t *>(sm.stage)[NT] = px;
+        if (next < n) fetch(next, pa, px);
         __syncthreads();
         for (uint32_t j = tid; j < (uint32_t)kK1Stage; j += NT)
             sm.hsh[j] = (uint16_t)hash3(sm.stage[j], sm.stage[j + 1], sm.stage[j + 2]);
         __syncthreads();
     };
+    fetch(0, pa, px);
     uint64_t sb = 0, swb = 0;
-    // histogram of the hashes (and the adler32 sums)
+    // histogram of the hashes (and the adler32 sums).  A wave's 64 lanes are 64
+    // consecutive positions; a run of equal hashes among them (runs of one byte
+    // value: most of a DCT index strip) adds its length with one atomic from its
+    // first lane -- 64 lanes adding to one LDS word serialise (round 4's K1 spent
+    // 2.2 bank-conflict cycles per LDS instruction there)
     for (uint32_t c0 = 0; c0 < n; c0 += kK1Stage) {
-        stage(c0);
+        stage(c0, c0 + kK1Stage < n ? c0 + kK1Stage : 0u);   // pass 2 starts at chunk 0 again
         for (uint32_t j = tid; j < (uint32_t)kK1Stage; j += NT) {
             const uint32_t p = c0 + j, b = sm.stage[j];
             sb += b;
             swb += (uint64_t)(p < n ? n - p : 0u) * b;
-            if (p < np) {
-                const uint32_t h = sm.hsh[j];
-                atomicAdd(&sm.cnt[h >> 1], 1u << ((h & 1) * 16));
+            const bool ins = p < np;
+            const uint32_t h = sm.hsh[j];
+            const uint32_t hprev = (uint32_t)__shfl_up((int)h, 1, 64);
+            const bool head = ins && (lane == 0 || hprev != h);
+            const uint64_t heads = __ballot(head), insm = __ballot(ins);
+            if (head) {
+                const uint64_t above = heads & ~((2ull << lane) - 1);   // the next run's first lane, if any
+                const uint32_t end = above ? (uint32_t)__ffsll((unsigned long long)above) - 1
+                                           : (uint32_t)__popcll(insm);   // inserted lanes are a prefix
+                atomicAdd(&sm.cnt[h >> 1], (end - lane) << ((h & 1) * 16));
             }
         }
     }
@@ -308,7 +351,7 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
     uint32_t distinct = 0;   // over the 64-position groups: their distinct hashes in this part
     const uint64_t lt = (1ull << lane) - 1;
     for (uint32_t c0 = 0; c0 < np; c0 += kK1Stage) {
-        stage(c0);
+        stage(c0, c0 + kK1Stage < np ? c0 + kK1Stage : n);
         for (uint32_t g = 0; g < (uint32_t)kK1Stage && c0 + g < np; g += 256) {
             uint32_t h[4], rank[4], cntj[4], old[4];
             uint64_t mine[4];
@@ -319,6 +362,9 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
                 h[q] = sm.hsh[j];
                 v[q] = c0 + j < np && (h[q] >> kHashShiftW) == w;
             }
+            // none of the 256 positions hashes into this wave's part (runs: all but one
+            // wave skip most groups)
+            if (!__ballot(v[0] || v[1] || v[2] || v[3])) continue;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 uint64_t rem = __ballot(v[q]), m0 = 0;
@@ -704,12 +750,24 @@ struct ParseSmem {
 };
 static_assert(offsetof(ParseSmem, lfreq) % 4 == 0, "packed adds into lfreq");
 // the lazy parse's sliding window of the strip: [wbase, wbase + kLazyWin) holds
-// every byte longest_match can read at the current position (back to
-// p - MAX_DIST, ahead to p + MAX_MATCH + 62); the parse shifts it forward in
-// 256-byte steps, so four strips (window + ParseSmem <= 40 KB) fit a CU
-constexpr uint32_t kLazyWin = 34560;
+// the bytes longest_match reads near the current position (back to p -
+// kNearDist, ahead to p + MAX_MATCH + 62); the parse shifts it forward in
+// 256-byte steps.  Candidates farther back (zlib's chains reach p - MAX_DIST)
+// read the strip in HBM.  Round 4 held all of [p - MAX_DIST, p + 320) (34.5 KB,
+// four strips per CU); the lazy parse is a per-wave dependency chain whose
+// throughput follows the strips a CU holds, so the 14 KB window (eight strips
+// per CU) buys more than the far reads cost
+#ifndef VCF_ZX_LAZYWIN   // A/B (diagnostic builds): the window's bytes (a multiple of 256)
+#define VCF_ZX_LAZYWIN 14080
+#endif
+constexpr uint32_t kLazyWin = VCF_ZX_LAZYWIN;
 constexpr uint32_t kLazyAhead = 320;
-static_assert(kLazyWin >= MAX_DIST + kLazyAhead + 1024, "window too short for its shifts");
+// the near distance the window keeps behind p after a shift: candidates at most
+// this far back read the window, farther ones (zlib reaches MAX_DIST back) read
+// the strip in HBM (Wave::far_*); shifts come every ~1 KB
+constexpr uint32_t kNearDist = kLazyWin >= MAX_DIST + kLazyAhead + 1024 ? (uint32_t)MAX_DIST
+                                                                        : kLazyWin - kLazyAhead - 1024;
+static_assert(kLazyWin % 256 == 0 && kNearDist >= 4096, "window too short");
 
 // LAZY (strips K1 found repetitive, kLazyDiv below): zlib's own order of work --
 // the strip in LDS and longest_match evaluated only where deflate_slow calls it
@@ -959,7 +1017,7 @@ struct Wave {
     __device__ __forceinline__ void ensure(uint32_t p)
     {
         if (p + kLazyAhead <= wbase + kLazyWin) return;
-        const uint32_t nb = (p > (uint32_t)MAX_DIST ? p - MAX_DIST : 0u) & ~255u;
+        const uint32_t nb = (p > kNearDist ? p - kNearDist : 0u) & ~255u;
         const uint32_t d = nb - wbase;   // > 0, a multiple of 256
         VCF_ZPROF_COUNT(n_shift);
         uint4 *w = reinterpret_cast<uint4 *>(lwin);
@@ -968,8 +1026,57 @@ struct Wave {
         wave_sync();
         const uint32_t old_end = wbase + kLazyWin;
         wbase = nb;
-        fill(old_end, nb + kLazyWin);
+        // the new bytes: 16 per lane from the strip where they lie inside it (the range is
+        // 256-aligned), the rest (past the end: zeros or the slid copy) one at a time
+        uint32_t from = old_end;
+        const uint32_t to = nb + kLazyWin;
+        if ((((uintptr_t)(src + from)) & 15) == 0) {
+            const uint32_t vend = min(to, n & ~15u);
+            for (uint32_t P = from + 16 * lane_id(); P < vend; P += 1024)
+                w[(P - wbase) >> 4] = *reinterpret_cast<const uint4 *>(src + P);
+            from = max(from, vend);
+        }
+        fill(from, to);
         wave_sync();
+    }
+    // ---- candidates farther back than the window: the strip's bytes in HBM
+    // (c + 274 < p <= n for every such read: real strip bytes, never the
+    // zeros or the slid copy past the end)
+    __device__ __forceinline__ uint32_t g4(uint32_t P) const   // 4 bytes at input position P (unaligned)
+    {
+        uint32_t d;
+        __builtin_memcpy(&d, src + P, 4);
+        return d;
+    }
+    // far_lcp: lane_lcp with the first string at input position c in HBM
+    __device__ __forceinline__ uint32_t far_lcp(uint32_t c, uint32_t b, uint32_t cap, uint32_t from)
+    {
+        uint32_t l = from;
+        while (l < cap) {
+            const uint32_t x0 = g4(c + l) ^ ld4(b + l), x1 = g4(c + l + 4) ^ ld4(b + l + 4);
+            const uint32_t x2 = g4(c + l + 8) ^ ld4(b + l + 8), x3 = g4(c + l + 12) ^ ld4(b + l + 12);
+            if (x0 | x1 | x2 | x3) {
+                l += x0 ? 0 : x1 ? 4 : x2 ? 8 : 12;
+                l += (uint32_t)__builtin_ctz(x0 ? x0 : x1 ? x1 : x2 ? x2 : x3) >> 3;
+                break;
+            }
+            l += 16;
+        }
+        return min(l, (uint32_t)MAX_MATCH);
+    }
+    // wave_lcp with the first string at input position c: from the window when it is there
+    __device__ __forceinline__ uint32_t wave_lcp_at(uint32_t c, uint32_t b)
+    {
+        if (c >= wbase) return wave_lcp(c - wbase, b);
+        const uint32_t x = g4(c + 4 * lane_id()) ^ ld4(b + 4 * lane_id());
+        const uint64_t m = __ballot(x != 0);
+        if (m) {
+            const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
+            return 4 * f + ((uint32_t)__builtin_ctz(lane_val(x, f)) >> 3);
+        }
+        uint32_t l = 256;
+        if (src[c + 256] == lwin[b + 256]) l = src[c + 257] == lwin[b + 257] ? 258 : 257;
+        return l;
     }
     __device__ __forceinline__ uint32_t ld4(uint32_t a)   // window offsets
     {
@@ -1124,7 +1231,7 @@ struct Wave {
             // compare, on every lane (a lane off the chain reads p's own bytes)
             struct RoundRd {
                 uint32_t c, wc, c4, x16[4];
-                bool v;
+                bool v, far;
             };
             auto rd = [&](uint32_t b) -> RoundRd {
                 RoundRd r;
@@ -1132,22 +1239,31 @@ struct Wave {
                 r.v = gk < chain && gk < ip;
                 r.c = !r.v ? 0u : b == 0 ? pre0 : b == 64 ? pre1 : wload16(sorted + ip - 1 - gk);
                 // sorted[] runs on past the bucket: a candidate of another bucket can be any
-                // position, also one outside the window (round 3 held the whole strip in LDS),
-                // so the bucket end must not be judged from window bytes there.  p's own
-                // bucket holds only earlier positions, and those past `limit` are in the
-                // window: c < p first, then the hash from the window.
+                // position, so the bucket end must not be judged from bytes read at it before
+                // it is known to be p's: p's own bucket holds only earlier positions, and those
+                // past `limit` are real strip bytes (in the window, or in HBM when farther back
+                // than the window reaches): c < p first, then the hash.
                 r.v = r.v && r.c < p && (gk == 0 || r.c > limit);
-                r.wc = r.v ? r.c - wbase : wp;
+                r.far = r.v && r.c < wbase;
+                r.wc = r.v && !r.far ? r.c - wbase : wp;
                 r.c4 = ld4(r.wc);
 #pragma unroll
                 for (int u = 0; u < 4; ++u) r.x16[u] = ld4(r.wc + 4 * u) ^ ld4(wp + 4 * u);
+                if (__ballot(r.far)) {   // wave-uniform: this round reaches past the window
+                    if (r.far) {
+                        r.c4 = g4(r.c);
+                        r.x16[0] = r.c4 ^ ld4(wp);
+#pragma unroll
+                        for (int u = 1; u < 4; ++u) r.x16[u] = g4(r.c + 4 * u) ^ ld4(wp + 4 * u);
+                    }
+                }
                 return r;
             };
             // round 0's reads issued with the head compare's (VCF_ZX_EARLY0; 0: in the round)
             RoundRd r0;
             if (VCF_ZX_EARLY0) r0 = rd(0);
             const uint32_t hp = hash_at(wp);
-            const uint32_t l1 = wave_lcp(hdp - wbase, wp);
+            const uint32_t l1 = wave_lcp_at(hdp, wp);
 #if VCF_ZLIB_PROF
             {
                 const unsigned long long th1 = clock64();
@@ -1174,14 +1290,23 @@ struct Wave {
                 const uint32_t gk = b + lane_id();
                 const RoundRd rr = VCF_ZX_EARLY0 && b == 0 ? r0 : rd(b);
                 bool v = rr.v;
+                const bool far = rr.far;
                 const uint32_t c = rr.c, wc = rr.wc, c4 = rr.c4;
                 const uint32_t *x16 = rr.x16;
                 // zlib's scan_end bytes at F (known only after the head compare)
-                const bool se = lwin[wc + F] == lwin[wp + F] && lwin[wc + F - 1] == lwin[wp + F - 1];
+                uint32_t e0 = lwin[wc + F - 1], e1 = lwin[wc + F];
+                if (__ballot(far)) {
+                    if (far) {
+                        e0 = src[c + F - 1];
+                        e1 = src[c + F];
+                    }
+                }
+                const bool se = e1 == lwin[wp + F] && e0 == lwin[wp + F - 1];
 #if VCF_ZX_WINCHECK
                 {
                     const uint32_t want = v ? win_src(c) | win_src(c + 1) << 8 | win_src(c + 2) << 16 | win_src(c + 3) << 24 : c4;
                     wincheck(3u, c, v && c4 != want, c4, want);
+                    wincheck(4u, c, v && !far && c < wbase, c, wbase);   // a near read below the window
                 }
 #endif
                 v = v && hash3(c4 & 0xffu, (c4 >> 8) & 0xffu, (c4 >> 16) & 0xffu) == hp;
@@ -1206,8 +1331,10 @@ struct Wave {
                     if (x) {
                         const uint32_t q = x16[0] ? 0u : x16[1] ? 4u : x16[2] ? 8u : 12u;
                         l = q + ((uint32_t)__builtin_ctz(x16[0] ? x16[0] : x16[1] ? x16[1] : x16[2] ? x16[2] : x16[3]) >> 3);
-                    } else {
+                    } else if (!far) {
                         l = lane_lcp(wc, wp, VCF_ZX_NOCAP ? (uint32_t)MAX_MATCH : Tn, 16u);
+                    } else {
+                        l = far_lcp(c, wp, VCF_ZX_NOCAP ? (uint32_t)MAX_MATCH : Tn, 16u);
                     }
                 }
 #if VCF_ZLIB_PROF
@@ -1226,7 +1353,7 @@ struct Wave {
                 if (hit) {
                     const uint32_t k = (uint32_t)__ffsll((unsigned long long)hit) - 1;
                     pos = lane_val(c, k);
-                    len = k == 0 && b == 0 ? l1 : wave_lcp(pos - wbase, wp);
+                    len = k == 0 && b == 0 ? l1 : wave_lcp_at(pos, wp);
                     return true;
                 }
                 // the first lane with the longest length beyond best: step from improvement
@@ -1353,7 +1480,8 @@ struct ParseShared<true> {
     uint32_t pad[VCF_ZX_LDSPAD / 4];
 #endif
 };
-static_assert(VCF_ZX_LDSPAD || sizeof(ParseShared<true>) <= 40960, "four lazy-parse workgroups per CU");
+static_assert(VCF_ZX_LDSPAD || VCF_ZX_LAZYWIN != 14080 || sizeof(ParseShared<true>) <= 20480,
+              "eight lazy-parse workgroups per CU");
 
 template <bool LAZY>
 __global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
@@ -1479,7 +1607,7 @@ int64_t vcf_zlib_workspace(int64_t n_strips)
 {
     if (n_strips < 0) return -1;
     const ZRounds zr(n_strips);
-    return zr.slots * zr.per * kWsPerStrip;
+    return zr.per * kWsPerStrip;
 }
 
 int64_t vcf_zlib_strip_count(int64_t frame_bytes, int32_t strip_bytes)
@@ -1512,44 +1640,35 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     const int chunks = (int)((std::min<int64_t>(strip_bytes, frame_bytes) + kChunk - 1) / kChunk);
     const unsigned hd_blocks = (unsigned)((std::min<int64_t>(strip_bytes, frame_bytes) + kHdThreads * kHdPer - 1) /
                                           (kHdThreads * kHdPer));
-    // A round: K1 and the head table on the slot's main stream; then the two kinds
-    // of strips side by side -- the lazy parse of the repetitive strips on the main
-    // stream, K2a/K2b and the register-window parse of the others on the slot's side
-    // stream (forked by an event, joined back before the slot's next round reuses
-    // its workspace).  The two sides touch disjoint strips: their own output slots,
+    // A round: K1 and the head table on the caller's stream; then the two kinds of
+    // strips side by side -- the lazy parse of the repetitive strips on the caller's
+    // stream, K2a/K2b and the register-window parse of the others on a library side
+    // stream (forked by an event, joined back before the next round reuses the
+    // workspace).  The two sides touch disjoint strips: their own output slots,
     // sizes and workspace regions; both only read K1's and the head kernel's tables.
-    // Slot 0's main stream is the caller's; slot 1's is a library stream forked from
-    // it at the start and joined back at the end, so the call keeps stream semantics.
+    // (Round 4's two workspace slots with rounds in flight are gone: with the
+    // device-sized budget a call is one round up to ~30 000 strips.)
     AuxStreams &ax = aux_for_current_device();
     std::lock_guard<std::mutex> lock(ax.mu);
     int rc = ax.init();
     if (rc != VCF_OK) return rc;
-    // the side streams at the highest priority: their strips are fewer but each takes
-    // longer (K2b walks every listed position's chain), and as normal-priority queues
-    // their workgroups only got a CU when a lazy parse left one
-    static hipStream_t side_hi[64][2] = {};
+    // the side stream at the highest priority: its strips are fewer but each takes
+    // longer (K2b walks every listed position's chain), and as a normal-priority queue
+    // its workgroups only got a CU when a lazy parse left one
+    static hipStream_t side_hi[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    for (int j = 0; j < 2 && !VCF_ZX_NOPRIO; ++j)
-        if (!side_hi[dev][j]) {
-            int least = 0, greatest = 0;
-            rc = hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-            if (rc == VCF_OK)
-                rc = hip_check(hipStreamCreateWithPriority(&side_hi[dev][j], hipStreamNonBlocking, greatest),
-                               "hipStreamCreateWithPriority");
-            if (rc != VCF_OK) return rc;
-        }
-    const ZRounds zr(total);
-    const int nslots = VCF_ZX_SERIAL ? 1 : (int)zr.slots;
-    hipStream_t main_s[2] = {st, ax.s[1]}, side_s[2];
-    for (int j = 0; j < 2; ++j) side_s[j] = VCF_ZX_SERIAL ? st : VCF_ZX_NOPRIO ? ax.s[2 + j] : side_hi[dev][j];
-    hipEvent_t fork_ev[2] = {ax.big[0], ax.big[1]}, join_ev[2] = {ax.join[0], ax.join[1]};
-    if (nslots > 1) {
-        if ((rc = hip_check(hipEventRecord(ax.fork, st), "hipEventRecord")) != VCF_OK) return rc;
-        if ((rc = hip_check(hipStreamWaitEvent(main_s[1], ax.fork, 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
+    if (!VCF_ZX_NOPRIO && !side_hi[dev]) {
+        int least = 0, greatest = 0;
+        rc = hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+        if (rc == VCF_OK)
+            rc = hip_check(hipStreamCreateWithPriority(&side_hi[dev], hipStreamNonBlocking, greatest),
+                           "hipStreamCreateWithPriority");
+        if (rc != VCF_OK) return rc;
     }
-    auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws, int j) -> int {
-        hipStream_t ms = main_s[j], ss = side_s[j];
+    const ZRounds zr(total);
+    const hipStream_t ms = st, ss = VCF_ZX_SERIAL ? st : VCF_ZX_NOPRIO ? ax.s[2] : side_hi[dev];
+    auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws) -> int {
         hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64 * kK1Waves), 0, ms, in_dev, frame_bytes, strip_bytes,
                            (int32_t)spf, ws, s0);
         int rc = hip_check(hipGetLastError(), "zlib_order_kernel launch");
@@ -1559,8 +1678,8 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
         rc = hip_check(hipGetLastError(), "zlib_head_kernel launch");
         if (rc != VCF_OK) return rc;
         if (ss != ms) {
-            if ((rc = hip_check(hipEventRecord(fork_ev[j], ms), "hipEventRecord")) != VCF_OK) return rc;
-            if ((rc = hip_check(hipStreamWaitEvent(ss, fork_ev[j], 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
+            if ((rc = hip_check(hipEventRecord(ax.big[0], ms), "hipEventRecord")) != VCF_OK) return rc;
+            if ((rc = hip_check(hipStreamWaitEvent(ss, ax.big[0], 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
         }
         hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, ss, in_dev,
                            frame_bytes, strip_bytes, (int32_t)spf, level, ws, s0);
@@ -1580,25 +1699,16 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
                                (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
             rc = hip_check(hipGetLastError(), "zlib_parse_kernel (lazy) launch");
         }
-        // join the side stream even after an error, so the main stream never runs ahead
+        // join the side stream even after an error, so the caller's stream never runs ahead
         if (ss != ms) {
-            int r2 = hip_check(hipEventRecord(join_ev[j], ss), "hipEventRecord");
-            if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(ms, join_ev[j], 0), "hipStreamWaitEvent");
+            int r2 = hip_check(hipEventRecord(ax.join[0], ss), "hipEventRecord");
+            if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(ms, ax.join[0], 0), "hipStreamWaitEvent");
             if (rc == VCF_OK) rc = r2;
         }
         return rc;
     };
-    int r = 0;
-    for (int64_t s0 = 0; s0 < total && rc == VCF_OK; s0 += zr.per, ++r) {
-        const int j = r % nslots;
-        rc = round(s0, (unsigned)std::min<int64_t>(zr.per, total - s0),
-                   (uint8_t *)ws_dev + (int64_t)j * zr.per * kWsPerStrip, j);
-    }
-    if (nslots > 1) {   // slot 1's stream joins the caller's, also after an error
-        int r2 = hip_check(hipEventRecord(ax.join[2], main_s[1]), "hipEventRecord");
-        if (r2 == VCF_OK) r2 = hip_check(hipStreamWaitEvent(st, ax.join[2], 0), "hipStreamWaitEvent");
-        if (rc == VCF_OK) rc = r2;
-    }
+    for (int64_t s0 = 0; s0 < total && rc == VCF_OK; s0 += zr.per)
+        rc = round(s0, (unsigned)std::min<int64_t>(zr.per, total - s0), (uint8_t *)ws_dev);
     return rc;
 }
 
