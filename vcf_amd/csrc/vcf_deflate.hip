@@ -755,19 +755,23 @@ static_assert(offsetof(ParseSmem, lfreq) % 4 == 0, "packed adds into lfreq");
 // 256-byte steps.  Candidates farther back (zlib's chains reach p - MAX_DIST)
 // read the strip in HBM.  Round 4 held all of [p - MAX_DIST, p + 320) (34.5 KB,
 // four strips per CU); the lazy parse is a per-wave dependency chain whose
-// throughput follows the strips a CU holds, so the 14 KB window (eight strips
-// per CU) buys more than the far reads cost
+// throughput follows the strips a CU holds, so smaller windows buy more than
+// their far reads cost, down to the 3 840-byte window that makes 16 strips per
+// CU (C4 deflate, ms: 34 560 B 245, 18 432 B 212, 14 080 B 189, 9 984 B 182,
+// 8 448 B 176, 7 168 B 172, 5 120 B 165, 3 840 B 161; 3 072 / 2 304 B 161 / 159:
+// no more than 16 workgroups reside on a CU)
 #ifndef VCF_ZX_LAZYWIN   // A/B (diagnostic builds): the window's bytes (a multiple of 256)
-#define VCF_ZX_LAZYWIN 14080
+#define VCF_ZX_LAZYWIN 3840
 #endif
 constexpr uint32_t kLazyWin = VCF_ZX_LAZYWIN;
 constexpr uint32_t kLazyAhead = 320;
 // the near distance the window keeps behind p after a shift: candidates at most
 // this far back read the window, farther ones (zlib reaches MAX_DIST back) read
 // the strip in HBM (Wave::far_*); shifts come every ~1 KB
-constexpr uint32_t kNearDist = kLazyWin >= MAX_DIST + kLazyAhead + 1024 ? (uint32_t)MAX_DIST
-                                                                        : kLazyWin - kLazyAhead - 1024;
-static_assert(kLazyWin % 256 == 0 && kNearDist >= 4096, "window too short");
+constexpr uint32_t kShiftSlack = kLazyWin >= 8192 ? 1024 : 512;   // bytes a shift leaves ahead
+constexpr uint32_t kNearDist = kLazyWin >= MAX_DIST + kLazyAhead + kShiftSlack ? (uint32_t)MAX_DIST
+                                                                               : kLazyWin - kLazyAhead - kShiftSlack;
+static_assert(kLazyWin % 256 == 0 && kNearDist >= 512, "window too short");
 
 // LAZY (strips K1 found repetitive, kLazyDiv below): zlib's own order of work --
 // the strip in LDS and longest_match evaluated only where deflate_slow calls it
@@ -1480,11 +1484,16 @@ struct ParseShared<true> {
     uint32_t pad[VCF_ZX_LDSPAD / 4];
 #endif
 };
-static_assert(VCF_ZX_LDSPAD || VCF_ZX_LAZYWIN != 14080 || sizeof(ParseShared<true>) <= 20480,
-              "eight lazy-parse workgroups per CU");
+static_assert(VCF_ZX_LDSPAD || VCF_ZX_LAZYWIN != 3840 || sizeof(ParseShared<true>) <= 10240,
+              "sixteen lazy-parse workgroups per CU");
 
+#ifdef VCF_ZX_WPE   // A/B (diagnostic builds): registers capped for this many waves per SIMD
+#define VCF_ZX_WPE_ATTR __attribute__((amdgpu_waves_per_eu(VCF_ZX_WPE, VCF_ZX_WPE)))
+#else
+#define VCF_ZX_WPE_ATTR
+#endif
 template <bool LAZY>
-__global__ __launch_bounds__(64) void zlib_parse_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+__global__ __launch_bounds__(64) VCF_ZX_WPE_ATTR void zlib_parse_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
                                                        int32_t strip_bytes, int32_t spf, int32_t level,
                                                        uint8_t *__restrict__ out, int64_t slot_bytes,
                                                        int32_t *__restrict__ sizes, uint8_t *__restrict__ ws,
