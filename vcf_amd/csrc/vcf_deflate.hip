@@ -113,8 +113,15 @@ constexpr int kK2bSplit = VCF_ZX_K2BSPLIT;   // K2b: workgroups per strip, the l
 // one distinct hash per kLazyDiv positions among its 64-position groups: such
 // repetitive content leaves most positions inside long matches, which zlib -- and
 // the lazy parse -- never search, while K2 would search them all.  Both orders
-// produce the same bytes; only the time differs.
-constexpr uint32_t kLazyDiv = 4;
+// produce the same bytes; only the time differs.  kLazyDiv 2
+// (round 4: 4) sends C4's borderline strips -- 3 % of them -- to the lazy parse
+// too: its side stream of K2a/K2b/K3 no longer competes with the lazy parse for
+// the CUs (C4 deflate 160 -> 107 ms), and raw RGB strips still take K2 (561 ms
+// either way; every strip lazy: 864 ms).
+#ifndef VCF_ZX_LAZYDIV   // A/B (diagnostic builds)
+#define VCF_ZX_LAZYDIV 2
+#endif
+constexpr uint32_t kLazyDiv = VCF_ZX_LAZYDIV;
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
@@ -421,7 +428,11 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
         sums[0] = a;
         sums[1] = b;
         *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 16) = 0;   // K2's worklist length
+#ifdef VCF_ZX_LAZYALL   // A/B (diagnostic builds): every strip through the lazy parse
+        *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = 1u;
+#else
         *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = dsum * kLazyDiv < np ? 1u : 0u;   // parse order
+#endif
     }
 }
 
