@@ -372,6 +372,22 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
             // none of the 256 positions hashes into this wave's part (runs: all but one
             // wave skip most groups)
             if (!__ballot(v[0] || v[1] || v[2] || v[3])) continue;
+            // all 256 positions in this part with one hash (inside a run of one byte
+            // value): their slots are the bucket cursor + 0..255, one atomic
+            const uint32_t h0 = uni(h[0]);
+            if (!__ballot(!(v[0] && v[1] && v[2] && v[3] && h[0] == h0 && h[1] == h0 && h[2] == h0 && h[3] == h0))) {
+                distinct += 4;   // one per 64-position group, as below
+                uint32_t o = 0;
+                if (lane == 0) o = atomicAdd(&sm.cnt[h0 >> 1], 256u << ((h0 & 1) * 16));
+                const uint32_t base = (uni(o) >> ((h0 & 1) * 16)) & 0xffffu;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t p = c0 + g + 64 * q + lane, slot = base + 64 * q + lane;
+                    idx[p] = (uint16_t)slot;
+                    sorted[slot] = (uint16_t)p;
+                }
+                continue;
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 uint64_t rem = __ballot(v[q]), m0 = 0;
