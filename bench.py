@@ -539,6 +539,55 @@ def c3_block(args, world: int, rank: int, group, frames):
                                         "frac": round(ops / (kms * 1e-3) / 1e12 / FP64_ISSUE_TOPS, 4),
                                         "fp64_ops_per_launch": int(ops),
                                         "ops_per_pixel": round(c3_fp64_ops_per_pixel(), 2)}}
+        # the opt-in lifting form (vcf_dwt_dz_*_lift, not bit-exact): the same
+        # timing, and its frame-0 output against the bit-exact path's
+        dpk_l, dout_l = DeviceBuffer(F * pb), DeviceBuffer(F * Ho * Wo * 3)
+        enc_l = lambda: DW.encode_device(din, F, H, W, w, Lv, Q, dpk_l, dws, st, lifting=True)   # noqa: E731
+        dec_l = lambda: DW.decode_device(dpk, F, H, W, w, Lv, Q, dout_l, dws, st, lifting=True)  # noqa: E731
+        lift = {"entry_points": "vcf_dwt_dz_encode_lift / vcf_dwt_dz_decode_lift (opt-in, +-1 tolerance)"}
+        for name, fn in (("encode", enc_l), ("decode", dec_l)):
+            for _ in range(3):
+                fn()
+            settle(fn, st, Event, 0.5, 3.0, chunk=8)
+            e0, e1 = Event(), Event()
+            group.barrier()
+            synchronize()
+            t0 = time.perf_counter()
+            e0.record(st)
+            for _ in range(args.c3_steps):
+                fn()
+            e1.record(st)
+            st.synchronize()
+            wall = (time.perf_counter() - t0) / args.c3_steps
+            wall = group.allreduce_max(wall) if world > 1 else wall
+            lift[name] = {"ms": round(wall * 1e3, 4), "value": round(world * F * H * W / wall / 1e6, 1),
+                          "unit": "Mpixels/s", "launch_ms_events": round(e0.elapsed_ms(e1) / args.c3_steps, 4)}
+        enc()   # the bit-exact subbands back in dpk, decoded into dout; dout_l = lifting decode of them
+        dec()
+        dec_l()
+        st.synchronize()
+        ex = DW.unpack(dpk.download(np.empty(pb, np.uint8)), H, W, Lv)
+        enc_l()
+        st.synchronize()
+        li = DW.unpack(dpk_l.download(np.empty(pb, np.uint8)), H, W, Lv)
+        bad = tot = worst = 0
+        for nm, v in ex.items():
+            d = v.astype(np.int64) - li[nm].astype(np.int64)
+            if not nm.startswith("LL"):
+                d = (d + 128) % 256 - 128
+            bad += int(np.count_nonzero(d))
+            tot += d.size
+            worst = max(worst, int(np.abs(d).max()))
+        ye = dout.download(np.empty((Ho, Wo, 3), np.uint8)).astype(np.int64)
+        yl = dout_l.download(np.empty((Ho, Wo, 3), np.uint8)).astype(np.int64)
+        lift["vs_bit_exact_frame0"] = {"indices_differing": bad, "indices": tot, "max_index_diff": worst,
+                                       "decoded_bytes_differing": int(np.count_nonzero(ye - yl)),
+                                       "max_byte_diff": int(np.abs(ye - yl).max())}
+        st.synchronize()
+        enc()   # leave the bit-exact subbands for the checker
+        dec()
+        st.synchronize()
+        info["lifting"] = lift
         if rank == 0:
             info["_check"] = (dpk, dout, pb, Ho, Wo)
     except Exception as e:   # reported in the block; the headline line still prints

@@ -1,5 +1,6 @@
 """Run the 2D-DWT encode (8 4K frames, l=5, bior4.4) N times with one variant: for rocprofv3 --pmc passes.
-python scripts/dwt_once.py VARIANT [N]   (DECODE=1: the decode of those frames' subbands)"""
+python scripts/dwt_once.py VARIANT [N]   (DECODE=1: the decode of those frames' subbands;
+LIFT=1: the opt-in lifting entry points instead of VARIANT)"""
 import os
 import sys
 
@@ -20,12 +21,20 @@ _, pb, wb = DW.layout(H, W, LV)
 frames = np.stack([bench.synth_frame(H, W, s) for s in range(F)])
 din, dws, dout = DeviceBuffer.from_array(frames), DeviceBuffer(F * wb), DeviceBuffer(F * pb)
 s = Stream()
+if os.environ.get("LIFT", "0") == "1":
+    def enc(*a):
+        L.call("vcf_dwt_dz_encode_lift", *a[1:])
+
+    def dec(*a):
+        L.call("vcf_dwt_dz_decode_lift", *a[1:])
+else:
+    enc, dec = L.dwt_encode_v, L.dwt_decode_v
 if os.environ.get("DECODE", "0") == "1":
     L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
     for _ in range(n):
-        L.dwt_decode_v(v, dout.ptr, F, H, W, w, LV, Q, din.ptr, dws.ptr, s.handle)
+        dec(v, dout.ptr, F, H, W, w, LV, Q, din.ptr, dws.ptr, s.handle)
 else:
     for _ in range(n):
-        L.dwt_encode_v(v, din.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
+        enc(v, din.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
 s.synchronize()
 print("ok", v, n)

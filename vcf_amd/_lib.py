@@ -113,6 +113,8 @@ SIGNATURES = {
     "vcf_dwt_layout": [_I32, _I32, _I32, _PI32, _PI32, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     "vcf_dwt_dz_encode": [_P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
     "vcf_dwt_dz_decode": [_P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
+    "vcf_dwt_dz_encode_lift": [_P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
+    "vcf_dwt_dz_decode_lift": [_P, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
     "vcf_ipp_block_match": [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P],
     "vcf_ipp_set_full_search_variant": [_I32],
     "vcf_ipp_motion_compensate": [_P, _P, _I32, _I32, _I32, _P, _P],

@@ -11,6 +11,7 @@ on the GPU through libvcf_amd.so (vcf_dwt_dz_encode / vcf_dwt_dz_decode).
 from __future__ import annotations
 
 import logging
+import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -47,6 +48,11 @@ class CoDec(EICCoDec):
         self.entropy = TIFFCodec()
         self.file_extension = self.entropy.file_extension
         self.QSS = int(getattr(args, "QSS", 32))
+        # opt-in (no reference counterpart): the lifting form of bior4.4, within
+        # +-1 of the bit-exact path; args.dwt_lifting or VCF_DWT_LIFTING=1
+        self.lifting = bool(getattr(args, "dwt_lifting", False)) or os.environ.get("VCF_DWT_LIFTING") == "1"
+        if self.lifting and self.wavelet != "bior4.4":
+            raise NotImplementedError("the lifting path is bior4.4 (CDF 9/7) only")
         logging.info(f"levels = {self.levels}")
         logging.info(f"wavelet={self.wavelet}")
 
@@ -72,7 +78,7 @@ class CoDec(EICCoDec):
         img = self.encode_read_fn(in_fn)
         if img.ndim != 3 or img.shape[2] != 3 or img.dtype != np.uint8:
             raise ValueError("Input image must be a 3D array (height, width, channels).")
-        subbands = DW.encode(img, self.wavelet, self.levels, self.QSS)[0]
+        subbands = DW.encode(img, self.wavelet, self.levels, self.QSS, lifting=self.lifting)[0]
         return self.write_decom_fn(subbands, out_fn)
 
     def encode(self):
@@ -95,7 +101,7 @@ class CoDec(EICCoDec):
     def decode_fn(self, in_fn, out_fn):
         subbands = self.read_decom_fn(in_fn)
         H, W = self._geometry(subbands)
-        y = DW.decode(subbands, H, W, self.wavelet, self.levels, self.QSS)
+        y = DW.decode(subbands, H, W, self.wavelet, self.levels, self.QSS, lifting=self.lifting)
         size = self.decode_write_fn(y, out_fn)
         self.BPP = (self.total_input_size * 8) / (y.shape[0] * y.shape[1])
         return size
@@ -119,7 +125,7 @@ class CoDec(EICCoDec):
                 sbs = [None] * len(chunk)
                 for shape, idx in groups.items():
                     for j, sb in zip(idx, DW.encode(np.stack([imgs[i] for i in idx]), self.wavelet, self.levels,
-                                                    self.QSS)):
+                                                    self.QSS, lifting=self.lifting)):
                         sbs[j] = sb
                 for i, s in enumerate(pool.map(lambda i: self.write_decom_fn(sbs[i], chunk[i][1]), range(len(chunk)))):
                     sizes[b0 + i] = s

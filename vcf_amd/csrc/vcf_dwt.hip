@@ -1229,6 +1229,8 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
 
 // line-based inverse level (the default for 10-tap filters)
 #include "vcf_idwt_line.h"
+// the opt-in lifting form of bior4.4 (not bit-exact)
+#include "vcf_dwt_lift.h"
 
 #ifndef VCF_DWT_KERNELS_ONLY   // (micro-experiments compile the kernels alone)
 // ---------------------------------------------------------------------------
@@ -1654,6 +1656,48 @@ bool pipeline_default(long long n_frames, int H, int W) { return n_frames >= 2 &
 // streams, and every decode pipeline were slower -- DESIGN.md §6)
 constexpr PipeShape kEncodePipe{2, 2, false};
 
+// ---------------------------------------------------------------------------
+// lifting path (vcf_dwt_lift.h): launches
+// ---------------------------------------------------------------------------
+// resident workgroups of one kernel on the device
+template <typename K>
+int resident_slots(K kern, int threads)
+{
+    int dev = 0, n_cu = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+        n_cu = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 4;
+    return n_cu * per_cu;
+}
+
+// band rows of a lifting launch: time ~ (rounds of resident workgroups) x
+// (row pairs per band + the 4 of the pipeline's warm-up)
+int lift_brows(long long per_band, int rows, int slots)
+{
+    int n_bands = 1;
+    long long best = -1;
+    for (int nb = 1; nb <= rows; ++nb) {
+        const int br = (rows + nb - 1) / nb;
+        if (nb > 1 && (rows + br - 1) / br != nb) continue;
+        const long long rounds = (per_band * nb + slots - 1) / slots;
+        const long long cost = rounds * (br + 4);
+        if (best < 0 || cost < best) {
+            best = cost;
+            n_bands = nb;
+        }
+    }
+    return (rows + n_bands - 1) / n_bands;
+}
+
+int lift_check(int wavelet)
+{
+    if (strcmp(kWavelets[wavelet].name, "bior4.4") != 0)
+        return set_error(VCF_ERR_INVALID, "lifting path: bior4.4 (CDF 9/7) only, not %s", kWavelets[wavelet].name);
+    return VCF_OK;
+}
+
 #endif  // VCF_DWT_KERNELS_ONLY
 }  // namespace
 }  // namespace vcf
@@ -1861,6 +1905,86 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
     hipLaunchKernelGGL(dwt_to_rgb_kernel, dim3((unsigned)((npx + 255) / 256), (unsigned)n_frames), dim3(256), 0, s,
                        prev, ws_stride, rgb_dev, npx, npx * 3);
     return hip_check(hipGetLastError(), "dwt to_rgb launch");
+}
+
+// The lifting path (vcf_dwt_lift.h): bior4.4 only, same buffers, layout and
+// workspace as vcf_dwt_dz_encode / _decode; results within +-1 of theirs.
+int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
+                           int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, void *stream)
+{
+    int rc = check_dwt(rgb_dev, packed_dev, n_frames, H, W, wavelet, levels, Q, false);
+    if (rc != VCF_OK || (rc = lift_check(wavelet)) != VCF_OK) return rc;
+    if (n_frames == 0) return VCF_OK;
+    if (!workspace_dev) return set_error(VCF_ERR_INVALID, "null workspace");
+    hipStream_t s = (hipStream_t)stream;
+    DwtGeom g;
+    dwt_geom(H, W, levels, 10, g);
+    const long long pd = plane_doubles(g);
+    // (the second plane starts 16-byte aligned: the kernels' double2 loads)
+    double *P[2] = {(double *)workspace_dev, (double *)workspace_dev + ((long long)g.hs[1] * g.ws[1] + 1) / 2 * 2};
+    for (int l = 1; l <= levels; ++l) {
+        const int h = g.hs[l - 1], w = g.ws[l - 1], hh = g.hs[l], hw = g.ws[l];
+        const bool first = l == 1, last = l == levels;
+        const int n_strips = (hw + lift::kValid - 1) / lift::kValid;
+        // the branch-free body for even planes with dword-aligned subband rows, else the general one
+        const bool aligned = w == 2 * hw && hw % 4 == 0 && g.packed_bytes % 4 == 0 && g.sb_off[l][0] % 4 == 0 &&
+                             (g.sb_off[l][1] - g.sb_off[l][0]) % 4 == 0;
+        const int n_int = aligned ? n_strips : 0;
+        const long long per_band = n_frames * n_strips;
+        auto kern = first ? (last ? lift::lift_fwd_kernel<true, true> : lift::lift_fwd_kernel<true, false>)
+                          : (last ? lift::lift_fwd_kernel<false, true> : lift::lift_fwd_kernel<false, false>);
+        const int brows = lift_brows(per_band, hh, resident_slots(kern, lift::kNT));
+        const int n_bands = (hh + brows - 1) / brows, n_edge = n_strips - n_int;
+        const int brows_e = brows, n_bands_e = n_bands;
+        const long long edge_blocks = n_frames * n_edge * n_bands_e;
+        const long long grid = n_frames * n_int * n_bands + edge_blocks;
+        if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, rgb_dev, (long long)H * W * 3,
+                           first ? nullptr : P[l & 1], pd, P[(l - 1) & 1], packed_dev, g.packed_bytes, g.ll_off,
+                           g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], h, w, hh, hw, Q, n_int, n_edge, n_bands,
+                           brows, n_bands_e, brows_e, (int)edge_blocks);
+        if ((rc = hip_check(hipGetLastError(), "lift_fwd_kernel launch")) != VCF_OK) return rc;
+    }
+    return VCF_OK;
+}
+
+int vcf_dwt_dz_decode_lift(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
+                           int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, void *stream)
+{
+    int rc = check_dwt(packed_dev, rgb_dev, n_frames, H, W, wavelet, levels, Q, true);
+    if (rc != VCF_OK || (rc = lift_check(wavelet)) != VCF_OK) return rc;
+    if (n_frames == 0) return VCF_OK;
+    if (!workspace_dev) return set_error(VCF_ERR_INVALID, "null workspace");
+    hipStream_t s = (hipStream_t)stream;
+    DwtGeom g;
+    dwt_geom(H, W, levels, 10, g);
+    const long long pd = plane_doubles(g);
+    double *P[2] = {(double *)workspace_dev, (double *)workspace_dev + ((long long)g.hs[1] * g.ws[1] + 1) / 2 * 2};
+    for (int r = levels; r >= 1; --r) {
+        const int h = g.hs[r], w = g.ws[r];
+        const int oh = r > 1 ? g.hs[r - 1] : 2 * h, ow = r > 1 ? g.ws[r - 1] : 2 * w;
+        const bool coarsest = r == levels, rgb = r == 1;
+        const int n_strips = (w + lift::kValid - 1) / lift::kValid;
+        // the branch-free body for even planes (and even trimmed outputs), else the general one
+        const bool aligned = w % 2 == 0 && ow % 2 == 0;
+        const int n_int = aligned ? n_strips : 0;
+        const long long per_band = n_frames * n_strips;
+        auto kern = coarsest ? (rgb ? lift::lift_inv_kernel<true, true> : lift::lift_inv_kernel<true, false>)
+                             : (rgb ? lift::lift_inv_kernel<false, true> : lift::lift_inv_kernel<false, false>);
+        const int brows = lift_brows(per_band, h, resident_slots(kern, lift::kNT));
+        const int n_bands = (h + brows - 1) / brows, n_edge = n_strips - n_int;
+        const int brows_e = brows, n_bands_e = n_bands;
+        const long long edge_blocks = n_frames * n_edge * n_bands_e;
+        const long long grid = n_frames * n_int * n_bands + edge_blocks;
+        if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
+        // level r reads the plane level r + 1 wrote (h x w, row stride w) and writes the other
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, packed_dev, g.packed_bytes, g.ll_off,
+                           g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], coarsest ? nullptr : P[(r + 1) & 1], pd,
+                           w, P[r & 1], rgb_dev, (long long)(2 * g.hs[1]) * (2 * g.ws[1]) * 3, h, w, oh, ow, Q, n_int,
+                           n_edge, n_bands, brows, n_bands_e, brows_e, (int)edge_blocks);
+        if ((rc = hip_check(hipGetLastError(), "lift_inv_kernel launch")) != VCF_OK) return rc;
+    }
+    return VCF_OK;
 }
 
 }  // extern "C"

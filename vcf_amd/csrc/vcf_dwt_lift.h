@@ -1,0 +1,575 @@
+// vcf_dwt_lift.h -- the opt-in lifting form of the bior4.4 (CDF 9/7) 2D-DWT
+// + deadzone encode and decode (vcf_dwt_dz_encode_lift / _decode_lift),
+// included by vcf_dwt.hip.
+//
+// NOT bit-exact.  The product entry points (vcf_dwt_dz_encode / _decode)
+// compute pywt's 'per' convolution tap by tap in pywt's order, which costs
+// 16 float64 products + 16 sums per sample and axis (the C3 decode's level 1
+// alone sits on the fp64 issue rate).  The same biorthogonal
+// transform factors into four lifting steps and a scaling (Daubechies &
+// Sweldens; the constants below):
+//   forward, pairs (s_n, e_n) = (x[2n], x[2n+1]) of the periodic line:
+//     e += a (s_n + s_n+1);  s += b (e_n-1 + e_n);  e += g (s_n + s_n+1);
+//     s += d (e_n-1 + e_n);  cA = K s,  cD = -e / K
+//   inverse: the same steps undone in reverse order.
+// pywt's 'per' mode pads an odd line with a copy of its last sample (the
+// forward here does the same); the phase of the pairs matches pywt's
+// periodized bior4.4 exactly.  4 fused multiply-adds per sample and axis in
+// place of 32 operations, but different roundings: an index or an output byte
+// can land one step off the bit-exact path where a value sits on a
+// quantization (or the final truncation) boundary.  Measured tolerance
+// (tests/test_dwt_lift_gpu.py): every index and every decoded byte within +-1
+// of the bit-exact path; no differences on the C3 synthetic 4K frame or on
+// uniform-noise frames, a few 1e-4 of the indices and up to half of the
+// decoded bytes of a flat white frame (255.0 reconstructed as 254.99999...).
+//
+// Kernels: one wave per (frame, YCoCg channel, strip of 124 coefficient
+// columns, band of rows); a workgroup = the three channel waves of one strip
+// and band.  Lane l holds coefficient columns j, j + 1 (j = strip * 124 - 2 +
+// 2 l), i.e. the four sample columns 2j .. 2j + 3, so the horizontal lifting
+// runs across the wave with one DPP lane shift per step (no LDS, no barrier)
+// and coefficient pairs 2..125 of the wave come out exact (4 steps reach +-2
+// pairs).  The vertical lifting streams down the band one row pair per step
+// with the pipeline state in registers (5 doubles per column forward, 4
+// inverse); a band of B output row pairs reads B + 4.  Every level is one
+// launch; LL planes are float64 in the caller's workspace (the product path's
+// workspace layout is big enough), details and the last LL go straight into
+// the packed layout.  Level 1 of the encode stages its RGB rows through LDS
+// (two dwords per thread), every level its detail bytes (dword stores), and
+// level 1 of the decode meets the three channels in LDS to form RGB.
+#pragma once
+
+namespace lift {
+
+// CDF 9/7 lifting constants (bior4.4)
+constexpr double kA = -1.586134342059924;
+constexpr double kB = -0.052980118572961;
+constexpr double kG = 0.882911075530934;
+constexpr double kD = 0.443506852043971;
+constexpr double kK = 1.149604398860241;
+constexpr double kIK = 1.0 / 1.149604398860241;
+
+constexpr int kP = 2;                   // coefficient pairs per lane (4 sample columns)
+constexpr int kValid = 64 * kP - 4;     // exact coefficient columns per wave: pairs 2 .. 64 kP - 3
+constexpr int kNT = 192;                // threads per workgroup: one wave per YCoCg channel
+
+// lane i <- lane i + 1 / i - 1 across the whole wave: DPP wave_shl:1 / wave_shr:1,
+// one VALU move per dword (the end lanes read 0: halo lanes, their values unused)
+template <int CTRL>
+__device__ __forceinline__ double dpp_move(double v)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32));
+}
+__device__ __forceinline__ double from_next(double v) { return dpp_move<0x130>(v); }   // wave_shl:1
+__device__ __forceinline__ double from_prev(double v) { return dpp_move<0x138>(v); }   // wave_shr:1
+
+// forward lifting of one row: the lane's two pairs (s[k], e[k]) = samples
+// (x[2j+2k], x[2j+2k+1]) -> (cA, cD) = (K s, -e / K); one lane shift per step
+__device__ __forceinline__ void fwd_row(double (&s)[2], double (&e)[2])
+{
+    e[0] = __builtin_fma(kA, s[0] + s[1], e[0]);
+    e[1] = __builtin_fma(kA, s[1] + from_next(s[0]), e[1]);
+    s[0] = __builtin_fma(kB, from_prev(e[1]) + e[0], s[0]);
+    s[1] = __builtin_fma(kB, e[0] + e[1], s[1]);
+    e[0] = __builtin_fma(kG, s[0] + s[1], e[0]);
+    e[1] = __builtin_fma(kG, s[1] + from_next(s[0]), e[1]);
+    s[0] = __builtin_fma(kD, from_prev(e[1]) + e[0], s[0]);
+    s[1] = __builtin_fma(kD, e[0] + e[1], s[1]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        s[k] = kK * s[k];
+        e[k] = -e[k] * kIK;
+    }
+}
+
+// inverse lifting of one row: (a[k], d[k]) = (cA, cD) of the lane's two
+// pairs -> samples (x[2j+2k], x[2j+2k+1])
+__device__ __forceinline__ void inv_row(double (&a)[2], double (&d)[2])
+{
+    double s[2] = {a[0] * kIK, a[1] * kIK}, e[2] = {-d[0] * kK, -d[1] * kK};
+    s[0] = __builtin_fma(-kD, from_prev(e[1]) + e[0], s[0]);
+    s[1] = __builtin_fma(-kD, e[0] + e[1], s[1]);
+    e[0] = __builtin_fma(-kG, s[0] + s[1], e[0]);
+    e[1] = __builtin_fma(-kG, s[1] + from_next(s[0]), e[1]);
+    s[0] = __builtin_fma(-kB, from_prev(e[1]) + e[0], s[0]);
+    s[1] = __builtin_fma(-kB, e[0] + e[1], s[1]);
+    e[0] = __builtin_fma(-kA, s[0] + s[1], e[0]);
+    e[1] = __builtin_fma(-kA, s[1] + from_next(s[0]), e[1]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        a[k] = s[k];
+        d[k] = e[k];
+    }
+}
+
+// workgroup barrier ordering LDS only: __syncthreads() also orders global
+// memory, which on gfx950 waits for every load and store in flight
+// (vmcnt(0)) -- the row prefetch and the last step's stores -- at each step
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ int wrap(int i, int n)
+{
+    i %= n;
+    return i < 0 ? i + n : i;
+}
+
+// the int16 YCoCg sample (A4): R/4 + G/2 + B/4, R/2 - B/2, -R/4 + G/2 - B/4
+// are exact in float64 and truncated toward zero -- integer division here.
+// ch must be wave-uniform (a scalar branch).
+__device__ __forceinline__ double ycocg(int R, int G, int B, int ch)
+{
+    const int v = ch == 0 ? (R + 2 * G + B) >> 2 : (ch == 1 ? (R - B) / 2 : (2 * G - R - B) / 4);
+    return (double)v;
+}
+
+__device__ __forceinline__ double ycocg(const uint8_t *px, int ch) { return ycocg(px[0], px[1], px[2], ch); }
+
+// Two bodies.  Planes whose rows are whole dwords and whose pairs never
+// straddle the periodic wrap (w = 2 hw, hw % 4 == 0 forward; w even inverse:
+// every C3 level) run a branch-free body (EDGE = false): every global load
+// and store is issued unconditionally -- halo lanes' and past-the-row stores
+// are buffer stores dropped past the buffer, the wrap is modular addressing
+// -- so the compiler's wait counts stay exact and one step's stores stay in
+// flight over the next step's loads (gfx950 counts both in vmcnt; a store
+// under a lane branch made it wait for everything: 460 -> 234 us on C3's
+// level 1).  Other shapes take the general body (EDGE = true).
+__device__ __forceinline__ int strip_of(bool, int idx, int) { return idx; }
+
+constexpr uint32_t kDrop = 0x80000000u;   // a buffer offset past any buffer: the store is dropped
+typedef unsigned int U32x2 __attribute__((__vector_size__(8)));
+typedef unsigned int U32x4 __attribute__((__vector_size__(16)));
+
+__device__ __forceinline__ U32x4 pack2(double a, double b)
+{
+    const U32x2 x = __builtin_bit_cast(U32x2, a), y = __builtin_bit_cast(U32x2, b);
+    return U32x4{x[0], x[1], y[0], y[1]};
+}
+
+// one forward level: plane h x w (level 1: the RGB frame) -> LL hh x hw
+// (float64 plane, or u16 packed at the last level) and the three detail
+// subbands (u8 packed)
+constexpr int kRowDw = 64 * kP * 2 * 3 / 4;            // dwords of one staged RGB row
+constexpr int kSbB = kValid * 3, kSbDw = 3 * kSbB / 4;  // bytes of one subband row, dwords of three
+
+template <bool FIRST, bool LAST, bool EDGE>
+__device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, long long rgb_stride,
+                                              const double *__restrict__ in, long long plane_stride,
+                                              double *__restrict__ LLout, uint8_t *__restrict__ packed,
+                                              long long packed_stride, long long ll_off, long long off_lh,
+                                              long long off_hl, long long off_hh, int h, int w, int hh, int hw, int Q,
+                                              int n_int, int n_set, int n_bands, int brows, int bid,
+                                              uint32_t *px_lds, uint32_t *sb_lds)
+{
+    // byte staging through LDS (interior strips; double-buffered, one barrier
+    // each): level 1's two RGB rows of 256 pixels come in as two dwords per
+    // thread, and the three detail subbands' kValid x 3 interleaved bytes
+    // leave as dwords (+ one dummy dword for the halo lanes' bytes)
+    const int t = threadIdx.x, lane = t & 63, ch = __builtin_amdgcn_readfirstlane(t >> 6);
+    int b = bid;
+    const int strip = strip_of(EDGE, b % n_set, n_int);
+    b /= n_set;
+    const int band = b % n_bands;
+    const long long frame = b / n_bands;
+    const long long plane = frame * 3 + ch;
+    const int jl = strip * kValid - 2 + kP * lane;             // the lane's first coefficient column
+    int col[2 * kP];                                           // its sample columns
+    uint32_t drop[kP];
+#pragma unroll
+    for (int k = 0; k < kP; ++k) {
+        if (EDGE) {
+            col[2 * k] = 2 * wrap(jl + k, hw);
+            col[2 * k + 1] = min(col[2 * k] + 1, w - 1);       // odd width: the last sample repeats
+        } else {
+            col[2 * k] = 2 * (wrap(jl, hw) + k);
+            col[2 * k + 1] = 2 * (wrap(jl, hw) + k) + 1;
+        }
+        const int p = kP * lane + k;
+        drop[k] = p >= 2 && p < 2 + kValid && jl + k < hw ? 0u : kDrop;
+    }
+    const int m0 = band * brows, m1 = min(m0 + brows, hh);
+    const uint8_t *src8 = FIRST ? rgb + frame * rgb_stride : nullptr;
+    const double *src = FIRST ? nullptr : in + plane * plane_stride;
+    uint8_t *pk = packed + frame * packed_stride;
+    const __amdgpu_buffer_rsrc_t rs_pk = __builtin_amdgcn_make_buffer_rsrc(pk, 0, (int)packed_stride, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_ll = __builtin_amdgcn_make_buffer_rsrc(
+        LAST ? (void *)pk : (void *)(LLout + plane * plane_stride), 0, LAST ? 0 : (int)((long long)hh * hw * 8),
+        0x00020000);
+    const int x0 = strip * 2 * kValid - 4;                     // first staged pixel (level 1)
+    // this thread's staged dword of a row, wrapped modulo the row's 3w bytes
+    // (w % 4 == 0: the wrapped dword stays aligned and on the same byte phase)
+    const int boff = wrap(3 * x0 + 4 * t, 3 * w);
+    // row pairs are read ahead of the one in use (wrapped index nf)
+    const int n_last = m1 + 1;
+    int nf = wrap(m0 - 2, hh);
+    auto next_pair = [&]() { nf = nf + 1 == hh ? 0 : nf + 1; };
+    auto fetch = [&]() -> uint2 {
+        const uint8_t *ra = src8 + (long long)(2 * nf) * w * 3 + boff;
+        const uint8_t *rb = src8 + (long long)min(2 * nf + 1, h - 1) * w * 3 + boff;
+        return make_uint2(*(const uint32_t *)ra, *(const uint32_t *)rb);
+    };
+    auto load = [&](double (&s2)[2 * kP], double (&e2)[2 * kP]) {
+        const int ra = 2 * nf, rb = min(2 * nf + 1, h - 1);     // odd height: the last row repeats
+        if (FIRST) {
+            const uint8_t *pa = src8 + (long long)ra * w * 3, *pb = src8 + (long long)rb * w * 3;
+#pragma unroll
+            for (int k = 0; k < 2 * kP; ++k) {
+                s2[k] = ycocg(pa + 3 * col[k], ch);
+                e2[k] = ycocg(pb + 3 * col[k], ch);
+            }
+        } else if (EDGE) {
+            const double *pa = src + (long long)ra * w, *pb = src + (long long)rb * w;
+#pragma unroll
+            for (int k = 0; k < 2 * kP; ++k) {
+                s2[k] = pa[col[k]];
+                e2[k] = pb[col[k]];
+            }
+        } else {
+            const double2 *qa = (const double2 *)(src + (long long)ra * w + col[0]);
+            const double2 *qb = (const double2 *)(src + (long long)rb * w + col[0]);
+#pragma unroll
+            for (int k = 0; k < kP; ++k) {
+                const double2 va = qa[k], vb = qb[k];
+                s2[2 * k] = va.x;
+                s2[2 * k + 1] = va.y;
+                e2[2 * k] = vb.x;
+                e2[2 * k + 1] = vb.y;
+            }
+        }
+    };
+    constexpr bool kStaged = FIRST && !EDGE;
+    uint2 q0 = make_uint2(0, 0), q1 = make_uint2(0, 0);
+    double ns[2 * kP], ne[2 * kP];
+    if (kStaged) {
+        q0 = fetch();
+        next_pair();
+        q1 = fetch();
+        next_pair();
+    } else {
+        load(ns, ne);
+        next_pair();
+    }
+    int buf = 0;
+
+    // the column pipelines: s_{n-1}, e_{n-1}, e1_{n-2}, s1_{n-2}, e2_{n-3} per sample column
+    double sp[2 * kP], ep[2 * kP], e1p[2 * kP], s1p[2 * kP], e2p[2 * kP];
+#pragma unroll
+    for (int k = 0; k < 2 * kP; ++k) sp[k] = ep[k] = e1p[k] = s1p[k] = e2p[k] = 0.0;
+    for (int n = m0 - 2; n <= n_last; ++n, buf ^= 1) {
+        double s[2 * kP], e[2 * kP];
+        if (kStaged) {
+            uint32_t *st = px_lds + 2 * kRowDw * buf;
+            st[t] = q0.x;
+            st[kRowDw + t] = q0.y;
+            q0 = q1;
+            q1 = fetch();      // (unconditional: a branch around it would cost exact wait counts;
+            next_pair();       // past the band it reads a wrapped row it does not use)
+            asm volatile("" ::: "memory");   // (a compiler barrier: issued here, not sunk past the stores)
+            lds_barrier();
+            // the lane's four pixels of each row: 12 bytes at 12 * lane
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t *d = st + r * kRowDw + 3 * lane;
+                const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+                double *o = r ? e : s;
+                o[0] = ycocg(d0 & 255, (d0 >> 8) & 255, (d0 >> 16) & 255, ch);
+                o[1] = ycocg(d0 >> 24, d1 & 255, (d1 >> 8) & 255, ch);
+                o[2] = ycocg((d1 >> 16) & 255, d1 >> 24, d2 & 255, ch);
+                o[3] = ycocg((d2 >> 8) & 255, (d2 >> 16) & 255, d2 >> 24, ch);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2 * kP; ++k) {
+                s[k] = ns[k];
+                e[k] = ne[k];
+            }
+            load(ns, ne);      // (unconditional, as above)
+            next_pair();
+            asm volatile("" ::: "memory");
+        }
+        double L[2 * kP], D[2 * kP];
+#pragma unroll
+        for (int k = 0; k < 2 * kP; ++k) {
+            const double e1 = __builtin_fma(kA, sp[k] + s[k], ep[k]);    // e1_{n-1}
+            const double s1 = __builtin_fma(kB, e1p[k] + e1, sp[k]);     // s1_{n-1}
+            const double e2 = __builtin_fma(kG, s1p[k] + s1, e1p[k]);    // e2_{n-2}
+            const double s2 = __builtin_fma(kD, e2p[k] + e2, s1p[k]);    // s2_{n-2}
+            L[k] = kK * s2;
+            D[k] = -e2 * kIK;
+            sp[k] = s[k];
+            ep[k] = e[k];
+            e1p[k] = e1;
+            s1p[k] = s1;
+            e2p[k] = e2;
+        }
+        const int m = n - 2;                                       // output row pair (uniform)
+        if (m < m0) continue;
+        double ll[2] = {L[0], L[2]}, hl[2] = {L[1], L[3]}, lh[2] = {D[0], D[2]}, hhv[2] = {D[1], D[3]};
+        fwd_row(ll, hl);    // (aa, ad) = (LL, HL)
+        fwd_row(lh, hhv);   // (da, dd) = (LH, HH)
+        const long long orow = (long long)m * hw;
+        uint8_t q[3][kP];
+#pragma unroll
+        for (int k = 0; k < kP; ++k) {
+            q[0][k] = quant_u8(lh[k], Q);
+            q[1][k] = quant_u8(hl[k], Q);
+            q[2][k] = quant_u8(hhv[k], Q);
+            const uint32_t o = (uint32_t)(orow + jl + k);          // (a halo lane's may be junk: dropped)
+            if (LAST)
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)quant_u16(ll[k], Q), rs_pk,
+                                                      ((uint32_t)ll_off + 2 * (3 * o + ch)) | drop[k], 0, 0);
+            else if (EDGE)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U32x2, ll[k]), rs_ll, (8 * o) | drop[k], 0,
+                                                      0);
+        }
+        if (!LAST && !EDGE)   // both pairs of a lane are in or out together (even jl, even hw): one 16-byte store
+            __builtin_amdgcn_raw_buffer_store_b128(pack2(ll[0], ll[1]), rs_ll, (8 * (uint32_t)(orow + jl)) | drop[0],
+                                                   0, 0);
+        if (!EDGE) {
+            uint8_t *so = (uint8_t *)(sb_lds + (kSbDw + 1) * buf);
+#pragma unroll
+            for (int k = 0; k < kP; ++k) {
+                const int p = drop[k] ? 3 * kSbB : 3 * (kP * lane + k - 2) + ch;   // halo lanes: the dummy dword
+                const int dsb = drop[k] ? 0 : kSbB;
+                so[p] = q[0][k];
+                so[p + dsb] = q[1][k];
+                so[p + 2 * dsb] = q[2][k];
+            }
+            lds_barrier();
+            const uint32_t base = (uint32_t)off_lh + 3 * (uint32_t)(orow + strip * kValid);
+            const int row_b = 3 * (hw - strip * kValid);            // the strip's bytes in the row
+            const uint32_t sstep = (uint32_t)(off_hl - off_lh);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int i = t + r * kNT;
+                const int ic = min(i, kSbDw - 1);
+                const int sub = ic / (kSbB / 4), d = ic - (kSbB / 4) * sub;
+                __builtin_amdgcn_raw_buffer_store_b32(sb_lds[(kSbDw + 1) * buf + ic], rs_pk,
+                                                      (base + sub * sstep + 4 * d) |
+                                                          (i < kSbDw && 4 * d < row_b ? 0u : kDrop),
+                                                      0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kP; ++k) {
+                const uint32_t o = 3 * (uint32_t)(orow + jl + k) + ch;
+                __builtin_amdgcn_raw_buffer_store_b8(q[0][k], rs_pk, ((uint32_t)off_lh + o) | drop[k], 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8(q[1][k], rs_pk, ((uint32_t)off_hl + o) | drop[k], 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8(q[2][k], rs_pk, ((uint32_t)off_hh + o) | drop[k], 0, 0);
+            }
+        }
+    }
+}
+
+// one launch per level: the edge strips' workgroups first, on bands of a
+// quarter of the rows (their general body is the slower per step: as long a
+// chain would be the launch's tail), then the interior strips'
+template <bool FIRST, bool LAST>
+__global__ __launch_bounds__(kNT) void lift_fwd_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
+                                                       const double *__restrict__ in, long long plane_stride,
+                                                       double *__restrict__ LLout, uint8_t *__restrict__ packed,
+                                                       long long packed_stride, long long ll_off, long long off_lh,
+                                                       long long off_hl, long long off_hh, int h, int w, int hh,
+                                                       int hw, int Q, int n_int, int n_edge, int n_bands, int brows,
+                                                       int n_bands_e, int brows_e, int edge_blocks)
+{
+    __shared__ uint32_t px_lds[FIRST ? 2 * 2 * kRowDw : 1];
+    __shared__ uint32_t sb_lds[2 * (kSbDw + 1)];
+    const int bid = blockIdx.x;
+    if (bid < edge_blocks)
+        lift_fwd_body<FIRST, LAST, true>(rgb, rgb_stride, in, plane_stride, LLout, packed, packed_stride, ll_off,
+                                         off_lh, off_hl, off_hh, h, w, hh, hw, Q, n_int, n_edge, n_bands_e, brows_e,
+                                         bid, px_lds, sb_lds);
+    else
+        lift_fwd_body<FIRST, LAST, false>(rgb, rgb_stride, in, plane_stride, LLout, packed, packed_stride, ll_off,
+                                          off_lh, off_hl, off_hh, h, w, hh, hw, Q, n_int, n_int, n_bands, brows,
+                                          bid - edge_blocks, px_lds, sb_lds);
+}
+
+// one inverse level: subbands h x w (LL float64 with row stride lda, or u16
+// packed at the coarsest level) -> plane oh x ow (<= 2h x 2w; float64), or
+// at level 1 RGB u8 (2h x 2w)
+constexpr int kOut = 4 * kP;                      // outputs per lane and step: 2 rows x 2 kP columns
+constexpr int kRgbRow = 2 * kValid * 3;           // bytes of one RGB output row of the strip
+constexpr int kRgbDw = 2 * kRgbRow / 4;
+
+template <bool FROM_PACKED, bool TO_RGB, bool EDGE>
+__device__ __forceinline__ void lift_inv_body(const uint8_t *__restrict__ packed, long long packed_stride,
+                                              long long ll_off, long long off_lh, long long off_hl, long long off_hh,
+                                              const double *__restrict__ in, long long plane_stride, int lda,
+                                              double *__restrict__ out, uint8_t *__restrict__ rgb_out,
+                                              long long rgb_stride, int h, int w, int oh, int ow, int Q, int n_int,
+                                              int n_set, int n_bands, int brows, int bid, double *xch,
+                                              uint32_t *rgb_lds)
+{
+    const int t = threadIdx.x, lane = t & 63, ch = __builtin_amdgcn_readfirstlane(t >> 6);
+    int b = bid;
+    const int strip = strip_of(EDGE, b % n_set, n_int);
+    b /= n_set;
+    const int band = b % n_bands;
+    const long long frame = b / n_bands;
+    const long long plane = frame * 3 + ch;
+    const int jl = strip * kValid - 2 + kP * lane;
+    int j[kP];
+    uint32_t drop[kP];
+#pragma unroll
+    for (int k = 0; k < kP; ++k) {
+        j[k] = wrap(jl + k, w);
+        const int p = kP * lane + k;
+        drop[k] = p >= 2 && p < 2 + kValid && jl + k < w ? 0u : kDrop;
+    }
+    const int m0 = band * brows, m1 = min(m0 + brows, h);
+    const uint8_t *pk = packed + frame * packed_stride;
+    const double *src = FROM_PACKED ? nullptr : in + plane * plane_stride;
+    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+        TO_RGB ? (void *)(rgb_out + frame * rgb_stride) : (void *)(out + plane * plane_stride), 0,
+        TO_RGB ? (int)rgb_stride : (int)((long long)oh * ow * 8), 0x00020000);
+
+    // the column pipelines: e_{q-1}, s1_{q-1}, e1_{q-2}, s2_{q-2} per output column
+    double ep[2 * kP], s1p[2 * kP], e1pp[2 * kP], s2pp[2 * kP];
+#pragma unroll
+    for (int k = 0; k < 2 * kP; ++k) ep[k] = s1p[k] = e1pp[k] = s2pp[k] = 0.0;
+    // the coefficients of row q + 1 are in flight over row q's lifting
+    int qf = wrap(m0 - 2, h);
+    double nA[kP];
+    int nb[3][kP];
+    auto load = [&]() {
+        const long long row = (long long)qf * w;
+        if (!FROM_PACKED && !EDGE) {
+            const double2 v = *(const double2 *)(src + (long long)qf * lda + j[0]);
+            nA[0] = v.x;
+            nA[1] = v.y;
+        }
+#pragma unroll
+        for (int k = 0; k < kP; ++k) {
+            const long long idx = row + j[k];
+            if (FROM_PACKED) nA[k] = dequant((int16_t)*(const uint16_t *)(pk + ll_off + 2 * (3 * idx + ch)), Q);
+            else if (EDGE) nA[k] = src[(long long)qf * lda + j[k]];
+            nb[0][k] = pk[off_hl + 3 * idx + ch];
+            nb[1][k] = pk[off_lh + 3 * idx + ch];
+            nb[2][k] = pk[off_hh + 3 * idx + ch];
+        }
+        qf = qf + 1 == h ? 0 : qf + 1;
+    };
+    load();
+    for (int q = m0 - 2; q <= m1 + 1; ++q) {
+        double a[kP], hl[kP], lh[kP], hhv[kP];
+#pragma unroll
+        for (int k = 0; k < kP; ++k) {
+            a[k] = nA[k];
+            hl[k] = dequant((int16_t)nb[0][k], Q);
+            lh[k] = dequant((int16_t)nb[1][k], Q);
+            hhv[k] = dequant((int16_t)nb[2][k], Q);
+        }
+        load();                // (unconditional: exact wait counts; past the band a wrapped row)
+        asm volatile("" ::: "memory");   // (a compiler barrier: issued here, not sunk past the stores)
+        inv_row(a, hl);     // row 'a' of the vertical pair: columns 2j .. 2j + 3
+        inv_row(lh, hhv);   // row 'd'
+        const double A[2 * kP] = {a[0], hl[0], a[1], hl[1]}, Dd[2 * kP] = {lh[0], hhv[0], lh[1], hhv[1]};
+        double o0[2 * kP], o1[2 * kP];
+#pragma unroll
+        for (int k = 0; k < 2 * kP; ++k) {
+            const double s = A[k] * kIK, e = -Dd[k] * kK;
+            const double s1 = __builtin_fma(-kD, ep[k] + e, s);          // s1_q
+            const double e1 = __builtin_fma(-kG, s1p[k] + s1, ep[k]);    // e1_{q-1}
+            const double s2 = __builtin_fma(-kB, e1pp[k] + e1, s1p[k]);  // s2_{q-1}
+            const double e2 = __builtin_fma(-kA, s2pp[k] + s2, e1pp[k]); // e2_{q-2}
+            o0[k] = s2pp[k];                                             // row 2(q-2)
+            o1[k] = e2;                                                  // row 2(q-2) + 1
+            ep[k] = e;
+            s1p[k] = s1;
+            e1pp[k] = e1;
+            s2pp[k] = s2;
+        }
+        const int m = q - 2;
+        if (m < m0) continue;
+        const int r0 = 2 * m, cc = 2 * jl;
+        if (TO_RGB) {
+            double *x = xch + ch * kOut * 64;
+#pragma unroll
+            for (int k = 0; k < 2 * kP; ++k) {
+                x[k * 64 + lane] = o0[k];
+                x[(2 * kP + k) * 64 + lane] = o1[k];
+            }
+            lds_barrier();
+#pragma unroll
+            for (int k = 0; k < kOut; ++k) {
+                const int r = k / (2 * kP), c = k % (2 * kP);     // output row r0 + r, column cc + c
+                const uint32_t dk = drop[c >> 1];
+                const double Y = xch[k * 64 + lane], Co = xch[(kOut + k) * 64 + lane],
+                             Cg = xch[(2 * kOut + k) * 64 + lane];
+                const double v = ch == 0 ? Y + Co - Cg : (ch == 1 ? Y + Cg : Y - Co - Cg);
+                const uint8_t u = (uint8_t)(v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v));
+                if (!EDGE) {
+                    const int pos = dk ? kRgbDw * 4 : kRgbRow * r + 3 * (cc + c - 2 * strip * kValid) + ch;
+                    ((uint8_t *)rgb_lds)[pos] = u;
+                } else {
+                    const uint32_t o = 3 * (uint32_t)((long long)(r0 + r) * ow + cc + c) + ch;
+                    __builtin_amdgcn_raw_buffer_store_b8(u, rs_out, o | dk, 0, 0);
+                }
+            }
+            lds_barrier();
+            if (!EDGE) {
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr) {
+                    const int i = t + rr * kNT;
+                    const int ic = min(i, kRgbDw - 1);
+                    const int row = ic >= kRgbRow / 4, d = ic - (kRgbRow / 4) * row;
+                    const uint32_t o = 3 * (uint32_t)((long long)(r0 + row) * ow + 2 * strip * kValid) + 4 * d;
+                    const uint32_t ok = i < kRgbDw && 4 * d < 3 * (ow - 2 * strip * kValid) ? 0u : kDrop;
+                    __builtin_amdgcn_raw_buffer_store_b32(rgb_lds[ic], rs_out, o | ok, 0, 0);
+                }
+            }
+        } else if (EDGE) {
+#pragma unroll
+            for (int k = 0; k < kOut; ++k) {
+                const int r = r0 + k / (2 * kP), c = cc + k % (2 * kP);
+                const uint32_t dk = (r < oh && c < ow) ? drop[(k % (2 * kP)) >> 1] : kDrop;
+                const double v = k < 2 * kP ? o0[k] : o1[k - 2 * kP];
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U32x2, v), rs_out,
+                                                      (8 * (uint32_t)((long long)r * ow + c)) | dk, 0, 0);
+            }
+        } else {   // (ow even here: a pair's two columns are in or out together) 16-byte stores
+#pragma unroll
+            for (int k = 0; k < 2 * kP; ++k) {
+                const int r = r0 + k / kP, c = cc + 2 * (k % kP);
+                const uint32_t dk = r < oh ? drop[k % kP] : kDrop;
+                const double *v = k < kP ? o0 : o1;
+                __builtin_amdgcn_raw_buffer_store_b128(pack2(v[2 * (k % kP)], v[2 * (k % kP) + 1]), rs_out,
+                                                       (8 * (uint32_t)((long long)r * ow + c)) | dk, 0, 0);
+            }
+        }
+    }
+}
+
+template <bool FROM_PACKED, bool TO_RGB>
+__global__ __launch_bounds__(kNT) void lift_inv_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
+                                                       long long ll_off, long long off_lh, long long off_hl,
+                                                       long long off_hh, const double *__restrict__ in,
+                                                       long long plane_stride, int lda, double *__restrict__ out,
+                                                       uint8_t *__restrict__ rgb_out, long long rgb_stride, int h,
+                                                       int w, int oh, int ow, int Q, int n_int, int n_edge,
+                                                       int n_bands, int brows, int n_bands_e, int brows_e,
+                                                       int edge_blocks)
+{
+    __shared__ double xch[TO_RGB ? 3 * kOut * 64 : 1];
+    __shared__ uint32_t rgb_lds[TO_RGB ? kRgbDw + 1 : 1];
+    const int bid = blockIdx.x;
+    if (bid < edge_blocks)
+        lift_inv_body<FROM_PACKED, TO_RGB, true>(packed, packed_stride, ll_off, off_lh, off_hl, off_hh, in,
+                                                 plane_stride, lda, out, rgb_out, rgb_stride, h, w, oh, ow, Q, n_int,
+                                                 n_edge, n_bands_e, brows_e, bid, xch, rgb_lds);
+    else
+        lift_inv_body<FROM_PACKED, TO_RGB, false>(packed, packed_stride, ll_off, off_lh, off_hl, off_hh, in,
+                                                  plane_stride, lda, out, rgb_out, rgb_stride, h, w, oh, ow, Q, n_int,
+                                                  n_int, n_bands, brows, bid - edge_blocks, xch, rgb_lds);
+}
+
+}  // namespace lift

@@ -1,6 +1,10 @@
 """2D-DWT + deadzone on the GPU (src/2D-DWT.py encode_fn :57-78 up to the
 TIFF writer, decode_fn :80-101 after the TIFF reader), through
-libvcf_amd.so (vcf_dwt_dz_encode / vcf_dwt_dz_decode).  No CPU path."""
+libvcf_amd.so (vcf_dwt_dz_encode / vcf_dwt_dz_decode).  No CPU path.
+
+lifting=True selects the opt-in lifting form of bior4.4 (vcf_dwt_dz_*_lift,
+csrc/vcf_dwt_lift.h): not bit-exact -- indices and decoded bytes within +-1
+of the default path."""
 from __future__ import annotations
 
 import ctypes
@@ -64,28 +68,33 @@ def _frames(a, what):
     return np.ascontiguousarray(a)
 
 
+def _entry(name: str, lifting: bool) -> str:
+    return name + "_lift" if lifting else name
+
+
 def encode_device(din: DeviceBuffer, n: int, H: int, W: int, wavelet: int, levels: int, Q: int,
-                  packed: DeviceBuffer, workspace: DeviceBuffer, stream=None) -> None:
+                  packed: DeviceBuffer, workspace: DeviceBuffer, stream=None, lifting: bool = False) -> None:
     """n HBM-resident H x W x 3 u8 frames -> their packed subbands (layout()'s
     bytes per frame), enqueued on `stream`; `wavelet` is wavelet_index()'s."""
     _, pb, wb = layout(H, W, levels)
     if din.nbytes < n * H * W * 3 or packed.nbytes < n * pb or workspace.nbytes < n * wb:
         raise ValueError("dwt encode_device: buffer smaller than n frames need")
-    L.call("vcf_dwt_dz_encode", din.ptr, n, H, W, int(wavelet), levels, int(Q), packed.ptr, workspace.ptr,
-           None if stream is None else stream.handle)
+    L.call(_entry("vcf_dwt_dz_encode", lifting), din.ptr, n, H, W, int(wavelet), levels, int(Q), packed.ptr,
+           workspace.ptr, None if stream is None else stream.handle)
 
 
 def decode_device(packed: DeviceBuffer, n: int, H: int, W: int, wavelet: int, levels: int, Q: int,
-                  out: DeviceBuffer, workspace: DeviceBuffer, stream=None) -> None:
+                  out: DeviceBuffer, workspace: DeviceBuffer, stream=None, lifting: bool = False) -> None:
     """n frames' packed subbands in HBM -> u8 RGB (2*ceil(H/2) x 2*ceil(W/2) x 3 each)."""
     shapes, pb, wb = layout(H, W, levels)
     if packed.nbytes < n * pb or out.nbytes < n * 4 * shapes[0][0] * shapes[0][1] * 3 or workspace.nbytes < n * wb:
         raise ValueError("dwt decode_device: buffer smaller than n frames need")
-    L.call("vcf_dwt_dz_decode", packed.ptr, n, H, W, int(wavelet), levels, int(Q), out.ptr, workspace.ptr,
-           None if stream is None else stream.handle)
+    L.call(_entry("vcf_dwt_dz_decode", lifting), packed.ptr, n, H, W, int(wavelet), levels, int(Q), out.ptr,
+           workspace.ptr, None if stream is None else stream.handle)
 
 
-def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32, variant: int = 0):
+def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32, variant: int = 0,
+           lifting: bool = False):
     """HxWx3 u8 (or N of them) -> list of {subband name: indices} per frame.
     variant: 0 the product kernels; any other value a variant of the A/B library
     (include/vcf_amd_ab.h: 1 fused level kernels, 2 separable kernels, 6 strip kernels on every
@@ -95,9 +104,11 @@ def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32, 
     _, pb, wb = layout(H, W, levels)
     din, dout, dws = DeviceBuffer.from_array(f), DeviceBuffer(n * pb), DeviceBuffer(n * wb)
     try:
+        if variant and lifting:
+            raise ValueError("lifting is a product entry point, not an A/B variant")
         if variant == 0:
-            L.call("vcf_dwt_dz_encode", din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q), dout.ptr,
-                   dws.ptr, None)
+            L.call(_entry("vcf_dwt_dz_encode", lifting), din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q),
+                   dout.ptr, dws.ptr, None)
         else:
             L.call_ab("vcf_dwt_dz_encode_variant", int(variant), din.ptr, n, H, W, wavelet_index(wavelet), levels,
                       int(Q), dout.ptr, dws.ptr, None)
@@ -110,7 +121,7 @@ def encode(rgb: np.ndarray, wavelet: str = "db5", levels: int = 5, Q: int = 32, 
 
 
 def decode(subbands, H: int, W: int, wavelet: str = "db5", levels: int = 5, Q: int = 32,
-           variant: int = 0) -> np.ndarray:
+           variant: int = 0, lifting: bool = False) -> np.ndarray:
     """{name: indices} (or a list of them) -> u8 RGB (2*ceil(H/2) x 2*ceil(W/2) x 3 each)."""
     single = isinstance(subbands, dict)
     sets = [subbands] if single else list(subbands)
@@ -120,9 +131,11 @@ def decode(subbands, H: int, W: int, wavelet: str = "db5", levels: int = 5, Q: i
     Ho, Wo = 2 * shapes[0][0], 2 * shapes[0][1]
     din, dout, dws = DeviceBuffer.from_array(packed), DeviceBuffer(n * Ho * Wo * 3), DeviceBuffer(n * wb)
     try:
+        if variant and lifting:
+            raise ValueError("lifting is a product entry point, not an A/B variant")
         if variant == 0:
-            L.call("vcf_dwt_dz_decode", din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q), dout.ptr,
-                   dws.ptr, None)
+            L.call(_entry("vcf_dwt_dz_decode", lifting), din.ptr, n, H, W, wavelet_index(wavelet), levels, int(Q),
+                   dout.ptr, dws.ptr, None)
         else:
             L.call_ab("vcf_dwt_dz_decode_variant", int(variant), din.ptr, n, H, W, wavelet_index(wavelet), levels,
                       int(Q), dout.ptr, dws.ptr, None)
