@@ -105,16 +105,6 @@ __device__ __forceinline__ void inv_row(double (&a)[2], double (&d)[2])
     }
 }
 
-// workgroup barrier ordering LDS only: __syncthreads() also orders global
-// memory, which on gfx950 waits for every load and store in flight
-// (vmcnt(0)) -- the row prefetch and the last step's stores -- at each step
-__device__ __forceinline__ void lds_barrier()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
 __device__ __forceinline__ int wrap(int i, int n)
 {
     i %= n;
@@ -272,7 +262,7 @@ __device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, l
             q1 = fetch();      // (unconditional: a branch around it would cost exact wait counts;
             next_pair();       // past the band it reads a wrapped row it does not use)
             asm volatile("" ::: "memory");   // (a compiler barrier: issued here, not sunk past the stores)
-            lds_barrier();
+            __syncthreads();
             // the lane's four pixels of each row: 12 bytes at 12 * lane
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
@@ -342,7 +332,7 @@ __device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, l
                 so[p + dsb] = q[1][k];
                 so[p + 2 * dsb] = q[2][k];
             }
-            lds_barrier();
+            __syncthreads();
             const uint32_t base = (uint32_t)off_lh + 3 * (uint32_t)(orow + strip * kValid);
             const int row_b = 3 * (hw - strip * kValid);            // the strip's bytes in the row
             const uint32_t sstep = (uint32_t)(off_hl - off_lh);
@@ -498,7 +488,7 @@ __device__ __forceinline__ void lift_inv_body(const uint8_t *__restrict__ packed
                 x[k * 64 + lane] = o0[k];
                 x[(2 * kP + k) * 64 + lane] = o1[k];
             }
-            lds_barrier();
+            __syncthreads();
 #pragma unroll
             for (int k = 0; k < kOut; ++k) {
                 const int r = k / (2 * kP), c = k % (2 * kP);     // output row r0 + r, column cc + c
@@ -515,7 +505,7 @@ __device__ __forceinline__ void lift_inv_body(const uint8_t *__restrict__ packed
                     __builtin_amdgcn_raw_buffer_store_b8(u, rs_out, o | dk, 0, 0);
                 }
             }
-            lds_barrier();
+            __syncthreads();
             if (!EDGE) {
 #pragma unroll
                 for (int rr = 0; rr < 2; ++rr) {
