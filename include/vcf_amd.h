@@ -201,7 +201,7 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
  * (VCF_ERR_INVALID for other wavelets): same arguments, buffers, layout and
  * workspace, four lifting steps per axis in place of pywt's convolution.
  * NOT bit-exact: every index and decoded byte lies within +-1 of
- * vcf_dwt_dz_encode / _decode's (measured).  No counterpart
+ * vcf_dwt_dz_encode / _decode's (measured, DESIGN.md §4.5, the lifting form).  No counterpart
  * in the reference -- an extension for callers who accept that tolerance. */
 int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                            int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, void *stream);

@@ -49,7 +49,7 @@ class CoDec(EICCoDec):
         self.file_extension = self.entropy.file_extension
         self.QSS = int(getattr(args, "QSS", 32))
         # opt-in (no reference counterpart): the lifting form of bior4.4, within
-        # +-1 of the bit-exact path; args.dwt_lifting or VCF_DWT_LIFTING=1
+        # +-1 of the bit-exact path (the lifting form); args.dwt_lifting or VCF_DWT_LIFTING=1
         self.lifting = bool(getattr(args, "dwt_lifting", False)) or os.environ.get("VCF_DWT_LIFTING") == "1"
         if self.lifting and self.wavelet != "bior4.4":
             raise NotImplementedError("the lifting path is bior4.4 (CDF 9/7) only")

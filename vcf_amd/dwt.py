@@ -4,7 +4,7 @@ libvcf_amd.so (vcf_dwt_dz_encode / vcf_dwt_dz_decode).  No CPU path.
 
 lifting=True selects the opt-in lifting form of bior4.4 (vcf_dwt_dz_*_lift,
 csrc/vcf_dwt_lift.h): not bit-exact -- indices and decoded bytes within +-1
-of the default path."""
+of the default path (the lifting form)."""
 from __future__ import annotations
 
 import ctypes
