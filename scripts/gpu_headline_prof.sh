@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; TAG=${1:-r05}; shift || true
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--c4-frames 0 --c5-frames 0 --no-cpu-baseline --steps 100 $*"
+ARGS="--c4-frames 0 --c5-frames 0 --c3-steps 0 --c2-reps 0 --no-cpu-baseline --steps 100 $*"
 timeout -k 10 300 python3 bench.py $ARGS > "$OUT/hl_$TAG.json" 2> "$OUT/hl_$TAG.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/hl_$TAG.json"; [ $rc -eq 0 ] || exit $rc
 cd /tmp
