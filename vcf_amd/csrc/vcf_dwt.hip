@@ -1931,8 +1931,14 @@ int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, 
                              (g.sb_off[l][1] - g.sb_off[l][0]) % 4 == 0;
         const int n_int = aligned ? n_strips : 0;
         const long long per_band = n_frames * n_strips;
-        auto kern = first ? (last ? lift::lift_fwd_kernel<true, true> : lift::lift_fwd_kernel<true, false>)
-                          : (last ? lift::lift_fwd_kernel<false, true> : lift::lift_fwd_kernel<false, false>);
+        const bool qp2 = (Q & (Q - 1)) == 0;
+        auto kern = qp2 ? (first ? (last ? lift::lift_fwd_kernel<true, true, true> : lift::lift_fwd_kernel<true, false, true>)
+                                 : (last ? lift::lift_fwd_kernel<false, true, true>
+                                         : lift::lift_fwd_kernel<false, false, true>))
+                        : (first ? (last ? lift::lift_fwd_kernel<true, true, false>
+                                         : lift::lift_fwd_kernel<true, false, false>)
+                                 : (last ? lift::lift_fwd_kernel<false, true, false>
+                                         : lift::lift_fwd_kernel<false, false, false>));
         const int brows = lift_brows(per_band, hh, resident_slots(kern, lift::kNT));
         const int n_bands = (hh + brows - 1) / brows, n_edge = n_strips - n_int;
         const int brows_e = brows, n_bands_e = n_bands;

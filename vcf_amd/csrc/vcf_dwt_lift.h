@@ -122,6 +122,30 @@ __device__ __forceinline__ double ycocg(int R, int G, int B, int ch)
 
 __device__ __forceinline__ double ycocg(const uint8_t *px, int ch) { return ycocg(px[0], px[1], px[2], ch); }
 
+// the same for a compile-time channel, truncating divisions as shifts:
+// t / 2 = (t + (t < 0)) >> 1, t / 4 = (t + 3 (t < 0)) >> 2
+template <int CH>
+__device__ __forceinline__ double ycocg_c(int R, int G, int B)
+{
+    if constexpr (CH == 0) {
+        return (double)((R + 2 * G + B) >> 2);
+    } else if constexpr (CH == 1) {
+        const int t = R - B;
+        return (double)((t + (int)((unsigned)t >> 31)) >> 1);
+    } else {
+        const int t = 2 * G - R - B;
+        return (double)((t + ((t >> 31) & 3)) >> 2);
+    }
+}
+
+// deadzone index + 128 as the packed byte / halfword (A5): a power-of-two Q
+// (QP2) is an exact scaling by 2^-qsh, else numpy's correctly rounded x / Q
+template <bool QP2>
+__device__ __forceinline__ int32_t qk(double x, int Q, int qsh)
+{
+    return (int32_t)(QP2 ? __builtin_ldexp(x, -qsh) : x / (double)Q);
+}
+
 // Two bodies.  Planes whose rows are whole dwords and whose pairs never
 // straddle the periodic wrap (w = 2 hw, hw % 4 == 0 forward; w even inverse:
 // every C3 level) run a branch-free body (EDGE = false): every global load
@@ -149,7 +173,7 @@ __device__ __forceinline__ U32x4 pack2(double a, double b)
 constexpr int kRowDw = 64 * kP * 2 * 3 / 4;            // dwords of one staged RGB row
 constexpr int kSbB = kValid * 3, kSbDw = 3 * kSbB / 4;  // bytes of one subband row, dwords of three
 
-template <bool FIRST, bool LAST, bool EDGE>
+template <bool FIRST, bool LAST, bool EDGE, bool QP2>
 __device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                               const double *__restrict__ in, long long plane_stride,
                                               double *__restrict__ LLout, uint8_t *__restrict__ packed,
@@ -158,6 +182,7 @@ __device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, l
                                               int n_int, int n_set, int n_bands, int brows, int bid,
                                               uint32_t *px_lds, uint32_t *sb_lds)
 {
+    const int qsh = QP2 ? __builtin_ctz((unsigned)Q) : 0;
     // byte staging through LDS (interior strips; double-buffered, one barrier
     // each): level 1's two RGB rows of 256 pixels come in as two dwords per
     // thread, and the three detail subbands' kValid x 3 interleaved bytes
@@ -263,17 +288,24 @@ __device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, l
             next_pair();       // past the band it reads a wrapped row it does not use)
             asm volatile("" ::: "memory");   // (a compiler barrier: issued here, not sunk past the stores)
             __syncthreads();
-            // the lane's four pixels of each row: 12 bytes at 12 * lane
+            // the lane's four pixels of each row: 12 bytes at 12 * lane; one
+            // scalar branch on the wave's channel around all eight samples
+            auto unpack = [&](auto chc) {
+                constexpr int C = decltype(chc)::value;
 #pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const uint32_t *d = st + r * kRowDw + 3 * lane;
-                const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
-                double *o = r ? e : s;
-                o[0] = ycocg(d0 & 255, (d0 >> 8) & 255, (d0 >> 16) & 255, ch);
-                o[1] = ycocg(d0 >> 24, d1 & 255, (d1 >> 8) & 255, ch);
-                o[2] = ycocg((d1 >> 16) & 255, d1 >> 24, d2 & 255, ch);
-                o[3] = ycocg((d2 >> 8) & 255, (d2 >> 16) & 255, d2 >> 24, ch);
-            }
+                for (int r = 0; r < 2; ++r) {
+                    const uint32_t *d = st + r * kRowDw + 3 * lane;
+                    const int d0 = (int)d[0], d1 = (int)d[1], d2 = (int)d[2];
+                    double *o = r ? e : s;
+                    o[0] = ycocg_c<C>(d0 & 255, (d0 >> 8) & 255, (d0 >> 16) & 255);
+                    o[1] = ycocg_c<C>((unsigned)d0 >> 24, d1 & 255, (d1 >> 8) & 255);
+                    o[2] = ycocg_c<C>((d1 >> 16) & 255, (unsigned)d1 >> 24, d2 & 255);
+                    o[3] = ycocg_c<C>((d2 >> 8) & 255, (d2 >> 16) & 255, (unsigned)d2 >> 24);
+                }
+            };
+            if (ch == 0) unpack(std::integral_constant<int, 0>{});
+            else if (ch == 1) unpack(std::integral_constant<int, 1>{});
+            else unpack(std::integral_constant<int, 2>{});
         } else {
 #pragma unroll
             for (int k = 0; k < 2 * kP; ++k) {
@@ -308,12 +340,12 @@ __device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, l
         uint8_t q[3][kP];
 #pragma unroll
         for (int k = 0; k < kP; ++k) {
-            q[0][k] = quant_u8(lh[k], Q);
-            q[1][k] = quant_u8(hl[k], Q);
-            q[2][k] = quant_u8(hhv[k], Q);
+            q[0][k] = (uint8_t)(uint32_t)(qk<QP2>(lh[k], Q, qsh) + 128);   // += 128, astype(uint8): wraps
+            q[1][k] = (uint8_t)(uint32_t)(qk<QP2>(hl[k], Q, qsh) + 128);
+            q[2][k] = (uint8_t)(uint32_t)(qk<QP2>(hhv[k], Q, qsh) + 128);
             const uint32_t o = (uint32_t)(orow + jl + k);          // (a halo lane's may be junk: dropped)
             if (LAST)
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)quant_u16(ll[k], Q), rs_pk,
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(uint32_t)(qk<QP2>(ll[k], Q, qsh) + 128), rs_pk,
                                                       ((uint32_t)ll_off + 2 * (3 * o + ch)) | drop[k], 0, 0);
             else if (EDGE)
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U32x2, ll[k]), rs_ll, (8 * o) | drop[k], 0,
@@ -358,10 +390,9 @@ __device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, l
     }
 }
 
-// one launch per level: the edge strips' workgroups first, on bands of a
-// quarter of the rows (their general body is the slower per step: as long a
-// chain would be the launch's tail), then the interior strips'
-template <bool FIRST, bool LAST>
+// one launch per level: the general body's workgroups first (odd shapes: all
+// of them), then the branch-free body's (QP2: a power-of-two Q)
+template <bool FIRST, bool LAST, bool QP2>
 __global__ __launch_bounds__(kNT) void lift_fwd_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                                        const double *__restrict__ in, long long plane_stride,
                                                        double *__restrict__ LLout, uint8_t *__restrict__ packed,
@@ -374,11 +405,11 @@ __global__ __launch_bounds__(kNT) void lift_fwd_kernel(const uint8_t *__restrict
     __shared__ uint32_t sb_lds[2 * (kSbDw + 1)];
     const int bid = blockIdx.x;
     if (bid < edge_blocks)
-        lift_fwd_body<FIRST, LAST, true>(rgb, rgb_stride, in, plane_stride, LLout, packed, packed_stride, ll_off,
+        lift_fwd_body<FIRST, LAST, true, QP2>(rgb, rgb_stride, in, plane_stride, LLout, packed, packed_stride, ll_off,
                                          off_lh, off_hl, off_hh, h, w, hh, hw, Q, n_int, n_edge, n_bands_e, brows_e,
                                          bid, px_lds, sb_lds);
     else
-        lift_fwd_body<FIRST, LAST, false>(rgb, rgb_stride, in, plane_stride, LLout, packed, packed_stride, ll_off,
+        lift_fwd_body<FIRST, LAST, false, QP2>(rgb, rgb_stride, in, plane_stride, LLout, packed, packed_stride, ll_off,
                                           off_lh, off_hl, off_hh, h, w, hh, hw, Q, n_int, n_int, n_bands, brows,
                                           bid - edge_blocks, px_lds, sb_lds);
 }
