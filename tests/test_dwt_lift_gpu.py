@@ -115,3 +115,26 @@ def test_lift_rejects_other_wavelets():
     import vcf_amd.dwt as DW
     with pytest.raises(ValueError):   # VCFInvalidArgument
         DW.encode(np.zeros((32, 32, 3), np.uint8), "db5", 2, 32, lifting=True)
+
+
+@pytest.mark.parametrize("H,W,L,Q", [(96, 240, 2, 32), (64, 480, 5, 32), (32, 176, 3, 7), (200, 496, 2, 300),
+                                     (2160, 3840, 5, 32)])
+def test_lift_fused_levels12_equal_unfused(monkeypatch, H, W, L, Q):
+    """Levels 1 + 2 in one launch (lift_fwd12_kernel: planes with W % 4 == 0,
+    W / 2 % 8 == 0, H % 4 == 0) compute the same operations as the two level
+    launches: identical bytes, one strip and several, partial last strips,
+    LL2 as the last level (u16) and as float64 for level 3."""
+    import vcf_amd.dwt as DW
+    rng = np.random.Generator(np.random.PCG64(H + W + L))
+    frames = (np.stack([bench.synth_frame(H, W, 5), rng.integers(0, 256, (H, W, 3), dtype=np.uint8)])
+              if H * W < 4e6 else bench.synth_frame(H, W, 5)[None])
+    fused = DW.encode(frames, "bior4.4", L, Q, lifting=True)
+    monkeypatch.setenv("VCF_LIFT_NOFUSE", "1")
+    split = DW.encode(frames, "bior4.4", L, Q, lifting=True)
+    for f in range(len(frames)):
+        for name in fused[f]:
+            assert np.array_equal(fused[f][name], split[f][name]), (f, name)
+    if H * W < 4e6:
+        ref = O.dwt_encode_frame(frames[0], "bior4.4", L, Q)
+        frac, worst = _index_diff(ref, fused[0])
+        assert worst <= INDEX_TOL and frac <= RARE_FINE, (frac, worst)

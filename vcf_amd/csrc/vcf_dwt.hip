@@ -1674,7 +1674,7 @@ int resident_slots(K kern, int threads)
 
 // band rows of a lifting launch: time ~ (rounds of resident workgroups) x
 // (row pairs per band + the 4 of the pipeline's warm-up)
-int lift_brows(long long per_band, int rows, int slots)
+int lift_brows(long long per_band, int rows, int slots, int steps_per_row = 1, int warmup = 4)
 {
     int n_bands = 1;
     long long best = -1;
@@ -1682,7 +1682,7 @@ int lift_brows(long long per_band, int rows, int slots)
         const int br = (rows + nb - 1) / nb;
         if (nb > 1 && (rows + br - 1) / br != nb) continue;
         const long long rounds = (per_band * nb + slots - 1) / slots;
-        const long long cost = rounds * (br + 4);
+        const long long cost = rounds * ((long long)steps_per_row * br + warmup);
         if (best < 0 || cost < best) {
             best = cost;
             n_bands = nb;
@@ -1922,7 +1922,29 @@ int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, 
     const long long pd = plane_doubles(g);
     // (the second plane starts 16-byte aligned: the kernels' double2 loads)
     double *P[2] = {(double *)workspace_dev, (double *)workspace_dev + ((long long)g.hs[1] * g.ws[1] + 1) / 2 * 2};
-    for (int l = 1; l <= levels; ++l) {
+    int l_start = 1;
+    // levels 1 + 2 in one launch (lift_fwd12_kernel) on planes that halve evenly twice
+    // with dword-aligned level-1 subband rows; VCF_LIFT_NOFUSE=1: one launch per level (A/B)
+    const bool qp2 = (Q & (Q - 1)) == 0;
+    if (levels >= 2 && W % 4 == 0 && H % 4 == 0 && (W / 2) % 8 == 0 && g.packed_bytes % 4 == 0 &&
+        g.sb_off[1][0] % 4 == 0 && (g.sb_off[1][1] - g.sb_off[1][0]) % 4 == 0 && !getenv("VCF_LIFT_NOFUSE")) {
+        const int hh = g.hs[1], hw = g.ws[1], hh2 = g.hs[2], hw2 = g.ws[2];
+        const bool last2 = levels == 2;
+        auto kern = qp2 ? (last2 ? lift::lift_fwd12_kernel<true, true> : lift::lift_fwd12_kernel<true, false>)
+                        : (last2 ? lift::lift_fwd12_kernel<false, true> : lift::lift_fwd12_kernel<false, false>);
+        const int n_strips = (hw2 + lift::kV2 - 1) / lift::kV2;
+        const long long per_band = n_frames * n_strips;
+        const int brows = lift_brows(per_band, hh2, resident_slots(kern, lift::kNT), 2, 12);
+        const int n_bands = (hh2 + brows - 1) / brows;
+        const long long grid = per_band * n_bands;
+        if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, rgb_dev, (long long)H * W * 3, P[1], pd,
+                           packed_dev, g.packed_bytes, g.ll_off, g.sb_off[1][0], g.sb_off[1][1], g.sb_off[2][0],
+                           g.sb_off[2][1], g.sb_off[2][2], H, W, hh, hw, hh2, hw2, Q, n_strips, n_bands, brows);
+        if ((rc = hip_check(hipGetLastError(), "lift_fwd12_kernel launch")) != VCF_OK) return rc;
+        l_start = 3;   // LL2 is in P[1], where level 2 would have left it
+    }
+    for (int l = l_start; l <= levels; ++l) {
         const int h = g.hs[l - 1], w = g.ws[l - 1], hh = g.hs[l], hw = g.ws[l];
         const bool first = l == 1, last = l == levels;
         const int n_strips = (hw + lift::kValid - 1) / lift::kValid;
@@ -1931,7 +1953,6 @@ int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, 
                              (g.sb_off[l][1] - g.sb_off[l][0]) % 4 == 0;
         const int n_int = aligned ? n_strips : 0;
         const long long per_band = n_frames * n_strips;
-        const bool qp2 = (Q & (Q - 1)) == 0;
         auto kern = qp2 ? (first ? (last ? lift::lift_fwd_kernel<true, true, true> : lift::lift_fwd_kernel<true, false, true>)
                                  : (last ? lift::lift_fwd_kernel<false, true, true>
                                          : lift::lift_fwd_kernel<false, false, true>))

@@ -593,4 +593,197 @@ __global__ __launch_bounds__(kNT) void lift_inv_kernel(const uint8_t *__restrict
                                                   n_int, n_bands, brows, bid - edge_blocks, xch, rgb_lds);
 }
 
+// ---- levels 1 and 2 in one launch (forward) ---------------------------------
+// LL1 (49.8 MB of float64 per 4K frame) never leaves the chip.  A lane's two
+// level-1 coefficient columns are one level-2 pair, so after each level-1 step
+// the lane holds its pair of the new LL1 row; every two LL1 rows feed one step
+// of a second column pipeline (level 2, 5 doubles per column) and a one-pair-
+// per-lane horizontal lifting across the wave.  Exact lanes: level 1 pairs
+// 2..125 of the wave, level 2 lanes 3..60, so a strip owns 58 level-2 columns
+// (116 LL1 columns, 232 input columns) and a band of level-2 rows [M0, M1)
+// runs 2 (M1 - M0) + 12 level-1 steps.  Even planes only (W % 4 == 0,
+// W / 2 % 8 == 0, H % 4 == 0: no repeated LL1 row or column); level-1 detail
+// bytes leave as dwords through LDS, level-2 ones as bytes (58 x 3 per row is
+// not a whole number of dwords), LL2 as float64 (or u16 at levels == 2).
+constexpr int kV2 = 58;                                   // owned level-2 columns per wave (lanes 3..60)
+constexpr int kV1 = 2 * kV2;                              // owned level-1 columns (116)
+constexpr int kSb1B = kV1 * 3, kSb1Dw = 3 * kSb1B / 4;    // 348 bytes per level-1 subband row, 261 dwords
+
+// forward lifting of one row when each lane holds one pair (s, e) -> (K s, -e / K)
+__device__ __forceinline__ void fwd_row1(double &s, double &e)
+{
+    e = __builtin_fma(kA, s + from_next(s), e);
+    s = __builtin_fma(kB, from_prev(e) + e, s);
+    e = __builtin_fma(kG, s + from_next(s), e);
+    s = __builtin_fma(kD, from_prev(e) + e, s);
+    s = kK * s;
+    e = -e * kIK;
+}
+
+template <bool QP2, bool LAST2>
+__global__ __launch_bounds__(kNT) void lift_fwd12_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
+                                                         double *__restrict__ LL2out, long long plane_stride,
+                                                         uint8_t *__restrict__ packed, long long packed_stride,
+                                                         long long ll_off, long long off1_lh, long long off1_hl,
+                                                         long long off2_lh, long long off2_hl, long long off2_hh,
+                                                         int h, int w, int hh, int hw, int hh2, int hw2, int Q,
+                                                         int n_strips, int n_bands, int brows)
+{
+    __shared__ uint32_t px_lds[2 * 2 * kRowDw];
+    __shared__ uint32_t sb_lds[2 * (kSb1Dw + 1)];
+    const int qsh = QP2 ? __builtin_ctz((unsigned)Q) : 0;
+    const int t = threadIdx.x, lane = t & 63, ch = __builtin_amdgcn_readfirstlane(t >> 6);
+    int b = blockIdx.x;
+    const int strip = b % n_strips;
+    b /= n_strips;
+    const int band = b % n_bands;
+    const long long frame = b / n_bands;
+    const long long plane = frame * 3 + ch;
+    const int jl = strip * kV1 - 6 + 2 * lane;                 // the lane's level-1 columns jl, jl + 1
+    const int j2 = strip * kV2 - 3 + lane;                     // = its level-2 column
+    const bool own = lane >= 3 && lane < 3 + kV2;
+    const uint32_t drop1 = own && jl < hw ? 0u : kDrop;        // (jl even, hw even: both columns)
+    const uint32_t drop2 = own && j2 < hw2 ? 0u : kDrop;
+    const int M0 = band * brows, M1 = min(M0 + brows, hh2);
+    const uint8_t *src8 = rgb + frame * rgb_stride;
+    uint8_t *pk = packed + frame * packed_stride;
+    const __amdgpu_buffer_rsrc_t rs_pk = __builtin_amdgcn_make_buffer_rsrc(pk, 0, (int)packed_stride, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_ll = __builtin_amdgcn_make_buffer_rsrc(
+        LAST2 ? (void *)pk : (void *)(LL2out + plane * plane_stride), 0,
+        LAST2 ? 0 : (int)((long long)hh2 * hw2 * 8), 0x00020000);
+    const int x0 = 2 * (strip * kV1 - 6);                      // first staged pixel
+    const int boff = wrap(3 * x0 + 4 * t, 3 * w);
+    int nf = wrap(2 * M0 - 6, hh);                             // the next input row pair to fetch
+    auto next_pair = [&]() { nf = nf + 1 == hh ? 0 : nf + 1; };
+    auto fetch = [&]() -> uint2 {
+        const uint8_t *ra = src8 + (long long)(2 * nf) * w * 3 + boff;
+        const uint8_t *rb = src8 + (long long)(2 * nf + 1) * w * 3 + boff;
+        return make_uint2(*(const uint32_t *)ra, *(const uint32_t *)rb);
+    };
+    uint2 q0 = fetch();
+    next_pair();
+    uint2 q1 = fetch();
+    next_pair();
+    int buf = 0;
+    double sp[4], ep[4], e1p[4], s1p[4], e2p[4];               // level-1 column pipelines
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sp[k] = ep[k] = e1p[k] = s1p[k] = e2p[k] = 0.0;
+    double tp[2], fp[2], f1p[2], t1p[2], f2p[2];               // level-2 column pipelines
+#pragma unroll
+    for (int k = 0; k < 2; ++k) tp[k] = fp[k] = f1p[k] = t1p[k] = f2p[k] = 0.0;
+    const uint32_t sstep1 = (uint32_t)(off1_hl - off1_lh);
+    const int row_b1 = 3 * (hw - strip * kV1);                 // the strip's bytes in a level-1 row
+
+    // one level-1 step: ingests the next input row pair, returns the lane's
+    // pair of LL1 row m and stores row m's level-1 details when the band owns it
+    auto l1_step = [&](int m, bool row_own, double (&ll)[2]) {
+        double s[4], e[4];
+        uint32_t *st = px_lds + 2 * kRowDw * buf;
+        st[t] = q0.x;
+        st[kRowDw + t] = q0.y;
+        q0 = q1;
+        q1 = fetch();
+        next_pair();
+        asm volatile("" ::: "memory");
+        __syncthreads();
+        auto unpack = [&](auto chc) {
+            constexpr int C = decltype(chc)::value;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t *d = st + r * kRowDw + 3 * lane;
+                const int d0 = (int)d[0], d1 = (int)d[1], d2 = (int)d[2];
+                double *o = r ? e : s;
+                o[0] = ycocg_c<C>(d0 & 255, (d0 >> 8) & 255, (d0 >> 16) & 255);
+                o[1] = ycocg_c<C>((unsigned)d0 >> 24, d1 & 255, (d1 >> 8) & 255);
+                o[2] = ycocg_c<C>((d1 >> 16) & 255, (unsigned)d1 >> 24, d2 & 255);
+                o[3] = ycocg_c<C>((d2 >> 8) & 255, (d2 >> 16) & 255, (unsigned)d2 >> 24);
+            }
+        };
+        if (ch == 0) unpack(std::integral_constant<int, 0>{});
+        else if (ch == 1) unpack(std::integral_constant<int, 1>{});
+        else unpack(std::integral_constant<int, 2>{});
+        double L[4], D[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double e1 = __builtin_fma(kA, sp[k] + s[k], ep[k]);
+            const double s1 = __builtin_fma(kB, e1p[k] + e1, sp[k]);
+            const double e2 = __builtin_fma(kG, s1p[k] + s1, e1p[k]);
+            const double s2 = __builtin_fma(kD, e2p[k] + e2, s1p[k]);
+            L[k] = kK * s2;
+            D[k] = -e2 * kIK;
+            sp[k] = s[k];
+            ep[k] = e[k];
+            e1p[k] = e1;
+            s1p[k] = s1;
+            e2p[k] = e2;
+        }
+        double a[2] = {L[0], L[2]}, hl[2] = {L[1], L[3]}, lh[2] = {D[0], D[2]}, hhv[2] = {D[1], D[3]};
+        fwd_row(a, hl);
+        fwd_row(lh, hhv);
+        ll[0] = a[0];
+        ll[1] = a[1];
+        uint8_t *so = (uint8_t *)(sb_lds + (kSb1Dw + 1) * buf);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int p = drop1 ? 3 * kSb1B : 3 * (2 * (lane - 3) + k) + ch;   // others: the dummy dword
+            const int dsb = drop1 ? 0 : kSb1B;
+            so[p] = (uint8_t)(uint32_t)(qk<QP2>(lh[k], Q, qsh) + 128);
+            so[p + dsb] = (uint8_t)(uint32_t)(qk<QP2>(hl[k], Q, qsh) + 128);
+            so[p + 2 * dsb] = (uint8_t)(uint32_t)(qk<QP2>(hhv[k], Q, qsh) + 128);
+        }
+        __syncthreads();
+        const uint32_t base = (uint32_t)off1_lh + 3 * (uint32_t)(m * hw + strip * kV1);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int i = t + r * kNT;
+            const int ic = min(i, kSb1Dw - 1);
+            const int sub = ic / (kSb1B / 4), d = ic - (kSb1B / 4) * sub;
+            const uint32_t ok = row_own && i < kSb1Dw && 4 * d < row_b1 ? 0u : kDrop;
+            __builtin_amdgcn_raw_buffer_store_b32(sb_lds[(kSb1Dw + 1) * buf + ic], rs_pk,
+                                                  (base + sub * sstep1 + 4 * d) | ok, 0, 0);
+        }
+        buf ^= 1;
+    };
+
+    double ll_e[2], ll_o[2];
+    // level-1 warm-up: input pairs 2 M0 - 6 .. 2 M0 - 3 (no LL1 row yet)
+    for (int u = 0; u < 4; ++u) l1_step(0, false, ll_e);
+    for (int k = M0 - 2; k <= M1 + 1; ++k) {
+        // LL1 rows 2k, 2k + 1 (owned: 2 M0 <= row < 2 M1)
+        l1_step(2 * k, k >= M0 && k < M1, ll_e);
+        l1_step(2 * k + 1, k >= M0 && k < M1, ll_o);
+        double L2[2], D2[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const double e1 = __builtin_fma(kA, tp[c] + ll_e[c], fp[c]);    // e1_{k-1}
+            const double s1 = __builtin_fma(kB, f1p[c] + e1, tp[c]);        // s1_{k-1}
+            const double e2 = __builtin_fma(kG, t1p[c] + s1, f1p[c]);       // e2_{k-2}
+            const double s2 = __builtin_fma(kD, f2p[c] + e2, t1p[c]);       // s2_{k-2}
+            L2[c] = kK * s2;
+            D2[c] = -e2 * kIK;
+            tp[c] = ll_e[c];
+            fp[c] = ll_o[c];
+            f1p[c] = e1;
+            t1p[c] = s1;
+            f2p[c] = e2;
+        }
+        fwd_row1(L2[0], L2[1]);   // (LL2, HL2)
+        fwd_row1(D2[0], D2[1]);   // (LH2, HH2)
+        const int m2 = k - 2;
+        const uint32_t d2 = m2 >= M0 ? drop2 : kDrop;          // level-2 row m2 once the pipeline is full
+        const uint32_t o2 = (uint32_t)(m2 * hw2 + j2);
+        if (LAST2)
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(uint32_t)(qk<QP2>(L2[0], Q, qsh) + 128), rs_pk,
+                                                  ((uint32_t)ll_off + 2 * (3 * o2 + ch)) | d2, 0, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U32x2, L2[0]), rs_ll, (8 * o2) | d2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(uint32_t)(qk<QP2>(D2[0], Q, qsh) + 128), rs_pk,
+                                             ((uint32_t)off2_lh + 3 * o2 + ch) | d2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(uint32_t)(qk<QP2>(L2[1], Q, qsh) + 128), rs_pk,
+                                             ((uint32_t)off2_hl + 3 * o2 + ch) | d2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(uint32_t)(qk<QP2>(D2[1], Q, qsh) + 128), rs_pk,
+                                             ((uint32_t)off2_hh + 3 * o2 + ch) | d2, 0, 0);
+    }
+}
+
 }  // namespace lift
