@@ -138,3 +138,23 @@ def test_lift_fused_levels12_equal_unfused(monkeypatch, H, W, L, Q):
         ref = O.dwt_encode_frame(frames[0], "bior4.4", L, Q)
         frac, worst = _index_diff(ref, fused[0])
         assert worst <= INDEX_TOL and frac <= RARE_FINE, (frac, worst)
+
+
+@pytest.mark.parametrize("H,W,L,Q", [(96, 240, 2, 32), (64, 480, 5, 32), (32, 176, 3, 7), (200, 496, 2, 300),
+                                     (2160, 3840, 5, 32)])
+def test_lift_fused_levels21_decode_equal_unfused(monkeypatch, H, W, L, Q):
+    """Inverse levels 2 + 1 in one launch (lift_inv21_kernel) against the two
+    level launches: identical RGB bytes."""
+    import vcf_amd.dwt as DW
+    rng = np.random.Generator(np.random.PCG64(H * W + L))
+    frames = (np.stack([bench.synth_frame(H, W, 6), rng.integers(0, 256, (H, W, 3), dtype=np.uint8)])
+              if H * W < 4e6 else bench.synth_frame(H, W, 6)[None])
+    sb = DW.encode(frames, "bior4.4", L, Q)
+    fused = DW.decode(sb, H, W, "bior4.4", L, Q, lifting=True)
+    monkeypatch.setenv("VCF_LIFT_NOFUSE", "1")
+    split = DW.decode(sb, H, W, "bior4.4", L, Q, lifting=True)
+    assert np.array_equal(fused, split)
+    if H * W < 4e6:
+        want = O.dwt_decode_frame(sb[0], H, W, "bior4.4", L, Q)
+        d = np.abs(fused[0].astype(np.int64) - want.astype(np.int64))
+        assert d.max() <= BYTE_TOL   # (a small smooth frame at l = 2 lands on ties often: 1.3 % here)

@@ -1987,7 +1987,11 @@ int vcf_dwt_dz_decode_lift(const uint8_t *packed_dev, int64_t n_frames, int32_t 
     dwt_geom(H, W, levels, 10, g);
     const long long pd = plane_doubles(g);
     double *P[2] = {(double *)workspace_dev, (double *)workspace_dev + ((long long)g.hs[1] * g.ws[1] + 1) / 2 * 2};
-    for (int r = levels; r >= 1; --r) {
+    // levels 2 + 1 in one launch (lift_inv21_kernel) when LL1 is exactly twice LL2 both ways;
+    // VCF_LIFT_NOFUSE=1: one launch per level (A/B)
+    const bool fuse21 = levels >= 2 && g.hs[1] == 2 * g.hs[2] && g.ws[1] == 2 * g.ws[2] && g.ws[2] % 2 == 0 &&
+                        !getenv("VCF_LIFT_NOFUSE");
+    for (int r = levels; r >= (fuse21 ? 3 : 1); --r) {
         const int h = g.hs[r], w = g.ws[r];
         const int oh = r > 1 ? g.hs[r - 1] : 2 * h, ow = r > 1 ? g.ws[r - 1] : 2 * w;
         const bool coarsest = r == levels, rgb = r == 1;
@@ -2010,6 +2014,24 @@ int vcf_dwt_dz_decode_lift(const uint8_t *packed_dev, int64_t n_frames, int32_t 
                            w, P[r & 1], rgb_dev, (long long)(2 * g.hs[1]) * (2 * g.ws[1]) * 3, h, w, oh, ow, Q, n_int,
                            n_edge, n_bands, brows, n_bands_e, brows_e, (int)edge_blocks);
         if ((rc = hip_check(hipGetLastError(), "lift_inv_kernel launch")) != VCF_OK) return rc;
+    }
+    if (fuse21) {
+        const int h2 = g.hs[2], w2 = g.ws[2], h1 = g.hs[1], w1 = g.ws[1];
+        const bool coarsest = levels == 2;
+        auto kern = coarsest ? lift::lift_inv21_kernel<true> : lift::lift_inv21_kernel<false>;
+        const int n_strips = (w2 + lift::kV2 - 1) / lift::kV2;
+        const long long per_band = n_frames * n_strips;
+        // a band of B level-2 rows: B + 6 level-2 steps, 2 B + 4 level-1 steps (the RGB ones dominate)
+        const int brows = lift_brows(per_band, h2, resident_slots(kern, lift::kNT), 2, 12);
+        const int n_bands = (h2 + brows - 1) / brows;
+        const long long grid = per_band * n_bands;
+        if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
+        // LL2 from the plane level 3 wrote (P[1]), or the packed u16 at levels == 2
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, packed_dev, g.packed_bytes, g.ll_off,
+                           g.sb_off[2][0], g.sb_off[2][1], g.sb_off[2][2], g.sb_off[1][0], g.sb_off[1][1],
+                           g.sb_off[1][2], coarsest ? nullptr : P[1], pd, rgb_dev, (long long)(2 * h1) * (2 * w1) * 3,
+                           h2, w2, h1, w1, Q, n_strips, n_bands, brows);
+        if ((rc = hip_check(hipGetLastError(), "lift_inv21_kernel launch")) != VCF_OK) return rc;
     }
     return VCF_OK;
 }

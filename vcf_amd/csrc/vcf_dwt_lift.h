@@ -786,4 +786,196 @@ __global__ __launch_bounds__(kNT) void lift_fwd12_kernel(const uint8_t *__restri
     }
 }
 
+// ---- levels 2 and 1 in one launch (inverse) ---------------------------------
+// The mirror of lift_fwd12_kernel: a lane's level-2 pair, inverted across the
+// wave (one pair per lane), is the lane's two LL1 columns; a level-2 column
+// pipeline turns each level-2 row into two LL1 rows, each of which is one step
+// of the level-1 inverse (two pairs per lane) down to RGB.  LL1 never reaches
+// HBM.  Exact lanes 3..60 (level 2 leaves lanes 2..61, level 1 narrows by
+// one); a band of level-2 rows [B0, B1) owns RGB rows [4 B0, 4 B1) and runs
+// B1 - B0 + 6 level-2 steps.  Planes that halve evenly (LL1 = 2x LL2 both
+// ways).
+constexpr int kRgbRow12 = 2 * kV1 * 3;                    // bytes of one owned RGB row (232 pixels)
+constexpr int kRgbDw12 = 2 * kRgbRow12 / 4;               // both rows, dwords (348)
+
+// inverse lifting of one row when each lane holds one pair (cA, cD) -> (x[2j], x[2j+1])
+__device__ __forceinline__ void inv_row1(double &a, double &d)
+{
+    double s = a * kIK, e = -d * kK;
+    s = __builtin_fma(-kD, from_prev(e) + e, s);
+    e = __builtin_fma(-kG, s + from_next(s), e);
+    s = __builtin_fma(-kB, from_prev(e) + e, s);
+    e = __builtin_fma(-kA, s + from_next(s), e);
+    a = s;
+    d = e;
+}
+
+template <bool FROM_PACKED2>
+__global__ __launch_bounds__(kNT) void lift_inv21_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
+                                                         long long ll_off, long long off2_lh, long long off2_hl,
+                                                         long long off2_hh, long long off1_lh, long long off1_hl,
+                                                         long long off1_hh, const double *__restrict__ in,
+                                                         long long plane_stride, uint8_t *__restrict__ rgb_out,
+                                                         long long rgb_stride, int h2, int w2, int h1, int w1, int Q,
+                                                         int n_strips, int n_bands, int brows)
+{
+    __shared__ double xch[3 * kOut * 64];
+    __shared__ uint32_t rgb_lds[kRgbDw12 + 1];
+    const int t = threadIdx.x, lane = t & 63, ch = __builtin_amdgcn_readfirstlane(t >> 6);
+    int b = blockIdx.x;
+    const int strip = b % n_strips;
+    b /= n_strips;
+    const int band = b % n_bands;
+    const long long frame = b / n_bands;
+    const long long plane = frame * 3 + ch;
+    const int j2o = strip * kV2 - 3 + lane;                    // the lane's level-2 column (unwrapped)
+    const int j2 = wrap(j2o, w2);
+    const int jl = 2 * j2;                                     // its level-1 columns jl, jl + 1 (even w1)
+    const bool own = lane >= 3 && lane < 3 + kV2 && j2o < w2;
+    const int B0 = band * brows, B1 = min(B0 + brows, h2);
+    const int ow = 2 * w1;                                     // RGB width
+    const uint8_t *pk = packed + frame * packed_stride;
+    const double *src = FROM_PACKED2 ? nullptr : in + plane * plane_stride;
+    const __amdgpu_buffer_rsrc_t rs_out =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(rgb_out + frame * rgb_stride), 0, (int)rgb_stride, 0x00020000);
+    const int row_b = 3 * (ow - 2 * strip * kV1);              // the strip's bytes in an RGB row
+
+    // prefetch: level-2 row q2f (LL2 and its three detail bytes), and the level-1
+    // detail bytes of the two LL1 rows the next step produces
+    int q2f = wrap(B0 - 3, h2);
+    double nA2;
+    int n2[3], n1[2][3][2];
+    auto load2 = [&]() {
+        const long long idx = (long long)q2f * w2 + j2;
+        nA2 = FROM_PACKED2 ? dequant((int16_t)*(const uint16_t *)(pk + ll_off + 2 * (3 * idx + ch)), Q)
+                           : src[(long long)q2f * w2 + j2];
+        n2[0] = pk[off2_hl + 3 * idx + ch];
+        n2[1] = pk[off2_lh + 3 * idx + ch];
+        n2[2] = pk[off2_hh + 3 * idx + ch];
+        q2f = q2f + 1 == h2 ? 0 : q2f + 1;
+    };
+    auto load1 = [&](int m2) {   // LL1 rows 2 m2, 2 m2 + 1 (wrapped)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const long long row = (long long)wrap(2 * m2 + r, h1) * w1;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const long long idx = row + jl + k;
+                n1[r][0][k] = pk[off1_hl + 3 * idx + ch];
+                n1[r][1][k] = pk[off1_lh + 3 * idx + ch];
+                n1[r][2][k] = pk[off1_hh + 3 * idx + ch];
+            }
+        }
+    };
+    // level-2 column pipelines (the lane's two LL1 columns), level-1 ones (its four output columns)
+    double ep2[2], s1p2[2], e1pp2[2], s2pp2[2], ep[4], s1p[4], e1pp[4], s2pp[4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) ep2[k] = s1p2[k] = e1pp2[k] = s2pp2[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ep[k] = s1p[k] = e1pp[k] = s2pp[k] = 0.0;
+
+    // one level-2 step: the prefetched row -> the lane's LL1 values of rows 2(q2-2), 2(q2-2)+1
+    auto l2_step = [&](double (&r0)[2], double (&r1)[2]) {
+        double a = nA2, hl = dequant((int16_t)n2[0], Q), lh = dequant((int16_t)n2[1], Q),
+               hh = dequant((int16_t)n2[2], Q);
+        load2();
+        asm volatile("" ::: "memory");
+        inv_row1(a, hl);   // 'a' row: LL1 columns jl, jl + 1 of the vertical low band
+        inv_row1(lh, hh);  // 'd' row
+        const double A[2] = {a, hl}, Dd[2] = {lh, hh};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const double s = A[k] * kIK, e = -Dd[k] * kK;
+            const double s1 = __builtin_fma(-kD, ep2[k] + e, s);
+            const double e1 = __builtin_fma(-kG, s1p2[k] + s1, ep2[k]);
+            const double s2 = __builtin_fma(-kB, e1pp2[k] + e1, s1p2[k]);
+            const double e2 = __builtin_fma(-kA, s2pp2[k] + s2, e1pp2[k]);
+            r0[k] = s2pp2[k];
+            r1[k] = e2;
+            ep2[k] = e;
+            s1p2[k] = s1;
+            e1pp2[k] = e1;
+            s2pp2[k] = s2;
+        }
+    };
+    // one level-1 step: LL1 row q (the lane's two values, the details in n1[r]) ->
+    // RGB rows 2(q-2), 2(q-2)+1, stored when `emit`
+    auto l1_step = [&](const double (&x)[2], const int (&db)[3][2], int q, bool emit) {
+        double a[2] = {x[0], x[1]}, hl[2], lh[2], hhv[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            hl[k] = dequant((int16_t)db[0][k], Q);
+            lh[k] = dequant((int16_t)db[1][k], Q);
+            hhv[k] = dequant((int16_t)db[2][k], Q);
+        }
+        inv_row(a, hl);
+        inv_row(lh, hhv);
+        const double A[4] = {a[0], hl[0], a[1], hl[1]}, Dd[4] = {lh[0], hhv[0], lh[1], hhv[1]};
+        double o0[4], o1[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double s = A[k] * kIK, e = -Dd[k] * kK;
+            const double s1 = __builtin_fma(-kD, ep[k] + e, s);
+            const double e1 = __builtin_fma(-kG, s1p[k] + s1, ep[k]);
+            const double s2 = __builtin_fma(-kB, e1pp[k] + e1, s1p[k]);
+            const double e2 = __builtin_fma(-kA, s2pp[k] + s2, e1pp[k]);
+            o0[k] = s2pp[k];
+            o1[k] = e2;
+            ep[k] = e;
+            s1p[k] = s1;
+            e1pp[k] = e1;
+            s2pp[k] = s2;
+        }
+        double *xo = xch + ch * kOut * 64;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            xo[k * 64 + lane] = o0[k];
+            xo[(4 + k) * 64 + lane] = o1[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kOut; ++k) {
+            const int rr = k / 4, c = k % 4;
+            const double Y = xch[k * 64 + lane], Co = xch[(kOut + k) * 64 + lane], Cg = xch[(2 * kOut + k) * 64 + lane];
+            const double v = ch == 0 ? Y + Co - Cg : (ch == 1 ? Y + Cg : Y - Co - Cg);
+            const uint8_t u = (uint8_t)(v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v));
+            const int pos = own ? kRgbRow12 * rr + 3 * (4 * (lane - 3) + c) + ch : kRgbDw12 * 4;   // others: dummy
+            ((uint8_t *)rgb_lds)[pos] = u;
+        }
+        __syncthreads();
+        const int r0 = 2 * (q - 2);
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2) {
+            const int i = t + i2 * kNT;
+            const int ic = min(i, kRgbDw12 - 1);
+            const int row = ic >= kRgbRow12 / 4, d = ic - (kRgbRow12 / 4) * row;
+            const uint32_t o = 3 * (uint32_t)((r0 + row) * ow + 2 * strip * kV1) + 4 * d;
+            const uint32_t ok = emit && i < kRgbDw12 && 4 * d < row_b ? 0u : kDrop;
+            __builtin_amdgcn_raw_buffer_store_b32(rgb_lds[ic], rs_out, o | ok, 0, 0);
+        }
+    };
+
+    load2();
+    // level-2 warm-up: rows B0 - 3 .. B0 (no LL1 row yet)
+    double r0[2], r1[2];
+    for (int u = 0; u < 4; ++u) l2_step(r0, r1);
+    load1(B0 - 1);
+    for (int q2 = B0 + 1; q2 <= B1 + 2; ++q2) {
+        const int m2 = q2 - 2;                                 // this step's LL1 rows 2 m2, 2 m2 + 1
+        l2_step(r0, r1);
+        int cur[2][3][2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) cur[r][u][k] = n1[r][u][k];
+        load1(m2 + 1);                                         // the next step's level-1 details
+        asm volatile("" ::: "memory");
+        // level-1 rows 2 m2, 2 m2 + 1: RGB row pairs 2 m2 - 2, 2 m2 - 1 (owned from 2 B0 on)
+        l1_step(r0, cur[0], 2 * m2, m2 >= B0 + 1);
+        l1_step(r1, cur[1], 2 * m2 + 1, m2 >= B0 + 1);
+    }
+}
+
 }  // namespace lift
