@@ -159,3 +159,19 @@ def test_codecs_accept_the_plugins_and_refuse_the_rest():
         CoDec(PP.parse(PP.dct_parser(quantizer="LloydMax"), ["encode", "-a", "LloydMax", "-L", "1"]))
     with pytest.raises(NotImplementedError):
         c.encode_indices(np.zeros((8, 8, 3), np.uint8))
+
+
+def test_dwt_codec_lifting_opt_in(monkeypatch):
+    """The opt-in lifting form (no reference counterpart): VCF_DWT_LIFTING=1 or
+    args.dwt_lifting; bior4.4 only, refused for any other wavelet."""
+    from vcf_amd.codec import parser as PP
+    from vcf_amd.codec.dwt2d import CoDec as DWTCoDec
+    assert not DWTCoDec(PP.parse(PP.dwt_parser(), ["encode", "-w", "bior4.4"])).lifting
+    monkeypatch.setenv("VCF_DWT_LIFTING", "1")
+    assert DWTCoDec(PP.parse(PP.dwt_parser(), ["encode", "-w", "bior4.4"])).lifting
+    with pytest.raises(NotImplementedError):
+        DWTCoDec(PP.parse(PP.dwt_parser(), ["encode"]))   # the reference's default -w db5
+    monkeypatch.delenv("VCF_DWT_LIFTING")
+    args = PP.parse(PP.dwt_parser(), ["encode", "-w", "bior4.4"])
+    args.dwt_lifting = True
+    assert DWTCoDec(args).lifting
