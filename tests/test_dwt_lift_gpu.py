@@ -118,12 +118,13 @@ def test_lift_rejects_other_wavelets():
 
 
 @pytest.mark.parametrize("H,W,L,Q", [(96, 240, 2, 32), (64, 480, 5, 32), (32, 176, 3, 7), (200, 496, 2, 300),
-                                     (2160, 3840, 5, 32)])
+                                     (256, 512, 4, 32), (256, 512, 5, 7), (2160, 3840, 5, 32)])
 def test_lift_fused_levels12_equal_unfused(monkeypatch, H, W, L, Q):
-    """Levels 1 + 2 in one launch (lift_fwd12_kernel: planes with W % 4 == 0,
-    W / 2 % 8 == 0, H % 4 == 0) compute the same operations as the two level
-    launches: identical bytes, one strip and several, partial last strips,
-    LL2 as the last level (u16) and as float64 for level 3."""
+    """Levels 1 + 2 (and 3 + 4: (256, 512, 4 / 5), C3) in one launch
+    (lift_fwd12_kernel: planes with w % 4 == 0, w / 2 % 8 == 0, h % 4 == 0)
+    compute the same operations as the level launches: identical bytes, one
+    strip and several, partial last strips, the pair's LL as the last level
+    (u16) and as float64 for the next."""
     import vcf_amd.dwt as DW
     rng = np.random.Generator(np.random.PCG64(H + W + L))
     frames = (np.stack([bench.synth_frame(H, W, 5), rng.integers(0, 256, (H, W, 3), dtype=np.uint8)])

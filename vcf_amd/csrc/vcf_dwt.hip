@@ -1922,31 +1922,44 @@ int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, 
     const long long pd = plane_doubles(g);
     // (the second plane starts 16-byte aligned: the kernels' double2 loads)
     double *P[2] = {(double *)workspace_dev, (double *)workspace_dev + ((long long)g.hs[1] * g.ws[1] + 1) / 2 * 2};
-    int l_start = 1;
-    // levels 1 + 2 in one launch (lift_fwd12_kernel) on planes that halve evenly twice
-    // with dword-aligned level-1 subband rows; VCF_LIFT_NOFUSE=1: one launch per level (A/B)
     const bool qp2 = (Q & (Q - 1)) == 0;
-    if (levels >= 2 && W % 4 == 0 && H % 4 == 0 && (W / 2) % 8 == 0 && g.packed_bytes % 4 == 0 &&
-        g.sb_off[1][0] % 4 == 0 && (g.sb_off[1][1] - g.sb_off[1][0]) % 4 == 0 && !getenv("VCF_LIFT_NOFUSE")) {
-        const int hh = g.hs[1], hw = g.ws[1], hh2 = g.hs[2], hw2 = g.ws[2];
-        const bool last2 = levels == 2;
-        auto kern = qp2 ? (last2 ? lift::lift_fwd12_kernel<true, true> : lift::lift_fwd12_kernel<true, false>)
-                        : (last2 ? lift::lift_fwd12_kernel<false, true> : lift::lift_fwd12_kernel<false, false>);
-        const int n_strips = (hw2 + lift::kV2 - 1) / lift::kV2;
-        const long long per_band = n_frames * n_strips;
-        const int brows = lift_brows(per_band, hh2, resident_slots(kern, lift::kNT), 2, 12);
-        const int n_bands = (hh2 + brows - 1) / brows;
-        const long long grid = per_band * n_bands;
-        if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, rgb_dev, (long long)H * W * 3, P[1], pd,
-                           packed_dev, g.packed_bytes, g.ll_off, g.sb_off[1][0], g.sb_off[1][1], g.sb_off[2][0],
-                           g.sb_off[2][1], g.sb_off[2][2], H, W, hh, hw, hh2, hw2, Q, n_strips, n_bands, brows);
-        if ((rc = hip_check(hipGetLastError(), "lift_fwd12_kernel launch")) != VCF_OK) return rc;
-        l_start = 3;   // LL2 is in P[1], where level 2 would have left it
-    }
-    for (int l = l_start; l <= levels; ++l) {
+    // explicit ping-pong: a launch reads `in` (level l - 1's LL) and writes the other plane
+    const double *in = nullptr;
+    int nb = 0;
+    const bool nofuse = getenv("VCF_LIFT_NOFUSE") != nullptr;   // one launch per level (A/B)
+    for (int l = 1; l <= levels;) {
         const int h = g.hs[l - 1], w = g.ws[l - 1], hh = g.hs[l], hw = g.ws[l];
-        const bool first = l == 1, last = l == levels;
+        const bool first = l == 1;
+        double *out = P[nb];
+        // levels l and l + 1 in one launch (lift_fwd12_kernel) on planes that halve evenly
+        // twice with dword-aligned level-l subband rows (C3: levels 1 + 2 and 3 + 4)
+        if (!nofuse && l + 1 <= levels && w % 4 == 0 && h % 4 == 0 && hw % 8 == 0 && w == 2 * hw &&
+            g.packed_bytes % 4 == 0 && g.sb_off[l][0] % 4 == 0 && (g.sb_off[l][1] - g.sb_off[l][0]) % 4 == 0) {
+            const int hh2 = g.hs[l + 1], hw2 = g.ws[l + 1];
+            const bool last2 = l + 1 == levels;
+            auto pick = [&](auto fc) {
+                constexpr bool F1 = decltype(fc)::value;
+                return qp2 ? (last2 ? lift::lift_fwd12_kernel<true, true, F1> : lift::lift_fwd12_kernel<true, false, F1>)
+                           : (last2 ? lift::lift_fwd12_kernel<false, true, F1> : lift::lift_fwd12_kernel<false, false, F1>);
+            };
+            auto kern = first ? pick(std::true_type{}) : pick(std::false_type{});
+            const int n_strips = (hw2 + lift::kV2 - 1) / lift::kV2;
+            const long long per_band = n_frames * n_strips;
+            const int brows = lift_brows(per_band, hh2, resident_slots(kern, lift::kNT), 2, 12);
+            const int n_bands = (hh2 + brows - 1) / brows;
+            const long long grid = per_band * n_bands;
+            if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
+            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, rgb_dev, (long long)H * W * 3, in,
+                               out, pd, packed_dev, g.packed_bytes, g.ll_off, g.sb_off[l][0], g.sb_off[l][1],
+                               g.sb_off[l + 1][0], g.sb_off[l + 1][1], g.sb_off[l + 1][2], h, w, hh, hw, hh2, hw2, Q,
+                               n_strips, n_bands, brows);
+            if ((rc = hip_check(hipGetLastError(), "lift_fwd12_kernel launch")) != VCF_OK) return rc;
+            in = out;
+            nb ^= 1;
+            l += 2;
+            continue;
+        }
+        const bool last = l == levels;
         const int n_strips = (hw + lift::kValid - 1) / lift::kValid;
         // the branch-free body for even planes with dword-aligned subband rows, else the general one
         const bool aligned = w == 2 * hw && hw % 4 == 0 && g.packed_bytes % 4 == 0 && g.sb_off[l][0] % 4 == 0 &&
@@ -1966,11 +1979,13 @@ int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, 
         const long long edge_blocks = n_frames * n_edge * n_bands_e;
         const long long grid = n_frames * n_int * n_bands + edge_blocks;
         if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, rgb_dev, (long long)H * W * 3,
-                           first ? nullptr : P[l & 1], pd, P[(l - 1) & 1], packed_dev, g.packed_bytes, g.ll_off,
-                           g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], h, w, hh, hw, Q, n_int, n_edge, n_bands,
-                           brows, n_bands_e, brows_e, (int)edge_blocks);
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, rgb_dev, (long long)H * W * 3, in, pd,
+                           out, packed_dev, g.packed_bytes, g.ll_off, g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], h,
+                           w, hh, hw, Q, n_int, n_edge, n_bands, brows, n_bands_e, brows_e, (int)edge_blocks);
         if ((rc = hip_check(hipGetLastError(), "lift_fwd_kernel launch")) != VCF_OK) return rc;
+        in = out;
+        nb ^= 1;
+        ++l;
     }
     return VCF_OK;
 }

@@ -620,8 +620,11 @@ __device__ __forceinline__ void fwd_row1(double &s, double &e)
     e = -e * kIK;
 }
 
-template <bool QP2, bool LAST2>
+// FIRST = false: the same pair of levels l, l + 1 over a float64 LL plane
+// (C3's levels 3 + 4), four input columns per lane as two 16-byte loads per row
+template <bool QP2, bool LAST2, bool FIRST = true>
 __global__ __launch_bounds__(kNT) void lift_fwd12_kernel(const uint8_t *__restrict__ rgb, long long rgb_stride,
+                                                         const double *__restrict__ in,
                                                          double *__restrict__ LL2out, long long plane_stride,
                                                          uint8_t *__restrict__ packed, long long packed_stride,
                                                          long long ll_off, long long off1_lh, long long off1_hl,
@@ -629,7 +632,7 @@ __global__ __launch_bounds__(kNT) void lift_fwd12_kernel(const uint8_t *__restri
                                                          int h, int w, int hh, int hw, int hh2, int hw2, int Q,
                                                          int n_strips, int n_bands, int brows)
 {
-    __shared__ uint32_t px_lds[2 * 2 * kRowDw];
+    __shared__ uint32_t px_lds[FIRST ? 2 * 2 * kRowDw : 1];
     __shared__ uint32_t sb_lds[2 * (kSb1Dw + 1)];
     const int qsh = QP2 ? __builtin_ctz((unsigned)Q) : 0;
     const int t = threadIdx.x, lane = t & 63, ch = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -645,7 +648,9 @@ __global__ __launch_bounds__(kNT) void lift_fwd12_kernel(const uint8_t *__restri
     const uint32_t drop1 = own && jl < hw ? 0u : kDrop;        // (jl even, hw even: both columns)
     const uint32_t drop2 = own && j2 < hw2 ? 0u : kDrop;
     const int M0 = band * brows, M1 = min(M0 + brows, hh2);
-    const uint8_t *src8 = rgb + frame * rgb_stride;
+    const uint8_t *src8 = FIRST ? rgb + frame * rgb_stride : nullptr;
+    const double *src = FIRST ? nullptr : in + plane * plane_stride;
+    const int cw = 2 * wrap(jl, hw);                           // float64 input: the lane's four columns
     uint8_t *pk = packed + frame * packed_stride;
     const __amdgpu_buffer_rsrc_t rs_pk = __builtin_amdgcn_make_buffer_rsrc(pk, 0, (int)packed_stride, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_ll = __builtin_amdgcn_make_buffer_rsrc(
@@ -656,14 +661,35 @@ __global__ __launch_bounds__(kNT) void lift_fwd12_kernel(const uint8_t *__restri
     int nf = wrap(2 * M0 - 6, hh);                             // the next input row pair to fetch
     auto next_pair = [&]() { nf = nf + 1 == hh ? 0 : nf + 1; };
     auto fetch = [&]() -> uint2 {
+        if constexpr (!FIRST) return make_uint2(0, 0);
         const uint8_t *ra = src8 + (long long)(2 * nf) * w * 3 + boff;
         const uint8_t *rb = src8 + (long long)(2 * nf + 1) * w * 3 + boff;
         return make_uint2(*(const uint32_t *)ra, *(const uint32_t *)rb);
     };
-    uint2 q0 = fetch();
-    next_pair();
-    uint2 q1 = fetch();
-    next_pair();
+    double ns[4] = {0, 0, 0, 0}, ne[4] = {0, 0, 0, 0};
+    auto dload = [&]() {
+        const double2 *qa = (const double2 *)(src + (long long)(2 * nf) * w + cw);
+        const double2 *qb = (const double2 *)(src + (long long)(2 * nf + 1) * w + cw);
+        const double2 a0 = qa[0], a1 = qa[1], b0 = qb[0], b1 = qb[1];
+        ns[0] = a0.x;
+        ns[1] = a0.y;
+        ns[2] = a1.x;
+        ns[3] = a1.y;
+        ne[0] = b0.x;
+        ne[1] = b0.y;
+        ne[2] = b1.x;
+        ne[3] = b1.y;
+    };
+    uint2 q0 = make_uint2(0, 0), q1 = make_uint2(0, 0);
+    if (FIRST) {
+        q0 = fetch();
+        next_pair();
+        q1 = fetch();
+        next_pair();
+    } else {
+        dload();
+        next_pair();
+    }
     int buf = 0;
     double sp[4], ep[4], e1p[4], s1p[4], e2p[4];               // level-1 column pipelines
 #pragma unroll
@@ -679,6 +705,16 @@ __global__ __launch_bounds__(kNT) void lift_fwd12_kernel(const uint8_t *__restri
     auto l1_step = [&](int m, bool row_own, double (&ll)[2]) {
         double s[4], e[4];
         uint32_t *st = px_lds + 2 * kRowDw * buf;
+        if constexpr (!FIRST) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                s[k] = ns[k];
+                e[k] = ne[k];
+            }
+            dload();
+            next_pair();
+            asm volatile("" ::: "memory");
+        } else {
         st[t] = q0.x;
         st[kRowDw + t] = q0.y;
         q0 = q1;
@@ -702,6 +738,7 @@ __global__ __launch_bounds__(kNT) void lift_fwd12_kernel(const uint8_t *__restri
         if (ch == 0) unpack(std::integral_constant<int, 0>{});
         else if (ch == 1) unpack(std::integral_constant<int, 1>{});
         else unpack(std::integral_constant<int, 2>{});
+        }
         double L[4], D[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
