@@ -142,7 +142,7 @@ def test_lift_fused_levels12_equal_unfused(monkeypatch, H, W, L, Q):
 
 
 @pytest.mark.parametrize("H,W,L,Q", [(96, 240, 2, 32), (64, 480, 5, 32), (32, 176, 3, 7), (200, 496, 2, 300),
-                                     (2160, 3840, 5, 32)])
+                                     (256, 512, 4, 32), (256, 512, 5, 7), (2160, 3840, 5, 32)])
 def test_lift_fused_levels21_decode_equal_unfused(monkeypatch, H, W, L, Q):
     """Inverse levels 2 + 1 in one launch (lift_inv21_kernel) against the two
     level launches: identical RGB bytes."""

@@ -2002,14 +2002,42 @@ int vcf_dwt_dz_decode_lift(const uint8_t *packed_dev, int64_t n_frames, int32_t 
     dwt_geom(H, W, levels, 10, g);
     const long long pd = plane_doubles(g);
     double *P[2] = {(double *)workspace_dev, (double *)workspace_dev + ((long long)g.hs[1] * g.ws[1] + 1) / 2 * 2};
-    // levels 2 + 1 in one launch (lift_inv21_kernel) when LL1 is exactly twice LL2 both ways;
-    // VCF_LIFT_NOFUSE=1: one launch per level (A/B)
-    const bool fuse21 = levels >= 2 && g.hs[1] == 2 * g.hs[2] && g.ws[1] == 2 * g.ws[2] && g.ws[2] % 2 == 0 &&
-                        !getenv("VCF_LIFT_NOFUSE");
-    for (int r = levels; r >= (fuse21 ? 3 : 1); --r) {
+    // explicit ping-pong: a launch reads `in` (the LL of the level above) and writes the other plane
+    const double *in = nullptr;
+    int nb = 0;
+    const bool nofuse = getenv("VCF_LIFT_NOFUSE") != nullptr;   // one launch per level (A/B)
+    for (int r = levels; r >= 1;) {
         const int h = g.hs[r], w = g.ws[r];
+        const bool coarsest = r == levels;
+        double *out = P[nb];
+        // levels r and r - 1 in one launch (lift_inv21_kernel) when each LL is exactly twice
+        // the one above both ways (C3: levels 4 + 3 and 2 + 1)
+        const int hl = r >= 2 ? g.hs[r - 1] : 0, wl = r >= 2 ? g.ws[r - 1] : 0;
+        if (!nofuse && r >= 2 && hl == 2 * h && wl == 2 * w && w % 2 == 0 &&
+            (r - 1 == 1 || (g.hs[r - 2] == 2 * hl && g.ws[r - 2] == 2 * wl))) {
+            const bool rgb = r - 1 == 1;
+            auto kern = coarsest ? (rgb ? lift::lift_inv21_kernel<true, true> : lift::lift_inv21_kernel<true, false>)
+                                 : (rgb ? lift::lift_inv21_kernel<false, true> : lift::lift_inv21_kernel<false, false>);
+            const int n_strips = (w + lift::kV2 - 1) / lift::kV2;
+            const long long per_band = n_frames * n_strips;
+            // a band of B upper-level rows: B + 6 of its steps, 2 B + 4 lower-level ones
+            const int brows = lift_brows(per_band, h, resident_slots(kern, lift::kNT), 2, 12);
+            const int n_bands = (h + brows - 1) / brows;
+            const long long grid = per_band * n_bands;
+            if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
+            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, packed_dev, g.packed_bytes, g.ll_off,
+                               g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], g.sb_off[r - 1][0],
+                               g.sb_off[r - 1][1], g.sb_off[r - 1][2], in, pd, out, rgb_dev,
+                               (long long)(2 * g.hs[1]) * (2 * g.ws[1]) * 3, h, w, hl, wl, Q, n_strips, n_bands,
+                               brows);
+            if ((rc = hip_check(hipGetLastError(), "lift_inv21_kernel launch")) != VCF_OK) return rc;
+            in = out;
+            nb ^= 1;
+            r -= 2;
+            continue;
+        }
         const int oh = r > 1 ? g.hs[r - 1] : 2 * h, ow = r > 1 ? g.ws[r - 1] : 2 * w;
-        const bool coarsest = r == levels, rgb = r == 1;
+        const bool rgb = r == 1;
         const int n_strips = (w + lift::kValid - 1) / lift::kValid;
         // the branch-free body for even planes (and even trimmed outputs), else the general one
         const bool aligned = w % 2 == 0 && ow % 2 == 0;
@@ -2023,30 +2051,15 @@ int vcf_dwt_dz_decode_lift(const uint8_t *packed_dev, int64_t n_frames, int32_t 
         const long long edge_blocks = n_frames * n_edge * n_bands_e;
         const long long grid = n_frames * n_int * n_bands + edge_blocks;
         if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
-        // level r reads the plane level r + 1 wrote (h x w, row stride w) and writes the other
+        // level r reads the plane the level above wrote (h x w, row stride w) and writes the other
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, packed_dev, g.packed_bytes, g.ll_off,
-                           g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], coarsest ? nullptr : P[(r + 1) & 1], pd,
-                           w, P[r & 1], rgb_dev, (long long)(2 * g.hs[1]) * (2 * g.ws[1]) * 3, h, w, oh, ow, Q, n_int,
-                           n_edge, n_bands, brows, n_bands_e, brows_e, (int)edge_blocks);
+                           g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], in, pd, w, out, rgb_dev,
+                           (long long)(2 * g.hs[1]) * (2 * g.ws[1]) * 3, h, w, oh, ow, Q, n_int, n_edge, n_bands,
+                           brows, n_bands_e, brows_e, (int)edge_blocks);
         if ((rc = hip_check(hipGetLastError(), "lift_inv_kernel launch")) != VCF_OK) return rc;
-    }
-    if (fuse21) {
-        const int h2 = g.hs[2], w2 = g.ws[2], h1 = g.hs[1], w1 = g.ws[1];
-        const bool coarsest = levels == 2;
-        auto kern = coarsest ? lift::lift_inv21_kernel<true> : lift::lift_inv21_kernel<false>;
-        const int n_strips = (w2 + lift::kV2 - 1) / lift::kV2;
-        const long long per_band = n_frames * n_strips;
-        // a band of B level-2 rows: B + 6 level-2 steps, 2 B + 4 level-1 steps (the RGB ones dominate)
-        const int brows = lift_brows(per_band, h2, resident_slots(kern, lift::kNT), 2, 12);
-        const int n_bands = (h2 + brows - 1) / brows;
-        const long long grid = per_band * n_bands;
-        if (grid > 0x7fffffffLL) return set_error(VCF_ERR_INVALID, "too many frames per call");
-        // LL2 from the plane level 3 wrote (P[1]), or the packed u16 at levels == 2
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(lift::kNT), 0, s, packed_dev, g.packed_bytes, g.ll_off,
-                           g.sb_off[2][0], g.sb_off[2][1], g.sb_off[2][2], g.sb_off[1][0], g.sb_off[1][1],
-                           g.sb_off[1][2], coarsest ? nullptr : P[1], pd, rgb_dev, (long long)(2 * h1) * (2 * w1) * 3,
-                           h2, w2, h1, w1, Q, n_strips, n_bands, brows);
-        if ((rc = hip_check(hipGetLastError(), "lift_inv21_kernel launch")) != VCF_OK) return rc;
+        in = out;
+        nb ^= 1;
+        --r;
     }
     return VCF_OK;
 }

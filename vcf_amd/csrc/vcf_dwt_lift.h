@@ -847,17 +847,20 @@ __device__ __forceinline__ void inv_row1(double &a, double &d)
     d = e;
 }
 
-template <bool FROM_PACKED2>
+// TO_RGB = false: the same pair of levels l + 1, l down to level l - 1's
+// float64 LL plane (2 h1 x 2 w1; C3's levels 4 + 3), 16-byte stores
+template <bool FROM_PACKED2, bool TO_RGB = true>
 __global__ __launch_bounds__(kNT) void lift_inv21_kernel(const uint8_t *__restrict__ packed, long long packed_stride,
                                                          long long ll_off, long long off2_lh, long long off2_hl,
                                                          long long off2_hh, long long off1_lh, long long off1_hl,
                                                          long long off1_hh, const double *__restrict__ in,
-                                                         long long plane_stride, uint8_t *__restrict__ rgb_out,
-                                                         long long rgb_stride, int h2, int w2, int h1, int w1, int Q,
-                                                         int n_strips, int n_bands, int brows)
+                                                         long long plane_stride, double *__restrict__ out,
+                                                         uint8_t *__restrict__ rgb_out, long long rgb_stride, int h2,
+                                                         int w2, int h1, int w1, int Q, int n_strips, int n_bands,
+                                                         int brows)
 {
-    __shared__ double xch[3 * kOut * 64];
-    __shared__ uint32_t rgb_lds[kRgbDw12 + 1];
+    __shared__ double xch[TO_RGB ? 3 * kOut * 64 : 1];
+    __shared__ uint32_t rgb_lds[TO_RGB ? kRgbDw12 + 1 : 1];
     const int t = threadIdx.x, lane = t & 63, ch = __builtin_amdgcn_readfirstlane(t >> 6);
     int b = blockIdx.x;
     const int strip = b % n_strips;
@@ -873,8 +876,9 @@ __global__ __launch_bounds__(kNT) void lift_inv21_kernel(const uint8_t *__restri
     const int ow = 2 * w1;                                     // RGB width
     const uint8_t *pk = packed + frame * packed_stride;
     const double *src = FROM_PACKED2 ? nullptr : in + plane * plane_stride;
-    const __amdgpu_buffer_rsrc_t rs_out =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(rgb_out + frame * rgb_stride), 0, (int)rgb_stride, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+        TO_RGB ? (void *)(rgb_out + frame * rgb_stride) : (void *)(out + plane * plane_stride), 0,
+        TO_RGB ? (int)rgb_stride : (int)((long long)ow * (2 * h1) * 8), 0x00020000);
     const int row_b = 3 * (ow - 2 * strip * kV1);              // the strip's bytes in an RGB row
 
     // prefetch: level-2 row q2f (LL2 and its three detail bytes), and the level-1
@@ -963,6 +967,18 @@ __global__ __launch_bounds__(kNT) void lift_inv21_kernel(const uint8_t *__restri
             e1pp[k] = e1;
             s2pp[k] = s2;
         }
+        if constexpr (!TO_RGB) {   // two 16-byte stores per output row (a pair's columns: in or out together)
+            const int r0 = 2 * (q - 2);
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const double *v = rr ? o1 : o0;
+                    const uint32_t ok = emit && own ? 0u : kDrop;
+                    const uint32_t o = 8 * (uint32_t)((r0 + rr) * ow + 2 * jl + 2 * k);
+                    __builtin_amdgcn_raw_buffer_store_b128(pack2(v[2 * k], v[2 * k + 1]), rs_out, o | ok, 0, 0);
+                }
+        } else {
         double *xo = xch + ch * kOut * 64;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -989,6 +1005,7 @@ __global__ __launch_bounds__(kNT) void lift_inv21_kernel(const uint8_t *__restri
             const uint32_t o = 3 * (uint32_t)((r0 + row) * ow + 2 * strip * kV1) + 4 * d;
             const uint32_t ok = emit && i < kRgbDw12 && 4 * d < row_b ? 0u : kDrop;
             __builtin_amdgcn_raw_buffer_store_b32(rgb_lds[ic], rs_out, o | ok, 0, 0);
+        }
         }
     };
 
