@@ -31,12 +31,15 @@
 // and coefficient pairs 2..125 of the wave come out exact (4 steps reach +-2
 // pairs).  The vertical lifting streams down the band one row pair per step
 // with the pipeline state in registers (5 doubles per column forward, 4
-// inverse); a band of B output row pairs reads B + 4.  Every level is one
-// launch; LL planes are float64 in the caller's workspace (the product path's
-// workspace layout is big enough), details and the last LL go straight into
-// the packed layout.  Level 1 of the encode stages its RGB rows through LDS
-// (two dwords per thread), every level its detail bytes (dword stores), and
-// level 1 of the decode meets the three channels in LDS to form RGB.
+// inverse); a band of B output row pairs reads B + 4.  Pairs of levels run
+// as one launch where the planes halve evenly (lift_fwd12_kernel /
+// lift_inv21_kernel below: C3's levels 1 + 2 and 3 + 4), single levels on
+// lift_fwd_kernel / lift_inv_kernel; LL planes between launches are float64
+// in the caller's workspace (the product path's workspace layout is big
+// enough), details and the last LL go straight into the packed layout.
+// Level 1 of the encode stages its RGB rows through LDS (two dwords per
+// thread), detail bytes leave through LDS as dwords, and level 1 of the
+// decode meets the three channels in LDS to form RGB.
 #pragma once
 
 namespace lift {
