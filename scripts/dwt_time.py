@@ -44,4 +44,7 @@ for name, fn in (("encode", enc), ("decode", dec)):
 enc()
 s.synchronize()
 out["packed_crc"] = int(np.frombuffer(dpk.download(np.empty(F * pb, np.uint8)), np.uint64).sum() % (1 << 61))
+dec()
+s.synchronize()
+out["rgb_crc"] = int(np.frombuffer(dout.download(np.empty(F * H * W * 3, np.uint8)), np.uint64).sum() % (1 << 61))
 print(json.dumps(out))
