@@ -39,18 +39,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 ALG_BYTES_PER_PIXEL = 6  # 3 B RGB read + 3 B index write
 
-
-def synth_frame(H: int, W: int, seed: int) -> np.ndarray:
-    """S-smooth of SURVEY.md §8(d): natural-like synthetic RGB (seeded)."""
-    rng = np.random.Generator(np.random.PCG64(seed))
-    y = np.arange(H, dtype=np.float32)[:, None]
-    x = np.arange(W, dtype=np.float32)[None, :]
-    chans = []
-    for c in range(3):
-        v = 128 + 60 * np.sin(x / 97 + c + seed) + 50 * np.cos(y / 61 - c - seed)
-        v = v + rng.normal(0, 4, (H, W)).astype(np.float32)
-        chans.append(v)
-    return np.clip(np.rint(np.stack(chans, -1)), 0, 255).astype(np.uint8)
+# the configs' synthetic frames (shared with the tests and scripts)
+from vcf_amd.synthetic import c4_frame, c5_frame, synth_frame  # noqa: E402,F401
 
 
 def spawn_ranks(ngpus: int) -> int:
@@ -213,13 +203,6 @@ def cpu_baseline(frame: np.ndarray, Q: int, budget_s: float):
     return out, k_c
 
 
-def c4_frame(bases, i: int) -> np.ndarray:
-    """Frame i of the C4 sequence: one of four S-smooth 1080p frames, shifted
-    by a frame-dependent constant (u8 wrap), so every frame's code-stream
-    differs and any rank can regenerate any frame cheaply."""
-    return bases[i % len(bases)] + np.uint8((i // len(bases)) * 7 % 256)
-
-
 C4_STAGES = ("dct_dz", "entropy", "pack", "sizes_allgather", "gatherv", "d2h_rank0")
 
 
@@ -358,13 +341,6 @@ def c4_verify(got, bases, job, N, H, W, Q, world, entropy="TCBAACP") -> str:
                 return f"decode MISMATCH at frame {i}"
     what = "every frame" if world > 1 else f"frames {list(frames)}"
     return f"ok: {what} equal to the frame coded alone; frames 0 and {N - 1} decode to their indices"
-
-
-def c5_frame(base, i: int, H: int, W: int) -> np.ndarray:
-    """Frame i of the C5 sequence: a window of a larger S-smooth picture panning
-    by (2i mod 41, 3i mod 53) pixels, so the motion search finds real vectors."""
-    dy, dx = (2 * i) % 41, (3 * i) % 53
-    return np.ascontiguousarray(base[dy:dy + H, dx:dx + W])
 
 
 def c5_block(args, world: int, rank: int, group):

@@ -207,6 +207,10 @@ int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, 
                            int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, void *stream);
 int vcf_dwt_dz_decode_lift(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                            int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, void *stream);
+/* A/B switch of the lifting calls, process-wide: fused = 1 (default) runs
+ * levels in pairs (1 + 2, 3 + 4 and their inverses) in one launch, 0 one
+ * launch per level.  Both give identical bytes (tests/test_dwt_lift_gpu.py). */
+int vcf_dwt_lift_set_fused(int32_t fused);
 
 
 
@@ -435,13 +439,17 @@ int64_t vcf_png_encode_bound(int32_t H, int32_t W);
  * strip_bytes <= 65536 (tifffile's strips for rows up to 64 KB);
  * slot_bytes a multiple of 4 >= vcf_zlib_bound(strip_bytes); ws_dev holds
  * vcf_zlib_workspace(total strips) bytes (16-byte aligned; out_dev and
- * sizes_dev 4-byte aligned) -- ~1.15 MB per strip, at most an eighth of the
- * device's memory (3.9 to 40 GB) whatever the batch: past that the strips are
- * coded in rounds that reuse it.  The call is asynchronous on `stream`;
+ * sizes_dev 4-byte aligned) -- ~1.15 MB per strip, at most the workspace
+ * budget whatever the batch: past that the strips are coded in rounds that
+ * reuse it.  The budget is fixed per device on first use: a quarter of the
+ * memory free then, clamped to 3.9..40 GB; vcf_zlib_set_workspace_budget(b)
+ * sets it for the current device (0 restores the default; b at least one
+ * strip's workspace), after which vcf_zlib_workspace must be asked again.  The call is asynchronous on `stream`;
  * internally part of each round runs on library streams forked from and
  * joined back to it, so the caller sees ordinary stream semantics. */
 int64_t vcf_zlib_bound(int64_t strip_bytes);
 int64_t vcf_zlib_workspace(int64_t n_strips);
+int vcf_zlib_set_workspace_budget(int64_t bytes);
 /* the largest strip_bytes vcf_zlib_strips takes (65536: frames with rows of
  * more than 64 KB -- 1-row strips past 21845 RGB pixels -- stay on the host writer) */
 int32_t vcf_zlib_max_strip(void);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # C3 per-kernel time: rocprofv3 kernel stats of 200 encodes and of 200 decodes
-# (8 x 4K, l=5 bior4.4, Q=32) through scripts/dwt_once.py.  Usage: scripts/gpu_c3_prof.sh TAG [VARIANT]
+# (8 x 4K, l=5 bior4.4, Q=32) through scripts/dwt_once.py.  Usage: scripts/debug/gpu/gpu_c3_prof.sh TAG [VARIANT]
 # (LIFT=1 in the environment: the lifting entry points)
 set -u
 cd "$GRAFT_REPO_ROOT"; ROOT=$(pwd); mkdir -p gpurun_out; export TMPDIR=/tmp; cd /tmp

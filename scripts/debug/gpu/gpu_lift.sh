@@ -5,4 +5,4 @@ cd "$GRAFT_REPO_ROOT"
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_dwt_lift_gpu.py \
     > gpurun_out/lift_tests.log 2>&1
 rc=$?; tail -5 gpurun_out/lift_tests.log; [ $rc -eq 0 ] || exit $rc
-LIFT=1 bash scripts/gpu_c3_prof.sh lift
+LIFT=1 bash scripts/debug/gpu/gpu_c3_prof.sh lift

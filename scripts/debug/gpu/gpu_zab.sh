@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU deflate check: the deflate tests, scripts/bench_zlib.py on C4 content (BUDGETS:
 # workspace budgets to A/B, default the device-sized one), and a rocprofv3 kernel trace.
-# Usage: scripts/gpu_zab.sh TAG
+# Usage: scripts/debug/gpu/gpu_zab.sh TAG
 set -u
 cd "${GRAFT_REPO_ROOT}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${1:-z}

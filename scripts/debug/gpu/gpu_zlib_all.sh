@@ -2,7 +2,7 @@
 # GPU deflate: parity tests, the throughput comparison, and rocprofv3 kernel
 # stats of the C4 workload (256 x 1080p shifted frames), each step bounded.
 set -u -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
 TAG=${TAG:-z}
 timeout -k 10 400 python -u -m pytest tests/test_deflate_gpu.py ${EXTRA_TESTS:-} -m gpu -x -v --timeout 180 --timeout-method thread > "$OUT/pytest_$TAG.log" 2>&1

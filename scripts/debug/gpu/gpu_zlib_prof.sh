@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel stats of the GPU deflate bench (per-kernel times of K1/K2/K3)
 set -u -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/zprof" -o run \

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of GPU deflate library variants (scripts/build_variant.sh) on C4 content, ABBA-ish order.
-# Usage: scripts/gpu_zwin.sh TAG VARIANT...   (VARIANT "0" = the product library)
+# Usage: scripts/debug/gpu/gpu_zwin.sh TAG VARIANT...   (VARIANT "0" = the product library)
 set -u
 cd "${GRAFT_REPO_ROOT}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=$1; shift

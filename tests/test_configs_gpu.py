@@ -60,7 +60,7 @@ def test_c1_512_codec_matches_reference_hashes(tmp_path, manifest, name):
 
 
 def _smooth(H, W, seed):
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     return synth_frame(H, W, seed)
 
 

@@ -76,7 +76,7 @@ def test_levels(level):
 
 def test_1080p_dct_frame_equals_host_tiff():
     """A 1080p frame of DCT indices (the C2 path): the GPU TIFF equals the host writer's bytes."""
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     from vcf_amd.codec.tiff import imwrite_bytes
     from vcf_amd.device import DeviceBuffer
     from vcf_amd.zlib_gpu import tiff_frames_device
@@ -189,7 +189,7 @@ def test_c4_workload_every_strip_equals_zlib():
     round's strip in the same slot) shows up here."""
     from concurrent.futures import ThreadPoolExecutor
 
-    import bench
+    from vcf_amd import synthetic as bench
     from vcf_amd import dct
     from vcf_amd.codec.tiff import strip_layout
     from vcf_amd.device import DeviceBuffer
@@ -213,7 +213,7 @@ _MULTI_ROUND = r'''
 import sys, zlib
 import numpy as np
 sys.path.insert(0, sys.argv[1])
-import bench
+from vcf_amd import synthetic as bench
 from vcf_amd import dct
 from vcf_amd import _lib as L
 from vcf_amd.codec.tiff import strip_layout

@@ -6,7 +6,7 @@ rounding boundary) at most 1e-4 of them off at all at Q = 32."""
 import numpy as np
 import pytest
 
-import bench
+from vcf_amd import synthetic as bench
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -117,6 +117,16 @@ def test_lift_rejects_other_wavelets():
         DW.encode(np.zeros((32, 32, 3), np.uint8), "db5", 2, 32, lifting=True)
 
 
+def _unfused(fn):
+    """fn() with the lifting path's level pairs unfused (one launch per level)."""
+    from vcf_amd import _lib as Lb
+    Lb.call("vcf_dwt_lift_set_fused", 0)
+    try:
+        return fn()
+    finally:
+        Lb.call("vcf_dwt_lift_set_fused", 1)
+
+
 @pytest.mark.parametrize("H,W,L,Q", [(96, 240, 2, 32), (64, 480, 5, 32), (32, 176, 3, 7), (200, 496, 2, 300),
                                      (256, 512, 4, 32), (256, 512, 5, 7), (2160, 3840, 5, 32)])
 def test_lift_fused_levels12_equal_unfused(monkeypatch, H, W, L, Q):
@@ -130,8 +140,7 @@ def test_lift_fused_levels12_equal_unfused(monkeypatch, H, W, L, Q):
     frames = (np.stack([bench.synth_frame(H, W, 5), rng.integers(0, 256, (H, W, 3), dtype=np.uint8)])
               if H * W < 4e6 else bench.synth_frame(H, W, 5)[None])
     fused = DW.encode(frames, "bior4.4", L, Q, lifting=True)
-    monkeypatch.setenv("VCF_LIFT_NOFUSE", "1")
-    split = DW.encode(frames, "bior4.4", L, Q, lifting=True)
+    split = _unfused(lambda: DW.encode(frames, "bior4.4", L, Q, lifting=True))
     for f in range(len(frames)):
         for name in fused[f]:
             assert np.array_equal(fused[f][name], split[f][name]), (f, name)
@@ -152,8 +161,7 @@ def test_lift_fused_levels21_decode_equal_unfused(monkeypatch, H, W, L, Q):
               if H * W < 4e6 else bench.synth_frame(H, W, 6)[None])
     sb = DW.encode(frames, "bior4.4", L, Q)
     fused = DW.decode(sb, H, W, "bior4.4", L, Q, lifting=True)
-    monkeypatch.setenv("VCF_LIFT_NOFUSE", "1")
-    split = DW.decode(sb, H, W, "bior4.4", L, Q, lifting=True)
+    split = _unfused(lambda: DW.decode(sb, H, W, "bior4.4", L, Q, lifting=True))
     assert np.array_equal(fused, split)
     if H * W < 4e6:
         want = O.dwt_decode_frame(sb[0], H, W, "bior4.4", L, Q)

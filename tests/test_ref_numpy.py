@@ -46,7 +46,7 @@ def test_ref_numpy_c1_by_hash(manifest, name):
 
 
 def test_ref_numpy_matches_c_port_on_a_4k_strip():
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     from oracle import oracle as O
     f = synth_frame(2160, 3840, 0)
     k = R.encode_frame(f, 32, workers=4)

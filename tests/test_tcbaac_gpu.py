@@ -87,7 +87,7 @@ def test_codec_container_and_errors():
 def test_dct_codec_with_tcbaac_frame(tmp_path):
     from PIL import Image
 
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     from oracle import oracle as O
     from vcf_amd.codec import parser as P
     from vcf_amd.codec.dct2d import CoDec
@@ -130,7 +130,7 @@ def test_prior_segments_equal_host_coder_and_round_trip(order, seg_len):
 def test_prior_codec_on_dct_indices():
     """A 1080p frame's indices through the version-2 codec: round trip, and
     short segments cost less rate than with fresh models."""
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     from oracle import oracle as O
     k = O.encode_frame(synth_frame(1080, 1920, 3), 32, 0)
     c = T.TiledCBAACCodec(order=0, seg_len=8192, prior=True)
@@ -148,7 +148,7 @@ def test_dct_codec_with_tcbaacp_frame(tmp_path):
     coder's, decoding gives the oracle frame."""
     from PIL import Image
 
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     from oracle import oracle as O
     from vcf_amd.codec import parser as P
     from vcf_amd.codec.dct2d import CoDec
@@ -294,7 +294,7 @@ def test_lane_kernels_on_dct_indices_many_segments():
     """A 1080p frame's indices in 256-symbol segments (24 300 segments: the
     automatic choice codes one per lane, 380 waves): every segment equals the
     host coder seeded with the frame's prior."""
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     from oracle import oracle as O
     k = O.encode_frame(synth_frame(1080, 1920, 5), 32, 0).ravel()
     c = T.TiledCoder(0, 256, prior=True)
@@ -343,7 +343,7 @@ def test_batch_decode_frames(variant):
 # ---- version 3: prior classes ---------------------------------------------------------
 
 def _dct_indices(H=1080, W=1920, seed=5):
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     from oracle import oracle as O
     return O.encode_frame(synth_frame(H, W, seed), 32, 0).ravel()
 

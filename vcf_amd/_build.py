@@ -25,7 +25,8 @@ SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_dct_any.hip", "vcf_quant.hi
            "vcf_png.cpp", "vcf_comm.cpp", "vcf_cbaac_gpu.hip", "vcf_plugins.hip", "vcf_deflate.hip",
            "vcf_inflate.hip"]
 HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h", "vcf_wavelets.h", "vcf_pocketfft.h", "vcf_pocketfft_tables.h",
-           "vcf_pocketfft_rt.h", "vcf_pocketfft_blue.h", "vcf_sincos.h", "vcf_pipeline.h", "vcf_dwt_band.h", "vcf_idwt_line.h", "vcf_deflate.h"]
+           "vcf_pocketfft_rt.h", "vcf_pocketfft_blue.h", "vcf_sincos.h", "vcf_pipeline.h", "vcf_dwt_band.h", "vcf_idwt_line.h", "vcf_dwt_lift.h",
+           "vcf_deflate.h"]
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("VCF_OFFLOAD_ARCH", "gfx950")
 
@@ -37,13 +38,44 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm is required to build libvcf_amd.so)")
 
 
+def deps_mtime(src: str) -> float:
+    """Newest mtime of a source and the local headers it includes (transitively)."""
+    seen, todo, newest = set(), [os.path.join(CSRC, src)], 0.0
+    while todo:
+        f = todo.pop()
+        if f in seen or not os.path.exists(f):
+            continue
+        seen.add(f)
+        newest = max(newest, os.path.getmtime(f))
+        for name in local_includes(f):
+            for d in (CSRC, os.path.join(ROOT, "include")):
+                if os.path.exists(os.path.join(d, name)):
+                    todo.append(os.path.join(d, name))
+                    break
+    return newest
+
+
+def local_includes(path: str) -> list:
+    """The `#include "..."` names of one file."""
+    out = []
+    for line in open(path, errors="replace"):
+        line = line.strip()
+        if line.startswith("#include \""):
+            out.append(line.split('"')[1])
+    return out
+
+
 def needs_rebuild() -> bool:
+    """True when either library is missing or older than any source or any
+    header a source includes, directly or transitively (the same scan
+    build() uses per object)."""
     if not os.path.exists(LIB) or not os.path.exists(AB_LIB):
         return True
     t = min(os.path.getmtime(LIB), os.path.getmtime(AB_LIB))
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS + AB_SOURCES]
+    deps = [os.path.join(CSRC, s) for s in HEADERS]
     deps += [os.path.join(ROOT, "include", h) for h in ("vcf_amd.h", "vcf_amd_ab.h")]
-    return any(os.path.getmtime(d) > t for d in deps)
+    newest = max([deps_mtime(s) for s in SOURCES + AB_SOURCES] + [os.path.getmtime(d) for d in deps if os.path.exists(d)])
+    return newest > t
 
 
 def _flags():
@@ -60,25 +92,6 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     from concurrent.futures import ThreadPoolExecutor
     os.makedirs(OBJDIR, exist_ok=True)
-
-    def deps_mtime(src):
-        """Newest mtime of a source and the local headers it includes (transitively)."""
-        seen, todo, newest = set(), [os.path.join(CSRC, src)], 0.0
-        while todo:
-            f = todo.pop()
-            if f in seen or not os.path.exists(f):
-                continue
-            seen.add(f)
-            newest = max(newest, os.path.getmtime(f))
-            for line in open(f, errors="replace"):
-                line = line.strip()
-                if line.startswith("#include \""):
-                    name = line.split('"')[1]
-                    for d in (CSRC, os.path.join(ROOT, "include")):
-                        if os.path.exists(os.path.join(d, name)):
-                            todo.append(os.path.join(d, name))
-                            break
-        return newest
 
     def compile_one(src):
         obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")

@@ -51,6 +51,10 @@ class CoDec(EICCoDec):
         # opt-in (no reference counterpart): the lifting form of bior4.4, within
         # +-1 of the bit-exact path (the lifting form); args.dwt_lifting or VCF_DWT_LIFTING=1
         self.lifting = bool(getattr(args, "dwt_lifting", False)) or os.environ.get("VCF_DWT_LIFTING") == "1"
+        if self.lifting:
+            logging.warning("2D-DWT: the opt-in lifting path is selected (%s): indices and decoded bytes are "
+                            "within +-1 of the reference, not bit-exact",
+                            "args.dwt_lifting" if getattr(args, "dwt_lifting", False) else "VCF_DWT_LIFTING=1")
         if self.lifting and self.wavelet != "bior4.4":
             raise NotImplementedError("the lifting path is bior4.4 (CDF 9/7) only")
         logging.info(f"levels = {self.levels}")

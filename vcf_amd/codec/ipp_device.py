@@ -88,7 +88,7 @@ class DeviceIPP:
         self.gray = DeviceBuffer(2 * self.H * self.W)
         self.out = DeviceBuffer(max(1, self.n_local * self.spf * self.slot))
         self.sizes = DeviceBuffer(max(4, self.n_local * self.spf * 4))
-        self.ws = DeviceBuffer(max(16, Z.workspace(max(1, self.n_local) * self.spf)))
+        self.ws = Z.workspace_buffer(max(1, self.n_local) * self.spf)
         self.exchange = Exchange(comm, self.rank, self.world, self.N, ranges, self.stream)
 
     def _frames_of_step(self, p: int):

@@ -37,8 +37,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
 
 #include "vcf_amd.h"
 #include "vcf_deflate.h"
@@ -70,28 +72,43 @@ constexpr int64_t kWsPerStrip = kSumOff + 32;
 // Rounds: the strips of a call are processed in rounds whose workspace stays
 // under the budget, one round after the other on the caller's stream.  Every
 // round ends in a tail (the last strips' serial parses on a draining GPU), so
-// fewer, larger rounds are faster: the budget is an eighth of the device's HBM
-// (36 GB on MI355X: C4's 25 344 strips in one round, 317 -> 245 ms against
-// round 4's fixed 3.9 GB), at least 3.9 GB and at most 40 GB.  It depends only
-// on the device, so vcf_zlib_workspace and vcf_zlib_strips agree.  (Rounds in
-// flight on library streams, each with its own workspace slot, measured
+// fewer, larger rounds are faster: the budget is a quarter of the device memory
+// that is free when the library first sizes it (MI355X with the bench's buffers
+// resident: 40 GB, C4's 25 344 strips in one round, 317 -> 245 ms against round
+// 4's fixed 3.9 GB), at least 3.9 GB and at most 40 GB.  It is fixed per device
+// on first use, so vcf_zlib_workspace and vcf_zlib_strips agree; a caller that
+// cannot hold it sets a smaller one with vcf_zlib_set_workspace_budget (the
+// strips then run in more rounds) and asks vcf_zlib_workspace again.  (Rounds
+// in flight on library streams, each with its own workspace slot, measured
 // slower -- 517 vs 453 ms for C4 -- and produced a wrong strip now and then on
 // MI355X)
 constexpr int64_t kWsBudget = 3900000000LL, kWsBudgetMax = 40000000000LL;
-// the budget in effect (VCF_ZX_BUDGET bytes overrides it: A/B of the round size)
+constexpr int kMaxDevices = 64;
+std::atomic<int64_t> g_ws_override[kMaxDevices];   // > 0: the caller's budget (vcf_zlib_set_workspace_budget)
+inline int current_device()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
+    return dev;
+}
+// the budget in effect on the current device (VCF_ZX_BUDGET bytes overrides the
+// default: A/B of the round size); thread-safe, computed once per device
 inline int64_t ws_budget()
 {
-    static int64_t b = 0;
-    if (!b) {
+    const int dev = current_device();
+    const int64_t o = g_ws_override[dev].load(std::memory_order_relaxed);
+    if (o > 0) return o;
+    static std::once_flag once[kMaxDevices];
+    static int64_t dflt[kMaxDevices];
+    std::call_once(once[dev], [dev] {
         int64_t v = kWsBudget;
-        int dev = 0;
-        size_t total = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceTotalMem(&total, dev) == hipSuccess)
-            v = std::min(kWsBudgetMax, std::max(kWsBudget, (int64_t)(total / 8)));
+        size_t free_b = 0, total = 0;
+        if (hipMemGetInfo(&free_b, &total) == hipSuccess)
+            v = std::min(kWsBudgetMax, std::max(kWsBudget, (int64_t)(free_b / 4)));
         const char *e = getenv("VCF_ZX_BUDGET");
-        b = e && atoll(e) > 0 ? atoll(e) : v;
-    }
-    return b;
+        dflt[dev] = e && atoll(e) > 0 ? atoll(e) : v;
+    });
+    return dflt[dev];
 }
 // A call's strips in rounds of `per` strips (at most 65535: the y grid dimension of
 // the head and K2a launches), the workspace of one round within the budget.
@@ -256,7 +273,7 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c)   
 #ifndef VCF_ZX_K1WAVES   // A/B (diagnostic builds): K1's waves per strip
 #define VCF_ZX_K1WAVES 8
 #endif
-constexpr int kK1Waves = VCF_ZX_K1WAVES, kK1Stage = 2048;
+constexpr int kK1Waves = VCF_ZX_K1WAVES, kK1Stage = 4 * 64 * kK1Waves;   // one dword of a chunk per thread
 struct OrderSmem4 {
     uint32_t cnt[1 << 14];              // 32768 u16 counters / cursors, packed in pairs
     uint8_t stage[kK1Stage + 64];
@@ -1044,7 +1061,9 @@ struct Wave {
     {
         for (uint32_t P = from + lane_id(); P < to; P += 64) lwin[P - wbase] = (uint8_t)win_src(P);
     }
-    // keep [p - MAX_DIST, p + kLazyAhead) in the window: shift it forward when p runs ahead
+    // keep [p - kNearDist, p + kLazyAhead) in the window: shift it forward when p runs
+    // ahead (chain candidates farther back than the window read the strip in HBM:
+    // Wave::g4 / far_lcp / wave_lcp_at)
     __device__ __forceinline__ void ensure(uint32_t p)
     {
         if (p + kLazyAhead <= wbase + kLazyWin) return;
@@ -1233,7 +1252,10 @@ struct Wave {
             // the first candidate (chain order) reaching max(nice, prev_len+1), else the
             // first reaching the longest length found, if longer than prev_len
             ensure(p);
-            const uint32_t wp = p - wbase;   // window offsets from here on (every candidate is >= wbase)
+            // window offsets from here on: p's own bytes are in the window; a candidate below
+            // wbase (at most MAX_DIST back, always c + 274 < p, so real strip bytes) is
+            // read from HBM instead (the `far` lanes)
+            const uint32_t wp = p - wbase;
 #if VCF_ZX_WINCHECK
             cur_p = p;
             for (uint32_t P0 = (p > 128u + wbase ? p - 128u : wbase); P0 < p + 256u; P0 += 64) {
@@ -1639,6 +1661,16 @@ int vcf_zlib_prof_read(unsigned long long *host16, int reset)
 }
 #endif
 
+int vcf_zlib_set_workspace_budget(int64_t bytes)
+{
+    if (bytes < 0) return set_error(VCF_ERR_INVALID, "negative workspace budget");
+    if (bytes > 0 && bytes < kWsPerStrip)
+        return set_error(VCF_ERR_INVALID, "workspace budget %lld below one strip's %lld bytes", (long long)bytes,
+                         (long long)kWsPerStrip);
+    g_ws_override[current_device()].store(bytes, std::memory_order_relaxed);
+    return VCF_OK;
+}
+
 int64_t vcf_zlib_workspace(int64_t n_strips)
 {
     if (n_strips < 0) return -1;
@@ -1691,9 +1723,8 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     // the side stream at the highest priority: its strips are fewer but each takes
     // longer (K2b walks every listed position's chain), and as a normal-priority queue
     // its workgroups only got a CU when a lazy parse left one
-    static hipStream_t side_hi[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    static hipStream_t side_hi[kMaxDevices] = {};
+    const int dev = current_device();
     if (!VCF_ZX_NOPRIO && !side_hi[dev]) {
         int least = 0, greatest = 0;
         rc = hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");

@@ -26,6 +26,8 @@
 // rows then columns per level and a final YCoCg->RGB kernel.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
@@ -1699,6 +1701,11 @@ int lift_check(int wavelet)
 }
 
 #endif  // VCF_DWT_KERNELS_ONLY
+// A/B knob of the opt-in lifting path (tests/test_dwt_lift_gpu.py compares the two
+// forms): vcf_dwt_lift_set_fused(0) selects one launch per level instead of the
+// fused level pairs, for the whole process.
+std::atomic<int> g_lift_fused{1};
+inline bool lift_nofuse() { return g_lift_fused.load(std::memory_order_relaxed) == 0; }
 }  // namespace
 }  // namespace vcf
 
@@ -1909,6 +1916,12 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
 
 // The lifting path (vcf_dwt_lift.h): bior4.4 only, same buffers, layout and
 // workspace as vcf_dwt_dz_encode / _decode; results within +-1 of theirs.
+int vcf_dwt_lift_set_fused(int32_t fused)
+{
+    g_lift_fused.store(fused ? 1 : 0, std::memory_order_relaxed);
+    return VCF_OK;
+}
+
 int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                            int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, void *stream)
 {
@@ -1926,7 +1939,7 @@ int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, 
     // explicit ping-pong: a launch reads `in` (level l - 1's LL) and writes the other plane
     const double *in = nullptr;
     int nb = 0;
-    const bool nofuse = getenv("VCF_LIFT_NOFUSE") != nullptr;   // one launch per level (A/B)
+    const bool nofuse = lift_nofuse();
     for (int l = 1; l <= levels;) {
         const int h = g.hs[l - 1], w = g.ws[l - 1], hh = g.hs[l], hw = g.ws[l];
         const bool first = l == 1;
@@ -2005,7 +2018,7 @@ int vcf_dwt_dz_decode_lift(const uint8_t *packed_dev, int64_t n_frames, int32_t 
     // explicit ping-pong: a launch reads `in` (the LL of the level above) and writes the other plane
     const double *in = nullptr;
     int nb = 0;
-    const bool nofuse = getenv("VCF_LIFT_NOFUSE") != nullptr;   // one launch per level (A/B)
+    const bool nofuse = lift_nofuse();
     for (int r = levels; r >= 1;) {
         const int h = g.hs[r], w = g.ws[r];
         const bool coarsest = r == levels;

@@ -34,6 +34,24 @@ def workspace(n_strips: int) -> int:
     return int(L.lib().vcf_zlib_workspace(int(n_strips)))
 
 
+def workspace_buffer(n_strips: int) -> DeviceBuffer:
+    """A device workspace for a vcf_zlib_strips call over n_strips strips.
+    When the library's default budget (a quarter of the memory free at first
+    use, up to 40 GB) cannot be allocated -- the caller holds large buffers,
+    or ranks share the device -- the budget is halved until it can: the
+    strips then run in more rounds over a smaller workspace (same bytes, more
+    time).  The new budget stays in effect for the device."""
+    need, one = workspace(n_strips), workspace(1)
+    while True:
+        try:
+            return DeviceBuffer(max(16, need))
+        except L.VCFError:
+            if need <= one:
+                raise
+            L.call("vcf_zlib_set_workspace_budget", max(one, need // 2))
+            need = workspace(n_strips)
+
+
 def max_strip() -> int:
     """The largest strip the GPU deflate takes (vcf_zlib_max_strip: 65536 bytes)."""
     return int(L.lib().vcf_zlib_max_strip())
@@ -65,6 +83,16 @@ class StripDeflater:
             b = self._bufs[name] = DeviceBuffer(max(int(nbytes), 16))
         return b
 
+    def _workspace(self) -> DeviceBuffer:
+        ws = self._bufs.get("ws")
+        if ws is not None and ws.nbytes >= workspace(self.total):
+            return ws
+        if ws is not None:
+            ws.free()
+            del self._bufs["ws"]
+        ws = self._bufs["ws"] = workspace_buffer(self.total)
+        return ws
+
     def launch(self, src: DeviceBuffer, n_frames: int, frame_bytes: int, strip_bytes: int, level: int = LEVEL,
                offset: int = 0, stream: Stream | None = None) -> None:
         """Queue the deflate of every strip on `stream` (default: the
@@ -84,7 +112,7 @@ class StripDeflater:
             return
         self.out = self._buf("out", self.total * self.slot)
         self._sizes = self._buf("sizes", self.total * 4)
-        ws = self._buf("ws", int(L.lib().vcf_zlib_workspace(self.total)))
+        ws = self._workspace()
         L.call("vcf_zlib_strips", src.address(offset), int(n_frames), int(frame_bytes), int(strip_bytes),
                int(level), self.out.ptr, self.slot, self._sizes.ptr, ws.ptr, stream.handle)
 
