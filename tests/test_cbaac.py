@@ -66,3 +66,61 @@ def test_errors():
         C.encode_symbols(np.zeros(4, np.uint8), 9)
     with pytest.raises(ValueError):
         C.CBAACCodec().compress(np.array([300], np.int32))
+
+
+class _RefModel:
+    """CBAAC.py:17-47's AdaptiveModel restated (its traces are pinned above):
+    256 ones, +1 per update, halve (f >> 1) + 1 when the stale total >= 16384."""
+
+    def __init__(self):
+        self.freq = [1] * 256
+        self.total = 256
+
+    def _cum(self, s):
+        return sum(self.freq[:s])
+
+    def get_range(self, s):
+        lo = self._cum(s)
+        return lo, lo + self.freq[s], self.total
+
+    def get_symbol_from_scaled_value(self, v):
+        acc = 0
+        for s, f in enumerate(self.freq):
+            if acc + f > v:
+                return s, acc, acc + f
+            acc += f
+
+    def update(self, s):
+        stale = self.total
+        self.freq[s] += 1
+        if stale >= 16384:
+            self.freq = [(f >> 1) + 1 for f in self.freq]
+        self.total = sum(self.freq)
+
+
+def _a8_encode(sym):
+    import sys
+    sys.path.insert(0, os.path.join(GOLDEN, "shims"))
+    from arithmetic_coding.arithmetic_coding import Arithmetic_Encoding
+    m, enc, bits = _RefModel(), Arithmetic_Encoding(), []
+    for s in sym.tolist():
+        enc.encode_symbol(s, m, bits)
+        m.update(s)
+    enc.flush(bits)
+    bits += [0] * (-len(bits) % 8)
+    return np.packbits(np.array(bits, np.uint8)).tobytes()
+
+
+@pytest.mark.parametrize("kind", ["skewed", "uniform", "two_level", "rescales"])
+def test_native_bytes_equal_a8_stand_in(kind):
+    """The native coder (bulk renormalisation, reciprocal division, held-back
+    MPS counts) writes exactly the bytes of A8 as the stand-in states it
+    symbol by symbol: pending-bit runs, E1/E2 prefixes and rescales included."""
+    rng = np.random.Generator(np.random.PCG64(21))
+    sym = {"skewed": np.where(rng.random(6000) < 0.02, rng.integers(0, 256, 6000), 128),
+           "uniform": rng.integers(0, 256, 3000),
+           "two_level": np.where(rng.random(6000) < 0.5, 127, 128),
+           "rescales": np.clip(np.rint(rng.laplace(128, 3, 40000)), 0, 255)}[kind].astype(np.uint8)
+    got = C.encode_symbols(sym, 0)
+    assert got == _a8_encode(sym)
+    assert np.array_equal(C.decode_symbols(got, sym.size, 0), sym)

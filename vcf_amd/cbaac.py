@@ -56,9 +56,11 @@ class CBAACCodec:
         # flatten().astype(int32) -> symbols; the model has 256 symbols, so
         # the values must be bytes (the reference's callers pass uint8)
         flat = img.ravel()
-        if flat.size and (flat.min() < 0 or flat.max() > 255):
-            raise ValueError("CBAAC codes byte symbols (0..255)")
-        b.write(encode_symbols(flat.astype(np.uint8), self.ORDER))
+        if flat.dtype != np.uint8:   # (uint8 input, the callers' case, needs no check or copy)
+            if flat.size and (flat.min() < 0 or flat.max() > 255):
+                raise ValueError("CBAAC codes byte symbols (0..255)")
+            flat = flat.astype(np.uint8)
+        b.write(encode_symbols(flat, self.ORDER))
         b.seek(0)
         return b
 
