@@ -203,6 +203,112 @@ def cpu_baseline(frame: np.ndarray, Q: int, budget_s: float):
     return out, k_c
 
 
+def _run_serial(fn, *a):
+    """fn(*a) on a worker thread: the host TIFF writer deflates a frame's strips
+    serially there (on the main thread it fans them out over a pool), so a
+    1-core leg really uses one core."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(1) as ex:
+        return ex.submit(fn, *a).result()
+
+
+def c4_cpu_baseline(budget_s: float, Q: int, files=None) -> dict:
+    """C4's reference path on host cores (checker leg, rank 0, N = 1): per frame
+    of the C4 sequence the oracle's C DCT + deadzone (oracle/vcf_oracle.c,
+    2D-DCT.py:276-361 restated) and the host TIFF writer (system zlib level 6,
+    TIFF.py:23-31), as III.py:77-115 runs 2D-DCT encode_fn per frame -- on 1
+    core, then with frames on a 16-thread pool; each leg stops after about half
+    the budget.  The first frames' files are compared with the GPU block's."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle as O
+    from vcf_amd.codec.tiff import imwrite_bytes
+    H, W = 1080, 1920
+    bases = [synth_frame(H, W, seed=100 + s) for s in range(4)]
+    code = lambda i: imwrite_bytes(O.encode_frame(c4_frame(bases, i), Q))   # noqa: E731
+    model, ncpu, avail = host_desc()
+    threads = min(16, avail, int(os.environ.get("OMP_NUM_THREADS", avail) or avail))
+
+    def one_core():
+        out, t0 = {}, time.perf_counter()
+        i = 0
+        while True:
+            out[i] = code(i)
+            i += 1
+            if time.perf_counter() - t0 >= budget_s / 2 or i >= 256:
+                return out, time.perf_counter() - t0
+    got1, el1 = _run_serial(one_core)
+    n_par = max(threads, min(256, int(round(len(got1) * threads * 0.8))))
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(code, range(n_par)))
+    elp = time.perf_counter() - t0
+    agree = None if not files else all(got1[i] == f for i, f in files.items() if i in got1)
+    return {"value": round(len(got1) * H * W / el1 / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": (f"frames 0..{len(got1) - 1} of the C4 sequence (1080p): oracle/vcf_oracle.c DCT+deadzone "
+                       f"then the host TIFF writer (system zlib level 6), one frame after the other on 1 core, "
+                       f"{el1:.1f} s"),
+            "threads": {"value": round(n_par * H * W / elp / 1e6, 2), "unit": "Mpixels/s", "cores": threads,
+                        "sample": f"{n_par} frames of the sequence on a {threads}-thread pool, {elp:.1f} s"},
+            "host": f"{model}; usable cores {avail}",
+            "files_equal_gpu": agree}
+
+
+def c5_cpu_baseline(budget_s: float, Q: int, base, H: int, W: int, G: int, files=None) -> dict:
+    """C5's reference path on host cores (checker leg, rank 0, N = 1): the IPP
+    GOP loop (IPP_DCT.py:397-575) restated by the C oracle -- I-frame DCT +
+    deadzone and its decode; per P-frame the full search (bs 16, S 8) against
+    the previous reconstruction, compensation, residual + 128, DCT + deadzone,
+    decode and reconstruction -- with every frame's indices written by the host
+    TIFF writer (system zlib level 6).  1 core: GOP 0 from its first frame
+    until half the budget is spent; then the first frames of every GOP on a
+    thread pool (GOPs are independent).  Files compared with the GPU block's."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle as O
+    from vcf_amd.codec.tiff import imwrite_bytes
+
+    def gop(g: int, n: int, deadline=None):
+        out, ref = {}, None
+        for j in range(n):
+            i = g * G + j
+            cur = c5_frame(base, i, H, W)
+            if ref is None:
+                k = O.encode_frame(cur, Q)
+                ref = O.decode_frame(k, H, W, Q)
+            else:
+                comp = O.ipp_motion_compensate(ref, O.ipp_block_matching(ref, cur, 16, 8, False), 16)
+                k = O.encode_frame(O.ipp_residual(cur, comp), Q)
+                ref = O.ipp_reconstruct(comp, O.decode_frame(k, H, W, Q))
+            out[i] = imwrite_bytes(k)
+            if deadline is not None and time.perf_counter() >= deadline:
+                break
+        return out
+    model, ncpu, avail = host_desc()
+    threads = min(16, avail, int(os.environ.get("OMP_NUM_THREADS", avail) or avail))
+    t0 = time.perf_counter()
+    got1 = _run_serial(gop, 0, G, t0 + budget_s / 2)
+    el1 = time.perf_counter() - t0
+    n_gops = max(1, (64 + G - 1) // G)
+    per = 2
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(min(threads, n_gops)) as ex:
+        outs = list(ex.map(lambda g: gop(g, per), range(n_gops)))
+    elp = time.perf_counter() - t0
+    n_par = sum(len(o) for o in outs)
+    agree = None if not files else all(got1[i] == f for i, f in files.items() if i in got1)
+    return {"value": round(len(got1) * H * W / el1 / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": (f"frames 0..{len(got1) - 1} of GOP 0 (4K; I then P frames): the C oracle's IPP GOP loop "
+                       f"(full search bs 16 / S 8, compensation, residual, DCT+deadzone, decode, reconstruction) "
+                       f"and the host TIFF writer (system zlib level 6), 1 core, {el1:.1f} s"),
+            "threads": {"value": round(n_par * H * W / elp / 1e6, 2), "unit": "Mpixels/s",
+                        "cores": min(threads, n_gops),
+                        "sample": (f"the first {per} frames of each of the {n_gops} GOPs, one GOP per thread "
+                                   f"(GOPs are independent; frames in a GOP are serial), {elp:.1f} s")},
+            "host": f"{model}; usable cores {avail}",
+            "files_equal_gpu": agree}
+
+
 C4_STAGES = ("dct_dz", "entropy", "pack", "sizes_allgather", "gatherv", "d2h_rank0")
 
 
@@ -281,6 +387,8 @@ def c4_block(args, world: int, rank: int, group, entropy: str = "TCBAACP"):
             info["code_bytes"] = int(sizes.sum())
             info["bits_per_symbol"] = round(8 * int(sizes.sum()) / (N * job.n_sym), 5)
             info["verified"] = c4_verify(got, bases, job, N, H, W, Q, world, entropy)
+            if entropy == "TIFF":   # for the checker leg's CPU baseline: its files against these
+                info["_files"] = {i: bytes(got[i]) for i in range(min(N, 4))}
     except Exception as e:   # reported in the block; the headline line still prints
         err = f"{type(e).__name__}: {e}"
     finally:
@@ -410,7 +518,7 @@ def c5_block(args, world: int, rank: int, group):
     return info
 
 
-def c5_check(info, Q: int) -> None:
+def c5_check(info, Q: int, budget_s: float = 0.0) -> None:
     """The checker leg (rank 0, N = 1, beside cpu_baseline): frames 0 and 1 of the
     C5 block's first GOP against the reference's GOP loop restated by the C oracle
     (IPP_DCT.py:397-575: the I-frame's indices; the P-frame's full-search motion
@@ -436,6 +544,9 @@ def c5_check(info, Q: int) -> None:
                         "loop's indices (C oracle), frame 1's motion field equal" if ok else
                         "MISMATCH: " + ", ".join(f"{k} {'ok' if v else 'differs'}" for k, v in parts.items()) +
                         f" (file sizes {len(got[0])}/{len(w0)}, {len(got[1])}/{len(w1)})")
+    if budget_s > 0:
+        info["cpu_baseline"] = c5_cpu_baseline(budget_s, Q, base, H, W, info.get("gop", 10),
+                                               {i: bytes(got[i]) for i in range(min(len(got), 4))})
 
 
 # config C3 (BASELINE.json configs[2]): 2D-DWT l=5 CDF-9/7 (pywt's bior4.4) + deadzone at 4K
@@ -731,6 +842,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0,
                     help="seconds of CPU time for cpu_baseline (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget-configs", type=float, default=8.0,
+                    help="seconds of CPU time for each of the C4 / C5 blocks' cpu_baseline (rank 0, N=1)")
     ap.add_argument("--variant", type=int, default=0, help="encode kernel (0 = automatic)")
     ap.add_argument("--c4-frames", type=int, default=256, help="frames of the C4 block (0 disables it)")
     ap.add_argument("--c4-steps", type=int, default=2)
@@ -817,13 +930,17 @@ def main():
         cpu, k_ref = cpu_baseline(distinct[0], Q, args.cpu_budget)
         k_gpu = dout.download(np.empty((Hp, Wp, 3), np.uint8))
         parity = "bit-exact vs oracle (frame 0)" if np.array_equal(k_gpu, k_ref) else "MISMATCH"
-        c5_check(c5, Q)
+        c5_check(c5, Q, args.cpu_budget_configs)
+        if c4t is not None and "_files" in c4t:
+            c4t["cpu_baseline"] = c4_cpu_baseline(args.cpu_budget_configs, Q, c4t.pop("_files"))
         c3_check(c3, distinct, Q)
         c2_check(c2, Q)
     else:
         for blk in (c5, c3):
             if blk is not None:
                 blk.pop("_check", None)
+        if c4t is not None:
+            c4t.pop("_files", None)
         for ec in ("CBAAC", "TCBAACP"):
             if c2 is not None and isinstance(c2.get(ec), dict):
                 c2[ec].pop("_check", None)

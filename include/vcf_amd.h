@@ -197,6 +197,11 @@ int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
 int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                       int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, void *stream);
 
+/* A/B switch of vcf_dwt_dz_decode, process-wide: on = 1 (default) runs the
+ * inverse levels 2 and 1 in one launch where the planes halve evenly (LL1
+ * stays on chip), 0 one launch per level.  Identical bytes either way. */
+int vcf_dwt_set_inverse_band21(int32_t on);
+
 /* Opt-in lifting form of the two calls above for bior4.4 (CDF 9/7) only
  * (VCF_ERR_INVALID for other wavelets): same arguments, buffers, layout and
  * workspace, four lifting steps per axis in place of pywt's convolution.
@@ -211,6 +216,13 @@ int vcf_dwt_dz_decode_lift(const uint8_t *packed_dev, int64_t n_frames, int32_t 
  * levels in pairs (1 + 2, 3 + 4 and their inverses) in one launch, 0 one
  * launch per level.  Both give identical bytes (tests/test_dwt_lift_gpu.py). */
 int vcf_dwt_lift_set_fused(int32_t fused);
+/* Diagnostic of the lifting form's precision (one frame, bior4.4): its float64
+ * subband coefficients before quantization.  coef_dev receives, for levels
+ * l = 1..levels, the details [LH, HL, HH][Y, Co, Cg][h_l x w_l] (the shapes of
+ * vcf_dwt_layout), then LL_levels [Y, Co, Cg][h x w]; packed_dev (packed bytes
+ * of vcf_dwt_layout) and workspace_dev are scratch. */
+int vcf_dwt_lift_analyze_f64(const uint8_t *rgb_dev, int32_t H, int32_t W, int32_t levels, double *coef_dev,
+                             uint8_t *packed_dev, void *workspace_dev, void *stream);
 
 
 

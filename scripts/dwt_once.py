@@ -7,7 +7,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 
-import bench
+from vcf_amd import synthetic as bench
 import vcf_amd._lib as L
 import vcf_amd.dwt as DW
 from vcf_amd.device import DeviceBuffer, Stream, set_device

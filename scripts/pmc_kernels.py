@@ -26,9 +26,10 @@ SIMDS = 4 * 256
 
 
 def short(name: str) -> str:
-    name = re.sub(r"\(.*$", "", name)            # drop the argument list
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"^void\s+", "", name)
-    name = re.sub(r"\b(vcf|dfl)::(\(anonymous namespace\)::)?", "", name)
+    name = re.sub(r"\b(vcf|dfl|lift)::", "", name)
+    name = re.sub(r"\(.*$", "", name)            # drop the argument list
     return name[:120]
 
 

@@ -29,4 +29,6 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_AC
   [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.log"; exit $rc; }
 done
 python3 "$ROOT/scripts/pmc_kernels.py" "$RAW" > "$OUT/summary.json"
+# the raw counter CSVs travel back too (small: one row per dispatch and counter)
+for d in "$RAW"/p* "$RAW"/trace; do mkdir -p "$OUT/raw/$(basename "$d")"; find "$d" -name "*.csv" -exec cp {} "$OUT/raw/$(basename "$d")/" \; ; done
 echo "summary: $OUT/summary.json"

@@ -297,3 +297,38 @@ def test_dwt_line_decode_4k(wavelet):
     out = DW.decode(got, H, W, wavelet, L, Q)
     assert np.array_equal(out, DW.decode(got, H, W, wavelet, L, Q, variant=17))
     assert np.array_equal(out[1], O.dwt_decode_frame(got[1], H, W, wavelet, L, Q))
+
+
+def _decode_unfused(DW, *a):
+    """DW.decode with the inverse levels 2 + 1 as two line-kernel launches."""
+    from vcf_amd import _lib as Lb
+    Lb.call("vcf_dwt_set_inverse_band21", 0)
+    try:
+        return DW.decode(*a)
+    finally:
+        Lb.call("vcf_dwt_set_inverse_band21", 1)
+
+
+@pytest.mark.parametrize("wavelet,H,W,L,Q", [
+    ("bior4.4", 2160, 3840, 5, 32),      # C3
+    ("db5", 2160, 3840, 5, 32),
+    ("bior4.4", 96, 136, 2, 32),          # LL2 from the packed u16 subband; a partial last tile
+    ("bior4.4", 120, 248, 3, 7),          # non-power-of-two Q
+    ("db5", 200, 480, 4, 300),            # Q > 256: the int16 dequant
+    ("bior4.4", 40, 40, 2, 1),            # subbands of 10 x 10: one tile, one band
+    ("bior4.4", 44, 60, 3, 32),           # h1 = 22 = 2 h2, w1 = 30 = 2 h2: level 2 of 11 x 15
+    ("bior4.4", 90, 140, 3, 32),          # h1 = 45 odd: the two launches (not halving evenly)
+])
+def test_dwt_decode_band21_equals_two_launches(wavelet, H, W, L, Q):
+    """The inverse levels 2 + 1 in one launch (idwt_band21_kernel, LL1 on chip)
+    give the bytes of the two line-kernel launches and of the oracle."""
+    import vcf_amd.dwt as DW
+    rng = np.random.Generator(np.random.PCG64(H * W + L))
+    frames = rng.integers(0, 256, (2, H, W, 3), dtype=np.uint8)
+    frames[1] = np.broadcast_to(np.arange(W, dtype=np.uint8)[None, :, None], (H, W, 3))
+    sb = DW.encode(frames, wavelet, L, Q)
+    fused = DW.decode(sb, H, W, wavelet, L, Q)
+    two = _decode_unfused(DW, sb, H, W, wavelet, L, Q)
+    assert np.array_equal(fused, two)
+    f = 1 if H * W > 1e6 else 0
+    assert np.array_equal(fused[f], O.dwt_decode_frame(sb[f], H, W, wavelet, L, Q))

@@ -138,6 +138,8 @@ SIGNATURES = {
     "vcf_zlib_workspace": [_I64],
     "vcf_zlib_set_workspace_budget": [_I64],
     "vcf_dwt_lift_set_fused": [_I32],
+    "vcf_dwt_set_inverse_band21": [_I32],
+    "vcf_dwt_lift_analyze_f64": [_P, _I32, _I32, _I32, _P, _P, _P, _P],
     "vcf_zlib_max_strip": [],
     "vcf_inflate_strips": [_P, _P, _P, _I64, _P, _P, _P, _P, _P],
     "vcf_zlib_strip_count": [_I64, _I32],

@@ -1231,6 +1231,8 @@ __global__ __launch_bounds__(256) void idwt_level_kernel(const uint8_t *__restri
 
 // line-based inverse level (the default for 10-tap filters)
 #include "vcf_idwt_line.h"
+// inverse levels 2 + 1 in one launch (the default where the planes halve evenly)
+#include "vcf_idwt_band21.h"
 // the opt-in lifting form of bior4.4 (not bit-exact)
 #include "vcf_dwt_lift.h"
 
@@ -1595,6 +1597,66 @@ void launch_line(int id, const LevelArgs &a, bool from_packed, bool to_rgb, uint
     else launch_line_id<0u, 0u, 2>(a, from_packed, to_rgb, rgb_out);
 }
 
+// Inverse levels 2 + 1 in one launch (idwt_band21_kernel): line_ok filters on
+// planes that halve evenly from level 2 to level 1 (h1 = 2 h2, w1 = 2 w2).
+std::atomic<int> g_band21{1};   // vcf_dwt_set_inverse_band21 (A/B and tests)
+bool band21_ok(const DwtGeom &g, const WaveletDef &wd, int &id)
+{
+    if (!g_band21.load(std::memory_order_relaxed) || g.levels < 2) return false;
+    const int h2 = g.hs[2], w2 = g.ws[2], h1 = g.hs[1], w1 = g.ws[1];
+    return h1 == 2 * h2 && w1 == 2 * w2 && line_ok(wd, h2, w2, id) && line_ok(wd, h1, w1, id);
+}
+
+template <bool FP, unsigned ZL, unsigned ZH, int CT>
+void launch_band21_t(const DwtGeom &g, const uint8_t *packed, long long n_frames, const double *prev,
+                     long long plane_stride, int lda, uint8_t *rgb, int Q, hipStream_t s)
+{
+    auto kern = Q <= 256 ? idwt_band21_kernel<FP, ZL, ZH, CT, true> : idwt_band21_kernel<FP, ZL, ZH, CT, false>;
+    static int slots = 0;   // resident workgroups on the device (per instantiation)
+    if (!slots) {
+        int dev = 0, n_cu = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+            n_cu = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kB21NT, 0) != hipSuccess || per_cu <= 0)
+            per_cu = 2;
+        slots = n_cu * per_cu;
+    }
+    const int h1 = g.hs[1], w1 = g.ws[1];
+    const int n_tiles = (w1 + kB21C - 1) / kB21C;
+    // bands of an even number of level-1 rows; time ~ rounds x (rows + 4 halo + level-2 warm-up)
+    const long long per_band = (long long)n_tiles * n_frames;
+    int brows = (h1 + 1) / 2 * 2;
+    long long best = -1;
+    for (int br = 2; br <= (h1 + 1) / 2 * 2; br += 2) {
+        const long long nb = (h1 + br - 1) / br;
+        const long long rounds = (per_band * nb + slots - 1) / slots;
+        const long long cost = rounds * (br + 7);
+        if (best < 0 || cost < best) {
+            best = cost;
+            brows = br;
+        }
+    }
+    const int n_bands = (h1 + brows - 1) / brows;
+    const long long grid = per_band * n_bands;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kB21NT), 0, s, packed, g.packed_bytes, g.ll_off,
+                       g.sb_off[2][0], g.sb_off[2][1], g.sb_off[2][2], g.sb_off[1][0], g.sb_off[1][1], g.sb_off[1][2],
+                       prev, plane_stride, lda, rgb, g.hs[2], g.ws[2], h1, w1, Q, n_tiles, n_bands, brows);
+}
+
+void launch_band21(int id, const DwtGeom &g, const uint8_t *packed, long long n_frames, const double *prev,
+                   long long plane_stride, int lda, uint8_t *rgb, int Q, hipStream_t s)
+{
+    const bool fp = g.levels == 2;   // LL2 from the packed u16 subband, else the level-3 plane
+    if (id == 1) {
+        if (fp) launch_band21_t<true, kB44RecLo, kB44RecHi, 1>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s);
+        else launch_band21_t<false, kB44RecLo, kB44RecHi, 1>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s);
+    } else {
+        if (fp) launch_band21_t<true, 0u, 0u, 2>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s);
+        else launch_band21_t<false, 0u, 0u, 2>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s);
+    }
+}
+
 #define VCF_DWT_FOR_EACH_F(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18)
 
 void fwd_level(int F, const LevelArgs &a, bool first, bool last)
@@ -1874,7 +1936,13 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
     int lda = 0;
     const bool short_lines = g.hs[levels] < F / 2 || g.ws[levels] < F / 2;
     if (fast_filter(F) && !short_lines) {
+        int id21 = 0;
+        const bool b21 = band21_ok(g, kWavelets[wavelet], id21);
         for (int r = levels; r >= 1; --r) {
+            if (b21 && r == 2) {   // levels 2 and 1 in one launch, LL1 on chip
+                launch_band21(id21, g, packed_dev, n_frames, prev, ws_stride, lda, rgb_dev, Q, s);
+                return hip_check(hipGetLastError(), "idwt_band21_kernel launch");
+            }
             const int h = g.hs[r], w = g.ws[r];
             const int oh = r > 1 ? g.hs[r - 1] : 2 * h, ow = r > 1 ? g.ws[r - 1] : 2 * w;
             double *out = (r & 1) ? P0 : P1;
@@ -1916,6 +1984,12 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
 
 // The lifting path (vcf_dwt_lift.h): bior4.4 only, same buffers, layout and
 // workspace as vcf_dwt_dz_encode / _decode; results within +-1 of theirs.
+int vcf_dwt_set_inverse_band21(int32_t on)
+{
+    g_band21.store(on ? 1 : 0, std::memory_order_relaxed);
+    return VCF_OK;
+}
+
 int vcf_dwt_lift_set_fused(int32_t fused)
 {
     g_lift_fused.store(fused ? 1 : 0, std::memory_order_relaxed);
@@ -2000,6 +2074,50 @@ int vcf_dwt_dz_encode_lift(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, 
         nb ^= 1;
         ++l;
     }
+    return VCF_OK;
+}
+
+// The lifting path's float64 coefficients before quantization, for one frame (the
+// tolerance measurement of tests/test_dwt_lift_gpu.py): one general-body launch per
+// level; coef_dev receives, per level l = 1..levels, the details [LH, HL, HH][Y, Co,
+// Cg][hs[l] x ws[l]], then LL_levels [Y, Co, Cg][hs x ws]; packed_dev (the packed
+// layout's bytes) receives Q = 1 indices as scratch.
+int vcf_dwt_lift_analyze_f64(const uint8_t *rgb_dev, int32_t H, int32_t W, int32_t levels, double *coef_dev,
+                             uint8_t *packed_dev, void *workspace_dev, void *stream)
+{
+    int32_t wavelet = 0;
+    int rc = vcf_wavelet_index("bior4.4", &wavelet);
+    if (rc != VCF_OK) return rc;
+    rc = check_dwt(rgb_dev, packed_dev, 1, H, W, wavelet, levels, 1, false);
+    if (rc != VCF_OK) return rc;
+    if (!coef_dev || !workspace_dev) return set_error(VCF_ERR_INVALID, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    DwtGeom g;
+    dwt_geom(H, W, levels, 10, g);
+    const long long pd = plane_doubles(g);
+    double *P[2] = {(double *)workspace_dev, (double *)workspace_dev + ((long long)g.hs[1] * g.ws[1] + 1) / 2 * 2};
+    const double *in = nullptr;
+    int nb = 0;
+    double *raw = coef_dev;
+    for (int l = 1; l <= levels; ++l) {
+        const int h = g.hs[l - 1], w = g.ws[l - 1], hh = g.hs[l], hw = g.ws[l];
+        double *out = P[nb];
+        const int n_strips = (hw + lift::kValid - 1) / lift::kValid, brows = 16;
+        const int n_bands = (hh + brows - 1) / brows;
+        auto kern = l == 1 ? lift::lift_fwd_raw_kernel<true> : lift::lift_fwd_raw_kernel<false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(n_strips * n_bands)), dim3(lift::kNT), 0, s, rgb_dev, in, pd, out,
+                           packed_dev, g.packed_bytes, g.sb_off[l][0], g.sb_off[l][1], g.sb_off[l][2], h, w, hh, hw,
+                           n_strips, n_bands, brows, raw);
+        if ((rc = hip_check(hipGetLastError(), "lift_fwd_raw_kernel launch")) != VCF_OK) return rc;
+        raw += 9LL * hh * hw;
+        in = out;
+        nb ^= 1;
+    }
+    const int hh = g.hs[levels], hw = g.ws[levels];
+    for (int ch = 0; ch < 3; ++ch)
+        if ((rc = hip_check(hipMemcpyAsync(raw + (long long)ch * hh * hw, in + ch * pd, sizeof(double) * hh * hw,
+                                           hipMemcpyDeviceToDevice, s), "hipMemcpyAsync")) != VCF_OK)
+            return rc;
     return VCF_OK;
 }
 

@@ -176,14 +176,17 @@ __device__ __forceinline__ U32x4 pack2(double a, double b)
 constexpr int kRowDw = 64 * kP * 2 * 3 / 4;            // dwords of one staged RGB row
 constexpr int kSbB = kValid * 3, kSbDw = 3 * kSbB / 4;  // bytes of one subband row, dwords of three
 
-template <bool FIRST, bool LAST, bool EDGE, bool QP2>
+// RAW (diagnostic, vcf_dwt_lift_analyze_f64 only): the general body also stores the
+// three detail subbands' float64 coefficients before quantization, raw[(sb * 3 +
+// ch) * hh * hw + row * hw + col] for sb = LH, HL, HH of a single frame
+template <bool FIRST, bool LAST, bool EDGE, bool QP2, bool RAW = false>
 __device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, long long rgb_stride,
                                               const double *__restrict__ in, long long plane_stride,
                                               double *__restrict__ LLout, uint8_t *__restrict__ packed,
                                               long long packed_stride, long long ll_off, long long off_lh,
                                               long long off_hl, long long off_hh, int h, int w, int hh, int hw, int Q,
                                               int n_int, int n_set, int n_bands, int brows, int bid,
-                                              uint32_t *px_lds, uint32_t *sb_lds)
+                                              uint32_t *px_lds, uint32_t *sb_lds, double *raw = nullptr)
 {
     const int qsh = QP2 ? __builtin_ctz((unsigned)Q) : 0;
     // byte staging through LDS (interior strips; double-buffered, one barrier
@@ -388,9 +391,31 @@ __device__ __forceinline__ void lift_fwd_body(const uint8_t *__restrict__ rgb, l
                 __builtin_amdgcn_raw_buffer_store_b8(q[0][k], rs_pk, ((uint32_t)off_lh + o) | drop[k], 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b8(q[1][k], rs_pk, ((uint32_t)off_hl + o) | drop[k], 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b8(q[2][k], rs_pk, ((uint32_t)off_hh + o) | drop[k], 0, 0);
+                if (RAW && !drop[k]) {
+                    const long long at = orow + jl + k, sbp = (long long)hh * hw;
+                    raw[(0 * 3 + ch) * sbp + at] = lh[k];
+                    raw[(1 * 3 + ch) * sbp + at] = hl[k];
+                    raw[(2 * 3 + ch) * sbp + at] = hhv[k];
+                }
             }
         }
     }
+}
+
+// the diagnostic launch: every workgroup on the general body, details also as float64
+template <bool FIRST>
+__global__ __launch_bounds__(kNT) void lift_fwd_raw_kernel(const uint8_t *__restrict__ rgb, const double *__restrict__ in,
+                                                           long long plane_stride, double *__restrict__ LLout,
+                                                           uint8_t *__restrict__ packed, long long packed_stride,
+                                                           long long off_lh, long long off_hl, long long off_hh, int h,
+                                                           int w, int hh, int hw, int n_strips, int n_bands, int brows,
+                                                           double *__restrict__ raw)
+{
+    __shared__ uint32_t px_lds[1];
+    __shared__ uint32_t sb_lds[2 * (kSbDw + 1)];
+    lift_fwd_body<FIRST, false, true, false, true>(rgb, 0, in, plane_stride, LLout, packed, packed_stride, 0, off_lh,
+                                                   off_hl, off_hh, h, w, hh, hw, 1, 0, n_strips, n_bands, brows,
+                                                   blockIdx.x, px_lds, sb_lds, raw);
 }
 
 // one launch per level: the general body's workgroups first (odd shapes: all

@@ -145,3 +145,32 @@ def decode(subbands, H: int, W: int, wavelet: str = "db5", levels: int = 5, Q: i
         dout.free()
         dws.free()
     return out[0] if single else out
+
+
+def lift_coefficients(rgb: np.ndarray, levels: int = 5):
+    """The opt-in lifting path's float64 coefficients of one HxWx3 u8 frame
+    before quantization (vcf_dwt_lift_analyze_f64, bior4.4): [cA, (cH, cV, cD)
+    per level, coarsest first] per YCoCg channel, pywt.wavedec2's order and
+    naming (cH = the reference's LH, cV = HL, cD = HH)."""
+    f = _frames(rgb, "rgb")
+    if f.shape[0] != 1:
+        raise ValueError("one frame")
+    _, H, W, _ = f.shape
+    shapes, pb, wb = layout(H, W, levels)
+    n_coef = sum(9 * h * w for h, w in shapes) + 3 * shapes[-1][0] * shapes[-1][1]
+    din, dco, dpk, dws = DeviceBuffer.from_array(f), DeviceBuffer(8 * n_coef), DeviceBuffer(pb), DeviceBuffer(wb)
+    try:
+        L.call("vcf_dwt_lift_analyze_f64", din.ptr, H, W, levels, dco.ptr, dpk.ptr, dws.ptr, None)
+        flat = dco.download(np.empty(n_coef, np.float64))
+    finally:
+        for b in (din, dco, dpk, dws):
+            b.free()
+    det, off = [], 0
+    for h, w in shapes:
+        d = flat[off:off + 9 * h * w].reshape(3, 3, h, w)   # [LH, HL, HH][channel]
+        det.append(d)
+        off += 9 * h * w
+    h, w = shapes[-1]
+    ll = flat[off:off + 3 * h * w].reshape(3, h, w)
+    return [[ll[c]] + [tuple(det[lv][s, c] for s in range(3)) for lv in range(levels - 1, -1, -1)]
+            for c in range(3)]
