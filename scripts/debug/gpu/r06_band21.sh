@@ -10,4 +10,6 @@ timeout -k 10 300 python -u scripts/dwt_toggle_ab.py vcf_dwt_set_inverse_band21 
 rc=$?; echo "ab rc=$rc"; cat gpurun_out/r06_band21_ab.json; [ $rc -eq 0 ] || exit $rc
 bash scripts/pmc_r06.sh c3_dec python3 scripts/dwt_once.py 0 3 || exit $?
 bash scripts/pmc_r06.sh zlib_c4 python3 scripts/zlib_once.py 256 1 || exit $?
-echo done
+
+timeout -k 10 300 python3 -u scripts/debug/zprof_run.py 256 > gpurun_out/r06_zprof.json 2> gpurun_out/r06_zprof.err
+rc=$?; echo "zprof rc=$rc"; cat gpurun_out/r06_zprof.json

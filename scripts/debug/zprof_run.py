@@ -5,7 +5,7 @@ import ctypes, json, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-from bench import synth_frame, c4_frame
+from vcf_amd.synthetic import synth_frame, c4_frame
 from vcf_amd import _lib as L, dct
 from vcf_amd.codec.tiff import strip_layout
 from vcf_amd.device import DeviceBuffer, Stream, Event
@@ -24,7 +24,7 @@ fb = flat.shape[1]; _, _, sb = strip_layout(frames.shape[1:], 1)
 spf = int(L.lib().vcf_zlib_strip_count(fb, sb)); total = spf * n; slot = int(L.lib().vcf_zlib_bound(sb))
 d = DeviceBuffer.from_array(flat); out = DeviceBuffer(total * slot); sizes = DeviceBuffer(total * 4)
 ws = DeviceBuffer(int(P.vcf_zlib_workspace(total))); st = Stream()
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 24)()
 for rep in range(2):
     P.vcf_zlib_prof_read(buf, 1)
     e0, e1 = Event(), Event()
@@ -45,4 +45,7 @@ print(json.dumps({"frames": n, "strips": total, "ms": round(e0.elapsed_ms(e1), 2
                   "cand_wait_cycles_per_longest": v[12] // max(1, v[3]),
                   "round_cycles_to_chain_ballot": v[13] // max(1, v[4]), "round_cycles_to_lengths": v[14] // max(1, v[4]),
                   "round_cycles_rest": v[15] // max(1, v[4]),
+                  "head_hit_frac": v[16] / max(1, v[3]), "far_round_frac": v[17] / max(1, v[4]),
+                  "far_lcp_lanes_per_round": v[18] / max(1, v[4]), "far_final_compare_per_call": v[19] / max(1, v[3]),
+                  "far_head_frac": v[20] / max(1, v[3]), "no_match_frac": v[21] / max(1, v[3]),
                   "lib": os.environ.get("ZPROF_LIB", "libvcf_zprof.so")}), flush=True)

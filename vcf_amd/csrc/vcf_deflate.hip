@@ -168,6 +168,12 @@ __device__ unsigned int g_zdbg[8];
 #ifndef VCF_ZX_EARLY0   // A/B (diagnostic builds): round 0's candidate reads before the head compare
 #define VCF_ZX_EARLY0 1
 #endif
+#ifndef VCF_ZX_FARWAVE   // A/B (diagnostic builds): far candidate compares past 16 bytes wave-wide
+#define VCF_ZX_FARWAVE 0
+#endif
+#ifndef VCF_ZX_G4DW   // A/B (diagnostic builds): far strip reads as aligned dwords + byte align
+#define VCF_ZX_G4DW 0
+#endif
 #ifndef VCF_ZX_SERIAL   // A/B (diagnostic builds): every kernel of a round on the caller's stream
 #define VCF_ZX_SERIAL 0
 #endif
@@ -179,7 +185,9 @@ __device__ unsigned int g_zdbg[8];
 // passing the scan_end test, [11] calls served by the prefetch, [12] cycles then waiting for
 // the first two rounds' candidates, [13..15] chain-round cycles: to the chain ballot, to the
 // lengths, the rest (rounds that end the call with a hit excluded from [15])
-__device__ unsigned long long g_zprof[16];
+// [16] calls ending at the head compare, [17] chain rounds holding a far lane, [18] lanes entering
+// far_lcp, [19] far wave_lcp_at calls, [20] calls whose chain head is far, [21] calls finding nothing
+__device__ unsigned long long g_zprof[24];
 #define VCF_ZPROF_COUNT(x) (++(x))
 #else
 #define VCF_ZPROF_COUNT(x) ((void)0)
@@ -1094,17 +1102,45 @@ struct Wave {
     // zeros or the slid copy past the end)
     __device__ __forceinline__ uint32_t g4(uint32_t P) const   // 4 bytes at input position P (unaligned)
     {
+#if VCF_ZX_G4DW
+        // two aligned dword loads and a byte align (a 4-byte memcpy of unknown alignment
+        // compiles to four byte loads); the dwords lie inside the frame buffer: the
+        // buffer is aligned and every far read ends well before the strip's end
+        const uintptr_t a = reinterpret_cast<uintptr_t>(src + P);
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+        return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+#else
         uint32_t d;
         __builtin_memcpy(&d, src + P, 4);
         return d;
+#endif
+    }
+    // 16 bytes at input position P: five aligned dwords (VCF_ZX_G4DW), else four g4
+    __device__ __forceinline__ void g16(uint32_t P, uint32_t (&o)[4]) const
+    {
+#if VCF_ZX_G4DW
+        const uintptr_t a = reinterpret_cast<uintptr_t>(src + P);
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3);
+        uint32_t w[5];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) w[u] = q[u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = __builtin_amdgcn_alignbyte(w[u + 1], w[u], sh);
+#else
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = g4(P + 4 * u);
+#endif
     }
     // far_lcp: lane_lcp with the first string at input position c in HBM
     __device__ __forceinline__ uint32_t far_lcp(uint32_t c, uint32_t b, uint32_t cap, uint32_t from)
     {
         uint32_t l = from;
         while (l < cap) {
-            const uint32_t x0 = g4(c + l) ^ ld4(b + l), x1 = g4(c + l + 4) ^ ld4(b + l + 4);
-            const uint32_t x2 = g4(c + l + 8) ^ ld4(b + l + 8), x3 = g4(c + l + 12) ^ ld4(b + l + 12);
+            uint32_t g[4];
+            g16(c + l, g);
+            const uint32_t x0 = g[0] ^ ld4(b + l), x1 = g[1] ^ ld4(b + l + 4);
+            const uint32_t x2 = g[2] ^ ld4(b + l + 8), x3 = g[3] ^ ld4(b + l + 12);
             if (x0 | x1 | x2 | x3) {
                 l += x0 ? 0 : x1 ? 4 : x2 ? 8 : 12;
                 l += (uint32_t)__builtin_ctz(x0 ? x0 : x1 ? x1 : x2 ? x2 : x3) >> 3;
@@ -1113,6 +1149,17 @@ struct Wave {
             l += 16;
         }
         return min(l, (uint32_t)MAX_MATCH);
+    }
+    // the common prefix of the strings at input position c (in HBM, far) and window offset
+    // b, given their first 16 bytes equal: one wave-wide compare of bytes 16 .. 271
+    // (c + 271 < p: far candidates lie kNearDist back)
+    __device__ __forceinline__ uint32_t far_wave_lcp16(uint32_t c, uint32_t b)
+    {
+        const uint32_t x = g4(c + 16 + 4 * lane_id()) ^ ld4(b + 16 + 4 * lane_id());
+        const uint64_t m = __ballot(x != 0);
+        if (!m) return (uint32_t)MAX_MATCH;
+        const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
+        return min(16 + 4 * f + ((uint32_t)__builtin_ctz(lane_val(x, f)) >> 3), (uint32_t)MAX_MATCH);
     }
     // wave_lcp with the first string at input position c: from the window when it is there
     __device__ __forceinline__ uint32_t wave_lcp_at(uint32_t c, uint32_t b)
@@ -1170,6 +1217,7 @@ struct Wave {
 #if VCF_ZLIB_PROF
     unsigned long long t_longest = 0, t_flush = 0, n_longest = 0, n_rounds = 0, n_shift = 0;
     unsigned long long t_head = 0, n_lcp = 0, n_cand = 0, n_pf = 0, t_wait = 0, t_r0 = 0, t_r1 = 0, t_r2 = 0;
+    unsigned long long n_headhit = 0, n_farround = 0, n_farlcp = 0, n_farwave = 0, n_farhead = 0, n_none = 0;
     __device__ __forceinline__ bool longest(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain, uint32_t nice,
                             uint32_t limit, uint32_t &len, uint32_t &pos)
     {
@@ -1304,10 +1352,11 @@ struct Wave {
                 for (int u = 0; u < 4; ++u) r.x16[u] = ld4(r.wc + 4 * u) ^ ld4(wp + 4 * u);
                 if (__ballot(r.far)) {   // wave-uniform: this round reaches past the window
                     if (r.far) {
-                        r.c4 = g4(r.c);
-                        r.x16[0] = r.c4 ^ ld4(wp);
+                        uint32_t g[4];
+                        g16(r.c, g);
+                        r.c4 = g[0];
 #pragma unroll
-                        for (int u = 1; u < 4; ++u) r.x16[u] = g4(r.c + 4 * u) ^ ld4(wp + 4 * u);
+                        for (int u = 0; u < 4; ++u) r.x16[u] = g[u] ^ ld4(wp + 4 * u);
                     }
                 }
                 return r;
@@ -1318,6 +1367,7 @@ struct Wave {
             const uint32_t hp = hash_at(wp);
             const uint32_t l1 = wave_lcp_at(hdp, wp);
 #if VCF_ZLIB_PROF
+            if (hdp < wbase) ++n_farhead;
             {
                 const unsigned long long th1 = clock64();
                 t_head += th1 - th0;
@@ -1328,6 +1378,9 @@ struct Wave {
             if (l1 >= Tn) {
                 len = l1;
                 pos = hdp;
+#if VCF_ZLIB_PROF
+                ++n_headhit;
+#endif
                 return true;
             }
             // only a candidate longer than F = max(prev_len, the head's length) can change the
@@ -1355,6 +1408,9 @@ struct Wave {
                     }
                 }
                 const bool se = e1 == lwin[wp + F] && e0 == lwin[wp + F - 1];
+#if VCF_ZLIB_PROF
+                if (__ballot(far)) ++n_farround;
+#endif
 #if VCF_ZX_WINCHECK
                 {
                     const uint32_t want = v ? win_src(c) | win_src(c + 1) << 8 | win_src(c + 2) << 16 | win_src(c + 3) << 24 : c4;
@@ -1386,10 +1442,24 @@ struct Wave {
                         l = q + ((uint32_t)__builtin_ctz(x16[0] ? x16[0] : x16[1] ? x16[1] : x16[2] ? x16[2] : x16[3]) >> 3);
                     } else if (!far) {
                         l = lane_lcp(wc, wp, VCF_ZX_NOCAP ? (uint32_t)MAX_MATCH : Tn, 16u);
-                    } else {
+                    } else if (!VCF_ZX_FARWAVE) {
                         l = far_lcp(c, wp, VCF_ZX_NOCAP ? (uint32_t)MAX_MATCH : Tn, 16u);
                     }
                 }
+#if VCF_ZX_FARWAVE
+                // far candidates whose first 16 bytes match (72 % of the chain rounds reach
+                // past the window): one wave-wide compare each -- bytes 16 .. 271 as 64 lanes x
+                // 4 in one round trip -- instead of the lane's 16-byte steps, one round trip
+                // each up to Tn; the length is exact (capped at MAX_MATCH)
+                for (uint64_t fm = __ballot(cand && far && !(x16[0] | x16[1] | x16[2] | x16[3])); fm; fm &= fm - 1) {
+                    const uint32_t k = (uint32_t)__ffsll((unsigned long long)fm) - 1;
+                    const uint32_t lk = far_wave_lcp16(lane_val(c, k), wp);
+                    if (lane_id() == k) l = lk;
+                }
+#endif
+#if VCF_ZLIB_PROF
+                n_farlcp += (unsigned long long)__popcll(__ballot(cand && far && !(x16[0] | x16[1] | x16[2] | x16[3])));
+#endif
 #if VCF_ZLIB_PROF
                 {
                     uint32_t ms = lcp_steps;
@@ -1406,6 +1476,9 @@ struct Wave {
                 if (hit) {
                     const uint32_t k = (uint32_t)__ffsll((unsigned long long)hit) - 1;
                     pos = lane_val(c, k);
+#if VCF_ZLIB_PROF
+                    if (!(k == 0 && b == 0) && pos < wbase) ++n_farwave;
+#endif
                     len = k == 0 && b == 0 ? l1 : wave_lcp_at(pos, wp);
                     return true;
                 }
@@ -1424,6 +1497,9 @@ struct Wave {
             }
             len = best;
             pos = bpos;
+#if VCF_ZLIB_PROF
+            if (!found) ++n_none;
+#endif
             return found;
         }
     }
@@ -1612,6 +1688,12 @@ __global__ __launch_bounds__(64) VCF_ZX_WPE_ATTR void zlib_parse_kernel(const ui
             atomicAdd(&g_zprof[13], wv.t_r0);
             atomicAdd(&g_zprof[14], wv.t_r1);
             atomicAdd(&g_zprof[15], wv.t_r2);
+            atomicAdd(&g_zprof[16], wv.n_headhit);
+            atomicAdd(&g_zprof[17], wv.n_farround);
+            atomicAdd(&g_zprof[18], wv.n_farlcp);
+            atomicAdd(&g_zprof[19], wv.n_farwave);
+            atomicAdd(&g_zprof[20], wv.n_farhead);
+            atomicAdd(&g_zprof[21], wv.n_none);
         } else {
             atomicAdd(&g_zprof[7], tp);
         }
@@ -1650,11 +1732,11 @@ int vcf_zlib_dbg_read(unsigned int *host8)
 }
 #endif
 #if VCF_ZLIB_PROF
-int vcf_zlib_prof_read(unsigned long long *host16, int reset)
+int vcf_zlib_prof_read(unsigned long long *host24, int reset)
 {
-    int rc = hip_check(hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_zprof), sizeof(g_zprof)), "hipMemcpyFromSymbol");
+    int rc = hip_check(hipMemcpyFromSymbol(host24, HIP_SYMBOL(g_zprof), sizeof(g_zprof)), "hipMemcpyFromSymbol");
     if (rc == VCF_OK && reset) {
-        static const unsigned long long z[16] = {};
+        static const unsigned long long z[24] = {};
         rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_zprof), z, sizeof(z)), "hipMemcpyToSymbol");
     }
     return rc;

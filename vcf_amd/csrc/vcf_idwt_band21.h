@@ -64,8 +64,8 @@ __global__ __launch_bounds__(kB21NT) void idwt_band21_kernel(
     struct Det {
         uint32_t hl, lh, hh;
     };
-    auto load1 = [&](int r) -> Det {   // level-1 row r (wrapped)
-        const uint8_t *row = pk + (long long)mod_n(r, h1) * w1 * 3;
+    auto load1 = [&](int rw) -> Det {   // level-1 row rw (already wrapped)
+        const uint8_t *row = pk + (long long)rw * w1 * 3;
         return Det{(row + off1_hl)[b1], (row + off1_lh)[b1], (row + off1_hh)[b1]};
     };
     // LL1 value slot of this lane's level-2 column: pair L & 31, parity L >> 5
@@ -86,8 +86,7 @@ __global__ __launch_bounds__(kB21NT) void idwt_band21_kernel(
         double ll;
         uint32_t hl, lh, hh;
     };
-    auto load2 = [&](int y) -> Row2 {   // level-2 row y (wrapped)
-        y = mod_n(y, h2);
+    auto load2 = [&](int y) -> Row2 {   // level-2 row y (already wrapped)
         const long long rb = (long long)y * w2 * 3;
         Row2 v;
         if (FROM_PACKED_LL2) v.ll = dequant((int16_t)*reinterpret_cast<const uint16_t *>(pk + ll_off + 2 * (rb + b2)), Q);
@@ -176,11 +175,14 @@ __global__ __launch_bounds__(kB21NT) void idwt_band21_kernel(
 
     // ---- prologue: the level-2 window up to m2 = m0/2 - 1, LL1 rows m0 - 2, m0 - 1 ----
     const int m2f = m0 / 2 - 1;     // (brows and m0 even)
-    int y2 = m2f - 2;               // the next level-2 row to stage
+    // the next level-2 row to stage, wrapped (advanced by one: no division per step)
+    int y2 = mod_n(m2f - 2, h2);
+    auto next_y2 = [&]() { y2 = y2 + 1 == h2 ? 0 : y2 + 1; };
 #pragma unroll
     for (int j = 0; j < 5; ++j) wk[j] = wr[j] = 0.0;
     for (int u = 0; u < 5; ++u) {   // rows m2f - 2 .. m2f + 2
-        put2(u & 1, load2(y2++));
+        put2(u & 1, load2(y2));
+        next_y2();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -190,7 +192,9 @@ __global__ __launch_bounds__(kB21NT) void idwt_band21_kernel(
     col2(ll_a, ll_b);
     int b2buf = 1;                  // the s2 buffer the next staged row goes to
     Row2 pre2;                      // loaded at an even step, staged at the next (odd) one
-    put1(0, ll_a, load1(m0 - 2));
+    int r1w = mod_n(m0 - 2, h1);   // the wrapped level-1 row of the next detail load
+    put1(0, ll_a, load1(r1w));
+    r1w = r1w + 1 == h1 ? 0 : r1w + 1;
     double ll_hold = ll_b;          // LL1 row r + 1 when r is even
     __syncthreads();
 
@@ -201,12 +205,16 @@ __global__ __launch_bounds__(kB21NT) void idwt_band21_kernel(
         for (int u = 0; u < 5; ++u) {
             const int t = t0 + u;
             if (t >= nsteps) break;
-            const int r = m0 - 2 + t;                  // this step's level-1 row
+            // this step's level-1 row is r = m0 - 2 + t
             const bool odd = (t & 1) != 0;             // r odd: a level-2 step makes LL1 rows r + 1, r + 2
             // prefetch: level-1 details of row r + 1; at even steps the level-2 row the
             // next (odd) step stages (issued a step ahead of its LDS store)
-            const Det d1 = load1(r + 1);
-            if (!odd) pre2 = load2(y2++);
+            const Det d1 = load1(r1w);   // row r + 1
+            r1w = r1w + 1 == h1 ? 0 : r1w + 1;
+            if (!odd) {
+                pre2 = load2(y2);
+                next_y2();
+            }
             // level-1 row pass of row r
             {
                 const double *S = &s1[t & 1][ch][0][lc - 2];
