@@ -532,6 +532,12 @@ VCF_HD uint32_t byte_sel(uint32_t w)
     return (w >> (8 * SEL)) & 0xffu;
 }
 
+// VCF_SDWA_ASM (default 1): the byte-operand adds as inline SDWA asm; 0 leaves them to the
+// compiler's SDWA peephole (A/B, DESIGN.md §6: the asm form costs a hazard s_nop after
+// each block, the compiler's form more plain adds)
+#ifndef VCF_SDWA_ASM
+#define VCF_SDWA_ASM 1
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 #define VCF_SDWA_BODY(OP, S0, S1)                                                                    \
     asm(OP " %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:" S0 " src1_sel:" S1          \
@@ -555,7 +561,7 @@ VCF_HD uint32_t byte_sel(uint32_t w)
 template <int B0, int B1>
 VCF_HD uint32_t add_sdwa(uint32_t a, uint32_t b)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && VCF_SDWA_ASM
     VCF_SDWA_FN("v_add_u32_sdwa")
 #else
     return (B0 < 0 ? a : byte_sel<(B0 < 0 ? 0 : B0)>(a)) + byte_sel<B1>(b);
@@ -566,7 +572,7 @@ VCF_HD uint32_t add_sdwa(uint32_t a, uint32_t b)
 template <int B0, int B1>
 VCF_HD uint32_t sub_sdwa(uint32_t a, uint32_t b)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && VCF_SDWA_ASM
     VCF_SDWA_FN("v_sub_u32_sdwa")
 #else
     return (B0 < 0 ? a : byte_sel<(B0 < 0 ? 0 : B0)>(a)) - byte_sel<B1>(b);
@@ -577,7 +583,7 @@ VCF_HD uint32_t sub_sdwa(uint32_t a, uint32_t b)
 template <int B1>
 VCF_HD uint32_t twice_byte(uint32_t b)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && VCF_SDWA_ASM
     constexpr int B0 = -1;
     const uint32_t a = 1;
     VCF_SDWA_FN("v_lshlrev_b32_sdwa")

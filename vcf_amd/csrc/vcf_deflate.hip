@@ -166,13 +166,15 @@ __device__ unsigned int g_zdbg[8];
 #define VCF_ZX_LDSZERO 0
 #endif
 #ifndef VCF_ZX_EARLY0   // A/B (diagnostic builds): round 0's candidate reads before the head compare
-#define VCF_ZX_EARLY0 1
+// (round 6: 0 -- the head compare no longer waits for the candidate list and the far
+// candidates' bytes, and round 0's far reads share one round trip with its scan_end
+// bytes: C4 deflate 102.3 -> 97.2 ms, ABBA, profiles/r06_zab_v2.json)
+#define VCF_ZX_EARLY0 0
 #endif
-#ifndef VCF_ZX_FARWAVE   // A/B (diagnostic builds): far candidate compares past 16 bytes wave-wide
-#define VCF_ZX_FARWAVE 0
-#endif
-#ifndef VCF_ZX_G4DW   // A/B (diagnostic builds): far strip reads as aligned dwords + byte align
-#define VCF_ZX_G4DW 0
+#ifndef VCF_ZX_PREDICT   // A/B (diagnostic builds): prefetch the exactly predicted next call position
+// (round 6: 1 -- 70 % -> 93 % of the calls find their candidates prefetched; C4 deflate
+// 101.3 -> 95.3 ms, ABBA, profiles/r06_zab_v3.json; 2: also p + 1, 98.4 ms)
+#define VCF_ZX_PREDICT 1
 #endif
 #ifndef VCF_ZX_SERIAL   // A/B (diagnostic builds): every kernel of a round on the caller's stream
 #define VCF_ZX_SERIAL 0
@@ -841,6 +843,7 @@ struct Wave {
     uint32_t *out32;
     uint32_t out_words;           // slot capacity in words
     uint32_t good;                // cfg.good: the reduced-chain results from prev_length >= good
+    uint32_t lazy = 0;            // cfg.lazy (VCF_ZX_PREDICT)
     uint32_t bitpos = 0;          // bits written so far (uniform)
     uint32_t nsym = 0;            // symbols of the current block (uniform)
     // 512-position windows: lane l holds positions base + 8l .. base + 8l + 7
@@ -1102,45 +1105,17 @@ struct Wave {
     // zeros or the slid copy past the end)
     __device__ __forceinline__ uint32_t g4(uint32_t P) const   // 4 bytes at input position P (unaligned)
     {
-#if VCF_ZX_G4DW
-        // two aligned dword loads and a byte align (a 4-byte memcpy of unknown alignment
-        // compiles to four byte loads); the dwords lie inside the frame buffer: the
-        // buffer is aligned and every far read ends well before the strip's end
-        const uintptr_t a = reinterpret_cast<uintptr_t>(src + P);
-        const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-        return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
-#else
         uint32_t d;
         __builtin_memcpy(&d, src + P, 4);
         return d;
-#endif
-    }
-    // 16 bytes at input position P: five aligned dwords (VCF_ZX_G4DW), else four g4
-    __device__ __forceinline__ void g16(uint32_t P, uint32_t (&o)[4]) const
-    {
-#if VCF_ZX_G4DW
-        const uintptr_t a = reinterpret_cast<uintptr_t>(src + P);
-        const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-        const uint32_t sh = (uint32_t)(a & 3);
-        uint32_t w[5];
-#pragma unroll
-        for (int u = 0; u < 5; ++u) w[u] = q[u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) o[u] = __builtin_amdgcn_alignbyte(w[u + 1], w[u], sh);
-#else
-#pragma unroll
-        for (int u = 0; u < 4; ++u) o[u] = g4(P + 4 * u);
-#endif
     }
     // far_lcp: lane_lcp with the first string at input position c in HBM
     __device__ __forceinline__ uint32_t far_lcp(uint32_t c, uint32_t b, uint32_t cap, uint32_t from)
     {
         uint32_t l = from;
         while (l < cap) {
-            uint32_t g[4];
-            g16(c + l, g);
-            const uint32_t x0 = g[0] ^ ld4(b + l), x1 = g[1] ^ ld4(b + l + 4);
-            const uint32_t x2 = g[2] ^ ld4(b + l + 8), x3 = g[3] ^ ld4(b + l + 12);
+            const uint32_t x0 = g4(c + l) ^ ld4(b + l), x1 = g4(c + l + 4) ^ ld4(b + l + 4);
+            const uint32_t x2 = g4(c + l + 8) ^ ld4(b + l + 8), x3 = g4(c + l + 12) ^ ld4(b + l + 12);
             if (x0 | x1 | x2 | x3) {
                 l += x0 ? 0 : x1 ? 4 : x2 ? 8 : 12;
                 l += (uint32_t)__builtin_ctz(x0 ? x0 : x1 ? x1 : x2 ? x2 : x3) >> 3;
@@ -1149,17 +1124,6 @@ struct Wave {
             l += 16;
         }
         return min(l, (uint32_t)MAX_MATCH);
-    }
-    // the common prefix of the strings at input position c (in HBM, far) and window offset
-    // b, given their first 16 bytes equal: one wave-wide compare of bytes 16 .. 271
-    // (c + 271 < p: far candidates lie kNearDist back)
-    __device__ __forceinline__ uint32_t far_wave_lcp16(uint32_t c, uint32_t b)
-    {
-        const uint32_t x = g4(c + 16 + 4 * lane_id()) ^ ld4(b + 16 + 4 * lane_id());
-        const uint64_t m = __ballot(x != 0);
-        if (!m) return (uint32_t)MAX_MATCH;
-        const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
-        return min(16 + 4 * f + ((uint32_t)__builtin_ctz(lane_val(x, f)) >> 3), (uint32_t)MAX_MATCH);
     }
     // wave_lcp with the first string at input position c: from the window when it is there
     __device__ __forceinline__ uint32_t wave_lcp_at(uint32_t c, uint32_t b)
@@ -1261,9 +1225,32 @@ struct Wave {
         const uint32_t o = off & 511u, e = o & 7;
         return (pick4(off < 512u ? iv : iv_n, o >> 3, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
     }
-    __device__ __forceinline__ void prefetch_next(uint32_t p, uint32_t len)
+    // VCF_ZX_PREDICT (A/B): the position deflate_slow calls longest_match at next follows
+    // from this call's result and prev_length: with match_length ml (this call's length,
+    // clamped to the lookahead, TOO_FAR applied; prev_length when nothing was found), the
+    // previous match is emitted when prev_length >= MIN_MATCH and ml <= prev_length (next
+    // call at p - 1 + prev_length), else a match of at least `lazy` is emitted at the next
+    // step (next call at p + ml), else the parse moves to p + 1.  Slot a takes that
+    // position; slot b (PREDICT 2) p + 1 as well, for the calls the hash head skips.
+    __device__ __forceinline__ uint32_t predict_next(uint32_t p, bool found, uint32_t len, uint32_t pos,
+                                                     uint32_t prev_len) const
     {
+        const uint32_t look = n - p;
+        uint32_t ml = found ? min(len, look) : min(prev_len, look);
+        if (found && ml == (uint32_t)MIN_MATCH && p - pos > (uint32_t)TOO_FAR) ml = MIN_MATCH - 1;
+        if (prev_len >= (uint32_t)MIN_MATCH && ml <= prev_len) return p - 1 + prev_len;
+        if (ml >= lazy && ml >= (uint32_t)MIN_MATCH) return p + ml;
+        return p + 1;
+    }
+    __device__ __forceinline__ void prefetch_next(uint32_t p, uint32_t len, bool found = false, uint32_t pos = 0,
+                                                  uint32_t prev_len = 0)
+    {
+#if VCF_ZX_PREDICT
+        const uint32_t qa = predict_next(p, found, len, pos, prev_len);
+        const uint32_t qb = VCF_ZX_PREDICT == 2 ? p + 1 : qa;
+#else
         const uint32_t qa = p + 1, qb = p + (len >= (uint32_t)MIN_MATCH ? len : 1u);
+#endif
         const uint32_t ia = idx_known(qa);
         pfa_p = ia != 0xffffffffu && qa + MIN_MATCH <= n ? qa : 0xffffffffu;
         if (pfa_p != 0xffffffffu) fetch_cands(ia, pfa0, pfa1);
@@ -1276,7 +1263,7 @@ struct Wave {
     {
         if constexpr (LAZY) {
             const bool r = lazy_longest(p, hdp, prev_len, chain, nice, limit, len, pos);
-            prefetch_next(p, r ? len : 0u);
+            prefetch_next(p, r ? len : 0u, r, pos, prev_len);
             return r;
         }
         // the K2 results: the full chain's, or the reduced chain's once prev_len >= good
@@ -1352,16 +1339,15 @@ struct Wave {
                 for (int u = 0; u < 4; ++u) r.x16[u] = ld4(r.wc + 4 * u) ^ ld4(wp + 4 * u);
                 if (__ballot(r.far)) {   // wave-uniform: this round reaches past the window
                     if (r.far) {
-                        uint32_t g[4];
-                        g16(r.c, g);
-                        r.c4 = g[0];
+                        r.c4 = g4(r.c);
+                        r.x16[0] = r.c4 ^ ld4(wp);
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) r.x16[u] = g[u] ^ ld4(wp + 4 * u);
+                        for (int u = 1; u < 4; ++u) r.x16[u] = g4(r.c + 4 * u) ^ ld4(wp + 4 * u);
                     }
                 }
                 return r;
             };
-            // round 0's reads issued with the head compare's (VCF_ZX_EARLY0; 0: in the round)
+            // round 0's reads in the round (VCF_ZX_EARLY0 = 1: issued with the head compare's)
             RoundRd r0;
             if (VCF_ZX_EARLY0) r0 = rd(0);
             const uint32_t hp = hash_at(wp);
@@ -1442,21 +1428,10 @@ struct Wave {
                         l = q + ((uint32_t)__builtin_ctz(x16[0] ? x16[0] : x16[1] ? x16[1] : x16[2] ? x16[2] : x16[3]) >> 3);
                     } else if (!far) {
                         l = lane_lcp(wc, wp, VCF_ZX_NOCAP ? (uint32_t)MAX_MATCH : Tn, 16u);
-                    } else if (!VCF_ZX_FARWAVE) {
+                    } else {
                         l = far_lcp(c, wp, VCF_ZX_NOCAP ? (uint32_t)MAX_MATCH : Tn, 16u);
                     }
                 }
-#if VCF_ZX_FARWAVE
-                // far candidates whose first 16 bytes match (72 % of the chain rounds reach
-                // past the window): one wave-wide compare each -- bytes 16 .. 271 as 64 lanes x
-                // 4 in one round trip -- instead of the lane's 16-byte steps, one round trip
-                // each up to Tn; the length is exact (capped at MAX_MATCH)
-                for (uint64_t fm = __ballot(cand && far && !(x16[0] | x16[1] | x16[2] | x16[3])); fm; fm &= fm - 1) {
-                    const uint32_t k = (uint32_t)__ffsll((unsigned long long)fm) - 1;
-                    const uint32_t lk = far_wave_lcp16(lane_val(c, k), wp);
-                    if (lane_id() == k) l = lk;
-                }
-#endif
 #if VCF_ZLIB_PROF
                 n_farlcp += (unsigned long long)__popcll(__ballot(cand && far && !(x16[0] | x16[1] | x16[2] | x16[3])));
 #endif
@@ -1643,6 +1618,7 @@ __global__ __launch_bounds__(64) VCF_ZX_WPE_ATTR void zlib_parse_kernel(const ui
     for (uint32_t i = lane; i < (uint32_t)kStgWords; i += 64) sm.stg[i] = 0;
     Wave<LAZY> wv(sm, S.src, S.n, S.ws, (uint32_t)cfg.good, reinterpret_cast<uint32_t *>(out + s * slot_bytes),
                   (uint32_t)(slot_bytes >> 2));
+    wv.lazy = (uint32_t)cfg.lazy;
     if constexpr (LAZY) {
         // the window's first kLazyWin bytes: the strip, then zeros (fill_window's high_water zeroing)
         uint8_t *win = reinterpret_cast<uint8_t *>(sh.win32);
