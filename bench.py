@@ -250,7 +250,7 @@ def c4_cpu_baseline(budget_s: float, Q: int, files=None) -> dict:
                        f"{el1:.1f} s"),
             "threads": {"value": round(n_par * H * W / elp / 1e6, 2), "unit": "Mpixels/s", "cores": threads,
                         "sample": f"{n_par} frames of the sequence on a {threads}-thread pool, {elp:.1f} s"},
-            "host": f"{model}; usable cores {avail}",
+            "host": f"{model}; {threads} threads used (os.cpu_count()={ncpu})",
             "files_equal_gpu": agree}
 
 
@@ -305,7 +305,7 @@ def c5_cpu_baseline(budget_s: float, Q: int, base, H: int, W: int, G: int, files
                         "cores": min(threads, n_gops),
                         "sample": (f"the first {per} frames of each of the {n_gops} GOPs, one GOP per thread "
                                    f"(GOPs are independent; frames in a GOP are serial), {elp:.1f} s")},
-            "host": f"{model}; usable cores {avail}",
+            "host": f"{model}; {min(threads, n_gops)} threads used (os.cpu_count()={ncpu})",
             "files_equal_gpu": agree}
 
 

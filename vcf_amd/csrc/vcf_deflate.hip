@@ -41,6 +41,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 
 #include "vcf_amd.h"
 #include "vcf_deflate.h"
@@ -199,10 +200,20 @@ __device__ __forceinline__ uint32_t lane_val(uint32_t v, uint32_t l)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)uni(l));
 }
+// The parse kernels' workgroups hold VCF_ZX_WG waves, one strip each, every wave with
+// its own LDS section and no data shared between them: a wave's LDS writes and reads
+// need only the ordering of its own instructions (the LDS serves one wave's DS
+// instructions in order) and the fence's wait counts -- no workgroup barrier, which
+// would tie the waves' independent control flows together.
+#ifndef VCF_ZX_WG   // A/B (diagnostic builds): strips (waves) per parse workgroup
+#define VCF_ZX_WG 1
+#endif
+constexpr int kParseWG = VCF_ZX_WG;
 __device__ __forceinline__ void wave_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_s_barrier();
+    if (kParseWG == 1) __builtin_amdgcn_s_barrier();
+    else __builtin_amdgcn_wave_barrier();
 }
 __device__ __forceinline__ uint32_t excl_scan(uint32_t v, uint32_t &total)
 {
@@ -818,6 +829,12 @@ static_assert(offsetof(ParseSmem, lfreq) % 4 == 0, "packed adds into lfreq");
 #define VCF_ZX_LAZYWIN 3840
 #endif
 constexpr uint32_t kLazyWin = VCF_ZX_LAZYWIN;
+#ifndef VCF_ZX_LWIN   // A/B (diagnostic builds): positions per lazy hd[] / idx[] register window (512 or 256)
+#define VCF_ZX_LWIN 512
+#endif
+constexpr uint32_t kLWin = VCF_ZX_LWIN;
+static_assert(kLWin == 512 || kLWin == 256, "lazy windows of 512 or 256 positions");
+using LVec = std::conditional_t<kLWin == 512, uint4, uint2>;
 constexpr uint32_t kLazyAhead = 320;
 // the near distance the window keeps behind p after a shift: candidates at most
 // this far back read the window, farther ones (zlib reaches MAX_DIST back) read
@@ -918,20 +935,41 @@ struct Wave {
         return *a;
 #endif
     }
+    // VCF_ZX_LWIN = 256 (A/B): the lazy windows of hd[] / idx[] as 256 positions, 4 per lane in
+    // a uint2 (8 fewer VGPRs than 512 in uint4s: room for more waves per SIMD)
+    LVec lhv, liv, lhv_n, liv_n;
+    __device__ __forceinline__ static LVec wloadL(const uint16_t *a)
+    {
+#if VCF_ZX_LWIN == 512
+        return wload4(a);
+#else
+        return *reinterpret_cast<const uint2 *>(a);
+#endif
+    }
+    __device__ __forceinline__ static uint32_t pickL(const LVec &v, uint32_t l, uint32_t d)   // dword d of lane l
+    {
+#if VCF_ZX_LWIN == 512
+        return pick4(v, l, d);
+#else
+        const uint32_t a = lane_val(v.x, l), b = lane_val(v.y, l);
+        return d == 0 ? a : b;
+#endif
+    }
     __device__ __forceinline__ void lazy_windows(uint32_t p)
     {
-        if (p - base < 512u) return;
-        const uint32_t nb = p & ~511u;
-        if (nb == base + 512u) {
-            hv = hv_n;
-            iv = iv_n;
+        constexpr uint32_t per = kLWin / 64;   // positions per lane
+        if (p - base < kLWin) return;
+        const uint32_t nb = p & ~(kLWin - 1);
+        if (nb == base + kLWin) {
+            lhv = lhv_n;
+            liv = liv_n;
         } else {
-            hv = wload4(hd + nb + 8 * lane_id());
-            iv = wload4(idx + nb + 8 * lane_id());
+            lhv = wloadL(hd + nb + per * lane_id());
+            liv = wloadL(idx + nb + per * lane_id());
         }
         base = ibase = nb;
-        hv_n = wload4(hd + nb + 512 + 8 * lane_id());
-        iv_n = wload4(idx + nb + 512 + 8 * lane_id());
+        lhv_n = wloadL(hd + nb + kLWin + per * lane_id());
+        liv_n = wloadL(idx + nb + kLWin + per * lane_id());
     }
     __device__ __forceinline__ void window(uint32_t p)
     {
@@ -1049,6 +1087,11 @@ struct Wave {
     __device__ __forceinline__ uint32_t head(uint32_t p)
     {
         window(p);
+        if constexpr (LAZY) {
+            constexpr uint32_t per = kLWin / 64;
+            const uint32_t off = p - base, l = off / per, e = off % per;
+            return (pickL(lhv, l, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
+        }
         const uint32_t off = p - base, l = off >> 3, e = off & 7;
         const uint32_t w = pick4(hv, l, e >> 1);
         return (w >> ((e & 1) * 16)) & 0xffffu;
@@ -1220,10 +1263,11 @@ struct Wave {
     }
     __device__ __forceinline__ uint32_t idx_known(uint32_t q)   // idx[q] from the windows, or ~0 if outside them
     {
+        constexpr uint32_t per = kLWin / 64;
         const uint32_t off = q - ibase;
-        if (off >= 1024u) return 0xffffffffu;
-        const uint32_t o = off & 511u, e = o & 7;
-        return (pick4(off < 512u ? iv : iv_n, o >> 3, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
+        if (off >= 2 * kLWin) return 0xffffffffu;
+        const uint32_t o = off & (kLWin - 1), e = o % per;
+        return (pickL(off < kLWin ? liv : liv_n, o / per, e >> 1) >> ((e & 1) * 16)) & 0xffffu;
     }
     // VCF_ZX_PREDICT (A/B): the position deflate_slow calls longest_match at next follows
     // from this call's result and prev_length: with match_length ml (this call's length,
@@ -1254,9 +1298,11 @@ struct Wave {
         const uint32_t ia = idx_known(qa);
         pfa_p = ia != 0xffffffffu && qa + MIN_MATCH <= n ? qa : 0xffffffffu;
         if (pfa_p != 0xffffffffu) fetch_cands(ia, pfa0, pfa1);
-        const uint32_t ib = qb != qa ? idx_known(qb) : 0xffffffffu;
-        pfb_p = ib != 0xffffffffu && qb + MIN_MATCH <= n ? qb : 0xffffffffu;
-        if (pfb_p != 0xffffffffu) fetch_cands(ib, pfb0, pfb1);
+        if constexpr (VCF_ZX_PREDICT != 1) {   // (1: one exact slot; b unused)
+            const uint32_t ib = qb != qa ? idx_known(qb) : 0xffffffffu;
+            pfb_p = ib != 0xffffffffu && qb + MIN_MATCH <= n ? qb : 0xffffffffu;
+            if (pfb_p != 0xffffffffu) fetch_cands(ib, pfb0, pfb1);
+        }
     }
     __device__ __forceinline__ bool longest_impl(uint32_t p, uint32_t hdp, uint32_t prev_len, uint32_t chain,
                                                  uint32_t nice, uint32_t limit, uint32_t &len, uint32_t &pos)
@@ -1584,7 +1630,7 @@ struct ParseShared<true> {
     uint32_t pad[VCF_ZX_LDSPAD / 4];
 #endif
 };
-static_assert(VCF_ZX_LDSPAD || VCF_ZX_LAZYWIN != 3840 || sizeof(ParseShared<true>) <= 10240,
+static_assert(VCF_ZX_LDSPAD || VCF_ZX_LAZYWIN != 3840 || VCF_ZX_WG != 1 || sizeof(ParseShared<true>) <= 10240,
               "sixteen lazy-parse workgroups per CU");
 
 #ifdef VCF_ZX_WPE   // A/B (diagnostic builds): registers capped for this many waves per SIMD
@@ -1593,15 +1639,17 @@ static_assert(VCF_ZX_LDSPAD || VCF_ZX_LAZYWIN != 3840 || sizeof(ParseShared<true
 #define VCF_ZX_WPE_ATTR
 #endif
 template <bool LAZY>
-__global__ __launch_bounds__(64) VCF_ZX_WPE_ATTR void zlib_parse_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
-                                                       int32_t strip_bytes, int32_t spf, int32_t level,
-                                                       uint8_t *__restrict__ out, int64_t slot_bytes,
-                                                       int32_t *__restrict__ sizes, uint8_t *__restrict__ ws,
-                                                       int64_t s0)
+__global__ __launch_bounds__(64 * kParseWG) VCF_ZX_WPE_ATTR void zlib_parse_kernel(
+    const uint8_t *__restrict__ in, int64_t frame_bytes, int32_t strip_bytes, int32_t spf, int32_t level,
+    uint8_t *__restrict__ out, int64_t slot_bytes, int32_t *__restrict__ sizes, uint8_t *__restrict__ ws, int64_t s0,
+    int64_t s_end)
 {
-    __shared__ __attribute__((aligned(16))) ParseShared<LAZY> sh;
+    __shared__ __attribute__((aligned(16))) ParseShared<LAZY> shs[kParseWG];
+    const int wv_id = kParseWG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    ParseShared<LAZY> &sh = shs[wv_id];
     ParseSmem &sm = sh.sm;
-    const int64_t s = s0 + blockIdx.x;
+    const int64_t s = s0 + (int64_t)blockIdx.x * kParseWG + wv_id;
+    if (s >= s_end) return;
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s);
     if (strip_lazy(S) != LAZY) return;   // the other kernel codes this strip
     const uint32_t lane = lane_id();
@@ -1815,13 +1863,15 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
             rc = hip_check(hipGetLastError(), "zlib_chain_kernel launch");
         }
         if (rc == VCF_OK) {
-            hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3(cnt), dim3(64), 0, ss, in_dev, frame_bytes,
-                               strip_bytes, (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
+            hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(64 * kParseWG),
+                               0, ss, in_dev, frame_bytes, strip_bytes, (int32_t)spf, level, out_dev, slot_bytes,
+                               sizes_dev, ws, s0, s0 + (int64_t)cnt);
             rc = hip_check(hipGetLastError(), "zlib_parse_kernel launch");
         }
         if (rc == VCF_OK) {
-            hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3(cnt), dim3(64), 0, ms, in_dev, frame_bytes, strip_bytes,
-                               (int32_t)spf, level, out_dev, slot_bytes, sizes_dev, ws, s0);
+            hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(64 * kParseWG),
+                               0, ms, in_dev, frame_bytes, strip_bytes, (int32_t)spf, level, out_dev, slot_bytes,
+                               sizes_dev, ws, s0, s0 + (int64_t)cnt);
             rc = hip_check(hipGetLastError(), "zlib_parse_kernel (lazy) launch");
         }
         // join the side stream even after an error, so the caller's stream never runs ahead
