@@ -25,7 +25,8 @@ SOURCES = ["vcf_runtime.hip", "vcf_dct_dz.hip", "vcf_dct_any.hip", "vcf_quant.hi
            "vcf_png.cpp", "vcf_comm.cpp", "vcf_cbaac_gpu.hip", "vcf_plugins.hip", "vcf_deflate.hip",
            "vcf_inflate.hip"]
 HEADERS = ["vcf_dct8.h", "vcf_dct_block.h", "vcf_internal.h", "vcf_wavelets.h", "vcf_pocketfft.h", "vcf_pocketfft_tables.h",
-           "vcf_pocketfft_rt.h", "vcf_pocketfft_blue.h", "vcf_sincos.h", "vcf_pipeline.h", "vcf_dwt_band.h", "vcf_idwt_line.h", "vcf_dwt_lift.h",
+           "vcf_pocketfft_rt.h", "vcf_pocketfft_blue.h", "vcf_sincos.h", "vcf_pipeline.h", "vcf_dwt_band.h", "vcf_idwt_line.h", "vcf_idwt_band21.h",
+           "vcf_dwt_lift.h",
            "vcf_deflate.h"]
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("VCF_OFFLOAD_ARCH", "gfx950")

@@ -172,6 +172,11 @@ __device__ unsigned int g_zdbg[8];
 // bytes: C4 deflate 102.3 -> 97.2 ms, ABBA, profiles/r06_zab_v2.json)
 #define VCF_ZX_EARLY0 0
 #endif
+#ifndef VCF_ZX_HEAD1   // A/B (diagnostic builds): hd[] from K1's third pass instead of the head kernel
+// (round 6: 1 -- the bucket bounds from K1's counters replace the head kernel's byte gathers
+// and its launch: C4 deflate 93.7 -> 84.8 ms, ABBA, profiles/r06_zab_v6.json)
+#define VCF_ZX_HEAD1 1
+#endif
 #ifndef VCF_ZX_PREDICT   // A/B (diagnostic builds): prefetch the exactly predicted next call position
 // (round 6: 1 -- 70 % -> 93 % of the calls find their candidates prefetched; C4 deflate
 // 101.3 -> 95.3 ms, ABBA, profiles/r06_zab_v3.json; 2: also p + 1, 98.4 ms)
@@ -470,6 +475,54 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
         sm.distinct[w] = distinct;
     }
     __syncthreads();
+#if VCF_ZX_HEAD1
+    // pass 3 (the head kernel's work): hd[p] = sorted[idx[p] - 1], the bucket's previous
+    // slot, unless p is its bucket's first position (NIL).  After the scatter every
+    // counter holds its bucket's end, so bucket h starts where bucket h - 1 ends: no byte
+    // gathers to compare the previous slot's hash with p's.  4 consecutive positions per
+    // thread and step, their bytes as two dwords, idx as one 8-byte load.
+    {
+        uint16_t *hdw = reinterpret_cast<uint16_t *>(S.ws + kHdOff);
+        auto start_of = [&](uint32_t hh) -> uint32_t {
+            return hh ? (sm.cnt[(hh - 1) >> 1] >> (((hh - 1) & 1) * 16)) & 0xffffu : 0u;
+        };
+        for (uint32_t p0 = 4 * tid; p0 < np; p0 += 4 * NT) {
+            uint32_t d0, d1;
+            if (al4 && p0 + 8 <= n) {
+                d0 = *reinterpret_cast<const uint32_t *>(S.src + p0);
+                d1 = *reinterpret_cast<const uint32_t *>(S.src + p0 + 4);
+            } else {
+                d0 = d1 = 0;
+                for (uint32_t i = 0; i < 8; ++i)
+                    if (p0 + i < n) (i < 4 ? d0 : d1) |= (uint32_t)S.src[p0 + i] << (8 * (i & 3));
+            }
+            const uint64_t bb = (uint64_t)d1 << 32 | d0;
+            const bool full = p0 + 4 <= np;
+            uint32_t sl[4];
+            if (full) {
+                const uint2 iv = *reinterpret_cast<const uint2 *>(idx + p0);
+                sl[0] = iv.x & 0xffffu; sl[1] = iv.x >> 16; sl[2] = iv.y & 0xffffu; sl[3] = iv.y >> 16;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) sl[u] = p0 + u < np ? (uint32_t)idx[p0 + u] : 0u;
+            }
+            uint32_t r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t hh = hash3((uint32_t)(bb >> (8 * u)) & 0xffu, (uint32_t)(bb >> (8 * u + 8)) & 0xffu,
+                                          (uint32_t)(bb >> (8 * u + 16)) & 0xffu);
+                r[u] = sl[u] > start_of(hh) ? (uint32_t)sorted[sl[u] - 1] : 0u;
+            }
+            if (full && (p0 & 3) == 0) {
+                *reinterpret_cast<uint2 *>(hdw + p0) = make_uint2(r[0] | r[1] << 16, r[2] | r[3] << 16);
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (p0 + u < np) hdw[p0 + u] = (uint16_t)r[u];
+            }
+        }
+    }
+#endif
     if (tid == 0) {
         uint64_t a = 0, b = 0;
         uint32_t dsum = 0;
@@ -830,7 +883,9 @@ static_assert(offsetof(ParseSmem, lfreq) % 4 == 0, "packed adds into lfreq");
 #endif
 constexpr uint32_t kLazyWin = VCF_ZX_LAZYWIN;
 #ifndef VCF_ZX_LWIN   // A/B (diagnostic builds): positions per lazy hd[] / idx[] register window (512 or 256)
-#define VCF_ZX_LWIN 512
+// (round 6: 256 -- uint2 windows, two readlanes per lookup instead of four, 8 fewer VGPRs:
+// C4 deflate 95.5 -> 89.5 ms, ABBA, profiles/r06_zab_v5.json)
+#define VCF_ZX_LWIN 256
 #endif
 constexpr uint32_t kLWin = VCF_ZX_LWIN;
 static_assert(kLWin == 512 || kLWin == 256, "lazy windows of 512 or 256 positions");
@@ -1846,10 +1901,12 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
                            (int32_t)spf, ws, s0);
         int rc = hip_check(hipGetLastError(), "zlib_order_kernel launch");
         if (rc != VCF_OK) return rc;
-        hipLaunchKernelGGL(zlib_head_kernel, dim3(hd_blocks, cnt), dim3(kHdThreads), 0, ms, in_dev, frame_bytes,
-                           strip_bytes, (int32_t)spf, ws, s0);
-        rc = hip_check(hipGetLastError(), "zlib_head_kernel launch");
-        if (rc != VCF_OK) return rc;
+        if (!VCF_ZX_HEAD1) {   // (VCF_ZX_HEAD1: K1's third pass writes hd[])
+            hipLaunchKernelGGL(zlib_head_kernel, dim3(hd_blocks, cnt), dim3(kHdThreads), 0, ms, in_dev, frame_bytes,
+                               strip_bytes, (int32_t)spf, ws, s0);
+            rc = hip_check(hipGetLastError(), "zlib_head_kernel launch");
+            if (rc != VCF_OK) return rc;
+        }
         if (ss != ms) {
             if ((rc = hip_check(hipEventRecord(ax.big[0], ms), "hipEventRecord")) != VCF_OK) return rc;
             if ((rc = hip_check(hipStreamWaitEvent(ss, ax.big[0], 0), "hipStreamWaitEvent")) != VCF_OK) return rc;

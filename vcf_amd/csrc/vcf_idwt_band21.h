@@ -33,6 +33,9 @@
 constexpr int kB21C = 60;            // owned level-1 subband columns per tile (64 lanes, 2 halo each side)
 constexpr int kB21S2 = 36;           // staged level-2 subband columns per row
 constexpr int kB21NT = 192;          // one wave per YCoCg channel
+#ifndef VCF_B21_SPLIT   // (A/B) the level-1 row pass's two halves kept apart: fewer live VGPRs
+#define VCF_B21_SPLIT 1
+#endif
 
 template <bool FROM_PACKED_LL2, unsigned ZLO, unsigned ZHI, int CT, bool QS>
 __global__ __launch_bounds__(kB21NT) void idwt_band21_kernel(
@@ -218,18 +221,19 @@ __global__ __launch_bounds__(kB21NT) void idwt_band21_kernel(
             // level-1 row pass of row r
             {
                 const double *S = &s1[t & 1][ch][0][lc - 2];
-                double xl[5], xh[5], yl[5], yh[5];
 #pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    xl[j] = S[4 - j];
-                    xh[j] = S[64 + 4 - j];
-                    yl[j] = S[2 * 64 + 4 - j];
-                    yh[j] = S[3 * 64 + 4 - j];
+                for (int half = 0; half < 2; ++half) {   // 'a' (LL, HL), then 'd' (LH, HH)
+                    double x[5], y[5];
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) {
+                        x[j] = S[2 * half * 64 + 4 - j];
+                        y[j] = S[(2 * half + 1) * 64 + 4 - j];
+                    }
+                    double(&o)[5][2] = half ? wd : wa;
+                    o[u][0] = inv_pair<ZLO, ZHI, CT, 0>(x, y);
+                    o[u][1] = inv_pair<ZLO, ZHI, CT, 1>(x, y);
+                    if (VCF_B21_SPLIT) asm volatile("" ::: "memory");   // the 'd' loads after the 'a' sums
                 }
-                wa[u][0] = inv_pair<ZLO, ZHI, CT, 0>(xl, xh);
-                wa[u][1] = inv_pair<ZLO, ZHI, CT, 1>(xl, xh);
-                wd[u][0] = inv_pair<ZLO, ZHI, CT, 0>(yl, yh);
-                wd[u][1] = inv_pair<ZLO, ZHI, CT, 1>(yl, yh);
             }
             // level-1 column pass: output pair m = r - 2 from rows r - 4 .. r
             if (t >= 4) {
