@@ -1,4 +1,4 @@
-"""Per-phase clock totals of the GPU deflate's parse kernels (diagnostic build
+"""Per-phase clock totals of the GPU deflate's parse kernels and K1 (zlib_sort_kernel) (diagnostic build
 scripts/libvcf_zprof.so, VCF_ZLIB_PROF): one vcf_zlib_strips call over the C4
 workload, then the counters.  Prints one JSON line."""
 import ctypes, json, os, sys
@@ -24,7 +24,7 @@ fb = flat.shape[1]; _, _, sb = strip_layout(frames.shape[1:], 1)
 spf = int(L.lib().vcf_zlib_strip_count(fb, sb)); total = spf * n; slot = int(L.lib().vcf_zlib_bound(sb))
 d = DeviceBuffer.from_array(flat); out = DeviceBuffer(total * slot); sizes = DeviceBuffer(total * 4)
 ws = DeviceBuffer(int(P.vcf_zlib_workspace(total))); st = Stream()
-buf = (ctypes.c_ulonglong * 24)()
+buf = (ctypes.c_ulonglong * 48)()
 for rep in range(2):
     P.vcf_zlib_prof_read(buf, 1)
     e0, e1 = Event(), Event()
@@ -48,4 +48,6 @@ print(json.dumps({"frames": n, "strips": total, "ms": round(e0.elapsed_ms(e1), 2
                   "head_hit_frac": v[16] / max(1, v[3]), "far_round_frac": v[17] / max(1, v[4]),
                   "far_lcp_lanes_per_round": v[18] / max(1, v[4]), "far_final_compare_per_call": v[19] / max(1, v[3]),
                   "far_head_frac": v[20] / max(1, v[3]), "no_match_frac": v[21] / max(1, v[3]),
+                  "sort_workgroups": v[47], **{f"sort_{nm}_cycles": v[40 + i] // max(1, v[47]) for i, nm in enumerate(
+                      ("count1", "scan1", "place1", "scan2", "place2", "firsts"))},
                   "lib": os.environ.get("ZPROF_LIB", "libvcf_zprof.so")}), flush=True)

@@ -5,14 +5,14 @@
 //
 // zlib's serial loop is split where its data dependences allow (DESIGN.md
 // §4.9; the restatement and its proofs of equivalence are vcf_deflate.h):
-//   K1 zlib_order_kernel, one wave per strip: the positions 0..n-3 bucketed
-//      by zlib's hash, stably (histogram, scan, ordered scatter 64 positions
-//      at a time with an exact same-hash lane mask; 32768 counters in LDS).
-//      zlib inserts every position, in order, and a position's hash depends
-//      on its 3 bytes only, so the hash chains do not depend on the parse:
-//      the chain of p is the earlier positions of p's bucket, newest first
-//      -- contiguous in sorted[].  A second ordered pass writes hd[p], the
-//      chain's head (zlib's head[] as p is inserted).  Also the adler32 sums.
+//   K1 zlib_sort_kernel, eight waves per strip: the positions 0..n-3 sorted
+//      by zlib's hash, stably (two counting passes over 8 + 7 hash bits, the
+//      strip's tiles split between the waves).  zlib inserts every position,
+//      in order, and a position's hash depends on its 3 bytes only, so the
+//      hash chains do not depend on the parse: the chain of p is the earlier
+//      positions of p's bucket, newest first -- contiguous in sorted[].  Also
+//      hd[p], the chain's head (zlib's head[] as p is inserted), and the
+//      adler32 sums.
 //   K2 zlib_match_kernel, 16 consecutive positions per thread, 4096 per
 //      workgroup: longest_match at p for both chain limits deflate_slow can
 //      use (max_chain, and max_chain >> 2 once prev_length >= good_match).
@@ -68,7 +68,9 @@ constexpr int64_t kListOff = kHdOff + (int64_t)MAX_STRIP * 2;
 constexpr int64_t kRfOff = kListOff + (int64_t)MAX_STRIP * 2;
 constexpr int64_t kRrOff = kRfOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSymOff = kRrOff + (int64_t)MAX_STRIP * 4;
-constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;   // adler sums (2 x u64), worklist length (u32)
+// adler sums (2 x u64), K2's worklist length, the parse order (lazy or not), K1's distinct-hash
+// count, the lazy parse's dispatch order (u32 each)
+constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;
 constexpr int64_t kWsPerStrip = kSumOff + 32;
 // Rounds: the strips of a call are processed in rounds whose workspace stays
 // under the budget, one round after the other on the caller's stream.  Every
@@ -112,7 +114,7 @@ inline int64_t ws_budget()
     return dflt[dev];
 }
 // A call's strips in rounds of `per` strips (at most 65535: the y grid dimension of
-// the head and K2a launches), the workspace of one round within the budget.
+// the K2a launch), the workspace of one round within the budget.
 struct ZRounds {
     int64_t rounds, per;
     explicit ZRounds(int64_t total)
@@ -172,11 +174,6 @@ __device__ unsigned int g_zdbg[8];
 // bytes: C4 deflate 102.3 -> 97.2 ms, ABBA, profiles/r06_zab_v2.json)
 #define VCF_ZX_EARLY0 0
 #endif
-#ifndef VCF_ZX_HEAD1   // A/B (diagnostic builds): hd[] from K1's third pass instead of the head kernel
-// (round 6: 1 -- the bucket bounds from K1's counters replace the head kernel's byte gathers
-// and its launch: C4 deflate 93.7 -> 84.8 ms, ABBA, profiles/r06_zab_v6.json)
-#define VCF_ZX_HEAD1 1
-#endif
 #ifndef VCF_ZX_PREDICT   // A/B (diagnostic builds): prefetch the exactly predicted next call position
 // (round 6: 1 -- 70 % -> 93 % of the calls find their candidates prefetched; C4 deflate
 // 101.3 -> 95.3 ms, ABBA, profiles/r06_zab_v3.json; 2: also p + 1, 98.4 ms)
@@ -195,7 +192,9 @@ __device__ unsigned int g_zdbg[8];
 // lengths, the rest (rounds that end the call with a hit excluded from [15])
 // [16] calls ending at the head compare, [17] chain rounds holding a far lane, [18] lanes entering
 // far_lcp, [19] far wave_lcp_at calls, [20] calls whose chain head is far, [21] calls finding nothing
-__device__ unsigned long long g_zprof[24];
+// [40..45] K1's phases (thread 0's clock at the barriers): pass-1 counts, scan, pass-1
+// placement, scan, pass-2 placement, the tiles' first elements; [47] K1 workgroups
+__device__ unsigned long long g_zprof[48];
 #define VCF_ZPROF_COUNT(x) (++(x))
 #else
 #define VCF_ZPROF_COUNT(x) ((void)0)
@@ -280,194 +279,267 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c)   
     return (a << 10 ^ b << 5 ^ c) & 0x7fffu;
 }
 
-// kK1Waves waves per strip, sharing the 32768 bucket counters in LDS; each
-// staged chunk's hashes are computed once into LDS.  Pass 1: the hash histogram
-// (and the adler32 sums), all waves.  Scan: wave w owns the buckets with
-// hash >> 12 == w (an eighth of the hash space) and scans them
-// from the total of the lower parts.  Pass 2, the ordered scatter: every
-// wave walks all positions (the chunk is staged once per workgroup) but acts on
-// its own part's only, so the waves never share a bucket and each keeps
-// zlib's order inside its buckets without any ordering between waves.  Per 256
-// positions (four 64-lane sub-groups): within a sub-group the same-hash lane
-// masks give each position its rank, the first lane of each hash (the leader)
-// adds the sub-group's count to the bucket cursor with one LDS atomic returning
-// the old cursor -- the four sub-groups' atomics issue back to back and execute
-// in order, so a later sub-group sees an earlier one's update -- and the other
-// lanes take the leader's old cursor by ds_bpermute.  hd[] (zlib's head[] as p
-// is inserted) is zlib_head_kernel's: every position in parallel from
-// sorted[idx[p]-1].
-#ifndef VCF_ZX_K1WAVES   // A/B (diagnostic builds): K1's waves per strip
-#define VCF_ZX_K1WAVES 8
-#endif
-constexpr int kK1Waves = VCF_ZX_K1WAVES, kK1Stage = 4 * 64 * kK1Waves;   // one dword of a chunk per thread
-struct OrderSmem4 {
-    uint32_t cnt[1 << 14];              // 32768 u16 counters / cursors, packed in pairs
-    uint8_t stage[kK1Stage + 64];
-    uint16_t hsh[kK1Stage];             // the chunk's hashes, computed once per chunk
-    uint32_t qtot[kK1Waves];
-    uint64_t sums[kK1Waves][2];
-    uint32_t distinct[kK1Waves];
+// Round 6 form: the hash order by a two-pass LSD radix sort.  Round 5's K1 built
+// the order with 32768 bucket counters in LDS and an ordered scatter in which each
+// wave owned an eighth of the hash space -- and repetitive content puts most
+// positions' hashes in one wave's part: that wave acted on ~250 of the strip's 256
+// groups while the others waited at each chunk's barrier (K1 27 ms of a C4 call, 80 %
+// of it in the scatter; a separate pass then wrote hd[]).  Sorting the positions by hash with two
+// stable counting passes over 8 + 7 hash bits instead splits the work by position:
+// the strip's tiles of 2048 positions go to the eight waves in turn, a tile's digit
+// counts are known before it is placed, the per-(tile, digit) cursors come from one
+// column scan, and each wave then places its tiles' positions with no exchange
+// between waves.  Inside a tile a group of 64 positions takes its ranks from
+// same-digit lane masks built from one ballot per digit bit (bits equal on every
+// lane skipped) and the tile's cursors in LDS, read by every lane and advanced by
+// each digit's first lane -- the LDS serves one wave's instructions in order.
+//   pass 1 (low 8 bits): the tile's bytes staged in LDS (all its loads in flight);
+//     the digit counts, then hash << 16 | position to the K2 result area rf[] (K2
+//     writes it only after this kernel) in digit order -- and each position's
+//     pass-2 (tile, digit) counted at its new slot, so pass 2 needs no count pass;
+//   pass 2 (high 7 bits) reads rf[] in that order, which keeps equal hashes in
+//     position order, and writes sorted[] and idx[].  The element before a
+//     position in the final order -- its bucket predecessor when the hashes match:
+//     zlib's head[] as p is inserted, hd[p] -- is the lane below it with the same
+//     digit, or for a digit's first lane the digit's last element of the tile's
+//     earlier groups (a per-wave LDS row); a digit's first element in a tile is
+//     completed after the pass from sorted[] and the strip bytes.
+// hd[] also gives each 64-position group's distinct hashes (the lazy-parse test): a
+// position is its hash's first in the group unless its bucket predecessor lies in it.
+constexpr int kSortWaves = 8;
+constexpr uint32_t kSortT = 2048;                  // positions per tile (both passes)
+constexpr uint32_t kSortTiles = MAX_STRIP / kSortT;
+constexpr uint32_t kSortH = 1024;                  // pass 1 stages a tile in halves
+constexpr uint32_t kSortStg = kSortH / 4 + 4;      // a wave's staged half tile, dwords (+ the 2 bytes after it)
+struct SortSmem {
+    uint32_t tab1[kSortTiles * 256 / 2];   // pass 1: u16 [t * 256 + d], digit d's count, then cursor, in tile t
+    uint32_t tab2[kSortTiles * 128 / 2];   // pass 2: u16 [t * 128 + d]
+    uint32_t stg[kSortWaves][kSortStg];    // pass 1: the wave's half tile of strip bytes; pass 2: its last key per digit
+    uint32_t dsum[kSortWaves];
+    uint64_t sums[kSortWaves][2];
+    uint32_t distinct[kSortWaves];
 };
-
-__global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t *__restrict__ in,
-                                                                  int64_t frame_bytes, int32_t strip_bytes,
-                                                                  int32_t spf, uint8_t *__restrict__ ws, int64_t s0)
+// the valid lanes whose digit equals this lane's: one ballot per digit bit, the bits
+// equal on every valid lane skipped (a scalar branch)
+template <int BITS>
+__device__ __forceinline__ uint64_t digit_mask(uint32_t d, bool valid)
 {
-    __shared__ __attribute__((aligned(16))) OrderSmem4 sm;
+    const uint64_t vm = __ballot(valid);
+    uint64_t m = vm;
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+        const uint32_t bit = (d >> b) & 1u;
+        const uint64_t B = __ballot(valid && bit);
+        if (B == 0 || B == vm) continue;
+        m &= ~(B ^ (bit ? ~0ull : 0ull));
+    }
+    return valid ? m : 0ull;
+}
+// a group's counts into the u16 table entries a: a run of one entry over consecutive
+// lanes (runs of one byte value) adds its length with one atomic from its first lane;
+// the valid lanes are a prefix
+__device__ __forceinline__ void tile_count(uint32_t *tab, uint32_t a, bool valid, uint32_t lane)
+{
+    const uint32_t aprev = (uint32_t)__shfl_up((int)a, 1, 64);
+    const bool head = valid && (lane == 0 || aprev != a);
+    const uint64_t heads = __ballot(head), vmask = __ballot(valid);
+    if (head) {
+        const uint64_t above = heads & ~((2ull << lane) - 1);
+        const uint32_t end = above ? (uint32_t)__ffsll((unsigned long long)above) - 1 : (uint32_t)__popcll(vmask);
+        atomicAdd(&tab[a >> 1], (end - lane) << ((a & 1) * 16));
+    }
+}
+// counts -> cursors: per digit (one thread each) the exclusive prefix over the tiles,
+// plus the digit's start (the exclusive prefix of the digit totals)
+template <uint32_t D>
+__device__ __forceinline__ void tile_scan(SortSmem &sm, uint16_t *tab16, uint32_t ntiles, uint32_t tid, uint32_t w,
+                                          uint32_t lane)
+{
+    uint32_t tot = 0;
+    if (tid < D)
+        for (uint32_t t = 0; t < ntiles; ++t) {
+            const uint32_t x = tab16[t * D + tid];
+            tab16[t * D + tid] = (uint16_t)tot;
+            tot += x;
+        }
+    uint32_t wsum;
+    uint32_t ex = excl_scan(tot, wsum);
+    if (lane == 0) sm.dsum[w] = wsum;
+    __syncthreads();
+    if (tid < D) {
+        for (uint32_t v = 0; v < w; ++v) ex += sm.dsum[v];
+        for (uint32_t t = 0; t < ntiles; ++t) tab16[t * D + tid] = (uint16_t)(tab16[t * D + tid] + ex);
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(64 * kSortWaves) void zlib_sort_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+                                                                   int32_t strip_bytes, int32_t spf,
+                                                                   uint8_t *__restrict__ ws, int64_t s0)
+{
+    __shared__ __attribute__((aligned(16))) SortSmem sm;
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s0 + blockIdx.x);
     uint16_t *idx = reinterpret_cast<uint16_t *>(S.ws + kIdxOff);
     uint16_t *sorted = reinterpret_cast<uint16_t *>(S.ws + kSortOff);
+    uint16_t *hd = reinterpret_cast<uint16_t *>(S.ws + kHdOff);
+    uint32_t *tmp = reinterpret_cast<uint32_t *>(S.ws + kRfOff);
+    uint16_t *tab1 = reinterpret_cast<uint16_t *>(sm.tab1), *tab2 = reinterpret_cast<uint16_t *>(sm.tab2);
+    constexpr uint32_t NT = 64 * kSortWaves;
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6, n = S.n;
-    constexpr uint32_t NT = 64 * kK1Waves;
-    constexpr uint32_t kHashShiftW = kK1Waves == 8 ? 12 : kK1Waves == 4 ? 13 : 14;   // wave w: hash >> shift == w
-    static_assert(kK1Waves == 2 || kK1Waves == 4 || kK1Waves == 8, "hash space split in powers of two");
     const uint32_t np = n >= 3 ? n - 2 : 0;   // positions 0..n-3 are inserted
-    for (uint32_t i = tid; i < (1u << 14); i += NT) sm.cnt[i] = 0;
-    // chunk staging: thread t holds the 4 bytes at c0 + 4t of the chunk (thread 0
-    // also the 4 after the chunk, for the last hashes) in registers, loaded while
-    // the previous chunk was processed -- the global latency of the 64 stagings
-    // per strip overlaps the work instead of sitting between two barriers
-    static_assert(kK1Stage == 4 * NT, "one dword of the chunk per thread");
-    const bool al4 = (((uintptr_t)S.src) & 3) == 0;
-    auto fetch = [&](uint32_t c0, uint32_t &a, uint32_t &x) {
-        const uint32_t q = c0 + 4 * tid;
-        auto dw = [&](uint32_t P) -> uint32_t {
-            if (al4 && P + 4 <= n) return *reinterpret_cast<const uint32_t *>(S.src + P);
-            uint32_t v = 0;
-            for (uint32_t i = 0; i < 4; ++i) v |= (P + i < n ? (uint32_t)S.src[P + i] : 0u) << (8 * i);
-            return v;
-        };
-        a = q < n ? dw(q) : 0u;
-        x = tid == 0 && c0 + kK1Stage < n ? dw(c0 + kK1Stage) : 0u;
-    };
-    uint32_t pa = 0, px = 0;
-    auto stage = [&](uint32_t c0, uint32_t next) {
-        __syncthreads();
-        reinterpret_cast<uint32_t *>(sm.stage)[tid] = pa;
-        if (tid == 0) reinterpret_cast<uint32_t *>(sm.stage)[NT] = px;
-        if (next < n) fetch(next, pa, px);
-        __syncthreads();
-        for (uint32_t j = tid; j < (uint32_t)kK1Stage; j += NT)
-            sm.hsh[j] = (uint16_t)hash3(sm.stage[j], sm.stage[j + 1], sm.stage[j + 2]);
-        __syncthreads();
-    };
-    fetch(0, pa, px);
-    uint64_t sb = 0, swb = 0;
-    // histogram of the hashes (and the adler32 sums).  A wave's 64 lanes are 64
-    // consecutive positions; a run of equal hashes among them (runs of one byte
-    // value: most of a DCT index strip) adds its length with one atomic from its
-    // first lane -- 64 lanes adding to one LDS word serialise (round 4's K1 spent
-    // 2.2 bank-conflict cycles per LDS instruction there)
-    for (uint32_t c0 = 0; c0 < n; c0 += kK1Stage) {
-        stage(c0, c0 + kK1Stage < n ? c0 + kK1Stage : 0u);   // pass 2 starts at chunk 0 again
-        for (uint32_t j = tid; j < (uint32_t)kK1Stage; j += NT) {
-            const uint32_t p = c0 + j, b = sm.stage[j];
-            sb += b;
-            swb += (uint64_t)(p < n ? n - p : 0u) * b;
-            const bool ins = p < np;
-            const uint32_t h = sm.hsh[j];
-            const uint32_t hprev = (uint32_t)__shfl_up((int)h, 1, 64);
-            const bool head = ins && (lane == 0 || hprev != h);
-            const uint64_t heads = __ballot(head), insm = __ballot(ins);
-            if (head) {
-                const uint64_t above = heads & ~((2ull << lane) - 1);   // the next run's first lane, if any
-                const uint32_t end = above ? (uint32_t)__ffsll((unsigned long long)above) - 1
-                                           : (uint32_t)__popcll(insm);   // inserted lanes are a prefix
-                atomicAdd(&sm.cnt[h >> 1], (end - lane) << ((h & 1) * 16));
-            }
-        }
-    }
-    __syncthreads();
-    // exclusive scan: wave w's part of the hash space (kQW words, kLW per lane), from the lower parts' total
-    constexpr uint32_t kQW = (1u << 14) / kK1Waves, kLW = kQW / 64;
-    uint32_t *qc = sm.cnt + w * kQW + lane * kLW;
-    uint32_t tsum = 0;
-    for (uint32_t i = 0; i < kLW; ++i) {
-        const uint32_t x = qc[i];
-        tsum += (x & 0xffffu) + (x >> 16);
-    }
-    uint32_t tot;
-    uint32_t run = excl_scan(tsum, tot);
-    if (lane == 0) sm.qtot[w] = tot;
-    __syncthreads();
-    for (uint32_t v = 0; v < w; ++v) run += sm.qtot[v];
-    for (uint32_t i = 0; i < kLW; ++i) {
-        const uint32_t x = qc[i];
-        const uint32_t c0 = x & 0xffffu, c1 = x >> 16;
-        qc[i] = run | ((run + c0) << 16);
-        run += c0 + c1;
-    }
-    // ordered scatter of this wave's part
-    uint32_t distinct = 0;   // over the 64-position groups: their distinct hashes in this part
     const uint64_t lt = (1ull << lane) - 1;
-    for (uint32_t c0 = 0; c0 < np; c0 += kK1Stage) {
-        stage(c0, c0 + kK1Stage < np ? c0 + kK1Stage : n);
-        for (uint32_t g = 0; g < (uint32_t)kK1Stage && c0 + g < np; g += 256) {
-            uint32_t h[4], rank[4], cntj[4], old[4];
-            uint64_t mine[4];
-            bool v[4];
+    const uint32_t nt1 = (n + kSortT - 1) / kSortT, nt2 = (np + kSortT - 1) / kSortT;
+    const uint8_t *src = S.src;
+    const bool al4 = (((uintptr_t)src) & 3) == 0;
+    const uint8_t *stg = reinterpret_cast<const uint8_t *>(sm.stg[w]);
+    uint32_t *lastk = sm.stg[w];
+#if VCF_ZLIB_PROF
+    unsigned long long ck[8];
+    int nck = 0;
+#define VCF_SORT_CLK() (ck[nck++] = clock64())
+#else
+#define VCF_SORT_CLK() ((void)0)
+#endif
+    // bytes [b0, b0 + H + 4) of the strip (zeros past n) into registers, every dword load in
+    // flight at once; then into the wave's staging area.  A wave's half tiles in order are
+    // k = 0, 1, ...: tile w + 8 (k / 2), half k % 2; the next one is fetched while the
+    // current one is processed.
+    constexpr uint32_t kSV = (kSortStg + 63) / 64;
+    auto fetch = [&](uint32_t b0, uint32_t (&v)[kSV]) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t j = g + 64 * q + lane;
-                h[q] = sm.hsh[j];
-                v[q] = c0 + j < np && (h[q] >> kHashShiftW) == w;
+        for (uint32_t k = 0; k < kSV; ++k) {
+            const uint32_t q = b0 + 4 * (lane + 64 * k);
+            if (al4 && q + 4 <= n) {
+                v[k] = *reinterpret_cast<const uint32_t *>(src + q);
+            } else {
+                v[k] = 0;
+                for (uint32_t i = 0; i < 4; ++i) v[k] |= (q + i < n ? (uint32_t)src[q + i] : 0u) << (8 * i);
             }
-            // none of the 256 positions hashes into this wave's part (runs: all but one
-            // wave skip most groups)
-            if (!__ballot(v[0] || v[1] || v[2] || v[3])) continue;
-            // all 256 positions in this part with one hash (inside a run of one byte
-            // value): their slots are the bucket cursor + 0..255, one atomic
-            const uint32_t h0 = uni(h[0]);
-            if (!__ballot(!(v[0] && v[1] && v[2] && v[3] && h[0] == h0 && h[1] == h0 && h[2] == h0 && h[3] == h0))) {
-                distinct += 4;   // one per 64-position group, as below
-                uint32_t o = 0;
-                if (lane == 0) o = atomicAdd(&sm.cnt[h0 >> 1], 256u << ((h0 & 1) * 16));
-                const uint32_t base = (uni(o) >> ((h0 & 1) * 16)) & 0xffffu;
+        }
+    };
+    auto commit = [&](const uint32_t (&v)[kSV]) {
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t p = c0 + g + 64 * q + lane, slot = base + 64 * q + lane;
-                    idx[p] = (uint16_t)slot;
+        for (uint32_t k = 0; k < kSV; ++k)
+            if (lane + 64 * k < kSortStg) sm.stg[w][lane + 64 * k] = v[k];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto half_base = [&](uint32_t k) { return (w + kSortWaves * (k >> 1)) * kSortT + (k & 1) * kSortH; };
+    for (uint32_t i = tid; i < (uint32_t)(sizeof(sm.tab1) / 4); i += NT) sm.tab1[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)(sizeof(sm.tab2) / 4); i += NT) sm.tab2[i] = 0;
+    __syncthreads();
+    VCF_SORT_CLK();
+    // pass 1 counts (low 8 hash bits) and the adler32 sums over every byte
+    uint64_t sb = 0, swb = 0;
+    uint32_t sv[kSV];
+    if (half_base(0) < n) fetch(half_base(0), sv);
+    for (uint32_t k = 0, hb = half_base(0); hb < n; hb = half_base(++k)) {
+        const uint32_t t = hb / kSortT;
+        commit(sv);
+        if (half_base(k + 1) < n) fetch(half_base(k + 1), sv);
+        for (uint32_t g = 0; g < kSortH && hb + g < n; g += 64) {
+            const uint32_t j = g + lane, p = hb + j;
+            const uint32_t b0 = stg[j];
+            sb += b0;
+            swb += (uint64_t)(p < n ? n - p : 0u) * b0;
+            const bool valid = p < np;
+            const uint32_t h = hash3(b0, stg[j + 1], stg[j + 2]);
+            tile_count(sm.tab1, t * 256 + (h & 255u), valid, lane);
+        }
+        __builtin_amdgcn_wave_barrier();   // the staging area is rewritten next
+    }
+    __syncthreads();
+    VCF_SORT_CLK();
+    tile_scan<256>(sm, tab1, nt1, tid, w, lane);
+    VCF_SORT_CLK();
+    // pass 1 placement: hash << 16 | position to tmp[] in low-digit order; pass 2's counts
+    if (half_base(0) < np) fetch(half_base(0), sv);
+    for (uint32_t k = 0, hb = half_base(0); hb < np; hb = half_base(++k)) {
+        const uint32_t t = hb / kSortT;
+        commit(sv);
+        if (half_base(k + 1) < np) fetch(half_base(k + 1), sv);
+        for (uint32_t g = 0; g < kSortH && hb + g < np; g += 64) {
+            const uint32_t j = g + lane, p = hb + j;
+            const bool valid = p < np;
+            const uint32_t h = hash3(stg[j], stg[j + 1], stg[j + 2]), d = h & 255u;
+            const uint64_t m = digit_mask<8>(d, valid);
+            const uint32_t a = t * 256 + d;
+            const uint32_t cur = valid ? (uint32_t)tab1[a] : 0u;
+            if (valid && (m & lt) == 0) tab1[a] = (uint16_t)(cur + (uint32_t)__popcll(m));
+            const uint32_t slot = cur + (uint32_t)__popcll(m & lt);
+            if (valid) tmp[slot] = h << 16 | p;
+            // pass 2's count at the new slot (equal hashes over consecutive lanes have
+            // consecutive slots: a run in one tile adds with one atomic)
+            tile_count(sm.tab2, (slot / kSortT) * 128 + (h >> 8), valid, lane);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    VCF_SORT_CLK();
+    tile_scan<128>(sm, tab2, nt2, tid, w, lane);
+    VCF_SORT_CLK();
+    // pass 2 placement (high 7 bits): sorted[], idx[], hd[] but for each digit's first element of a tile
+    uint32_t distinct = 0;
+    for (uint32_t t = w; t < nt2; t += kSortWaves) {
+        lastk[lane] = 0xffffffffu;   // no element of any digit yet in this tile
+        lastk[lane + 64] = 0xffffffffu;
+        for (uint32_t half = 0; half < kSortT / 1024 && t * kSortT + half * 1024 < np; ++half) {
+            uint32_t e[16];   // the half tile's 16 groups, all loads in flight at once
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) {
+                const uint32_t i = t * kSortT + half * 1024 + 64 * k + lane;
+                e[k] = i < np ? tmp[i] : 0u;
+            }
+            for (uint32_t k = 0; k < 16 && t * kSortT + half * 1024 + 64 * k < np; ++k) {
+                const uint32_t i = t * kSortT + half * 1024 + 64 * k + lane;
+                const bool valid = i < np;
+                const uint32_t ek = e[k], d = ek >> 24;
+                const uint64_t m = digit_mask<7>(d, valid);
+                const uint32_t a = t * 128 + d;
+                const uint64_t below = m & lt;
+                const bool lead = valid && below == 0;
+                const uint32_t cur = valid ? (uint32_t)tab2[a] : 0u;
+                const uint32_t lk = lead ? lastk[d] : 0u;   // read before this group's update below
+                if (lead) tab2[a] = (uint16_t)(cur + (uint32_t)__popcll(m));
+                if (valid && (m >> lane) == 1) lastk[d] = ek;   // the digit's last lane in the group
+                const int pl = below ? 63 - __clzll((long long)below) : (int)lane;
+                const uint32_t ebelow = (uint32_t)__shfl((int)ek, pl, 64);
+                if (valid) {
+                    const uint32_t slot = cur + (uint32_t)__popcll(below), p = ek & 0xffffu;
                     sorted[slot] = (uint16_t)p;
-                }
-                continue;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                uint64_t rem = __ballot(v[q]), m0 = 0;
-                while (rem) {   // one distinct hash per round
-                    ++distinct;
-                    const uint32_t l = (uint32_t)__ffsll((unsigned long long)rem) - 1;
-                    const uint32_t hl = lane_val(h[q], l);
-                    const uint64_t m = __ballot(v[q] && h[q] == hl);
-                    if (v[q] && h[q] == hl) m0 = m;
-                    rem &= ~m;
-                }
-                mine[q] = m0;
-                rank[q] = (uint32_t)__popcll(m0 & lt);
-                cntj[q] = (uint32_t)__popcll(m0);
-            }
-            // the leaders' cursor updates, back to back (LDS executes them in order)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                old[q] = 0;
-                if (v[q] && rank[q] == 0) old[q] = atomicAdd(&sm.cnt[h[q] >> 1], cntj[q] << ((h[q] & 1) * 16));
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int leader = mine[q] ? __ffsll((unsigned long long)mine[q]) - 1 : (int)lane;
-                const uint32_t o = (uint32_t)__shfl((int)old[q], leader, 64);
-                if (v[q]) {
-                    const uint32_t p = c0 + g + 64 * q + lane;
-                    const uint32_t slot = ((o >> ((h[q] & 1) * 16)) & 0xffffu) + rank[q];
                     idx[p] = (uint16_t)slot;
-                    sorted[slot] = (uint16_t)p;
+                    const uint32_t prev = lead ? lk : ebelow;
+                    if (prev != 0xffffffffu) {
+                        const bool same = (prev >> 16) == (ek >> 16);
+                        hd[p] = same ? (uint16_t)(prev & 0xffffu) : (uint16_t)0;
+                        distinct += same && (prev & 0xffffu) >= (p & ~63u) ? 0u : 1u;
+                    }
                 }
             }
         }
+        __builtin_amdgcn_wave_barrier();
     }
-    for (int d = 32; d >= 1; d >>= 1) {
-        sb += __shfl_xor(sb, d, 64);
-        swb += __shfl_xor(swb, d, 64);
+    __syncthreads();
+    VCF_SORT_CLK();
+    // each digit's first element of a tile: its predecessor is the slot before it (another
+    // tile's, or another digit's: then the hashes differ), the hashes from the strip bytes
+    for (uint32_t pr = tid; pr < nt2 * 128; pr += NT) {
+        const uint32_t t = pr >> 7, d = pr & 127u;
+        const uint32_t end = tab2[pr];
+        const uint32_t start = t ? (uint32_t)tab2[pr - 128] : d ? (uint32_t)tab2[(nt2 - 1) * 128 + d - 1] : 0u;
+        if (end > start) {
+            const uint32_t p = sorted[start];
+            const uint32_t q = start ? (uint32_t)sorted[start - 1] : 0u;
+            const bool same = start && hash3(src[p], src[p + 1], src[p + 2]) == hash3(src[q], src[q + 1], src[q + 2]);
+            hd[p] = same ? (uint16_t)q : (uint16_t)0;
+            distinct += same && q >= (p & ~63u) ? 0u : 1u;
+        }
+    }
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        sb += __shfl_xor(sb, dd, 64);
+        swb += __shfl_xor(swb, dd, 64);
+        distinct += (uint32_t)__shfl_xor((int)distinct, dd, 64);
     }
     if (lane == 0) {
         sm.sums[w][0] = sb;
@@ -475,58 +547,18 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
         sm.distinct[w] = distinct;
     }
     __syncthreads();
-#if VCF_ZX_HEAD1
-    // pass 3 (the head kernel's work): hd[p] = sorted[idx[p] - 1], the bucket's previous
-    // slot, unless p is its bucket's first position (NIL).  After the scatter every
-    // counter holds its bucket's end, so bucket h starts where bucket h - 1 ends: no byte
-    // gathers to compare the previous slot's hash with p's.  4 consecutive positions per
-    // thread and step, their bytes as two dwords, idx as one 8-byte load.
-    {
-        uint16_t *hdw = reinterpret_cast<uint16_t *>(S.ws + kHdOff);
-        auto start_of = [&](uint32_t hh) -> uint32_t {
-            return hh ? (sm.cnt[(hh - 1) >> 1] >> (((hh - 1) & 1) * 16)) & 0xffffu : 0u;
-        };
-        for (uint32_t p0 = 4 * tid; p0 < np; p0 += 4 * NT) {
-            uint32_t d0, d1;
-            if (al4 && p0 + 8 <= n) {
-                d0 = *reinterpret_cast<const uint32_t *>(S.src + p0);
-                d1 = *reinterpret_cast<const uint32_t *>(S.src + p0 + 4);
-            } else {
-                d0 = d1 = 0;
-                for (uint32_t i = 0; i < 8; ++i)
-                    if (p0 + i < n) (i < 4 ? d0 : d1) |= (uint32_t)S.src[p0 + i] << (8 * (i & 3));
-            }
-            const uint64_t bb = (uint64_t)d1 << 32 | d0;
-            const bool full = p0 + 4 <= np;
-            uint32_t sl[4];
-            if (full) {
-                const uint2 iv = *reinterpret_cast<const uint2 *>(idx + p0);
-                sl[0] = iv.x & 0xffffu; sl[1] = iv.x >> 16; sl[2] = iv.y & 0xffffu; sl[3] = iv.y >> 16;
-            } else {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) sl[u] = p0 + u < np ? (uint32_t)idx[p0 + u] : 0u;
-            }
-            uint32_t r[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t hh = hash3((uint32_t)(bb >> (8 * u)) & 0xffu, (uint32_t)(bb >> (8 * u + 8)) & 0xffu,
-                                          (uint32_t)(bb >> (8 * u + 16)) & 0xffu);
-                r[u] = sl[u] > start_of(hh) ? (uint32_t)sorted[sl[u] - 1] : 0u;
-            }
-            if (full && (p0 & 3) == 0) {
-                *reinterpret_cast<uint2 *>(hdw + p0) = make_uint2(r[0] | r[1] << 16, r[2] | r[3] << 16);
-            } else {
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (p0 + u < np) hdw[p0 + u] = (uint16_t)r[u];
-            }
-        }
+    VCF_SORT_CLK();
+#if VCF_ZLIB_PROF
+    if (tid == 0) {
+        for (int i = 0; i + 1 < nck && i < 7; ++i) atomicAdd(&g_zprof[40 + i], ck[i + 1] - ck[i]);
+        atomicAdd(&g_zprof[47], 1ull);
     }
 #endif
+#undef VCF_SORT_CLK
     if (tid == 0) {
         uint64_t a = 0, b = 0;
         uint32_t dsum = 0;
-        for (int v = 0; v < kK1Waves; ++v) {
+        for (int v = 0; v < kSortWaves; ++v) {
             a += sm.sums[v][0];
             b += sm.sums[v][1];
             dsum += sm.distinct[v];
@@ -535,48 +567,12 @@ __global__ __launch_bounds__(64 * kK1Waves) void zlib_order_kernel(const uint8_t
         sums[0] = a;
         sums[1] = b;
         *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 16) = 0;   // K2's worklist length
+        *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 24) = dsum;   // the lazy parse's dispatch order key
 #ifdef VCF_ZX_LAZYALL   // A/B (diagnostic builds): every strip through the lazy parse
         *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = 1u;
 #else
         *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = dsum * kLazyDiv < np ? 1u : 0u;   // parse order
 #endif
-    }
-}
-
-// hd[p]: zlib's head[] as p is inserted -- the newest earlier position with
-// p's hash, i.e. the bucket's previous slot sorted[idx[p]-1] when that slot is
-// still p's bucket (same hash), else NIL (0, which zlib's position 0 also is).
-// Every position in parallel: kHdPer consecutive positions per thread.
-constexpr int kHdThreads = 256, kHdPer = 8;
-__global__ __launch_bounds__(kHdThreads) void zlib_head_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
-                                                              int32_t strip_bytes, int32_t spf,
-                                                              uint8_t *__restrict__ ws, int64_t s0)
-{
-    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s0 + blockIdx.y);
-    const uint32_t np = S.n >= 3 ? S.n - 2 : 0;
-    const uint32_t p0 = (blockIdx.x * kHdThreads + threadIdx.x) * kHdPer;
-    if (p0 >= np) return;
-    const uint16_t *idx = reinterpret_cast<const uint16_t *>(S.ws + kIdxOff);
-    const uint16_t *sorted = reinterpret_cast<const uint16_t *>(S.ws + kSortOff);
-    uint16_t *hd = reinterpret_cast<uint16_t *>(S.ws + kHdOff);
-    const uint32_t pn = min((uint32_t)kHdPer, np - p0);
-    uint32_t b[kHdPer + 2], q[kHdPer];
-#pragma unroll
-    for (int u = 0; u < kHdPer + 2; ++u) b[u] = (uint32_t)u < pn + 2 ? S.src[p0 + u] : 0u;
-#pragma unroll
-    for (int u = 0; u < kHdPer; ++u) {
-        const uint32_t i = (uint32_t)u < pn ? (uint32_t)idx[p0 + u] : 0u;
-        q[u] = i ? (uint32_t)sorted[i - 1] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < kHdPer; ++u) {
-        if ((uint32_t)u >= pn) break;
-        uint32_t r = 0;
-        if (q[u] && q[u] < p0 + u) {   // an earlier slot holds an earlier position; same bucket iff same hash
-            const uint32_t hq = hash3(S.src[q[u]], S.src[q[u] + 1], S.src[q[u] + 2]);
-            if (hq == hash3(b[u], b[u + 1], b[u + 2])) r = q[u];
-        }
-        hd[p0 + u] = (uint16_t)r;
     }
 }
 
@@ -972,7 +968,7 @@ struct Wave {
     // as soon as the current one is in use (the parse only moves forward, at most
     // MAX_MATCH positions at a time, so it always enters the next window)
     uint4 hv_n, iv_n;
-    // VCF_ZX_COHERENT (A/B): the workspace tables K1 and the head kernel wrote, read at agent scope
+    // VCF_ZX_COHERENT (A/B): the workspace tables K1 wrote, read at agent scope
     __device__ __forceinline__ static uint4 wload4(const uint16_t *a)
     {
 #if VCF_ZX_COHERENT
@@ -1693,6 +1689,44 @@ static_assert(VCF_ZX_LDSPAD || VCF_ZX_LAZYWIN != 3840 || VCF_ZX_WG != 1 || sizeo
 #else
 #define VCF_ZX_WPE_ATTR
 #endif
+// The lazy parse's dispatch order: a strip's parse time grows with its literals and
+// short matches, and the last workgroups dispatched form the kernel's tail on an
+// otherwise idle GPU -- so the strips go out longest first (by K1's distinct-hash
+// count, in 256 classes), the short ones last.  One workgroup: a counting sort of the
+// round's strips by class, descending; position i of the order is stored in strip
+// slot i's workspace (kSumOff + 28).  The order inside a class is whatever the
+// atomics give: it changes only the schedule, never a strip's bytes.
+#ifndef VCF_ZX_LPT   // A/B (diagnostic builds)
+#define VCF_ZX_LPT 1
+#endif
+constexpr int kLptThreads = 1024;
+__device__ __forceinline__ uint32_t lpt_class(uint32_t dsum) { return 255u - min(255u, dsum >> 7); }
+__global__ __launch_bounds__(kLptThreads) void zlib_lpt_kernel(uint8_t *__restrict__ ws, uint32_t cnt)
+{
+    __shared__ uint32_t hist[256];
+    const uint32_t tid = threadIdx.x;
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < cnt; i += kLptThreads)
+        atomicAdd(&hist[lpt_class(*reinterpret_cast<const uint32_t *>(ws + i * kWsPerStrip + kSumOff + 24))], 1u);
+    __syncthreads();
+    if (tid < 64) {   // exclusive scan of the 256 classes, 4 per lane
+        uint32_t c[4], t = 0;
+        for (int k = 0; k < 4; ++k) t += (c[k] = hist[4 * tid + k]);
+        uint32_t tot;
+        uint32_t run = excl_scan(t, tot);
+        for (int k = 0; k < 4; ++k) {
+            hist[4 * tid + k] = run;
+            run += c[k];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < cnt; i += kLptThreads) {
+        const uint32_t k = lpt_class(*reinterpret_cast<const uint32_t *>(ws + i * kWsPerStrip + kSumOff + 24));
+        const uint32_t pos = atomicAdd(&hist[k], 1u);
+        *reinterpret_cast<uint32_t *>(ws + (uint64_t)pos * kWsPerStrip + kSumOff + 28) = i;
+    }
+}
 template <bool LAZY>
 __global__ __launch_bounds__(64 * kParseWG) VCF_ZX_WPE_ATTR void zlib_parse_kernel(
     const uint8_t *__restrict__ in, int64_t frame_bytes, int32_t strip_bytes, int32_t spf, int32_t level,
@@ -1703,8 +1737,10 @@ __global__ __launch_bounds__(64 * kParseWG) VCF_ZX_WPE_ATTR void zlib_parse_kern
     const int wv_id = kParseWG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     ParseShared<LAZY> &sh = shs[wv_id];
     ParseSmem &sm = sh.sm;
-    const int64_t s = s0 + (int64_t)blockIdx.x * kParseWG + wv_id;
+    int64_t s = s0 + (int64_t)blockIdx.x * kParseWG + wv_id;
     if (s >= s_end) return;
+    if (LAZY && VCF_ZX_LPT)   // the longest-first order (zlib_lpt_kernel)
+        s = s0 + *reinterpret_cast<const uint32_t *>(ws + (s - s0) * kWsPerStrip + kSumOff + 28);
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s);
     if (strip_lazy(S) != LAZY) return;   // the other kernel codes this strip
     const uint32_t lane = lane_id();
@@ -1815,7 +1851,7 @@ int vcf_zlib_prof_read(unsigned long long *host24, int reset)
 {
     int rc = hip_check(hipMemcpyFromSymbol(host24, HIP_SYMBOL(g_zprof), sizeof(g_zprof)), "hipMemcpyFromSymbol");
     if (rc == VCF_OK && reset) {
-        static const unsigned long long z[24] = {};
+        static const unsigned long long z[48] = {};
         rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_zprof), z, sizeof(z)), "hipMemcpyToSymbol");
     }
     return rc;
@@ -1867,14 +1903,12 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     const int64_t total = spf * n_frames;
     hipStream_t st = (hipStream_t)stream;
     const int chunks = (int)((std::min<int64_t>(strip_bytes, frame_bytes) + kChunk - 1) / kChunk);
-    const unsigned hd_blocks = (unsigned)((std::min<int64_t>(strip_bytes, frame_bytes) + kHdThreads * kHdPer - 1) /
-                                          (kHdThreads * kHdPer));
-    // A round: K1 and the head table on the caller's stream; then the two kinds of
+    // A round: K1 on the caller's stream; then the two kinds of
     // strips side by side -- the lazy parse of the repetitive strips on the caller's
     // stream, K2a/K2b and the register-window parse of the others on a library side
     // stream (forked by an event, joined back before the next round reuses the
     // workspace).  The two sides touch disjoint strips: their own output slots,
-    // sizes and workspace regions; both only read K1's and the head kernel's tables.
+    // sizes and workspace regions; both only read K1's tables.
     // (Round 4's two workspace slots with rounds in flight are gone: with the
     // device-sized budget a call is one round up to ~30 000 strips.)
     AuxStreams &ax = aux_for_current_device();
@@ -1897,33 +1931,40 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     const ZRounds zr(total);
     const hipStream_t ms = st, ss = VCF_ZX_SERIAL ? st : VCF_ZX_NOPRIO ? ax.s[2] : side_hi[dev];
     auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws) -> int {
-        hipLaunchKernelGGL(zlib_order_kernel, dim3(cnt), dim3(64 * kK1Waves), 0, ms, in_dev, frame_bytes, strip_bytes,
+        hipLaunchKernelGGL(zlib_sort_kernel, dim3(cnt), dim3(64 * kSortWaves), 0, ms, in_dev, frame_bytes, strip_bytes,
                            (int32_t)spf, ws, s0);
-        int rc = hip_check(hipGetLastError(), "zlib_order_kernel launch");
+        int rc = hip_check(hipGetLastError(), "zlib_sort_kernel launch");
         if (rc != VCF_OK) return rc;
-        if (!VCF_ZX_HEAD1) {   // (VCF_ZX_HEAD1: K1's third pass writes hd[])
-            hipLaunchKernelGGL(zlib_head_kernel, dim3(hd_blocks, cnt), dim3(kHdThreads), 0, ms, in_dev, frame_bytes,
-                               strip_bytes, (int32_t)spf, ws, s0);
-            rc = hip_check(hipGetLastError(), "zlib_head_kernel launch");
-            if (rc != VCF_OK) return rc;
-        }
         if (ss != ms) {
             if ((rc = hip_check(hipEventRecord(ax.big[0], ms), "hipEventRecord")) != VCF_OK) return rc;
             if ((rc = hip_check(hipStreamWaitEvent(ss, ax.big[0], 0), "hipStreamWaitEvent")) != VCF_OK) return rc;
         }
+#ifdef VCF_ZX_NOSIDE   // diagnostic builds only: no side kernels (wrong output for non-lazy strips)
+        if (false)
+#endif
         hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, ss, in_dev,
                            frame_bytes, strip_bytes, (int32_t)spf, level, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_match_kernel launch");
+#ifdef VCF_ZX_NOSIDE
+        if (false)
+#endif
         if (rc == VCF_OK) {
             hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt, kK2bSplit), dim3(kK2bThreads), 0, ss, in_dev, frame_bytes,
                                strip_bytes, (int32_t)spf, level, ws, s0);
             rc = hip_check(hipGetLastError(), "zlib_chain_kernel launch");
         }
+#ifdef VCF_ZX_NOSIDE
+        if (false)
+#endif
         if (rc == VCF_OK) {
             hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(64 * kParseWG),
                                0, ss, in_dev, frame_bytes, strip_bytes, (int32_t)spf, level, out_dev, slot_bytes,
                                sizes_dev, ws, s0, s0 + (int64_t)cnt);
             rc = hip_check(hipGetLastError(), "zlib_parse_kernel launch");
+        }
+        if (rc == VCF_OK && VCF_ZX_LPT) {
+            hipLaunchKernelGGL(zlib_lpt_kernel, dim3(1), dim3(kLptThreads), 0, ms, ws, cnt);
+            rc = hip_check(hipGetLastError(), "zlib_lpt_kernel launch");
         }
         if (rc == VCF_OK) {
             hipLaunchKernelGGL(zlib_parse_kernel<true>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(64 * kParseWG),
