@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 
 
 def frame_indices(H, W, seed=0, Q=32):
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     import vcf_amd.dct as D
     return D.encode(synth_frame(H, W, seed), Q)
 
@@ -138,7 +138,7 @@ def frames_throughput(H, W, n_frames=16, seg_len=1 << 15, streams=8, reps=3):
 def c2_end_to_end(reps=5):
     from PIL import Image
 
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     from vcf_amd.codec import parser as P
     from vcf_amd.codec.dct2d import CoDec
     rows = []

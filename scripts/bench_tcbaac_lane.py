@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     import vcf_amd.dct as D
     from vcf_amd import _lib as L
     from vcf_amd import tcbaac as T

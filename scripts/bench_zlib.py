@@ -24,13 +24,13 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--only", default="", help="comma-separated workload names")
     args = ap.parse_args()
-    from bench import synth_frame
+    from vcf_amd.synthetic import synth_frame
     from vcf_amd import _lib as L
     from vcf_amd import dct
     from vcf_amd.codec.tiff import strip_layout
     from vcf_amd.device import DeviceBuffer, Event, Stream
     st = Stream()
-    from bench import c4_frame
+    from vcf_amd.synthetic import c4_frame
     sets = [("dct_1080p", (1080, 1920), "dct"), ("dct_c4_1080p", (1080, 1920), "c4"), ("dct_4k", (2160, 3840), "dct"),
             ("rgb_1080p", (1080, 1920), "rgb")]
     if args.only:

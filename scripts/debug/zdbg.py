@@ -5,7 +5,7 @@ import ctypes, sys, os, zlib
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-from bench import synth_frame, c4_frame
+from vcf_amd.synthetic import synth_frame, c4_frame
 from vcf_amd import _lib as L, dct
 from vcf_amd.codec.tiff import strip_layout
 from vcf_amd.device import DeviceBuffer, Stream

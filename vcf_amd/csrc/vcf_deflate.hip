@@ -69,9 +69,10 @@ constexpr int64_t kRfOff = kListOff + (int64_t)MAX_STRIP * 2;
 constexpr int64_t kRrOff = kRfOff + (int64_t)MAX_STRIP * 4;
 constexpr int64_t kSymOff = kRrOff + (int64_t)MAX_STRIP * 4;
 // adler sums (2 x u64), K2's worklist length, the parse order (lazy or not), K1's distinct-hash
-// count, the lazy parse's dispatch order (u32 each)
+// count, the lazy parse's dispatch order, the round's list of non-lazy strips (entry i in slot
+// i), their count (slot 0) (u32 each)
 constexpr int64_t kSumOff = kSymOff + (int64_t)LIT_BUFSIZE * 4;
-constexpr int64_t kWsPerStrip = kSumOff + 32;
+constexpr int64_t kWsPerStrip = kSumOff + 48;
 // Rounds: the strips of a call are processed in rounds whose workspace stays
 // under the budget, one round after the other on the caller's stream.  Every
 // round ends in a tail (the last strips' serial parses on a draining GPU), so
@@ -268,6 +269,20 @@ __device__ __forceinline__ Strip strip_of(const uint8_t *in, int64_t frame_bytes
             ws + (s - s0) * kWsPerStrip};
 }
 
+// The round's non-lazy strips, listed by K1: the side kernels (K2a, K2b, K3) loop over
+// this list on small grids instead of launching a workgroup per strip of the round that
+// returns at once for a lazy strip -- half a million such workgroups per C4 call
+// (K2a's with 36 KB of LDS, K2b's with 64 KB) competed with the lazy parse for
+// dispatch and CUs: 2-5 ms of a 65 ms call, different from one library load to the next.
+__device__ __forceinline__ uint32_t side_count(const uint8_t *ws)
+{
+    return *reinterpret_cast<const uint32_t *>(ws + kSumOff + 40);
+}
+__device__ __forceinline__ uint32_t side_strip(const uint8_t *ws, uint32_t i)
+{
+    return *reinterpret_cast<const uint32_t *>(ws + (int64_t)i * kWsPerStrip + kSumOff + 32);
+}
+
 // ---- K1: hash-bucket order of the positions, and the adler32 sums ----------
 // sorted[] lists the positions 0..n-3 bucket by bucket (buckets in hash order,
 // positions increasing inside a bucket) and idx[p] is p's slot, so zlib's chain
@@ -438,15 +453,46 @@ __global__ __launch_bounds__(64 * kSortWaves) void zlib_sort_kernel(const uint8_
         const uint32_t t = hb / kSortT;
         commit(sv);
         if (half_base(k + 1) < n) fetch(half_base(k + 1), sv);
-        for (uint32_t g = 0; g < kSortH && hb + g < n; g += 64) {
-            const uint32_t j = g + lane, p = hb + j;
-            const uint32_t b0 = stg[j];
-            sb += b0;
-            swb += (uint64_t)(p < n ? n - p : 0u) * b0;
-            const bool valid = p < np;
-            const uint32_t h = hash3(b0, stg[j + 1], stg[j + 2]);
-            tile_count(sm.tab1, t * 256 + (h & 255u), valid, lane);
+        // four consecutive positions per lane (a quad of 256 positions per step): a run of
+        // one digit adds its length with one atomic from its first position, the run's end
+        // being the next run's first position -- in this lane, else the next lane holding
+        // one (its first), else the quad's valid end
+        uint32_t qsb = 0, qswb = 0;   // this half tile's adler32 terms (< 2^32 over 1024 bytes)
+        for (uint32_t Q = 0; Q < kSortH / 256 && hb + Q * 256 < n; ++Q) {
+            const uint32_t j0 = Q * 256 + 4 * lane;
+            const uint64_t bb = (uint64_t)sm.stg[w][Q * 64 + lane + 1] << 32 | sm.stg[w][Q * 64 + lane];
+            const uint32_t V = np > hb + Q * 256 ? min(256u, np - (hb + Q * 256)) : 0u;   // valid positions
+            uint32_t d[4], hm = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t b = (uint32_t)(bb >> (8 * k)) & 0xffu, p = hb + j0 + k;
+                if (p < n) {
+                    qsb += b;
+                    qswb += (n - p) * b;
+                }
+                d[k] = hash3(b, (uint32_t)(bb >> (8 * k + 8)) & 0xffu, (uint32_t)(bb >> (8 * k + 16)) & 0xffu) & 255u;
+            }
+            const uint32_t dl = (uint32_t)__shfl_up((int)d[3], 1, 64);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool head = 4 * lane + k < V && (k ? d[k - 1] != d[k] : (lane == 0 || dl != d[0]));
+                hm |= (head ? 1u : 0u) << k;
+            }
+            const uint64_t above = __ballot(hm != 0) & ~((2ull << lane) - 1);
+            const int l2 = above ? __ffsll((unsigned long long)above) - 1 : (int)lane;
+            const uint32_t fh2 = (uint32_t)__shfl((int)(hm ? __builtin_ctz(hm) : 0u), l2, 64);
+            const uint32_t nxt = above ? 4u * (uint32_t)l2 + fh2 : V;   // the next lane's first run
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((hm >> k) & 1u) {
+                    const uint32_t rest = hm >> (k + 1);
+                    const uint32_t end = rest ? 4 * lane + k + 1 + __builtin_ctz(rest) : nxt;
+                    const uint32_t a = t * 256 + d[k];
+                    atomicAdd(&sm.tab1[a >> 1], (end - 4 * lane - k) << ((a & 1) * 16));
+                }
         }
+        sb += qsb;
+        swb += qswb;
         __builtin_amdgcn_wave_barrier();   // the staging area is rewritten next
     }
     __syncthreads();
@@ -569,10 +615,15 @@ __global__ __launch_bounds__(64 * kSortWaves) void zlib_sort_kernel(const uint8_
         *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 16) = 0;   // K2's worklist length
         *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 24) = dsum;   // the lazy parse's dispatch order key
 #ifdef VCF_ZX_LAZYALL   // A/B (diagnostic builds): every strip through the lazy parse
-        *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = 1u;
+        const bool lazy = true;
 #else
-        *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = dsum * kLazyDiv < np ? 1u : 0u;   // parse order
+        const bool lazy = dsum * kLazyDiv < np;
 #endif
+        *reinterpret_cast<uint32_t *>(S.ws + kSumOff + 20) = lazy ? 1u : 0u;   // parse order
+        if (!lazy) {   // onto the side kernels' list
+            const uint32_t i = atomicAdd(reinterpret_cast<uint32_t *>(ws + kSumOff + 40), 1u);
+            *reinterpret_cast<uint32_t *>(ws + (int64_t)i * kWsPerStrip + kSumOff + 32) = blockIdx.x;
+        }
     }
 }
 
@@ -582,16 +633,15 @@ __global__ __launch_bounds__(64 * kSortWaves) void zlib_sort_kernel(const uint8_
 // L-1 and L (longest_match's scan_end test), and when the first candidate of
 // p+1 is the first candidate of p plus one, its common prefix is p's minus
 // one (one byte is checked when p's reached the MAX_MATCH cap).
-__global__ __launch_bounds__(kK2Threads) void zlib_match_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
-                                                               int32_t strip_bytes, int32_t spf, int32_t level,
-                                                               uint8_t *__restrict__ ws, int64_t s0)
+__device__ __forceinline__ void k2a_strip(const uint8_t *__restrict__ in, int64_t frame_bytes, int32_t strip_bytes,
+                                          int32_t spf, int32_t level, uint8_t *__restrict__ ws, int64_t s0, int64_t s,
+                                          uint32_t *win32)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t win32[kK2Win / 4 + 4];
     uint8_t *win = reinterpret_cast<uint8_t *>(win32);
-    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s0 + blockIdx.y);
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s);
     const uint32_t n = S.n, p0 = blockIdx.x * kChunk;
     const uint32_t np = n >= 3 ? n - 2 : 0;
-    if (p0 >= np || strip_lazy(S)) return;
+    if (p0 >= np) return;
     Config cfg;
     level_config(level, cfg);
     const uint16_t *hd = reinterpret_cast<const uint16_t *>(S.ws + kHdOff);
@@ -705,6 +755,19 @@ __global__ __launch_bounds__(kK2Threads) void zlib_match_kernel(const uint8_t *_
     }
 }
 
+constexpr unsigned kSideK2a = 256, kSideK2b = 128, kSideK3 = 4096;   // side kernels' strips in flight
+__global__ __launch_bounds__(kK2Threads) void zlib_match_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+                                                               int32_t strip_bytes, int32_t spf, int32_t level,
+                                                               uint8_t *__restrict__ ws, int64_t s0)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t win32[kK2Win / 4 + 4];
+    const uint32_t cnt = side_count(ws);
+    for (uint32_t i = blockIdx.y; i < cnt; i += gridDim.y) {
+        k2a_strip(in, frame_bytes, strip_bytes, spf, level, ws, s0, s0 + side_strip(ws, i), win32);
+        __syncthreads();   // the window is refilled for the next strip
+    }
+}
+
 // ---- K2b: the listed positions' chains, 64 candidates per wave step ----------
 // One workgroup of 16 waves per strip, the whole strip in LDS; a wave takes one
 // listed position at a time.  Lane t evaluates candidate k = 1 + t (+64 per
@@ -712,16 +775,15 @@ __global__ __launch_bounds__(kK2Threads) void zlib_match_kernel(const uint8_t *_
 // beat the first candidate's length len1 (longest_match's scan_end test), so
 // only those do the full compare.  The reductions keep zlib's order: the first
 // candidate reaching nice, else the first reaching the longest length.
-__global__ __launch_bounds__(kK2bThreads) void zlib_chain_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
-                                                                int32_t strip_bytes, int32_t spf, int32_t level,
-                                                                uint8_t *__restrict__ ws, int64_t s0)
+__device__ __forceinline__ void k2b_strip(const uint8_t *__restrict__ in, int64_t frame_bytes, int32_t strip_bytes,
+                                          int32_t spf, int32_t level, uint8_t *__restrict__ ws, int64_t s0, int64_t s,
+                                          uint32_t *win32)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t win32[(MAX_STRIP + MAX_MATCH + 64) / 4];
     uint8_t *win = reinterpret_cast<uint8_t *>(win32);
-    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s0 + blockIdx.x);
+    const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s);
     const uint32_t n = S.n;
     const uint32_t cnt = *reinterpret_cast<const uint32_t *>(S.ws + kSumOff + 16);
-    if (cnt == 0 || strip_lazy(S)) return;
+    if (cnt == 0) return;
     Config cfg;
     level_config(level, cfg);
     const uint16_t *idx = reinterpret_cast<const uint16_t *>(S.ws + kIdxOff);
@@ -844,6 +906,17 @@ __global__ __launch_bounds__(kK2bThreads) void zlib_chain_kernel(const uint8_t *
             rf[p] = bf << 16 | (p - bfp);
             rr[p] = br << 16 | (p - brp);
         }
+    }
+}
+__global__ __launch_bounds__(kK2bThreads) void zlib_chain_kernel(const uint8_t *__restrict__ in, int64_t frame_bytes,
+                                                                int32_t strip_bytes, int32_t spf, int32_t level,
+                                                                uint8_t *__restrict__ ws, int64_t s0)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t win32[(MAX_STRIP + MAX_MATCH + 64) / 4];
+    const uint32_t cnt = side_count(ws);
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        k2b_strip(in, frame_bytes, strip_bytes, spf, level, ws, s0, s0 + side_strip(ws, i), win32);
+        __syncthreads();   // the strip copy is refilled for the next strip
     }
 }
 
@@ -1727,22 +1800,15 @@ __global__ __launch_bounds__(kLptThreads) void zlib_lpt_kernel(uint8_t *__restri
         *reinterpret_cast<uint32_t *>(ws + (uint64_t)pos * kWsPerStrip + kSumOff + 28) = i;
     }
 }
+// one strip's deflate_slow, trees and bits by the calling wave
 template <bool LAZY>
-__global__ __launch_bounds__(64 * kParseWG) VCF_ZX_WPE_ATTR void zlib_parse_kernel(
-    const uint8_t *__restrict__ in, int64_t frame_bytes, int32_t strip_bytes, int32_t spf, int32_t level,
-    uint8_t *__restrict__ out, int64_t slot_bytes, int32_t *__restrict__ sizes, uint8_t *__restrict__ ws, int64_t s0,
-    int64_t s_end)
+__device__ __forceinline__ void parse_strip(const uint8_t *__restrict__ in, int64_t frame_bytes, int32_t strip_bytes,
+                                            int32_t spf, int32_t level, uint8_t *__restrict__ out, int64_t slot_bytes,
+                                            int32_t *__restrict__ sizes, uint8_t *__restrict__ ws, int64_t s0,
+                                            int64_t s, ParseShared<LAZY> &sh)
 {
-    __shared__ __attribute__((aligned(16))) ParseShared<LAZY> shs[kParseWG];
-    const int wv_id = kParseWG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    ParseShared<LAZY> &sh = shs[wv_id];
     ParseSmem &sm = sh.sm;
-    int64_t s = s0 + (int64_t)blockIdx.x * kParseWG + wv_id;
-    if (s >= s_end) return;
-    if (LAZY && VCF_ZX_LPT)   // the longest-first order (zlib_lpt_kernel)
-        s = s0 + *reinterpret_cast<const uint32_t *>(ws + (s - s0) * kWsPerStrip + kSumOff + 28);
     const Strip S = strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s);
-    if (strip_lazy(S) != LAZY) return;   // the other kernel codes this strip
     const uint32_t lane = lane_id();
 #ifndef VCF_ZX_PARSEPRIO   // the lazy parse at wave priority 3: beside the side stream's K2b waves on a CU it wins issue (-0.7 %)
 #define VCF_ZX_PARSEPRIO 3
@@ -1821,6 +1887,34 @@ __global__ __launch_bounds__(64 * kParseWG) VCF_ZX_WPE_ATTR void zlib_parse_kern
     if (wv.bitpos & 31) wv.store_words(wv.bitpos >> 5, 1);
     const bool ovf = __ballot(wv.overflow) != 0;
     if (lane == 0) sizes[s] = ovf ? -1 : (int32_t)(wv.bitpos >> 3);
+}
+// LAZY: one strip per wave of the round, in the longest-first order (zlib_lpt_kernel),
+// non-lazy strips returning at once; K3 (!LAZY): the waves loop over K1's list of the
+// round's non-lazy strips
+template <bool LAZY>
+__global__ __launch_bounds__(64 * kParseWG) VCF_ZX_WPE_ATTR void zlib_parse_kernel(
+    const uint8_t *__restrict__ in, int64_t frame_bytes, int32_t strip_bytes, int32_t spf, int32_t level,
+    uint8_t *__restrict__ out, int64_t slot_bytes, int32_t *__restrict__ sizes, uint8_t *__restrict__ ws, int64_t s0,
+    int64_t s_end)
+{
+    __shared__ __attribute__((aligned(16))) ParseShared<LAZY> shs[kParseWG];
+    const int wv_id = kParseWG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    ParseShared<LAZY> &sh = shs[wv_id];
+    if constexpr (LAZY) {
+        int64_t s = s0 + (int64_t)blockIdx.x * kParseWG + wv_id;
+        if (s >= s_end) return;
+        if (VCF_ZX_LPT)   // the longest-first order (zlib_lpt_kernel)
+            s = s0 + *reinterpret_cast<const uint32_t *>(ws + (s - s0) * kWsPerStrip + kSumOff + 28);
+        if (!strip_lazy(strip_of(in, frame_bytes, strip_bytes, spf, ws, s0, s))) return;   // K3 codes this strip
+        parse_strip<true>(in, frame_bytes, strip_bytes, spf, level, out, slot_bytes, sizes, ws, s0, s, sh);
+    } else {
+        const uint32_t cnt = side_count(ws);
+        for (uint32_t i = blockIdx.x * kParseWG + wv_id; i < cnt; i += gridDim.x * kParseWG) {
+            parse_strip<false>(in, frame_bytes, strip_bytes, spf, level, out, slot_bytes, sizes, ws, s0,
+                               s0 + side_strip(ws, i), sh);
+            wave_sync();   // the wave's LDS is reused for its next strip
+        }
+    }
 }
 
 }  // namespace
@@ -1931,6 +2025,8 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
     const ZRounds zr(total);
     const hipStream_t ms = st, ss = VCF_ZX_SERIAL ? st : VCF_ZX_NOPRIO ? ax.s[2] : side_hi[dev];
     auto round = [&](int64_t s0, unsigned cnt, uint8_t *ws) -> int {
+        int rc0 = hip_check(hipMemsetAsync(ws + kSumOff + 40, 0, 4, ms), "hipMemsetAsync");   // K1's list: empty
+        if (rc0 != VCF_OK) return rc0;
         hipLaunchKernelGGL(zlib_sort_kernel, dim3(cnt), dim3(64 * kSortWaves), 0, ms, in_dev, frame_bytes, strip_bytes,
                            (int32_t)spf, ws, s0);
         int rc = hip_check(hipGetLastError(), "zlib_sort_kernel launch");
@@ -1942,14 +2038,14 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
 #ifdef VCF_ZX_NOSIDE   // diagnostic builds only: no side kernels (wrong output for non-lazy strips)
         if (false)
 #endif
-        hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, cnt), dim3(kK2Threads), 0, ss, in_dev,
+        hipLaunchKernelGGL(zlib_match_kernel, dim3((unsigned)chunks, std::min(cnt, kSideK2a)), dim3(kK2Threads), 0, ss, in_dev,
                            frame_bytes, strip_bytes, (int32_t)spf, level, ws, s0);
         rc = hip_check(hipGetLastError(), "zlib_match_kernel launch");
 #ifdef VCF_ZX_NOSIDE
         if (false)
 #endif
         if (rc == VCF_OK) {
-            hipLaunchKernelGGL(zlib_chain_kernel, dim3(cnt, kK2bSplit), dim3(kK2bThreads), 0, ss, in_dev, frame_bytes,
+            hipLaunchKernelGGL(zlib_chain_kernel, dim3(std::min(cnt, kSideK2b), kK2bSplit), dim3(kK2bThreads), 0, ss, in_dev, frame_bytes,
                                strip_bytes, (int32_t)spf, level, ws, s0);
             rc = hip_check(hipGetLastError(), "zlib_chain_kernel launch");
         }
@@ -1957,7 +2053,8 @@ int vcf_zlib_strips(const uint8_t *in_dev, int64_t n_frames, int64_t frame_bytes
         if (false)
 #endif
         if (rc == VCF_OK) {
-            hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(64 * kParseWG),
+            hipLaunchKernelGGL(zlib_parse_kernel<false>, dim3((std::min(cnt, kSideK3) + kParseWG - 1) / kParseWG),
+                               dim3(64 * kParseWG),
                                0, ss, in_dev, frame_bytes, strip_bytes, (int32_t)spf, level, out_dev, slot_bytes,
                                sizes_dev, ws, s0, s0 + (int64_t)cnt);
             rc = hip_check(hipGetLastError(), "zlib_parse_kernel launch");
