@@ -1637,6 +1637,8 @@ void launch_band21_t(const DwtGeom &g, const uint8_t *packed, long long n_frames
             brows = br;
         }
     }
+    if (const char *e = getenv("VCF_IDWT21_BROWS"))   // tuning knob (A/B of the band cut): level-1 rows per band
+        brows = std::max(2, std::min(atoi(e) / 2 * 2, (h1 + 1) / 2 * 2));
     const int n_bands = (h1 + brows - 1) / brows;
     const long long grid = per_band * n_bands;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kB21NT), 0, s, packed, g.packed_bytes, g.ll_off,
