@@ -159,6 +159,31 @@ def test_dct_codec_with_context_coders(tmp_path, monkeypatch, ec, ext):
     assert np.array_equal(np.asarray(Image.open(dec)), O.decode_frame(k, 40, 48, 32, 0))
 
 
+def test_dct_codec_cbaac_1080p(tmp_path, monkeypatch):
+    """Config C2 at its own size: one 1080p frame through -c CBAAC (the reference's
+    .adpt_arith, the host coder) -- the code stream decodes to the oracle's indices and
+    decode_fn's PNG equals the oracle's reconstruction (the reference-format
+    coder was tested at 40 x 48 only under -m gpu)."""
+    from oracle import oracle as O
+    from vcf_amd.codec.dct2d import CoDec
+    from vcf_amd.synthetic import synth_frame
+    monkeypatch.chdir(tmp_path)
+    H, W = 1080, 1920
+    rgb = synth_frame(H, W, seed=7)
+    src = _png(tmp_path / "o.png", rgb)
+    enc = str(tmp_path / "enc")
+    c = CoDec(_args("encode", ["-c", "CBAAC"]))
+    c.encode_fn(src, enc)
+    d = CoDec(_args("decode", ["-c", "CBAAC"]))
+    with open(enc + c.file_extension, "rb") as f:
+        got_k = d.decompress(f.read())
+    k = O.encode_frame(rgb, 32, 0)
+    assert np.array_equal(np.asarray(got_k).reshape(k.shape), k)
+    dec = str(tmp_path / "d.png")
+    d.decode_fn(enc, dec)
+    assert np.array_equal(np.asarray(Image.open(dec)), O.decode_frame(k, H, W, 32, 0))
+
+
 @pytest.mark.parametrize("n,batch", [(7, 3), (5, 8), (9, 2)])
 def test_staged_pipeline_equals_single_frames(tmp_path, n, batch):
     """encode_fns through the pinned double-buffered slots (equal-shaped PNGs)

@@ -350,6 +350,31 @@ __device__ __forceinline__ uint64_t digit_mask(uint32_t d, bool valid)
     }
     return valid ? m : 0ull;
 }
+// the same mask from one round per distinct digit (a lane's digit compared with a
+// leader's by readlane + ballot): fewer instructions when a group holds few digits, as
+// repetitive content does; past kDigitRounds rounds the bit-sliced form finishes
+#ifndef VCF_ZX_DIGITLOOP   // A/B (diagnostic builds)
+#define VCF_ZX_DIGITLOOP 1
+#endif
+constexpr int kDigitRounds = 6;
+template <int BITS>
+__device__ __forceinline__ uint64_t digit_mask_r(uint32_t d, bool valid)
+{
+    if (!VCF_ZX_DIGITLOOP) return digit_mask<BITS>(d, valid);
+    uint64_t rem = __ballot(valid), m0 = 0;
+    for (int r = 0; r < kDigitRounds && rem; ++r) {
+        const uint32_t hl = lane_val(d, (uint32_t)__ffsll((unsigned long long)rem) - 1);
+        const bool eq = valid && d == hl;
+        const uint64_t m = __ballot(eq);
+        if (eq) m0 = m;
+        rem &= ~m;
+    }
+    if (rem) {   // many digits (e.g. raw RGB): the rest bit-sliced
+        const uint64_t mb = digit_mask<BITS>(d, valid);
+        if ((rem >> lane_id()) & 1) m0 = mb;
+    }
+    return m0;
+}
 // a group's counts into the u16 table entries a: a run of one entry over consecutive
 // lanes (runs of one byte value) adds its length with one atomic from its first lane;
 // the valid lanes are a prefix
@@ -509,7 +534,7 @@ __global__ __launch_bounds__(64 * kSortWaves) void zlib_sort_kernel(const uint8_
             const uint32_t j = g + lane, p = hb + j;
             const bool valid = p < np;
             const uint32_t h = hash3(stg[j], stg[j + 1], stg[j + 2]), d = h & 255u;
-            const uint64_t m = digit_mask<8>(d, valid);
+            const uint64_t m = digit_mask_r<8>(d, valid);
             const uint32_t a = t * 256 + d;
             const uint32_t cur = valid ? (uint32_t)tab1[a] : 0u;
             if (valid && (m & lt) == 0) tab1[a] = (uint16_t)(cur + (uint32_t)__popcll(m));
@@ -541,7 +566,7 @@ __global__ __launch_bounds__(64 * kSortWaves) void zlib_sort_kernel(const uint8_
                 const uint32_t i = t * kSortT + half * 1024 + 64 * k + lane;
                 const bool valid = i < np;
                 const uint32_t ek = e[k], d = ek >> 24;
-                const uint64_t m = digit_mask<7>(d, valid);
+                const uint64_t m = digit_mask_r<7>(d, valid);
                 const uint32_t a = t * 128 + d;
                 const uint64_t below = m & lt;
                 const bool lead = valid && below == 0;
