@@ -1624,19 +1624,18 @@ void launch_band21_t(const DwtGeom &g, const uint8_t *packed, long long n_frames
     }
     const int h1 = g.hs[1], w1 = g.ws[1];
     const int n_tiles = (w1 + kB21C - 1) / kB21C;
-    // bands of an even number of level-1 rows; time ~ rounds x (rows + 4 halo + level-2 warm-up)
+    // bands of an even number of level-1 rows: the shortest bands (each re-reads a 7-row
+    // halo) that still leave at most three workgroups per resident slot -- measured
+    // (scripts/dwt_bands_scan.py, profiles/r06_dwt_band_cuts_decode.json): C3 decode 0.546 ms
+    // with one round of 216-row bands (the previous rounds x (rows + 7) model's pick), 0.529
+    // with 60-108 rows, 0.655 with 360: a few rounds of shorter bands balance better
     const long long per_band = (long long)n_tiles * n_frames;
     int brows = (h1 + 1) / 2 * 2;
-    long long best = -1;
-    for (int br = 2; br <= (h1 + 1) / 2 * 2; br += 2) {
-        const long long nb = (h1 + br - 1) / br;
-        const long long rounds = (per_band * nb + slots - 1) / slots;
-        const long long cost = rounds * (br + 7);
-        if (best < 0 || cost < best) {
-            best = cost;
+    for (int br = 16; br <= (h1 + 1) / 2 * 2; br += 2)
+        if (per_band * ((h1 + br - 1) / br) <= 3 * slots) {
             brows = br;
+            break;
         }
-    }
     if (const char *e = getenv("VCF_IDWT21_BROWS"))   // tuning knob (A/B of the band cut): level-1 rows per band
         brows = std::max(2, std::min(atoi(e) / 2 * 2, (h1 + 1) / 2 * 2));
     const int n_bands = (h1 + brows - 1) / brows;
