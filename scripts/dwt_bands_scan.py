@@ -1,7 +1,8 @@
 """The C3 encode (8 4K frames, l=5, bior4.4, Q=32) for several band cuts of the fused
 levels 1 + 2 kernel (VCF_DWT_BANDS: bands, read at each launch; 0 = the library's
 cost model) -- or with WHAT=decode the C3 decode for several cuts of the inverse
-2 + 1 kernel (VCF_IDWT21_BROWS: level-1 rows per band) -- interleaved over R rounds
+2 + 1 kernel (VCF_IDWT21_BROWS: level-1 rows per band; WHAT=decode_line: VCF_IDWT_BANDS, bands of the
+inverse line kernels of levels 3..5) -- interleaved over R rounds
 of N launches, HIP events; output checksums compared (the cut never changes a byte).
 python scripts/dwt_bands_scan.py [N] [R] [cuts...]"""
 import json
@@ -30,7 +31,7 @@ s = Stream()
 
 
 WHAT = os.environ.get("WHAT", "encode")
-KNOB = "VCF_DWT_BANDS" if WHAT == "encode" else "VCF_IDWT21_BROWS"
+KNOB = {"encode": "VCF_DWT_BANDS", "decode": "VCF_IDWT21_BROWS", "decode_line": "VCF_IDWT_BANDS"}[WHAT]
 dout = DeviceBuffer(F * H * W * 3)
 L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, LV, Q, dpk.ptr, dws.ptr, s.handle)
 
