@@ -353,9 +353,6 @@ __device__ __forceinline__ uint64_t digit_mask(uint32_t d, bool valid)
 // the same mask from one round per distinct digit (a lane's digit compared with a
 // leader's by readlane + ballot): fewer instructions when a group holds few digits, as
 // repetitive content does; past kDigitRounds rounds the bit-sliced form finishes
-#ifndef VCF_ZX_TMP16   // A/B (diagnostic builds): K1's pass-1 output as positions only, pass 2 re-hashing
-#define VCF_ZX_TMP16 1
-#endif
 #ifndef VCF_ZX_DIGITLOOP   // A/B (diagnostic builds)
 #define VCF_ZX_DIGITLOOP 1
 #endif
@@ -426,7 +423,6 @@ __global__ __launch_bounds__(64 * kSortWaves) void zlib_sort_kernel(const uint8_
     uint16_t *sorted = reinterpret_cast<uint16_t *>(S.ws + kSortOff);
     uint16_t *hd = reinterpret_cast<uint16_t *>(S.ws + kHdOff);
     uint32_t *tmp = reinterpret_cast<uint32_t *>(S.ws + kRfOff);
-    uint16_t *tmp16 = reinterpret_cast<uint16_t *>(S.ws + kRfOff);   // (VCF_ZX_TMP16: positions only)
     uint16_t *tab1 = reinterpret_cast<uint16_t *>(sm.tab1), *tab2 = reinterpret_cast<uint16_t *>(sm.tab2);
     constexpr uint32_t NT = 64 * kSortWaves;
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6, n = S.n;
@@ -543,10 +539,7 @@ __global__ __launch_bounds__(64 * kSortWaves) void zlib_sort_kernel(const uint8_
             const uint32_t cur = valid ? (uint32_t)tab1[a] : 0u;
             if (valid && (m & lt) == 0) tab1[a] = (uint16_t)(cur + (uint32_t)__popcll(m));
             const uint32_t slot = cur + (uint32_t)__popcll(m & lt);
-            if (valid) {
-                if (VCF_ZX_TMP16) tmp16[slot] = (uint16_t)p;
-                else tmp[slot] = h << 16 | p;
-            }
+            if (valid) tmp[slot] = h << 16 | p;
             // pass 2's count at the new slot (equal hashes over consecutive lanes have
             // consecutive slots: a run in one tile adds with one atomic)
             tile_count(sm.tab2, (slot / kSortT) * 128 + (h >> 8), valid, lane);
@@ -567,22 +560,12 @@ __global__ __launch_bounds__(64 * kSortWaves) void zlib_sort_kernel(const uint8_
 #pragma unroll
             for (uint32_t k = 0; k < 16; ++k) {
                 const uint32_t i = t * kSortT + half * 1024 + 64 * k + lane;
-                e[k] = i < np ? (VCF_ZX_TMP16 ? (uint32_t)tmp16[i] : tmp[i]) : 0u;
+                e[k] = i < np ? tmp[i] : 0u;
             }
             for (uint32_t k = 0; k < 16 && t * kSortT + half * 1024 + 64 * k < np; ++k) {
                 const uint32_t i = t * kSortT + half * 1024 + 64 * k + lane;
                 const bool valid = i < np;
-                uint32_t ek = e[k];
-                if (VCF_ZX_TMP16 && valid) {   // the hash again, from the position's bytes
-                    uint32_t b4;
-                    if (ek + 4 <= n) {
-                        __builtin_memcpy(&b4, src + ek, 4);
-                    } else {
-                        b4 = (uint32_t)src[ek] | (uint32_t)src[ek + 1] << 8 | (uint32_t)src[ek + 2] << 16;
-                    }
-                    ek |= hash3(b4 & 0xffu, (b4 >> 8) & 0xffu, (b4 >> 16) & 0xffu) << 16;
-                }
-                const uint32_t d = ek >> 24;
+                const uint32_t ek = e[k], d = ek >> 24;
                 const uint64_t m = digit_mask_r<7>(d, valid);
                 const uint32_t a = t * 128 + d;
                 const uint64_t below = m & lt;
