@@ -2,7 +2,9 @@
 levels 1 + 2 kernel (VCF_DWT_BANDS: bands, read at each launch; 0 = the library's
 cost model) -- or with WHAT=decode the C3 decode for several cuts of the inverse
 2 + 1 kernel (VCF_IDWT21_BROWS: level-1 rows per band; WHAT=decode_line: VCF_IDWT_BANDS, bands of the
-inverse line kernels of levels 3..5) -- interleaved over R rounds
+inverse line kernels of levels 3..5; WHAT=decode_pipe: VCF_DWT_DEC_PIPE 0 / 1, the decode on
+one stream or as the two-chunk frame pipeline; WHAT=encode_pipe: VCF_DWT_ENC_PIPE likewise for
+the encode) -- interleaved over R rounds
 of N launches, HIP events; output checksums compared (the cut never changes a byte).
 python scripts/dwt_bands_scan.py [N] [R] [cuts...]"""
 import json
@@ -31,20 +33,21 @@ s = Stream()
 
 
 WHAT = os.environ.get("WHAT", "encode")
-KNOB = {"encode": "VCF_DWT_BANDS", "decode": "VCF_IDWT21_BROWS", "decode_line": "VCF_IDWT_BANDS"}[WHAT]
+KNOB = {"encode": "VCF_DWT_BANDS", "decode": "VCF_IDWT21_BROWS", "decode_line": "VCF_IDWT_BANDS",
+        "decode_pipe": "VCF_DWT_DEC_PIPE", "encode_pipe": "VCF_DWT_ENC_PIPE"}[WHAT]
 dout = DeviceBuffer(F * H * W * 3)
 L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, LV, Q, dpk.ptr, dws.ptr, s.handle)
 
 
 def enc():
-    if WHAT == "encode":
+    if WHAT.startswith("encode"):
         L.call("vcf_dwt_dz_encode", din.ptr, F, H, W, w, LV, Q, dpk.ptr, dws.ptr, s.handle)
     else:
         L.call("vcf_dwt_dz_decode", dpk.ptr, F, H, W, w, LV, Q, dout.ptr, dws.ptr, s.handle)
 
 
 def setcut(c):
-    if c:
+    if c or WHAT.endswith("_pipe"):   # (*_pipe: 0 = one stream, 1 = the two-chunk pipeline)
         os.environ[KNOB] = str(c)
     else:
         os.environ.pop(KNOB, None)
@@ -56,8 +59,9 @@ for c in cuts:
     for _ in range(20):
         enc()
     s.synchronize()
-    crc[c] = zlib.crc32((dpk if WHAT == "encode" else dout).download(
-        np.empty(F * pb if WHAT == "encode" else F * H * W * 3, np.uint8)).tobytes())
+    enc_side = WHAT.startswith("encode")
+    crc[c] = zlib.crc32((dpk if enc_side else dout).download(
+        np.empty(F * pb if enc_side else F * H * W * 3, np.uint8)).tobytes())
 for r in range(R):
     for c in (cuts if r % 2 == 0 else cuts[::-1]):
         setcut(c)

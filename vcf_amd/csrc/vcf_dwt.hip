@@ -1474,7 +1474,7 @@ bool band12_ok(const DwtGeom &g, const WaveletDef &wd, int &id)
 
 template <unsigned ZL, unsigned ZH, int CT>
 void launch_band12_t(const DwtGeom &g, const uint8_t *rgb, long long n_frames, double *LL2, long long plane_stride,
-                     uint8_t *packed, int Q, hipStream_t s)
+                     uint8_t *packed, int Q, hipStream_t s, long long rule_frames)
 {
     const int h2 = g.hs[2], w2 = g.ws[2];
     const int n_tiles = (w2 + kBT2 - 1) / kBT2;
@@ -1489,7 +1489,8 @@ void launch_band12_t(const DwtGeom &g, const uint8_t *rgb, long long n_frames, d
                    ? v
                    : 256;
     }
-    const long long slots = 2LL * n_cu, per_band = 3LL * n_frames * n_tiles;
+    // (rule_frames: the frames of the whole call -- a pipelined call's chunks run side by side)
+    const long long slots = 2LL * n_cu, per_band = 3LL * rule_frames * n_tiles;
     int n_bands = 1;
     long long best = -1;
     for (int nb = 1; nb <= std::max(1, h2 / 2); ++nb) {
@@ -1519,10 +1520,10 @@ void launch_band12_t(const DwtGeom &g, const uint8_t *rgb, long long n_frames, d
 }
 
 void launch_band12(int id, const DwtGeom &g, const uint8_t *rgb, long long n_frames, double *LL2,
-                   long long plane_stride, uint8_t *packed, int Q, hipStream_t s)
+                   long long plane_stride, uint8_t *packed, int Q, hipStream_t s, long long rule_frames)
 {
-    if (id == 1) launch_band12_t<kB44DecLo, kB44DecHi, 1>(g, rgb, n_frames, LL2, plane_stride, packed, Q, s);
-    else launch_band12_t<0u, 0u, 2>(g, rgb, n_frames, LL2, plane_stride, packed, Q, s);
+    if (id == 1) launch_band12_t<kB44DecLo, kB44DecHi, 1>(g, rgb, n_frames, LL2, plane_stride, packed, Q, s, rule_frames);
+    else launch_band12_t<0u, 0u, 2>(g, rgb, n_frames, LL2, plane_stride, packed, Q, s, rule_frames);
 }
 
 // Line-based inverse level (idwt_line_kernel): 10-tap reconstruction filters
@@ -1609,7 +1610,7 @@ bool band21_ok(const DwtGeom &g, const WaveletDef &wd, int &id)
 
 template <bool FP, unsigned ZL, unsigned ZH, int CT>
 void launch_band21_t(const DwtGeom &g, const uint8_t *packed, long long n_frames, const double *prev,
-                     long long plane_stride, int lda, uint8_t *rgb, int Q, hipStream_t s)
+                     long long plane_stride, int lda, uint8_t *rgb, int Q, hipStream_t s, long long rule_frames)
 {
     auto kern = Q <= 256 ? idwt_band21_kernel<FP, ZL, ZH, CT, true> : idwt_band21_kernel<FP, ZL, ZH, CT, false>;
     static int slots = 0;   // resident workgroups on the device (per instantiation)
@@ -1629,7 +1630,8 @@ void launch_band21_t(const DwtGeom &g, const uint8_t *packed, long long n_frames
     // (scripts/dwt_bands_scan.py, profiles/r06_dwt_band_cuts_decode.json): C3 decode 0.546 ms
     // with one round of 216-row bands (the previous rounds x (rows + 7) model's pick), 0.529
     // with 60-108 rows, 0.655 with 360: a few rounds of shorter bands balance better
-    const long long per_band = (long long)n_tiles * n_frames;
+    // (rule_frames: the frames of the whole call -- a pipelined call's chunks run side by side)
+    const long long per_band = (long long)n_tiles * rule_frames;
     int brows = (h1 + 1) / 2 * 2;
     for (int br = 16; br <= (h1 + 1) / 2 * 2; br += 2)
         if (per_band * ((h1 + br - 1) / br) <= 3 * slots) {
@@ -1639,22 +1641,23 @@ void launch_band21_t(const DwtGeom &g, const uint8_t *packed, long long n_frames
     if (const char *e = getenv("VCF_IDWT21_BROWS"))   // tuning knob (A/B of the band cut): level-1 rows per band
         brows = std::max(2, std::min(atoi(e) / 2 * 2, (h1 + 1) / 2 * 2));
     const int n_bands = (h1 + brows - 1) / brows;
-    const long long grid = per_band * n_bands;
+    const long long grid = (long long)n_tiles * n_frames * n_bands;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kB21NT), 0, s, packed, g.packed_bytes, g.ll_off,
                        g.sb_off[2][0], g.sb_off[2][1], g.sb_off[2][2], g.sb_off[1][0], g.sb_off[1][1], g.sb_off[1][2],
                        prev, plane_stride, lda, rgb, g.hs[2], g.ws[2], h1, w1, Q, n_tiles, n_bands, brows);
 }
 
 void launch_band21(int id, const DwtGeom &g, const uint8_t *packed, long long n_frames, const double *prev,
-                   long long plane_stride, int lda, uint8_t *rgb, int Q, hipStream_t s)
+                   long long plane_stride, int lda, uint8_t *rgb, int Q, hipStream_t s, long long rule_frames)
 {
     const bool fp = g.levels == 2;   // LL2 from the packed u16 subband, else the level-3 plane
+    const long long rf = rule_frames;
     if (id == 1) {
-        if (fp) launch_band21_t<true, kB44RecLo, kB44RecHi, 1>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s);
-        else launch_band21_t<false, kB44RecLo, kB44RecHi, 1>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s);
+        if (fp) launch_band21_t<true, kB44RecLo, kB44RecHi, 1>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s, rf);
+        else launch_band21_t<false, kB44RecLo, kB44RecHi, 1>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s, rf);
     } else {
-        if (fp) launch_band21_t<true, 0u, 0u, 2>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s);
-        else launch_band21_t<false, 0u, 0u, 2>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s);
+        if (fp) launch_band21_t<true, 0u, 0u, 2>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s, rf);
+        else launch_band21_t<false, 0u, 0u, 2>(g, packed, n_frames, prev, plane_stride, lda, rgb, Q, s, rf);
     }
 }
 
@@ -1815,7 +1818,7 @@ constexpr long long kSepArea = 40000;
 
 static int encode_chain(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                         int32_t levels, int32_t Q, uint8_t *packed_dev, void *workspace_dev, hipStream_t s,
-                        const PipeHook *hook)
+                        const PipeHook *hook, long long rule_frames)
 {
     int rc = VCF_OK;
     Filters flt;
@@ -1855,7 +1858,7 @@ static int encode_chain(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int
     if (fused && band12_ok(g, kWavelets[wavelet], band_id)) {
         // levels 1 and 2 in one launch: LL1 never leaves the chip; LL2 lands where level 2's would
         if ((rc = hook_wait(hook, s)) != VCF_OK) return rc;
-        launch_band12(band_id, g, rgb_dev, n_frames, LL1, ws_stride, packed_dev, Q, s);
+        launch_band12(band_id, g, rgb_dev, n_frames, LL1, ws_stride, packed_dev, Q, s, rule_frames);
         if ((rc = hip_check(hipGetLastError(), "dwt_band12_kernel launch")) != VCF_OK) return rc;
         if ((rc = hook_rec(hook, s)) != VCF_OK) return rc;
         in = LL1;
@@ -1898,14 +1901,17 @@ int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
     // level-1+2 band kernel one launch fills the chip (C3: 0.594 ms on one
     // stream vs 0.635 ms pipelined, ABBA)
     const bool band = fast_filter(g.F) && band12_ok(g, kWavelets[wavelet], id);
-    if (!band && fast_filter(g.F) && pipeline_default(n_frames, H, W)) {
+    bool pipe = !band && fast_filter(g.F) && pipeline_default(n_frames, H, W);
+    // (A/B: VCF_DWT_ENC_PIPE=0/1, read per call; with the band kernel the chunks keep the call's band cut)
+    if (const char *e = getenv("VCF_DWT_ENC_PIPE")) pipe = atoi(e) != 0 && fast_filter(g.F) && pipeline_default(n_frames, H, W);
+    if (pipe) {
         const long long fpx = (long long)H * W * 3, wsf = 3 * plane_doubles(g);
         return run_pipelined(n_frames, kEncodePipe, s, [&](long long f0, long long n, hipStream_t cs, const PipeHook *hook) {
             return encode_chain(rgb_dev + f0 * fpx, n, H, W, wavelet, levels, Q, packed_dev + f0 * g.packed_bytes,
-                                (double *)workspace_dev + f0 * wsf, cs, hook);
+                                (double *)workspace_dev + f0 * wsf, cs, hook, n_frames);
         });
     }
-    return encode_chain(rgb_dev, n_frames, H, W, wavelet, levels, Q, packed_dev, workspace_dev, s, nullptr);
+    return encode_chain(rgb_dev, n_frames, H, W, wavelet, levels, Q, packed_dev, workspace_dev, s, nullptr, n_frames);
 }
 
 // one stream's level chain of the decode: coarsest level first; the line
@@ -1913,6 +1919,58 @@ int vcf_dwt_dz_encode(const uint8_t *rgb_dev, int64_t n_frames, int32_t H, int32
 // subbands shorter than F/2 (pywt's short-input branch: the coefficients wrap
 // around more than once) and filters longer than kMaxFastF on the separable
 // kernels, whose loads take any index modulo the line length
+// the fast decode's level chain over n_frames frames on stream s (the frame pipeline
+// calls it per chunk); rule_frames: the call's frames, for the band cut of levels 2 + 1
+static int decode_chain_fast(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
+                             int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, hipStream_t s,
+                             long long rule_frames)
+{
+    int rc = VCF_OK;
+    Filters flt;
+    if ((rc = device_filters(wavelet, flt)) != VCF_OK) return rc;
+    DwtGeom g;
+    dwt_geom(H, W, levels, kWavelets[wavelet].len, g);
+    const int F = g.F;
+    const long long pd = plane_doubles(g);
+    double *base = (double *)workspace_dev;
+    const long long ws_stride = pd;
+    double *A = base, *D = base + std::max<long long>((long long)g.hs[1] * g.ws[0], (long long)g.hs[1] * 2 * g.ws[1]);
+    double *P0 = D + (D - A), *P1 = P0 + 4LL * g.hs[1] * g.ws[1];
+    const double *prev = nullptr;
+    int lda = 0;
+    int id21 = 0;
+    const bool b21 = band21_ok(g, kWavelets[wavelet], id21);
+    for (int r = levels; r >= 1; --r) {
+        if (b21 && r == 2) {   // levels 2 and 1 in one launch, LL1 on chip
+            launch_band21(id21, g, packed_dev, n_frames, prev, ws_stride, lda, rgb_dev, Q, s, rule_frames);
+            return hip_check(hipGetLastError(), "idwt_band21_kernel launch");
+        }
+        const int h = g.hs[r], w = g.ws[r];
+        const int oh = r > 1 ? g.hs[r - 1] : 2 * h, ow = r > 1 ? g.ws[r - 1] : 2 * w;
+        double *out = (r & 1) ? P0 : P1;
+        const LevelArgs a{nullptr, 0, prev, ws_stride, out, const_cast<uint8_t *>(packed_dev), g.packed_bytes,
+                          g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], h, w, oh, ow, Q, lda,
+                          (unsigned)n_frames, flt, &kWavelets[wavelet], s};
+        int id = 0;
+        if (line_ok(kWavelets[wavelet], h, w, id)) launch_line(id, a, r == levels, r == 1, rgb_dev);
+        else inv_level(F, a, r == levels, r == 1, rgb_dev);
+        prev = out;
+        lda = ow;
+        if ((rc = hip_check(hipGetLastError(), "idwt level launch")) != VCF_OK) return rc;
+    }
+    return VCF_OK;
+}
+
+// The decode as a frame pipeline (two chunks on two library streams, one chunk's small
+// coarse levels beside the other chunk's levels 2 + 1 band, the band cut kept at the
+// whole call's): off -- measured slower in every form, round 6's with the fused band
+// included (C3 0.591 vs 0.528 ms, profiles/r06_dwt_decode_pipeline_not_kept.json).
+// VCF_DWT_DEC_PIPE=1 (read per call) selects it for A/B.
+constexpr PipeShape kDecodePipe{2, 2, false};
+#ifndef VCF_DWT_DEC_PIPE_DEFAULT
+#define VCF_DWT_DEC_PIPE_DEFAULT 0
+#endif
+
 int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, int32_t W, int32_t wavelet,
                       int32_t levels, int32_t Q, uint8_t *rgb_dev, void *workspace_dev, void *stream)
 {
@@ -1938,26 +1996,17 @@ int vcf_dwt_dz_decode(const uint8_t *packed_dev, int64_t n_frames, int32_t H, in
     const bool short_lines = g.hs[levels] < F / 2 || g.ws[levels] < F / 2;
     if (fast_filter(F) && !short_lines) {
         int id21 = 0;
-        const bool b21 = band21_ok(g, kWavelets[wavelet], id21);
-        for (int r = levels; r >= 1; --r) {
-            if (b21 && r == 2) {   // levels 2 and 1 in one launch, LL1 on chip
-                launch_band21(id21, g, packed_dev, n_frames, prev, ws_stride, lda, rgb_dev, Q, s);
-                return hip_check(hipGetLastError(), "idwt_band21_kernel launch");
-            }
-            const int h = g.hs[r], w = g.ws[r];
-            const int oh = r > 1 ? g.hs[r - 1] : 2 * h, ow = r > 1 ? g.ws[r - 1] : 2 * w;
-            double *out = (r & 1) ? P0 : P1;
-            const LevelArgs a{nullptr, 0, prev, ws_stride, out, const_cast<uint8_t *>(packed_dev), g.packed_bytes,
-                              g.ll_off, g.sb_off[r][0], g.sb_off[r][1], g.sb_off[r][2], h, w, oh, ow, Q, lda,
-                              (unsigned)n_frames, flt, &kWavelets[wavelet], s};
-            int id = 0;
-            if (line_ok(kWavelets[wavelet], h, w, id)) launch_line(id, a, r == levels, r == 1, rgb_dev);
-            else inv_level(F, a, r == levels, r == 1, rgb_dev);
-            prev = out;
-            lda = ow;
-            if ((rc = hip_check(hipGetLastError(), "idwt level launch")) != VCF_OK) return rc;
+        bool pipe = VCF_DWT_DEC_PIPE_DEFAULT && band21_ok(g, kWavelets[wavelet], id21) && levels > 2 &&
+                    pipeline_default(n_frames, H, W);
+        if (const char *e = getenv("VCF_DWT_DEC_PIPE")) pipe = atoi(e) != 0 && pipeline_default(n_frames, H, W);
+        if (pipe) {
+            const long long fpx = (long long)H * W * 3, wsf = 3 * pd;
+            return run_pipelined(n_frames, kDecodePipe, s, [&](long long f0, long long n, hipStream_t cs, const PipeHook *) {
+                return decode_chain_fast(packed_dev + f0 * g.packed_bytes, n, H, W, wavelet, levels, Q,
+                                         rgb_dev + f0 * fpx, (double *)workspace_dev + f0 * wsf, cs, n_frames);
+            });
         }
-        return VCF_OK;
+        return decode_chain_fast(packed_dev, n_frames, H, W, wavelet, levels, Q, rgb_dev, workspace_dev, s, n_frames);
     }
     for (int r = levels; r >= 1; --r) {
         const int h = g.hs[r], w = g.ws[r];
