@@ -950,17 +950,21 @@ __global__ __launch_bounds__(kK2bThreads) void zlib_chain_kernel(const uint8_t *
 // codes are written by gen_codes after its last frequency read, and the next
 // block's counts start from zero after its last code read.  The block's symbol
 // counts go straight into the frequency arrays (packed 16-bit LDS adds).
+// stg[0] carries the output's partial word from one block to the next; everything from
+// lfreq on is used only while a block is flushed (the frequencies are counted from the
+// block's symbols at its flush), so the lazy parse lays its window over that part
+// (ParseShared<true>) and reloads the window after each flush
 struct ParseSmem {
+    uint32_t stg[kStgWords];
+    uint32_t bcast[4];
     uint16_t lfreq[HEAP_SIZE + 1], ldad[HEAP_SIZE], llen[HEAP_SIZE];
     uint16_t dfreq[2 * D_CODES + 1 + 1], ddad[2 * D_CODES + 1], dlen[2 * D_CODES + 1];
     uint16_t bfreq[2 * BL_CODES + 1 + 1], bdad[2 * BL_CODES + 1], blen[2 * BL_CODES + 1];
     int16_t heap[HEAP_SIZE];
     uint8_t depth[HEAP_SIZE];
     uint16_t bl_count[MAX_BITS + 1];
-    uint32_t stg[kStgWords];
-    uint32_t bcast[4];
 };
-static_assert(offsetof(ParseSmem, lfreq) % 4 == 0, "packed adds into lfreq");
+static_assert(offsetof(ParseSmem, lfreq) % 16 == 0, "packed adds into lfreq; the lazy window over it");
 // the lazy parse's sliding window of the strip: [wbase, wbase + kLazyWin) holds
 // the bytes longest_match reads near the current position (back to p -
 // kNearDist, ahead to p + MAX_MATCH + 62); the parse shifts it forward in
@@ -972,8 +976,13 @@ static_assert(offsetof(ParseSmem, lfreq) % 4 == 0, "packed adds into lfreq");
 // CU (C4 deflate, ms: 34 560 B 245, 18 432 B 212, 14 080 B 189, 9 984 B 182,
 // 8 448 B 176, 7 168 B 172, 5 120 B 165, 3 840 B 161; 3 072 / 2 304 B 161 / 159:
 // no more than 16 workgroups reside on a CU)
+#ifndef VCF_ZX_ALIAS   // A/B (diagnostic builds): the lazy window laid over the flush-only LDS
+// (round 6: 1 -- the window grows from 3 840 to 9 216 bytes at the same 16 strips per CU,
+// so chain candidates up to 7 872 bytes back read LDS instead of HBM)
+#define VCF_ZX_ALIAS 1
+#endif
 #ifndef VCF_ZX_LAZYWIN   // A/B (diagnostic builds): the window's bytes (a multiple of 256)
-#define VCF_ZX_LAZYWIN 3840
+#define VCF_ZX_LAZYWIN (VCF_ZX_ALIAS ? 9216 : 3840)
 #endif
 constexpr uint32_t kLazyWin = VCF_ZX_LAZYWIN;
 #ifndef VCF_ZX_LWIN   // A/B (diagnostic builds): positions per lazy hd[] / idx[] register window (512 or 256)
@@ -1263,6 +1272,23 @@ struct Wave {
     __device__ __forceinline__ void fill(uint32_t from, uint32_t to)   // window bytes of input positions [from, to)
     {
         for (uint32_t P = from + lane_id(); P < to; P += 64) lwin[P - wbase] = (uint8_t)win_src(P);
+    }
+    // the whole window [wbase, wbase + kLazyWin) again (after a flush, whose tree arrays share
+    // its LDS): 16 bytes per lane from the strip where they lie inside it, the rest one at a time
+    __device__ __forceinline__ void reload()
+    {
+        wave_sync();
+        uint4 *w = reinterpret_cast<uint4 *>(lwin);
+        uint32_t from = wbase;
+        const uint32_t to = wbase + kLazyWin;
+        if ((((uintptr_t)(src + from)) & 15) == 0) {
+            const uint32_t vend = min(to, n & ~15u);
+            for (uint32_t P = from + 16 * lane_id(); P < vend; P += 1024)
+                w[(P - wbase) >> 4] = *reinterpret_cast<const uint4 *>(src + P);
+            from = max(from, vend);
+        }
+        fill(from, to);
+        wave_sync();
     }
     // keep [p - kNearDist, p + kLazyAhead) in the window: shift it forward when p runs
     // ahead (chain candidates farther back than the window read the strip in HBM:
@@ -1710,6 +1736,7 @@ struct Wave {
     {
         __threadfence();   // the block's symbols (lane 0's stores) before the other lanes read them
         wave_sync();
+        init_freqs();   // (here, not after the flush: the lazy window lies over these arrays in between)
         count_block();
         if (lane_id() == 0) {
             int max_blindex = 0;
@@ -1759,8 +1786,10 @@ struct Wave {
             emit_par(lane_id() == 0 ? sm.lfreq[END_BLOCK] : 0u, lane_id() == 0 ? sm.llen[END_BLOCK] : 0u);
         }
         nsym = 0;
-        init_freqs();
         if (last) windup();
+        if constexpr (LAZY) {
+            if (VCF_ZX_ALIAS && !last) reload();   // the flush used the window's LDS
+        }
     }
 };
 
@@ -1773,13 +1802,26 @@ template <>
 #define VCF_ZX_LDSPAD 0
 #endif
 struct ParseShared<true> {
+#if VCF_ZX_ALIAS
+    union {
+        ParseSmem sm;
+        struct {
+            uint32_t keep[offsetof(ParseSmem, lfreq) / 4];   // stg, bcast
+            uint32_t win32[kLazyWin / 4];                    // the sliding window (Wave::ensure)
+        } w;
+    };
+#else
     ParseSmem sm;
-    uint32_t win32[kLazyWin / 4];   // the sliding window of the strip (Wave::ensure)
+    struct {
+        uint32_t win32[kLazyWin / 4];   // the sliding window of the strip (Wave::ensure)
+    } w;
+#endif
 #if VCF_ZX_LDSPAD
     uint32_t pad[VCF_ZX_LDSPAD / 4];
 #endif
 };
-static_assert(VCF_ZX_LDSPAD || VCF_ZX_LAZYWIN != 3840 || VCF_ZX_WG != 1 || sizeof(ParseShared<true>) <= 10240,
+static_assert(VCF_ZX_LDSPAD || VCF_ZX_WG != 1 || sizeof(ParseShared<true>) <= 10240 ||
+                  (!VCF_ZX_ALIAS && VCF_ZX_LAZYWIN != 3840),
               "sixteen lazy-parse workgroups per CU");
 
 #ifdef VCF_ZX_WPE   // A/B (diagnostic builds): registers capped for this many waves per SIMD
@@ -1851,10 +1893,10 @@ __device__ __forceinline__ void parse_strip(const uint8_t *__restrict__ in, int6
     wv.lazy = (uint32_t)cfg.lazy;
     if constexpr (LAZY) {
         // the window's first kLazyWin bytes: the strip, then zeros (fill_window's high_water zeroing)
-        uint8_t *win = reinterpret_cast<uint8_t *>(sh.win32);
+        uint8_t *win = reinterpret_cast<uint8_t *>(sh.w.win32);
         if (((uintptr_t)S.src & 3) == 0) {
             const uint32_t *s32 = reinterpret_cast<const uint32_t *>(S.src);
-            for (uint32_t q = lane; q < kLazyWin / 4; q += 64) sh.win32[q] = 4 * q + 4 <= S.n ? s32[q] : 0u;
+            for (uint32_t q = lane; q < kLazyWin / 4; q += 64) sh.w.win32[q] = 4 * q + 4 <= S.n ? s32[q] : 0u;
             wave_sync();
             for (uint32_t p = (S.n & ~3u) + lane; p < min(S.n, kLazyWin); p += 64) win[p] = S.src[p];
         } else {
@@ -1867,7 +1909,8 @@ __device__ __forceinline__ void parse_strip(const uint8_t *__restrict__ in, int6
         wv.idx = reinterpret_cast<const uint16_t *>(S.ws + kIdxOff);
         wv.sorted = reinterpret_cast<const uint16_t *>(S.ws + kSortOff);
     }
-    wv.init_freqs();   // includes the barrier for the staging words and the window
+    if (!LAZY || !VCF_ZX_ALIAS) wv.init_freqs();   // (each flush zeroes them again first)
+    wave_sync();   // the staging words and the window
 
     const uint32_t hdr = zlib_header(level);
     wv.emit_par(lane == 0 ? ((hdr >> 8) | ((hdr & 0xffu) << 8)) : 0u, lane == 0 ? 16u : 0u);
