@@ -975,7 +975,8 @@ static_assert(offsetof(ParseSmem, lfreq) % 16 == 0, "packed adds into lfreq; the
 // their far reads cost, down to the 3 840-byte window that makes 16 strips per
 // CU (C4 deflate, ms: 34 560 B 245, 18 432 B 212, 14 080 B 189, 9 984 B 182,
 // 8 448 B 176, 7 168 B 172, 5 120 B 165, 3 840 B 161; 3 072 / 2 304 B 161 / 159:
-// no more than 16 workgroups reside on a CU)
+// no more than 16 workgroups reside on a CU).  Round 6 lays the window over the
+// flush-only part of ParseSmem (VCF_ZX_ALIAS): 9 216 bytes at the same 16 strips per CU.
 #ifndef VCF_ZX_ALIAS   // A/B (diagnostic builds): the lazy window laid over the flush-only LDS
 // (round 6: 1 -- the window grows from 3 840 to 9 216 bytes at the same 16 strips per CU,
 // so chain candidates up to 7 872 bytes back read LDS instead of HBM)
