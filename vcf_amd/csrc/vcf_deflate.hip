@@ -998,7 +998,10 @@ constexpr uint32_t kLazyAhead = 320;
 // the near distance the window keeps behind p after a shift: candidates at most
 // this far back read the window, farther ones (zlib reaches MAX_DIST back) read
 // the strip in HBM (Wave::far_*); shifts come every ~1 KB
-constexpr uint32_t kShiftSlack = kLazyWin >= 8192 ? 1024 : 512;   // bytes a shift leaves ahead
+#ifndef VCF_ZX_SLACK   // A/B (diagnostic builds): bytes a window shift leaves ahead
+#define VCF_ZX_SLACK (kLazyWin >= 8192 ? 1024 : 512)
+#endif
+constexpr uint32_t kShiftSlack = VCF_ZX_SLACK;   // bytes a shift leaves ahead
 constexpr uint32_t kNearDist = kLazyWin >= MAX_DIST + kLazyAhead + kShiftSlack ? (uint32_t)MAX_DIST
                                                                                : kLazyWin - kLazyAhead - kShiftSlack;
 static_assert(kLazyWin % 256 == 0 && kNearDist >= 512, "window too short");
